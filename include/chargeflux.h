@@ -1,0 +1,154 @@
+/*
+ * chargeflux.h — C-ABI boundary of the MI355X-native ChargeFlux (CoulForce) evaluator.
+ *
+ * This is the drop-in boundary for the reference's hot path
+ *   CoulPlugin::CalcCoulForceKernel::{initialize, execute}
+ *   (reference: openmmapi/include/CoulKernels.h:15-38,
+ *    platforms/reference/src/ReferenceCoulKernels.cpp:230-636).
+ *
+ * Plain C: pointers, sizes and int error codes only.  No C++ exceptions, no torch
+ * types cross it.  An OpenMM plugin or a ctypes/cffi binding
+ * calls these functions; the Python mirror `openmmcoul` in this repo does exactly that.
+ *
+ * Units follow the reference (OpenMM): nm, e, kJ/mol, rad.  All arithmetic is fp64.
+ */
+#ifndef CHARGEFLUX_H_
+#define CHARGEFLUX_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#if defined(_WIN32)
+#define CF_EXPORT __declspec(dllexport)
+#else
+#define CF_EXPORT __attribute__((visibility("default")))
+#endif
+
+#define CF_API_VERSION 1
+
+/* Error codes (negative).  cf_last_error() returns the message of the last failure
+ * on the calling thread.  Mirrors the reference's OpenMMException paths. */
+#define CF_OK 0
+#define CF_ERR_INVALID -1  /* bad argument / parameter validation failed     */
+#define CF_ERR_HIP -2      /* a HIP runtime call failed                       */
+#define CF_ERR_STATE -3    /* call sequence error (e.g. end without begin)    */
+#define CF_ERR_NOMEM -4    /* device allocation failed                        */
+
+/* Coulomb constant ONE_4PI_EPS0 (kJ mol^-1 nm e^-2), OpenMM 7.x value used by the
+ * reference via openmm/reference/SimTKOpenMMRealType.h (ReferenceCoulKernels.cpp:7). */
+#define CF_ONE_4PI_EPS0 138.935456
+
+/*
+ * Force parameters: the flat storage of CoulPlugin::CoulForce
+ * (reference: openmmapi/include/CoulForce.h:138-149, openmmapi/src/CoulForce.cpp:12-140).
+ * Arrays are host memory, read only during cf_create.
+ */
+typedef struct cf_params {
+    int32_t num_particles;
+    const double* charges;  /* [N]  addParticle(charge, ...)          CoulForce.cpp:18-22 */
+    const double* sigmas;   /* [N]  LJ sigma (nm)                                          */
+    const double* epsilons; /* [N]  LJ epsilon (kJ/mol)                                    */
+
+    int32_t num_exceptions;
+    const int32_t* exceptions; /* [2E] excluded pairs (p1,p2)         CoulForce.cpp:56-68 */
+
+    int32_t num_flux_bonds;
+    const int32_t* flux_bond_idx;    /* [2B] (p1,p2)                  CoulForce.cpp:78-94   */
+    const double* flux_bond_params;  /* [2B] (k [e/nm], b [nm])                             */
+    int32_t num_flux_angles;
+    const int32_t* flux_angle_idx;   /* [3A] (p1,p2,p3), p2 central   CoulForce.cpp:96-114  */
+    const double* flux_angle_params; /* [2A] (k [e/rad], theta0 [rad])                      */
+    int32_t num_flux_waters;
+    const int32_t* flux_water_idx;   /* [3W] (O,H1,H2)                CoulForce.cpp:116-140 */
+    const double* flux_water_params; /* [5W] (k1,k2,kub [e/nm], b0,ub0 [nm])                */
+
+    int32_t use_pbc;          /* setUsesPeriodicBoundaryConditions   CoulForce.cpp:52-54   */
+    double cutoff;            /* setCutoffDistance (nm), PBC only                          */
+    double ewald_tol;         /* setEwaldErrorTolerance                                    */
+    double default_box[9];    /* System::getDefaultPeriodicBoxVectors, rows a,b,c (nm);
+                                 kmax is derived from THIS box (ReferenceCoulKernels.cpp:399-420) */
+} cf_params;
+
+/* Execution options (all-zero = single GPU, device 0, default stream). */
+typedef struct cf_options {
+    int32_t device;      /* HIP device ordinal                                             */
+    void* stream;        /* hipStream_t to enqueue on (NULL = the null stream)             */
+    int32_t rank;        /* atom-decomposition rank (0..world_size-1)                       */
+    int32_t world_size;  /* 0 or 1 = single GPU                                            */
+    int32_t kspace_algo; /* 0 = default (MFMA fp64 separable), 1 = direct VALU (check path) */
+    int32_t reserved[7];
+} cf_options;
+
+/* compute flags */
+#define CF_INCLUDE_FORCES 1
+#define CF_INCLUDE_ENERGY 2
+
+typedef struct cf_handle cf_handle;
+
+CF_EXPORT int cf_api_version(void);
+CF_EXPORT const char* cf_last_error(void);
+
+/* Replaces ReferenceCalcCoulForceKernel::initialize (ReferenceCoulKernels.cpp:230-422). */
+CF_EXPORT int cf_create(const cf_params* params, const cf_options* options, cf_handle** out);
+CF_EXPORT int cf_destroy(cf_handle* h);
+
+/* Ewald parameters chosen at initialize: alpha (nm^-1) and odd kmax per axis
+ * (ReferenceCoulKernels.cpp:32-35, 401-420). */
+CF_EXPORT int cf_get_ewald_params(const cf_handle* h, double* alpha, int32_t kmax[3]);
+/* Owned atom range [lo, hi) of this rank (all atoms when world_size <= 1). */
+CF_EXPORT int cf_get_owned_range(const cf_handle* h, int32_t* lo, int32_t* hi);
+/* Host-only (no device needed): the atom decomposition cf_create would use.  Ranges are
+ * contiguous and never split a molecule (connected component of flux terms + exceptions). */
+CF_EXPORT int cf_partition(const cf_params* params, int32_t world_size, int32_t rank, int32_t* lo, int32_t* hi);
+
+/*
+ * Replaces ReferenceCalcCoulForceKernel::execute (ReferenceCoulKernels.cpp:424-636).
+ * Device-resident, asynchronous on the handle's stream:
+ *   pos_dev    [N*3] fp64 positions (nm), AoS x,y,z, DEVICE memory
+ *   box9       host array, current periodic box vectors (rows); ignored without PBC
+ *   forces_dev [N*3] fp64 DEVICE buffer; forces are ADDED (+=) like the reference
+ *              (ReferenceCoulKernels.cpp:426, 455, 585, 630).  Only owned atoms when world_size>1.
+ *   energy_dev [1] fp64 DEVICE scalar, OVERWRITTEN with the (partial, per rank) energy.
+ * Either output may be NULL.  Energy semantics follow the reference, including its
+ * quirk that the self/real-space/exclusion terms are accumulated even without
+ * CF_INCLUDE_ENERGY in periodic mode (ReferenceCoulKernels.cpp:507-510, 592, 619).
+ */
+CF_EXPORT int cf_compute(cf_handle* h, const double* pos_dev, const double* box9, int flags,
+                         double* forces_dev, double* energy_dev);
+
+/* Split-phase form for multi-GPU: begin computes charges and this rank's partial
+ * structure factors; the caller all-reduces (sum) the buffer returned by
+ * cf_kspace_buffer (fp64, on device, on the handle's stream ordering); end finishes. */
+CF_EXPORT int cf_compute_begin(cf_handle* h, const double* pos_dev, const double* box9, int flags);
+CF_EXPORT int cf_kspace_buffer(cf_handle* h, double** buf_dev, int64_t* count);
+CF_EXPORT int cf_compute_end(cf_handle* h, double* forces_dev, double* energy_dev);
+
+/* Synchronous host-memory convenience (H2D positions, D2H forces/energy): what an
+ * OpenMM Reference/CPU-platform adapter calls.  forces_host is ADDED to. */
+CF_EXPORT int cf_compute_host(cf_handle* h, const double* pos_host, const double* box9, int flags,
+                              double* forces_host, double* energy_host);
+
+/* Diagnostics of the last evaluation (synchronous, host outputs).
+ *   charges [N]  realcharges after charge flux          (ReferenceCoulKernels.cpp:37-228)
+ *   dedq    [N]  dE/dq_i (complete: self+recip+direct+exclusion)
+ *   terms   [4]  E_self, E_recip, E_direct(incl. LJ), E_exclusion (PBC); [0,0,E,0] without PBC */
+CF_EXPORT int cf_get_charges(cf_handle* h, double* charges_host);
+CF_EXPORT int cf_get_dedq(cf_handle* h, double* dedq_host);
+CF_EXPORT int cf_get_energy_terms(cf_handle* h, double terms[4]);
+CF_EXPORT int cf_synchronize(cf_handle* h);
+
+/* Per-kernel timing: when enabled, start/stop hipEvents are recorded on the handle's
+ * stream around every kernel launch of every evaluation (negligible overhead).
+ * cf_get_timing synchronises and returns, per phase, the summed milliseconds and the
+ * number of recorded launches since cf_set_timing; names are 16-byte NUL-padded. */
+CF_EXPORT int cf_set_timing(cf_handle* h, int enable);
+CF_EXPORT int cf_get_timing(cf_handle* h, int32_t max_phases, char* names, double* total_ms, int32_t* calls,
+                            int32_t* nphases);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CHARGEFLUX_H_ */

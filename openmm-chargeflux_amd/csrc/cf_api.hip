@@ -1,0 +1,669 @@
+// cf_api.hip — the C-ABI (include/chargeflux.h) over the HIP kernels.
+//
+// cf_create  replaces ReferenceCalcCoulForceKernel::initialize (ReferenceCoulKernels.cpp:230-422)
+// cf_compute replaces ReferenceCalcCoulForceKernel::execute    (ReferenceCoulKernels.cpp:424-636)
+//
+// Host-side work happens only in cf_create (topology, CSR gathers, Ewald parameters,
+// launch plans, device allocation).  A compute call is a fixed sequence of kernel
+// launches on the handle's stream with no host synchronisation (unless the caller asks
+// for host outputs), so it can be captured into a hipGraph.
+#include <hip/hip_runtime.h>
+
+#include <hipcub/hipcub.hpp>
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <numeric>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "cf_internal.h"
+
+// Per-kernel HIP-event timing (cf_set_timing / cf_get_timing): start/stop events are
+// recorded on the handle's stream around every launch, so bench.py can report kernel
+// durations measured on the stream the kernels actually run on.
+enum Phase { PH_FLUX, PH_PREP, PH_CELLS, PH_TABLES, PH_SFAC, PH_COEFFS, PH_FORCE, PH_DIRECT, PH_ASSEMBLE,
+             PH_ENERGY, PH_COUNT };
+static const char* kPhaseNames[PH_COUNT] = {"flux_terms", "atoms_prep", "cell_sort", "kspace_tables",
+                                            "kspace_sfac", "kspace_coeffs", "kspace_force", "direct",
+                                            "assemble", "energy"};
+constexpr int kMaxTimed = 8192;
+
+struct cf_handle {
+    cf::Handle h;
+    bool timing = false;
+    std::vector<hipEvent_t> ev[PH_COUNT];  // pairs (start, stop)
+    int nrec[PH_COUNT] = {};
+    std::vector<void*> allocs;
+    double* pos_host_dev = nullptr;   // cf_compute_host staging
+    double* frc_host_dev = nullptr;
+    double* ene_host_dev = nullptr;
+    const double* pos_pending = nullptr;
+};
+
+namespace {
+
+thread_local std::string g_err;
+
+struct CfError : std::runtime_error {
+    int code;
+    CfError(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+[[noreturn]] void fail(int code, const std::string& msg) { throw CfError(code, msg); }
+
+template <class F>
+int guarded(F&& f) {
+    try {
+        f();
+        return CF_OK;
+    } catch (const CfError& e) {
+        g_err = e.what();
+        return e.code;
+    } catch (const std::bad_alloc&) {
+        g_err = "host allocation failed";
+        return CF_ERR_NOMEM;
+    } catch (const std::exception& e) {
+        g_err = e.what();
+        return CF_ERR_HIP;
+    }
+}
+
+template <class T>
+T* dalloc(cf_handle* H, size_t count) {
+    if (count == 0) count = 1;
+    void* p = nullptr;
+    hipError_t e = hipMalloc(&p, count * sizeof(T));
+    if (e != hipSuccess) fail(CF_ERR_NOMEM, std::string("hipMalloc failed: ") + hipGetErrorString(e));
+    H->allocs.push_back(p);
+    return static_cast<T*>(p);
+}
+
+template <class T>
+T* dupload(cf_handle* H, const std::vector<T>& v) {
+    T* p = dalloc<T>(H, v.size());
+    if (!v.empty()) cf::check_hip(hipMemcpy(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice), "upload");
+    return p;
+}
+
+// getEwaldParamValue, ReferenceCoulKernels.cpp:32-35
+double ewald_param_value(int kmax, double width, double alpha) {
+    double t = kmax * M_PI / (width * alpha);
+    return 0.05 * std::sqrt(width * alpha) * kmax * std::exp(-t * t);
+}
+
+void check_box_orthorhombic(const double* b, const char* what) {
+    if (b[1] != 0 || b[2] != 0 || b[3] != 0 || b[5] != 0 || b[6] != 0 || b[7] != 0)
+        fail(CF_ERR_INVALID, std::string(what) + ": only orthorhombic periodic boxes are supported");
+    if (!(b[0] > 0 && b[4] > 0 && b[8] > 0)) fail(CF_ERR_INVALID, std::string(what) + ": box lengths must be > 0");
+}
+
+int find_root(std::vector<int>& p, int x) {
+    while (p[x] != x) { p[x] = p[p[x]]; x = p[x]; }
+    return x;
+}
+
+void set_cells(cf_handle* H, const double L[3]) {
+    cf::Handle& h = H->h;
+    int nc[3];
+    for (int d = 0; d < 3; d++) {
+        double v = std::floor(L[d] / h.cutoff);
+        nc[d] = (int)std::max(1.0, std::min(v, 1024.0));
+    }
+    int64_t ncell = (int64_t)nc[0] * nc[1] * nc[2];
+    if (ncell > h.ncell_alloc) {
+        // grow (not graph-capture safe; only happens when the box grows past the initial grid)
+        if (h.cell_start) { (void)hipFree(h.cell_start); (void)hipFree(h.cell_end); }
+        cf::check_hip(hipMalloc(&h.cell_start, sizeof(int) * ncell), "cells");
+        cf::check_hip(hipMalloc(&h.cell_end, sizeof(int) * ncell), "cells");
+        h.ncell_alloc = (int)ncell;
+    }
+    h.nc[0] = nc[0]; h.nc[1] = nc[1]; h.nc[2] = nc[2];
+}
+
+void set_box(cf_handle* H, const double* box9) {
+    cf::Handle& h = H->h;
+    if (!h.pbc) { h.box_L[0] = h.box_L[1] = h.box_L[2] = 1.0; return; }
+    if (!box9) fail(CF_ERR_INVALID, "periodic box required");
+    check_box_orthorhombic(box9, "current box");
+    double L[3] = {box9[0], box9[4], box9[8]};
+    for (int d = 0; d < 3; d++)
+        if (h.cutoff > 0.5 * L[d] * (1 + 1e-12))
+            fail(CF_ERR_INVALID, "cutoff exceeds half the periodic box (minimum image would be ambiguous)");
+    h.box_L[0] = L[0]; h.box_L[1] = L[1]; h.box_L[2] = L[2];
+    set_cells(H, L);
+}
+
+// Atom decomposition: contiguous owned ranges [lo,hi), cut only where no molecule
+// (connected component of flux terms + exclusions) is split, so the chain rule and the
+// exclusion correction stay rank-local.
+void partition(const cf_params* p, int world, int rank, int* lo, int* hi) {
+    const int n = p->num_particles;
+    if (world <= 1) { *lo = 0; *hi = n; return; }
+    std::vector<int> par(n);
+    std::iota(par.begin(), par.end(), 0);
+    auto unite = [&](int a, int b) {
+        if (a < 0 || a >= n || b < 0 || b >= n) fail(CF_ERR_INVALID, "particle index out of range");
+        a = find_root(par, a); b = find_root(par, b);
+        if (a != b) par[std::max(a, b)] = std::min(a, b);
+    };
+    for (int t = 0; t < p->num_flux_bonds; t++) unite(p->flux_bond_idx[2 * t], p->flux_bond_idx[2 * t + 1]);
+    for (int t = 0; t < p->num_flux_angles; t++) {
+        unite(p->flux_angle_idx[3 * t], p->flux_angle_idx[3 * t + 1]);
+        unite(p->flux_angle_idx[3 * t], p->flux_angle_idx[3 * t + 2]);
+    }
+    for (int t = 0; t < p->num_flux_waters; t++) {
+        unite(p->flux_water_idx[3 * t], p->flux_water_idx[3 * t + 1]);
+        unite(p->flux_water_idx[3 * t], p->flux_water_idx[3 * t + 2]);
+    }
+    for (int k = 0; k < p->num_exceptions; k++) unite(p->exceptions[2 * k], p->exceptions[2 * k + 1]);
+    std::vector<int> cmax(n, 0);
+    for (int i = 0; i < n; i++) { int r = find_root(par, i); cmax[r] = std::max(cmax[r], i); }
+    // cut c is valid iff every atom < c belongs to a component ending before c
+    std::vector<char> valid(n + 1, 0);
+    valid[0] = valid[n] = 1;
+    int pm = -1;
+    for (int c = 1; c < n; c++) {
+        pm = std::max(pm, cmax[find_root(par, c - 1)]);
+        valid[c] = pm < c;
+    }
+    auto nearest_cut = [&](int64_t target) {
+        for (int64_t d = 0; d <= n; d++) {
+            if (target - d >= 0 && valid[target - d]) return (int)(target - d);
+            if (target + d <= n && valid[target + d]) return (int)(target + d);
+        }
+        return n;
+    };
+    *lo = nearest_cut((int64_t)n * rank / world);
+    *hi = nearest_cut((int64_t)n * (rank + 1) / world);
+    if (*hi < *lo) *hi = *lo;
+}
+
+struct Timed {
+    cf_handle* H; int ph; bool on;
+    Timed(cf_handle* H_, int ph_) : H(H_), ph(ph_), on(H_->timing && H_->nrec[ph_] < kMaxTimed) {
+        if (!on) return;
+        auto& v = H->ev[ph];
+        size_t need = 2 * (size_t)(H->nrec[ph] + 1);
+        while (v.size() < need) {
+            hipEvent_t e;
+            cf::check_hip(hipEventCreate(&e), "hipEventCreate");
+            v.push_back(e);
+        }
+        cf::check_hip(hipEventRecord(v[2 * H->nrec[ph]], H->h.stream), "hipEventRecord");
+    }
+    ~Timed() {
+        if (!on) return;
+        (void)hipEventRecord(H->ev[ph][2 * H->nrec[ph] + 1], H->h.stream);
+        H->nrec[ph]++;
+    }
+};
+
+void launch_check(const char* what) {
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) fail(CF_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+}  // namespace
+
+namespace cf {
+void check_hip(hipError_t e, const char* what) {
+    if (e != hipSuccess) fail(CF_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+}  // namespace cf
+
+using cf::check_hip;
+
+extern "C" {
+
+CF_EXPORT int cf_api_version(void) { return CF_API_VERSION; }
+CF_EXPORT const char* cf_last_error(void) { return g_err.c_str(); }
+
+CF_EXPORT int cf_create(const cf_params* p, const cf_options* opt, cf_handle** out) {
+    if (out) *out = nullptr;
+    cf_handle* H = nullptr;
+    int rc = guarded([&] {
+        if (!p || !out) fail(CF_ERR_INVALID, "null argument");
+        const int n = p->num_particles;
+        if (n <= 0) fail(CF_ERR_INVALID, "num_particles must be > 0");
+        if (!p->charges || !p->sigmas || !p->epsilons) fail(CF_ERR_INVALID, "particle arrays are null");
+        cf_options o;
+        std::memset(&o, 0, sizeof(o));
+        if (opt) o = *opt;
+        int world = o.world_size <= 1 ? 1 : o.world_size;
+        if (o.rank < 0 || o.rank >= world) fail(CF_ERR_INVALID, "rank out of range");
+
+        int ndev = 0;
+        check_hip(hipGetDeviceCount(&ndev), "hipGetDeviceCount");
+        if (ndev <= 0) fail(CF_ERR_HIP, "no HIP device available");
+        if (o.device < 0 || o.device >= ndev) fail(CF_ERR_INVALID, "device ordinal out of range");
+        check_hip(hipSetDevice(o.device), "hipSetDevice");
+
+        H = new cf_handle();
+        cf::Handle& h = H->h;
+        h.n = n;
+        h.device = o.device;
+        h.rank = o.rank;
+        h.world = world;
+        h.kspace_algo = o.kspace_algo == 1 ? 1 : 0;
+        if (o.stream) {
+            h.stream = (hipStream_t)o.stream;
+        } else {
+            check_hip(hipStreamCreateWithFlags(&h.stream, hipStreamNonBlocking), "stream");
+            h.own_stream = true;
+        }
+
+        // ---- particles: q0, LJ (sigma/2, 2 sqrt(eps))   RCK:234-240
+        std::vector<double> q0(n);
+        std::vector<double2> lj(n);
+        for (int i = 0; i < n; i++) {
+            if (!(p->epsilons[i] >= 0)) fail(CF_ERR_INVALID, "epsilon must be >= 0");
+            q0[i] = p->charges[i];
+            lj[i] = make_double2(0.5 * p->sigmas[i], 2.0 * std::sqrt(p->epsilons[i]));
+        }
+
+        // ---- flux terms  RCK:242-284
+        const int B = p->num_flux_bonds, A = p->num_flux_angles, W = p->num_flux_waters;
+        if (B < 0 || A < 0 || W < 0) fail(CF_ERR_INVALID, "negative flux term count");
+        if ((B && (!p->flux_bond_idx || !p->flux_bond_params)) || (A && (!p->flux_angle_idx || !p->flux_angle_params)) ||
+            (W && (!p->flux_water_idx || !p->flux_water_params)))
+            fail(CF_ERR_INVALID, "flux term arrays are null");
+        auto chk = [&](int a, const char* what) {
+            if (a < 0 || a >= n) fail(CF_ERR_INVALID, std::string(what) + " particle index out of range");
+        };
+        const int T = B + A + W;
+        std::vector<int4> tidx(T);
+        std::vector<double> tpar((size_t)T * 5, 0.0);
+        std::vector<std::vector<int>> term_atoms(T);
+        for (int t = 0; t < B; t++) {
+            int a0 = p->flux_bond_idx[2 * t], a1 = p->flux_bond_idx[2 * t + 1];
+            chk(a0, "flux bond"); chk(a1, "flux bond");
+            tidx[t] = make_int4(0, a0, a1, -1);
+            tpar[5 * t] = p->flux_bond_params[2 * t]; tpar[5 * t + 1] = p->flux_bond_params[2 * t + 1];
+            term_atoms[t] = {a0, a1};
+        }
+        for (int u = 0; u < A; u++) {
+            int t = B + u;
+            int a0 = p->flux_angle_idx[3 * u], a1 = p->flux_angle_idx[3 * u + 1], a2 = p->flux_angle_idx[3 * u + 2];
+            chk(a0, "flux angle"); chk(a1, "flux angle"); chk(a2, "flux angle");
+            tidx[t] = make_int4(1, a0, a1, a2);
+            tpar[5 * t] = p->flux_angle_params[2 * u]; tpar[5 * t + 1] = p->flux_angle_params[2 * u + 1];
+            term_atoms[t] = {a0, a1, a2};
+        }
+        for (int u = 0; u < W; u++) {
+            int t = B + A + u;
+            int a0 = p->flux_water_idx[3 * u], a1 = p->flux_water_idx[3 * u + 1], a2 = p->flux_water_idx[3 * u + 2];
+            chk(a0, "flux water"); chk(a1, "flux water"); chk(a2, "flux water");
+            tidx[t] = make_int4(2, a0, a1, a2);
+            for (int k = 0; k < 5; k++) tpar[5 * t + k] = p->flux_water_params[5 * u + k];
+            term_atoms[t] = {a0, a1, a2};
+        }
+        h.nb = B; h.na = A; h.nw = W; h.nterms = T;
+        h.nslots_dq = 2 * B + 3 * A + 3 * W;
+        h.nd = 4 * B + 9 * A + 9 * W;
+        // charge-delta slots -> atoms, in term order (the reference's += order RCK:61-62,113-115,191-193)
+        std::vector<int> slot_atom(h.nslots_dq);
+        {
+            int s = 0;
+            for (int t = 0; t < T; t++)
+                for (int a : term_atoms[t]) slot_atom[s++] = a;
+        }
+        std::vector<int> qs(n + 1, 0), qslot(h.nslots_dq);
+        for (int s = 0; s < h.nslots_dq; s++) qs[slot_atom[s] + 1]++;
+        for (int i = 0; i < n; i++) qs[i + 1] += qs[i];
+        {
+            std::vector<int> fill(qs.begin(), qs.end() - 1);
+            for (int s = 0; s < h.nslots_dq; s++) qslot[fill[slot_atom[s]]++] = s;
+        }
+        // dq/dx entries (q-atom major, x-atom minor per term, RCK:286-383) -> gather by x-atom
+        std::vector<int> ent_q(h.nd), ent_x(h.nd);
+        {
+            int e = 0;
+            for (int t = 0; t < T; t++)
+                for (int u : term_atoms[t])
+                    for (int v : term_atoms[t]) { ent_q[e] = u; ent_x[e] = v; e++; }
+        }
+        std::vector<int> cs(n + 1, 0);
+        std::vector<int2> ce(h.nd);
+        for (int e = 0; e < h.nd; e++) cs[ent_x[e] + 1]++;
+        for (int i = 0; i < n; i++) cs[i + 1] += cs[i];
+        {
+            std::vector<int> fill(cs.begin(), cs.end() - 1);
+            for (int e = 0; e < h.nd; e++) ce[fill[ent_x[e]]++] = make_int2(e, ent_q[e]);
+        }
+
+        // ---- exclusions: unique, ordered, no self pairs (std::set semantics RCK:385-391)
+        const int E = p->num_exceptions;
+        if (E < 0 || (E && !p->exceptions)) fail(CF_ERR_INVALID, "bad exception list");
+        std::vector<std::vector<int>> ex(n);
+        for (int k = 0; k < E; k++) {
+            int a0 = p->exceptions[2 * k], a1 = p->exceptions[2 * k + 1];
+            chk(a0, "exception"); chk(a1, "exception");
+            if (a0 == a1) continue;
+            ex[a0].push_back(a1);
+            ex[a1].push_back(a0);
+        }
+        std::vector<int> exs(n + 1, 0), exl;
+        for (int i = 0; i < n; i++) {
+            std::sort(ex[i].begin(), ex[i].end());
+            ex[i].erase(std::unique(ex[i].begin(), ex[i].end()), ex[i].end());
+            exs[i + 1] = exs[i] + (int)ex[i].size();
+            h.max_excl = std::max(h.max_excl, (int)ex[i].size());
+            exl.insert(exl.end(), ex[i].begin(), ex[i].end());
+        }
+
+        // ---- ownership for atom decomposition (see partition())
+        partition(p, world, o.rank, &h.lo, &h.hi);
+
+        // ---- periodic / Ewald parameters  RCK:394-421
+        h.pbc = p->use_pbc ? 1 : 0;
+        if (h.pbc) {
+            h.cutoff = p->cutoff;
+            h.tol = p->ewald_tol;
+            if (!(h.cutoff > 0)) fail(CF_ERR_INVALID, "cutoff must be > 0");
+            if (!(h.tol > 0 && h.tol < 0.5)) fail(CF_ERR_INVALID, "ewald tolerance must be in (0, 0.5)");
+            check_box_orthorhombic(p->default_box, "default box");
+            double L[3] = {p->default_box[0], p->default_box[4], p->default_box[8]};
+            for (int d = 0; d < 3; d++)
+                if (h.cutoff > 0.5 * L[d] * (1 + 1e-12))
+                    fail(CF_ERR_INVALID, "cutoff exceeds half the periodic box (minimum image would be ambiguous)");
+            h.alpha = (1.0 / h.cutoff) * std::sqrt(-std::log(2.0 * h.tol));
+            for (int d = 0; d < 3; d++) {
+                int k = 1;
+                while (ewald_param_value(k, L[d], h.alpha) > h.tol) k++;
+                if (k % 2 == 0) k++;
+                h.kmax[d] = k;
+            }
+            h.kg.KX = h.kmax[0];
+            cf::kspace_plan(h);
+            h.khalf = h.kg.k_half();
+        }
+
+        // ---- device allocation + upload
+        h.q0 = dupload(H, q0);
+        h.lj = dupload(H, lj);
+        h.term_idx = dupload(H, tidx);
+        h.term_par = dupload(H, tpar);
+        h.dq_slot = dalloc<double>(H, h.nslots_dq);
+        h.qcsr_start = dupload(H, qs);
+        h.qcsr_slot = dupload(H, qslot);
+        h.dqdx = dalloc<double>(H, (size_t)3 * h.nd);
+        h.ccsr_start = dupload(H, cs);
+        h.ccsr_ent = dupload(H, ce);
+        h.ex_start = dupload(H, exs);
+        h.ex_list = dupload(H, exl);
+        h.q = dalloc<double>(H, n);
+        h.dedq_self = dalloc<double>(H, n);
+        h.dedq = dalloc<double>(H, n);
+        h.e_atom = dalloc<double>(H, (size_t)3 * n);
+        h.f_part = dalloc<double>(H, (size_t)3 * n);
+        h.terms_dev = dalloc<double>(H, 4);
+        h.energy_dev = dalloc<double>(H, 1);
+        check_hip(hipMemset(h.dedq, 0, sizeof(double) * n), "memset");
+        check_hip(hipMemset(h.f_part, 0, sizeof(double) * 3 * n), "memset");
+        check_hip(hipMemset(h.e_atom, 0, sizeof(double) * 3 * n), "memset");
+        check_hip(hipMemset(h.terms_dev, 0, sizeof(double) * 4), "memset");
+        int nown = h.hi - h.lo;
+        if (h.pbc) {
+            const cf::KGeom& g = h.kg;
+            set_cells(H, std::vector<double>{p->default_box[0], p->default_box[4], p->default_box[8]}.data());
+            h.cell_key = dalloc<int>(H, n); h.cell_key_sorted = dalloc<int>(H, n);
+            h.atom_val = dalloc<int>(H, n); h.atom_sorted = dalloc<int>(H, n);
+            h.pos4s = dalloc<double4>(H, n);
+            h.ljs = dalloc<double2>(H, n);
+            size_t tmp = 0;
+            check_hip(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, h.cell_key, h.cell_key_sorted, h.atom_val,
+                                                         h.atom_sorted, n, 0, 31, h.stream),
+                      "sort temp query");
+            h.sort_tmp_bytes = tmp;
+            h.sort_tmp = dalloc<char>(H, tmp);
+            if (h.kspace_algo == 0) {
+                // phase tables: padded rows stay zero forever (memset once)
+                h.tab_xq = dalloc<double2>(H, (size_t)h.npad * g.KX);
+                h.tab_y = dalloc<double2>(H, (size_t)h.npad * g.NYP);
+                h.tab_cs = dalloc<double>(H, (size_t)g.NB * h.npad * g.CSW);
+                check_hip(hipMemset(h.tab_xq, 0, sizeof(double2) * h.npad * g.KX), "memset");
+                check_hip(hipMemset(h.tab_y, 0, sizeof(double2) * h.npad * g.NYP), "memset");
+                check_hip(hipMemset(h.tab_cs, 0, sizeof(double) * g.NB * h.npad * g.CSW), "memset");
+                h.s_slab = dalloc<double>(H, (size_t)h.sp.nchunks * 2 * g.nslots() * g.NZP);
+                h.s_red = dalloc<double>(H, (size_t)2 * g.nslots() * g.NZP);
+                size_t ncoef = (size_t)g.nmtiles() * g.nksteps() * 64;
+                h.coef_a = dalloc<double>(H, ncoef);
+                check_hip(hipMemset(h.coef_a, 0, sizeof(double) * ncoef), "memset coef");
+                h.t_part = dalloc<double>(H, (size_t)h.fp.nparts() * nown * 4);
+                h.e_rec_part = dalloc<double>(H, (size_t)(g.KX * g.NY * g.KZ + 255) / 256 + 1);
+            } else {
+                int blocks_k = (int)((h.khalf + 255) / 256);
+                h.sk_nchunk = std::max(1, std::min((2048 + blocks_k - 1) / blocks_k, std::max(1, nown / 256)));
+                h.kvec = dalloc<double4>(H, h.khalf);
+                h.sk_slab = dalloc<double>(H, (size_t)h.sk_nchunk * 2 * h.khalf);
+                h.sk_red = dalloc<double>(H, (size_t)2 * h.khalf);
+                h.t_part = dalloc<double>(H, (size_t)nown * 4);
+                h.e_rec_part = dalloc<double>(H, (size_t)(h.khalf + 255) / 256 + 1);
+            }
+        }
+        check_hip(hipDeviceSynchronize(), "create sync");
+        *out = H;
+    });
+    if (rc != CF_OK && H) {
+        for (void* p2 : H->allocs) (void)hipFree(p2);
+        delete H;
+    }
+    return rc;
+}
+
+CF_EXPORT int cf_destroy(cf_handle* H) {
+    if (!H) return CF_OK;
+    return guarded([&] {
+        (void)hipSetDevice(H->h.device);
+        (void)hipStreamSynchronize(H->h.stream);
+        for (void* p : H->allocs) (void)hipFree(p);
+        for (auto& v : H->ev)
+            for (hipEvent_t e : v) (void)hipEventDestroy(e);
+        if (H->h.cell_start) (void)hipFree(H->h.cell_start);
+        if (H->h.cell_end) (void)hipFree(H->h.cell_end);
+        if (H->h.own_stream) (void)hipStreamDestroy(H->h.stream);
+        delete H;
+    });
+}
+
+CF_EXPORT int cf_partition(const cf_params* p, int32_t world_size, int32_t rank, int32_t* lo, int32_t* hi) {
+    return guarded([&] {
+        if (!p || !lo || !hi) fail(CF_ERR_INVALID, "null argument");
+        if (p->num_particles <= 0) fail(CF_ERR_INVALID, "num_particles must be > 0");
+        int world = world_size <= 1 ? 1 : world_size;
+        if (rank < 0 || rank >= world) fail(CF_ERR_INVALID, "rank out of range");
+        int l = 0, h = 0;
+        partition(p, world, rank, &l, &h);
+        *lo = l; *hi = h;
+    });
+}
+
+CF_EXPORT int cf_get_ewald_params(const cf_handle* H, double* alpha, int32_t kmax[3]) {
+    if (!H) { g_err = "null handle"; return CF_ERR_INVALID; }
+    if (alpha) *alpha = H->h.alpha;
+    if (kmax) { kmax[0] = H->h.kmax[0]; kmax[1] = H->h.kmax[1]; kmax[2] = H->h.kmax[2]; }
+    return CF_OK;
+}
+
+CF_EXPORT int cf_get_owned_range(const cf_handle* H, int32_t* lo, int32_t* hi) {
+    if (!H) { g_err = "null handle"; return CF_ERR_INVALID; }
+    if (lo) *lo = H->h.lo;
+    if (hi) *hi = H->h.hi;
+    return CF_OK;
+}
+
+CF_EXPORT int cf_compute_begin(cf_handle* H, const double* pos_dev, const double* box9, int flags) {
+    return guarded([&] {
+        if (!H || !pos_dev) fail(CF_ERR_INVALID, "null argument");
+        cf::Handle& h = H->h;
+        if (h.pending_flags >= 0) fail(CF_ERR_STATE, "cf_compute_begin called twice without cf_compute_end");
+        check_hip(hipSetDevice(h.device), "hipSetDevice");
+        set_box(H, box9);
+        const int forces = flags & CF_INCLUDE_FORCES, energy = flags & CF_INCLUDE_ENERGY;
+        { Timed t(H, PH_FLUX); cf::launch_flux_terms(h, pos_dev); }
+        { Timed t(H, PH_PREP); cf::launch_atoms_prep(h, pos_dev); }
+        if (h.pbc) {
+            { Timed t(H, PH_CELLS); cf::launch_cell_sort(h, pos_dev); }
+            if ((forces || energy) && h.hi > h.lo) {
+                if (h.kspace_algo == 0) {
+                    { Timed t(H, PH_TABLES); cf::launch_kspace_tables(h, pos_dev); }
+                    { Timed t(H, PH_SFAC); cf::launch_kspace_sfac(h); }
+                } else {
+                    Timed t(H, PH_SFAC);
+                    cf::launch_kspace_direct_sfac(h, pos_dev);
+                }
+            } else if (forces || energy) {
+                int64_t cnt = 0;
+                double* buf = cf::kspace_reduce_buffer(h, &cnt);
+                check_hip(hipMemsetAsync(buf, 0, sizeof(double) * cnt, h.stream), "memset S");
+            }
+        }
+        launch_check("compute_begin");
+        h.pending_flags = flags;
+        H->pos_pending = pos_dev;
+    });
+}
+
+CF_EXPORT int cf_kspace_buffer(cf_handle* H, double** buf, int64_t* count) {
+    return guarded([&] {
+        if (!H || !buf || !count) fail(CF_ERR_INVALID, "null argument");
+        if (!H->h.pbc) { *buf = nullptr; *count = 0; return; }
+        *buf = cf::kspace_reduce_buffer(H->h, count);
+    });
+}
+
+CF_EXPORT int cf_compute_end(cf_handle* H, double* forces_dev, double* energy_dev) {
+    return guarded([&] {
+        if (!H) fail(CF_ERR_INVALID, "null handle");
+        cf::Handle& h = H->h;
+        if (h.pending_flags < 0) fail(CF_ERR_STATE, "cf_compute_end without cf_compute_begin");
+        const int flags = h.pending_flags;
+        h.pending_flags = -1;
+        check_hip(hipSetDevice(h.device), "hipSetDevice");
+        const int forces = flags & CF_INCLUDE_FORCES, energy = flags & CF_INCLUDE_ENERGY;
+        const double* pos = H->pos_pending;
+        if (h.hi > h.lo) {
+            if (h.pbc) {
+                if (forces || energy) {
+                    Timed t(H, PH_COEFFS);
+                    if (h.kspace_algo == 0) cf::launch_kspace_coeffs(h, energy);
+                    else cf::launch_kspace_direct_coeffs(h, energy);
+                }
+                if (forces) {
+                    Timed t(H, PH_FORCE);
+                    if (h.kspace_algo == 0) cf::launch_kspace_force(h, pos);
+                    else cf::launch_kspace_direct_force(h, pos);
+                }
+                { Timed t(H, PH_DIRECT); cf::launch_direct(h, pos, forces); }
+            } else {
+                Timed t(H, PH_DIRECT);
+                cf::launch_nopbc(h, pos, forces, energy);
+            }
+            if (forces && forces_dev) { Timed t(H, PH_ASSEMBLE); cf::launch_assemble(h, forces_dev); }
+        }
+        { Timed t(H, PH_ENERGY); cf::launch_energy(h, energy, energy_dev); }
+        launch_check("compute_end");
+    });
+}
+
+CF_EXPORT int cf_compute(cf_handle* H, const double* pos_dev, const double* box9, int flags, double* forces_dev,
+                         double* energy_dev) {
+    int rc = cf_compute_begin(H, pos_dev, box9, flags);
+    if (rc != CF_OK) return rc;
+    return cf_compute_end(H, forces_dev, energy_dev);
+}
+
+CF_EXPORT int cf_compute_host(cf_handle* H, const double* pos_host, const double* box9, int flags,
+                              double* forces_host, double* energy_host) {
+    return guarded([&] {
+        if (!H || !pos_host) fail(CF_ERR_INVALID, "null argument");
+        if (H->h.world > 1) fail(CF_ERR_STATE, "cf_compute_host is single-rank only; use the split-phase API");
+        cf::Handle& h = H->h;
+        check_hip(hipSetDevice(h.device), "hipSetDevice");
+        const int n = h.n;
+        if (!H->pos_host_dev) {
+            H->pos_host_dev = dalloc<double>(H, (size_t)3 * n);
+            H->frc_host_dev = dalloc<double>(H, (size_t)3 * n);
+            H->ene_host_dev = dalloc<double>(H, 1);
+        }
+        check_hip(hipMemcpyAsync(H->pos_host_dev, pos_host, sizeof(double) * 3 * n, hipMemcpyHostToDevice, h.stream),
+                  "H2D positions");
+        check_hip(hipMemsetAsync(H->frc_host_dev, 0, sizeof(double) * 3 * n, h.stream), "memset forces");
+        int rc = cf_compute(H, H->pos_host_dev, box9, flags, H->frc_host_dev, H->ene_host_dev);
+        if (rc != CF_OK) throw CfError(rc, g_err);
+        std::vector<double> f(forces_host ? 3 * (size_t)n : 0);
+        double e = 0;
+        if (forces_host)
+            check_hip(hipMemcpyAsync(f.data(), H->frc_host_dev, sizeof(double) * 3 * n, hipMemcpyDeviceToHost, h.stream),
+                      "D2H forces");
+        check_hip(hipMemcpyAsync(&e, H->ene_host_dev, sizeof(double), hipMemcpyDeviceToHost, h.stream), "D2H energy");
+        check_hip(hipStreamSynchronize(h.stream), "sync");
+        if (forces_host && (flags & CF_INCLUDE_FORCES))
+            for (size_t k = 0; k < 3 * (size_t)n; k++) forces_host[k] += f[k];
+        if (energy_host) *energy_host = e;
+    });
+}
+
+CF_EXPORT int cf_get_charges(cf_handle* H, double* out) {
+    return guarded([&] {
+        if (!H || !out) fail(CF_ERR_INVALID, "null argument");
+        check_hip(hipStreamSynchronize(H->h.stream), "sync");
+        check_hip(hipMemcpy(out, H->h.q, sizeof(double) * H->h.n, hipMemcpyDeviceToHost), "D2H charges");
+    });
+}
+
+CF_EXPORT int cf_get_dedq(cf_handle* H, double* out) {
+    return guarded([&] {
+        if (!H || !out) fail(CF_ERR_INVALID, "null argument");
+        check_hip(hipStreamSynchronize(H->h.stream), "sync");
+        check_hip(hipMemcpy(out, H->h.dedq, sizeof(double) * H->h.n, hipMemcpyDeviceToHost), "D2H dedq");
+    });
+}
+
+CF_EXPORT int cf_get_energy_terms(cf_handle* H, double terms[4]) {
+    return guarded([&] {
+        if (!H || !terms) fail(CF_ERR_INVALID, "null argument");
+        check_hip(hipStreamSynchronize(H->h.stream), "sync");
+        check_hip(hipMemcpy(terms, H->h.terms_dev, sizeof(double) * 4, hipMemcpyDeviceToHost), "D2H terms");
+    });
+}
+
+CF_EXPORT int cf_set_timing(cf_handle* H, int enable) {
+    return guarded([&] {
+        if (!H) fail(CF_ERR_INVALID, "null handle");
+        check_hip(hipStreamSynchronize(H->h.stream), "sync");
+        H->timing = enable != 0;
+        for (int p = 0; p < PH_COUNT; p++) H->nrec[p] = 0;
+    });
+}
+
+CF_EXPORT int cf_get_timing(cf_handle* H, int32_t max_phases, char* names, double* total_ms, int32_t* calls,
+                            int32_t* nphases) {
+    return guarded([&] {
+        if (!H || !nphases) fail(CF_ERR_INVALID, "null argument");
+        check_hip(hipStreamSynchronize(H->h.stream), "sync");
+        *nphases = PH_COUNT;
+        for (int p = 0; p < PH_COUNT && p < max_phases; p++) {
+            double tot = 0;
+            for (int k = 0; k < H->nrec[p]; k++) {
+                float ms = 0;
+                check_hip(hipEventElapsedTime(&ms, H->ev[p][2 * k], H->ev[p][2 * k + 1]), "hipEventElapsedTime");
+                tot += ms;
+            }
+            if (names) { std::strncpy(names + 16 * p, kPhaseNames[p], 15); names[16 * p + 15] = 0; }
+            if (total_ms) total_ms[p] = tot;
+            if (calls) calls[p] = H->nrec[p];
+        }
+    });
+}
+
+CF_EXPORT int cf_synchronize(cf_handle* H) {
+    return guarded([&] {
+        if (!H) fail(CF_ERR_INVALID, "null handle");
+        check_hip(hipStreamSynchronize(H->h.stream), "sync");
+    });
+}
+
+}  // extern "C"

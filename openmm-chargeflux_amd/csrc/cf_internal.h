@@ -1,0 +1,159 @@
+// cf_internal.h — device-side layout and kernel launch declarations of the MI355X
+// ChargeFlux evaluator.  See DESIGN.md for the data layout in HBM and the roofline of
+// each kernel.  Everything here is fp64.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/chargeflux.h"
+
+namespace cf {
+
+constexpr double kOne4PiEps0 = CF_ONE_4PI_EPS0;
+constexpr double kPi = 3.14159265358979323846;
+
+// ---------------------------------------------------------------------------------
+// k-space geometry (separable MFMA formulation)
+//   combos  (nx, ny): nx in [0,KX), ny_idx in [0,NYP) with ny = ny_idx-(KY-1), valid < NY
+//   columns j = 2*nz + {0:cos,1:sin}, nz in [0,KZ), padded to NZP (multiple of 16)
+// ---------------------------------------------------------------------------------
+struct KGeom {
+    int KX = 0, KY = 0, KZ = 0;
+    int NY = 0;    // 2KY-1
+    int NYB = 0;   // ceil(NY/16)  (S-pass combo groups per nx)
+    int NYP = 0;   // 16*NYB
+    int NYB4 = 0;  // ceil(NY/4)   (force-pass m-tiles per nx)
+    int NZP = 0;   // 2KZ rounded up to 16
+    int NB = 0;    // column blocks of <= 64 (CS table blocks, S-pass n-blocks, force K-chunks)
+    int CSW = 0;   // CS table block width: min(64, NZP)
+    __host__ __device__ int nslots() const { return KX * NYP; }
+    __host__ __device__ int ngroups() const { return KX * NYB; }
+    __host__ __device__ int nmtiles() const { return KX * NYB4; }
+    __host__ __device__ int nksteps() const { return NZP / 4; }
+    __host__ __device__ int64_t k_half() const {
+        return (int64_t)(KZ - 1) + (int64_t)(KY - 1) * (2 * KZ - 1) +
+               (int64_t)(KX - 1) * (2 * KY - 1) * (2 * KZ - 1);
+    }
+};
+
+// S-pass launch plan: workgroups = nxgroups(16 groups each) x nblocks(<=64 cols) x nchunks
+struct SPassPlan {
+    int wg_groups = 0;    // number of 16-group workgroup tiles
+    int nchunks = 0;      // atom chunks (split-K)
+    int chunk_atoms = 0;  // atoms per chunk (multiple of tile_atoms)
+    int tile_atoms = 0;   // atoms staged in LDS per step (16 or 32)
+    size_t lds_bytes = 0;
+};
+
+// force-pass launch plan: workgroups = atom groups x kchunks x msplit
+struct FPassPlan {
+    int na = 0;           // 16-atom tiles per wave
+    int waves = 0;        // waves per workgroup
+    int natom_groups = 0; // workgroups along atoms
+    int kchunks = 0;      // K (column) chunks of <= 64
+    int msplit = 0;       // m-tile range split
+    int nparts() const { return kchunks * msplit; }
+};
+
+struct Handle {
+    // ---- configuration -------------------------------------------------------
+    int n = 0;
+    int pbc = 0;
+    double cutoff = 1.0, tol = 1e-4, alpha = 0.0;
+    int kmax[3] = {0, 0, 0};
+    int device = 0;
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    int rank = 0, world = 1;
+    int lo = 0, hi = 0;  // owned atoms [lo,hi)
+    int kspace_algo = 0;
+    KGeom kg;
+    SPassPlan sp;
+    FPassPlan fp;
+
+    // ---- topology (device) ---------------------------------------------------
+    double* q0 = nullptr;       // [N]
+    double2* lj = nullptr;      // [N] (sigma/2, 2 sqrt(eps))
+    int nb = 0, na = 0, nw = 0; // flux terms
+    int nterms = 0, nslots_dq = 0, nd = 0;
+    int4* term_idx = nullptr;   // [T] (type, a0, a1, a2)
+    double* term_par = nullptr; // [T*5]
+    double* dq_slot = nullptr;  // [S] per-term charge deltas
+    int* qcsr_start = nullptr;  // [N+1] slots contributing to atom charge
+    int* qcsr_slot = nullptr;
+    double* dqdx = nullptr;     // [D*3] reference entry order
+    int* ccsr_start = nullptr;  // [N+1] chain-rule entries by x-atom
+    int2* ccsr_ent = nullptr;   // (entry, q-atom)
+    int* ex_start = nullptr;    // [N+1] unique exclusion partners
+    int* ex_list = nullptr;
+    int max_excl = 0;
+
+    // ---- per-evaluation work buffers -------------------------------------------
+    double* q = nullptr;        // [N] realcharges
+    double* dedq_self = nullptr;// [N]
+    double* dedq = nullptr;     // [N] total dE/dq
+    double* e_atom = nullptr;   // [N*3] per-atom (self, direct, exclusion) energy
+    double* f_part = nullptr;   // [N*3] non-chain forces (recip + direct + excl)
+    // cell list
+    int ncell_alloc = 0;
+    int nc[3] = {0, 0, 0};
+    int* cell_key = nullptr; int* cell_key_sorted = nullptr;
+    int* atom_val = nullptr; int* atom_sorted = nullptr;
+    int* cell_start = nullptr; int* cell_end = nullptr;
+    double4* pos4s = nullptr;   // [N] sorted wrapped (x,y,z,q)
+    double2* ljs = nullptr;     // [N] sorted LJ
+    void* sort_tmp = nullptr; size_t sort_tmp_bytes = 0;
+    // k-space (MFMA path)
+    int npad = 0;               // owned rows of the phase tables, padded to the S-pass tile
+    double2* tab_xq = nullptr;  // [Nown][KX]
+    double2* tab_y = nullptr;   // [Nown][NYP]
+    double* tab_cs = nullptr;   // [Nown][NZP]
+    double* s_slab = nullptr;   // [nchunks][2][slots][NZP]
+    double* s_red = nullptr;    // [2][slots][NZP]  <- all-reduced buffer
+    double* coef_a = nullptr;   // [mtiles][ksteps][64]
+    double* t_part = nullptr;   // [nparts][Nown][4]
+    double* e_rec_part = nullptr; // [nblk]
+    int e_rec_nblk = 0;
+    // k-space (direct VALU check path)
+    int64_t khalf = 0;
+    double* sk_slab = nullptr;  // [nchunk][2][khalf]
+    double* sk_red = nullptr;   // [2][khalf]
+    double4* kvec = nullptr;    // [khalf] (kx,ky,kz, w=2*c*eak)
+    int sk_nchunk = 0;
+    // energy
+    double* terms_dev = nullptr; // [4]
+    double* energy_dev = nullptr;// [1] internal
+    // state
+    int pending_flags = -1;     // flags of a begun evaluation
+    double box_L[3] = {0, 0, 0};
+};
+
+// ---- launchers (cf_kernels_*.hip) ------------------------------------------------
+void launch_flux_terms(Handle& h, const double* pos);
+void launch_atoms_prep(Handle& h, const double* pos);
+void launch_cell_sort(Handle& h, const double* pos);
+void launch_direct(Handle& h, const double* pos, int include_forces);
+void launch_nopbc(Handle& h, const double* pos, int include_forces, int include_energy);
+void launch_assemble(Handle& h, double* forces_out);
+void launch_energy(Handle& h, int include_energy, double* energy_out);
+
+void kspace_plan(Handle& h);
+size_t kspace_alloc_bytes(const Handle& h);
+void launch_kspace_tables(Handle& h, const double* pos);
+void launch_kspace_sfac(Handle& h);
+double* kspace_reduce_buffer(Handle& h, int64_t* count);
+void launch_kspace_coeffs(Handle& h, int include_energy);
+void launch_kspace_force(Handle& h, const double* pos);
+
+// direct VALU reference path of the reciprocal sum (kspace_algo = 1)
+void launch_kspace_direct_sfac(Handle& h, const double* pos);
+void launch_kspace_direct_coeffs(Handle& h, int include_energy);
+void launch_kspace_direct_force(Handle& h, const double* pos);
+
+void check_hip(hipError_t e, const char* what);
+
+}  // namespace cf

@@ -1,0 +1,507 @@
+// cf_kernels_core.hip — charge flux, cell list, direct space, exclusions, chain rule,
+// energy assembly.  Hand-written HIP for gfx950 (wave64).  All per-atom sums are
+// gathers in a fixed order (no atomics), so results are bitwise reproducible.
+//
+// Reference semantics: platforms/reference/src/ReferenceCoulKernels.cpp (RCK).
+#include <hipcub/hipcub.hpp>
+
+#include "cf_internal.h"
+
+namespace cf {
+
+// OpenMM ReferenceForce::getDeltaR[Periodic]: d = J - I, minimum image per axis of an
+// orthorhombic box via floor(d/L + 0.5)  (used by RCK:53-55, 567, 601).
+__device__ __forceinline__ double3 delta_r(double3 pi, double3 pj, double3 L, int pbc) {
+    double3 d = make_double3(pj.x - pi.x, pj.y - pi.y, pj.z - pi.z);
+    if (pbc) {
+        d.z -= L.z * floor(d.z / L.z + 0.5);
+        d.y -= L.y * floor(d.y / L.y + 0.5);
+        d.x -= L.x * floor(d.x / L.x + 0.5);
+    }
+    return d;
+}
+
+__device__ __forceinline__ double3 ld3(const double* p, int i) {
+    return make_double3(p[3 * i], p[3 * i + 1], p[3 * i + 2]);
+}
+
+// ---------------------------------------------------------------------------------
+// 1. flux terms: one lane per term writes its charge deltas (slots) and its dq/dx
+//    block in the reference's entry order.  Bonds RCK:42-80, angles RCK:81-162,
+//    waters RCK:163-227.
+// ---------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_flux_terms(int nterms, int nb, int na, const int4* __restrict__ tidx,
+                                                    const double* __restrict__ tpar, const double* __restrict__ pos,
+                                                    double3 L, int pbc, double* __restrict__ dq_slot,
+                                                    double* __restrict__ dqdx) {
+    int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= nterms) return;
+    int4 ti = tidx[t];
+    const double* p = tpar + 5 * t;
+    if (ti.x == 0) {  // bond p1-p2
+        double3 d = delta_r(ld3(pos, ti.y), ld3(pos, ti.z), L, pbc);
+        double r = sqrt(d.x * d.x + d.y * d.y + d.z * d.z);
+        double k = p[0], dq = k * (r - p[1]);
+        dq_slot[2 * t] = dq;
+        dq_slot[2 * t + 1] = -dq;
+        double c = k / r;
+        double v[3] = {c * d.x, c * d.y, c * d.z};
+        double* o = dqdx + 3 * (4 * t);
+#pragma unroll
+        for (int j = 0; j < 3; j++) { o[j] = -v[j]; o[3 + j] = v[j]; o[6 + j] = v[j]; o[9 + j] = -v[j]; }
+    } else if (ti.x == 1) {  // angle p1-p2-p3, p2 central
+        int a = t - nb;
+        double3 x1 = ld3(pos, ti.y), x2 = ld3(pos, ti.z), x3 = ld3(pos, ti.w);
+        double3 d21 = delta_r(x2, x1, L, pbc), d23 = delta_r(x2, x3, L, pbc), d13 = delta_r(x1, x3, L, pbc);
+        double r21_2 = d21.x * d21.x + d21.y * d21.y + d21.z * d21.z;
+        double r23_2 = d23.x * d23.x + d23.y * d23.y + d23.z * d23.z;
+        double r13_2 = d13.x * d13.x + d13.y * d13.y + d13.z * d13.z;
+        double r21 = sqrt(r21_2), r23 = sqrt(r23_2);
+        double cost = (r23_2 + r21_2 - r13_2) / 2 / r21 / r23;
+        double k = p[0];
+        double dq = k * (acos(cost) - p[1]);
+        int s = 2 * nb + 3 * a;
+        dq_slot[s] = dq; dq_slot[s + 1] = -2 * dq; dq_slot[s + 2] = dq;
+        double inv_s = 1 / sqrt(1 - cost * cost);
+        double c1 = k * (1.0 / r21 / r23) * inv_s;
+        double c21 = k * cost * inv_s / r21_2;
+        double c23 = k * cost * inv_s / r23_2;
+        double a21[3] = {d21.x, d21.y, d21.z}, a23[3] = {d23.x, d23.y, d23.z};
+        double* o = dqdx + 3 * (4 * nb + 9 * a);
+#pragma unroll
+        for (int j = 0; j < 3; j++) {
+            double v1 = -c1 * a23[j] + c21 * a21[j];
+            double v3 = -c1 * a21[j] + c23 * a23[j];
+            double v2 = -v1 - v3;
+            o[j] = v1; o[3 + j] = v2; o[6 + j] = v3;
+            o[9 + j] = -2 * v1; o[12 + j] = -2 * v2; o[15 + j] = -2 * v3;
+            o[18 + j] = v1; o[21 + j] = v2; o[24 + j] = v3;
+        }
+    } else {  // water O,H1,H2
+        int w = t - nb - na;
+        double3 x1 = ld3(pos, ti.y), x2 = ld3(pos, ti.z), x3 = ld3(pos, ti.w);
+        double3 d12 = delta_r(x1, x2, L, pbc), d13 = delta_r(x1, x3, L, pbc), d23 = delta_r(x2, x3, L, pbc);
+        double r12 = sqrt(d12.x * d12.x + d12.y * d12.y + d12.z * d12.z);
+        double r13 = sqrt(d13.x * d13.x + d13.y * d13.y + d13.z * d13.z);
+        double r23 = sqrt(d23.x * d23.x + d23.y * d23.y + d23.z * d23.z);
+        double k1 = p[0], k2 = p[1], kub = p[2], b0 = p[3], ub0 = p[4];
+        double dq2 = k1 * (r12 - b0) + k2 * (r13 - b0) + kub * (r23 - ub0);
+        double dq3 = k1 * (r13 - b0) + k2 * (r12 - b0) + kub * (r23 - ub0);
+        int s = 2 * nb + 3 * na + 3 * w;
+        dq_slot[s] = -dq2 - dq3; dq_slot[s + 1] = dq2; dq_slot[s + 2] = dq3;
+        double e12[3] = {d12.x, d12.y, d12.z}, e13[3] = {d13.x, d13.y, d13.z}, e23[3] = {d23.x, d23.y, d23.z};
+        double* o = dqdx + 3 * (4 * nb + 9 * na + 9 * w);
+#pragma unroll
+        for (int j = 0; j < 3; j++) {
+            double n12 = e12[j] / r12, n13 = e13[j] / r13, n23 = e23[j] / r23;
+            double a12k1 = k1 * n12, a12k2 = k2 * n12, a13k1 = k1 * n13, a13k2 = k2 * n13, ub = kub * n23;
+            o[0 + j] = a12k1 + a12k2 + a13k1 + a13k2;
+            o[3 + j] = -a12k1 - a12k2 + 2 * ub;
+            o[6 + j] = -a13k2 - a13k1 - 2 * ub;
+            o[9 + j] = -a12k1 - a13k2;
+            o[12 + j] = a12k1 - ub;
+            o[15 + j] = a13k2 + ub;
+            o[18 + j] = -a12k2 - a13k1;
+            o[21 + j] = a12k2 - ub;
+            o[24 + j] = a13k1 + ub;
+        }
+    }
+}
+
+// 2. per-atom charges q_i = q0_i + sum of its slots (term order), self term
+//    (RCK:38-40, 507-510).
+__global__ void __launch_bounds__(256) k_atoms_prep(int n, const double* __restrict__ q0,
+                                                    const int* __restrict__ qs, const int* __restrict__ qslot,
+                                                    const double* __restrict__ dq_slot, int pbc, double alpha,
+                                                    double* __restrict__ q, double* __restrict__ dedq_self,
+                                                    double* __restrict__ e_atom) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    double qi = q0[i];
+    for (int s = qs[i]; s < qs[i + 1]; s++) qi += dq_slot[qslot[s]];
+    q[i] = qi;
+    if (pbc) {
+        const double c = kOne4PiEps0 * alpha / sqrt(kPi);
+        dedq_self[i] = -2 * c * qi;
+        e_atom[3 * i] = -c * qi * qi;
+    } else {
+        dedq_self[i] = 0;
+        e_atom[3 * i] = 0;
+    }
+}
+
+// ---------------------------------------------------------------------------------
+// 3. cell list (replaces OpenMM computeNeighborListVoxelHash, RCK:559): wrap, bin,
+//    stable radix sort by cell, cell bounds, gather sorted (x,y,z,q) and LJ.
+// ---------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_cell_keys(int n, const double* __restrict__ pos, double3 L, int3 nc,
+                                                   int* __restrict__ key, int* __restrict__ val) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    double3 x = ld3(pos, i);
+    double w[3] = {x.x - floor(x.x / L.x) * L.x, x.y - floor(x.y / L.y) * L.y, x.z - floor(x.z / L.z) * L.z};
+    double Ls[3] = {L.x, L.y, L.z};
+    int ncs[3] = {nc.x, nc.y, nc.z};
+    int c[3];
+#pragma unroll
+    for (int d = 0; d < 3; d++) {
+        int ci = (int)(w[d] / Ls[d] * ncs[d]);
+        c[d] = ci < 0 ? 0 : (ci >= ncs[d] ? ncs[d] - 1 : ci);
+    }
+    key[i] = (c[0] * nc.y + c[1]) * nc.z + c[2];
+    val[i] = i;
+}
+
+__global__ void __launch_bounds__(256) k_cell_gather(int n, const int* __restrict__ key_s, const int* __restrict__ idx_s,
+                                                     const double* __restrict__ pos, const double* __restrict__ q,
+                                                     const double2* __restrict__ lj, double3 L,
+                                                     int* __restrict__ cstart, int* __restrict__ cend,
+                                                     double4* __restrict__ pos4s, double2* __restrict__ ljs) {
+    int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= n) return;
+    int k = key_s[s];
+    if (s == 0 || key_s[s - 1] != k) cstart[k] = s;
+    if (s == n - 1 || key_s[s + 1] != k) cend[k] = s + 1;
+    int i = idx_s[s];
+    double3 x = ld3(pos, i);
+    pos4s[s] = make_double4(x.x - floor(x.x / L.x) * L.x, x.y - floor(x.y / L.y) * L.y,
+                            x.z - floor(x.z / L.z) * L.z, q[i]);
+    ljs[s] = lj[i];
+}
+
+// ---------------------------------------------------------------------------------
+// 4. direct space + exclusion correction, one lane per owned atom i (full neighbour
+//    list: each pair is evaluated from both sides, every per-atom sum is a gather).
+//    Real-space pair RCK:562-593, exclusion erf correction RCK:596-622.
+//    Finishes dE/dq_i (self + recip + direct + excl) and the non-chain forces.
+// ---------------------------------------------------------------------------------
+constexpr int kMaxRegExcl = 8;
+
+struct DirectArgs {
+    int n, lo, hi, include_forces;
+    double3 L; int3 nc; int brute;
+    double rc2, alpha;
+    const int* atom_sorted; const int* key_sorted;
+    const int* cstart; const int* cend;
+    const double4* pos4s; const double2* ljs;
+    const double* pos; const double* q;
+    const int* ex_start; const int* ex_list;
+    const double* dedq_self;
+    const double* t_part; int nparts; int nown;  // reciprocal partials [p][nown][4]
+    double* dedq; double* f_part; double* e_atom;
+};
+
+__device__ __forceinline__ bool in_excl(int j, const int* reg, int cnt, const int* ex_list, int ex0) {
+    int m = cnt < kMaxRegExcl ? cnt : kMaxRegExcl;
+#pragma unroll
+    for (int k = 0; k < kMaxRegExcl; k++)
+        if (k < m && reg[k] == j) return true;
+    for (int k = kMaxRegExcl; k < cnt; k++)
+        if (ex_list[ex0 + k] == j) return true;
+    return false;
+}
+
+__global__ void __launch_bounds__(256) k_direct(DirectArgs a) {
+    int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= a.n) return;
+    int i = a.atom_sorted[s];
+    if (i < a.lo || i >= a.hi) return;
+    const double4 pi = a.pos4s[s];
+    const double2 li = a.ljs[s];
+    const int ex0 = a.ex_start[i], exc = a.ex_start[i + 1] - ex0;
+    int reg[kMaxRegExcl];
+#pragma unroll
+    for (int k = 0; k < kMaxRegExcl; k++) reg[k] = k < exc ? a.ex_list[ex0 + k] : -1;
+
+    const double ke = kOne4PiEps0;
+    const double two_over_sqrtpi = 2.0 / sqrt(kPi);
+    double fx = 0, fy = 0, fz = 0, dq = 0, e = 0;
+
+    auto pair = [&](const double4& pj, const double2& lj2, double dx, double dy, double dz, double r2) {
+        double r = sqrt(r2);
+        double inv_r = 1.0 / r, ar = a.alpha * r;
+        double ec = erfc(ar);
+        double sig = li.x + lj2.x;
+        double s2 = inv_r * sig; s2 *= s2;
+        double sig6 = s2 * s2 * s2;
+        double es6 = sig6 * li.y * lj2.y;
+        double qq = ke * pi.w * pj.w * inv_r;
+        if (a.include_forces) {
+            double dEdR = qq * inv_r * inv_r * (ec + ar * exp(-ar * ar) * two_over_sqrtpi);
+            dEdR += es6 * (12 * sig6 - 6) * inv_r * inv_r;
+            fx += dEdR * dx; fy += dEdR * dy; fz += dEdR * dz;
+            dq += ke * pj.w * inv_r * ec;
+        }
+        e += 0.5 * (qq * ec + es6 * (sig6 - 1));
+    };
+
+    if (!a.brute) {
+        int key = a.key_sorted[s];
+        int cz = key % a.nc.z, cy = (key / a.nc.z) % a.nc.y, cx = key / (a.nc.y * a.nc.z);
+        for (int ox = -1; ox <= 1; ox++) {
+            int x = cx + ox; double sx = 0;
+            if (x < 0) { x += a.nc.x; sx = -a.L.x; } else if (x >= a.nc.x) { x -= a.nc.x; sx = a.L.x; }
+            for (int oy = -1; oy <= 1; oy++) {
+                int y = cy + oy; double sy = 0;
+                if (y < 0) { y += a.nc.y; sy = -a.L.y; } else if (y >= a.nc.y) { y -= a.nc.y; sy = a.L.y; }
+                for (int oz = -1; oz <= 1; oz++) {
+                    int z = cz + oz; double sz = 0;
+                    if (z < 0) { z += a.nc.z; sz = -a.L.z; } else if (z >= a.nc.z) { z -= a.nc.z; sz = a.L.z; }
+                    int c = (x * a.nc.y + y) * a.nc.z + z;
+                    int t1 = a.cend[c];
+                    for (int t = a.cstart[c]; t < t1; t++) {
+                        double4 pj = a.pos4s[t];
+                        double dx = pi.x - (pj.x + sx), dy = pi.y - (pj.y + sy), dz = pi.z - (pj.z + sz);
+                        double r2 = dx * dx + dy * dy + dz * dz;
+                        if (r2 > a.rc2 || t == s) continue;
+                        int j = a.atom_sorted[t];
+                        if (exc && in_excl(j, reg, exc, a.ex_list, ex0)) continue;
+                        pair(pj, a.ljs[t], dx, dy, dz, r2);
+                    }
+                }
+            }
+        }
+    } else {
+        for (int t = 0; t < a.n; t++) {
+            if (t == s) continue;
+            double4 pj = a.pos4s[t];
+            double3 d = delta_r(make_double3(pj.x, pj.y, pj.z), make_double3(pi.x, pi.y, pi.z), a.L, 1);
+            double r2 = d.x * d.x + d.y * d.y + d.z * d.z;
+            if (r2 > a.rc2) continue;
+            int j = a.atom_sorted[t];
+            if (exc && in_excl(j, reg, exc, a.ex_list, ex0)) continue;
+            pair(pj, a.ljs[t], d.x, d.y, d.z, r2);
+        }
+    }
+
+    // exclusion correction: subtract the erf (Gaussian-screened) part for EVERY excluded
+    // pair, no cutoff test, no LJ (RCK:596-622).  d = pos_i - pos_j minimum image.
+    double ex_e = 0;
+    if (exc) {
+        double3 xi = ld3(a.pos, i);
+        double qi = a.q[i];
+        for (int k = 0; k < exc; k++) {
+            int j = a.ex_list[ex0 + k];
+            double3 d = delta_r(ld3(a.pos, j), xi, a.L, 1);
+            double r = sqrt(d.x * d.x + d.y * d.y + d.z * d.z);
+            double inv_r = 1.0 / r, ar = a.alpha * r;
+            double ef = erf(ar);
+            double qj = a.q[j];
+            if (a.include_forces) {
+                double g = ke * qi * qj * inv_r * inv_r * inv_r * (ef - ar * exp(-ar * ar) * two_over_sqrtpi);
+                fx -= g * d.x; fy -= g * d.y; fz -= g * d.z;
+                dq -= ke * qj * inv_r * ef;
+            }
+            ex_e -= 0.5 * ke * qi * qj * inv_r * ef;
+        }
+    }
+    a.e_atom[3 * i + 1] = e;
+    a.e_atom[3 * i + 2] = ex_e;
+    if (a.include_forces) {
+        double dr = 0, rx = 0, ry = 0, rz = 0;
+        int io = i - a.lo;
+        for (int p = 0; p < a.nparts; p++) {
+            const double* tp = a.t_part + ((size_t)p * a.nown + io) * 4;
+            dr += tp[0]; rx += tp[1]; ry += tp[2]; rz += tp[3];
+        }
+        a.dedq[i] = a.dedq_self[i] + dr + dq;
+        a.f_part[3 * i] = rx + fx;
+        a.f_part[3 * i + 1] = ry + fy;
+        a.f_part[3 * i + 2] = rz + fz;
+    }
+}
+
+// ---------------------------------------------------------------------------------
+// 5. non-periodic all pairs (RCK:436-491).  The reference adds every pair i<j and then
+//    subtracts the excluded ones with the same formula; here excluded pairs are simply
+//    skipped.  One lane per owned atom, j tiles staged in LDS.
+// ---------------------------------------------------------------------------------
+constexpr int kNopbcTile = 256;
+
+__global__ void __launch_bounds__(kNopbcTile) k_nopbc(int n, int lo, int hi, int include_forces, int include_energy,
+                                                      const double* __restrict__ pos, const double* __restrict__ q,
+                                                      const double2* __restrict__ lj, const int* __restrict__ ex_start,
+                                                      const int* __restrict__ ex_list, double* __restrict__ dedq,
+                                                      double* __restrict__ f_part, double* __restrict__ e_atom) {
+    __shared__ double4 sp[kNopbcTile];
+    __shared__ double2 sl[kNopbcTile];
+    int i = lo + blockIdx.x * blockDim.x + threadIdx.x;
+    bool active = i < hi;
+    double4 pi = make_double4(0, 0, 0, 0);
+    double2 li = make_double2(0, 0);
+    int ex0 = 0, exc = 0;
+    int reg[kMaxRegExcl];
+    if (active) {
+        pi = make_double4(pos[3 * i], pos[3 * i + 1], pos[3 * i + 2], q[i]);
+        li = lj[i];
+        ex0 = ex_start[i]; exc = ex_start[i + 1] - ex0;
+    }
+#pragma unroll
+    for (int k = 0; k < kMaxRegExcl; k++) reg[k] = k < exc ? ex_list[ex0 + k] : -1;
+    const double ke = kOne4PiEps0;
+    double fx = 0, fy = 0, fz = 0, dq = 0, e = 0;
+    for (int base = 0; base < n; base += kNopbcTile) {
+        int j = base + threadIdx.x;
+        __syncthreads();
+        if (j < n) {
+            sp[threadIdx.x] = make_double4(pos[3 * j], pos[3 * j + 1], pos[3 * j + 2], q[j]);
+            sl[threadIdx.x] = lj[j];
+        }
+        __syncthreads();
+        int m = min(kNopbcTile, n - base);
+        if (!active) continue;
+        for (int t = 0; t < m; t++) {
+            int jj = base + t;
+            if (jj == i) continue;
+            if (exc && in_excl(jj, reg, exc, ex_list, ex0)) continue;
+            double4 pj = sp[t];
+            double2 lj2 = sl[t];
+            double dx = pj.x - pi.x, dy = pj.y - pi.y, dz = pj.z - pi.z;  // getDeltaR(i, j)
+            double inv_r = 1.0 / sqrt(dx * dx + dy * dy + dz * dz);
+            double sig = li.x + lj2.x;
+            double s2 = inv_r * sig; s2 *= s2;
+            double sig6 = s2 * s2 * s2;
+            double es6 = sig6 * li.y * lj2.y;
+            double qq = ke * pi.w * pj.w * inv_r;
+            if (include_energy) e += 0.5 * (qq + es6 * (sig6 - 1));
+            if (include_forces) {
+                double dEdR = (es6 * (12 * sig6 - 6) + qq) * inv_r * inv_r;
+                fx -= dEdR * dx; fy -= dEdR * dy; fz -= dEdR * dz;
+                dq += ke * pj.w * inv_r;
+            }
+        }
+    }
+    if (!active) return;
+    e_atom[3 * i + 1] = e;
+    e_atom[3 * i + 2] = 0;
+    if (include_forces) {
+        dedq[i] = dq;
+        f_part[3 * i] = fx; f_part[3 * i + 1] = fy; f_part[3 * i + 2] = fz;
+    }
+}
+
+// ---------------------------------------------------------------------------------
+// 6. assemble: F_b += F_part_b - sum_e dE/dq[a_e] * dq_{a_e}/dx_b   (chain rule as a
+//    per-x-atom gather; reference scatter RCK:493-499, 626-632)
+// ---------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_assemble(int lo, int hi, const int* __restrict__ cs, const int2* __restrict__ ce,
+                                                  const double* __restrict__ dedq, const double* __restrict__ dqdx,
+                                                  const double* __restrict__ f_part, double* __restrict__ out) {
+    int b = lo + blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= hi) return;
+    double fx = f_part[3 * b], fy = f_part[3 * b + 1], fz = f_part[3 * b + 2];
+    for (int k = cs[b]; k < cs[b + 1]; k++) {
+        int2 en = ce[k];
+        double g = dedq[en.y];
+        fx -= g * dqdx[3 * en.x];
+        fy -= g * dqdx[3 * en.x + 1];
+        fz -= g * dqdx[3 * en.x + 2];
+    }
+    out[3 * b] += fx;
+    out[3 * b + 1] += fy;
+    out[3 * b + 2] += fz;
+}
+
+// 7. energy: one workgroup, fixed-order tree reduction (deterministic).
+__global__ void __launch_bounds__(1024) k_energy(int lo, int hi, const double* __restrict__ e_atom,
+                                                 const double* __restrict__ e_rec_part, int nrec,
+                                                 int pbc, double* __restrict__ terms, double* __restrict__ energy_out,
+                                                 double* __restrict__ energy_int) {
+    __shared__ double red[4][1024];
+    double a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+    for (int i = lo + threadIdx.x; i < hi; i += blockDim.x) {
+        a0 += e_atom[3 * i]; a2 += e_atom[3 * i + 1]; a3 += e_atom[3 * i + 2];
+    }
+    for (int k = threadIdx.x; k < nrec; k += blockDim.x) a1 += e_rec_part[k];
+    red[0][threadIdx.x] = a0; red[1][threadIdx.x] = a1; red[2][threadIdx.x] = a2; red[3][threadIdx.x] = a3;
+    __syncthreads();
+    for (int w = blockDim.x / 2; w > 0; w >>= 1) {
+        if (threadIdx.x < w)
+#pragma unroll
+            for (int c = 0; c < 4; c++) red[c][threadIdx.x] += red[c][threadIdx.x + w];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        double t0 = red[0][0], t1 = red[1][0], t2 = red[2][0], t3 = red[3][0];
+        terms[0] = t0; terms[1] = t1; terms[2] = t2; terms[3] = t3;
+        double e = pbc ? (t0 + t1 + t2 + t3) : t2;
+        *energy_int = e;
+        if (energy_out) *energy_out = e;
+    }
+}
+
+// ---------------------------------------------------------------------------------
+// launchers
+// ---------------------------------------------------------------------------------
+static inline int nblk(int64_t n, int b) { return (int)((n + b - 1) / b); }
+
+void launch_flux_terms(Handle& h, const double* pos) {
+    if (h.nterms == 0) return;
+    double3 L = make_double3(h.box_L[0], h.box_L[1], h.box_L[2]);
+    hipLaunchKernelGGL(k_flux_terms, dim3(nblk(h.nterms, 256)), dim3(256), 0, h.stream, h.nterms, h.nb, h.na,
+                       h.term_idx, h.term_par, pos, L, h.pbc, h.dq_slot, h.dqdx);
+}
+
+void launch_atoms_prep(Handle& h, const double* pos) {
+    (void)pos;
+    hipLaunchKernelGGL(k_atoms_prep, dim3(nblk(h.n, 256)), dim3(256), 0, h.stream, h.n, h.q0, h.qcsr_start,
+                       h.qcsr_slot, h.dq_slot, h.pbc, h.alpha, h.q, h.dedq_self, h.e_atom);
+}
+
+void launch_cell_sort(Handle& h, const double* pos) {
+    double3 L = make_double3(h.box_L[0], h.box_L[1], h.box_L[2]);
+    int3 nc = make_int3(h.nc[0], h.nc[1], h.nc[2]);
+    int ncell = nc.x * nc.y * nc.z;
+    hipLaunchKernelGGL(k_cell_keys, dim3(nblk(h.n, 256)), dim3(256), 0, h.stream, h.n, pos, L, nc, h.cell_key,
+                       h.atom_val);
+    int end_bit = 1;
+    while ((1 << end_bit) < ncell) end_bit++;
+    size_t bytes = h.sort_tmp_bytes;
+    check_hip(hipcub::DeviceRadixSort::SortPairs(h.sort_tmp, bytes, h.cell_key, h.cell_key_sorted, h.atom_val,
+                                                 h.atom_sorted, h.n, 0, end_bit, h.stream),
+              "radix sort");
+    check_hip(hipMemsetAsync(h.cell_start, 0, sizeof(int) * ncell, h.stream), "memset cell_start");
+    check_hip(hipMemsetAsync(h.cell_end, 0, sizeof(int) * ncell, h.stream), "memset cell_end");
+    hipLaunchKernelGGL(k_cell_gather, dim3(nblk(h.n, 256)), dim3(256), 0, h.stream, h.n, h.cell_key_sorted,
+                       h.atom_sorted, pos, h.q, h.lj, L, h.cell_start, h.cell_end, h.pos4s, h.ljs);
+}
+
+void launch_direct(Handle& h, const double* pos, int include_forces) {
+    DirectArgs a;
+    a.n = h.n; a.lo = h.lo; a.hi = h.hi; a.include_forces = include_forces;
+    a.L = make_double3(h.box_L[0], h.box_L[1], h.box_L[2]);
+    a.nc = make_int3(h.nc[0], h.nc[1], h.nc[2]);
+    a.brute = (h.nc[0] < 3 || h.nc[1] < 3 || h.nc[2] < 3) ? 1 : 0;
+    a.rc2 = h.cutoff * h.cutoff; a.alpha = h.alpha;
+    a.atom_sorted = h.atom_sorted; a.key_sorted = h.cell_key_sorted;
+    a.cstart = h.cell_start; a.cend = h.cell_end;
+    a.pos4s = h.pos4s; a.ljs = h.ljs;
+    a.q = h.q; a.ex_start = h.ex_start; a.ex_list = h.ex_list;
+    a.dedq_self = h.dedq_self;
+    a.nparts = h.kspace_algo == 1 ? 1 : h.fp.nparts();
+    a.t_part = h.t_part; a.nown = h.hi - h.lo;
+    a.dedq = h.dedq; a.f_part = h.f_part; a.e_atom = h.e_atom;
+    a.pos = pos;
+    hipLaunchKernelGGL(k_direct, dim3(nblk(h.n, 256)), dim3(256), 0, h.stream, a);
+}
+
+void launch_nopbc(Handle& h, const double* pos, int include_forces, int include_energy) {
+    int nown = h.hi - h.lo;
+    hipLaunchKernelGGL(k_nopbc, dim3(nblk(nown, kNopbcTile)), dim3(kNopbcTile), 0, h.stream, h.n, h.lo, h.hi,
+                       include_forces, include_energy, pos, h.q, h.lj, h.ex_start, h.ex_list, h.dedq, h.f_part,
+                       h.e_atom);
+}
+
+void launch_assemble(Handle& h, double* forces_out) {
+    int nown = h.hi - h.lo;
+    hipLaunchKernelGGL(k_assemble, dim3(nblk(nown, 256)), dim3(256), 0, h.stream, h.lo, h.hi, h.ccsr_start,
+                       h.ccsr_ent, h.dedq, h.dqdx, h.f_part, forces_out);
+}
+
+void launch_energy(Handle& h, int include_energy, double* energy_out) {
+    int nrec = (h.pbc && include_energy && h.rank == 0) ? h.e_rec_nblk : 0;
+    hipLaunchKernelGGL(k_energy, dim3(1), dim3(1024), 0, h.stream, h.lo, h.hi, h.e_atom, h.e_rec_part, nrec, h.pbc,
+                       h.terms_dev, energy_out, h.energy_dev);
+}
+
+}  // namespace cf

@@ -1,0 +1,66 @@
+"""Atom decomposition over GPUs (one process per GPU, torch.distributed over RCCL).
+
+The reference is single-device (platforms/cuda/src/CudaCoulKernelFactory.cpp:40 binds
+contexts[0]); this is new.  The only data-path exchange is the structure factor S(k):
+every rank sums S over its owned atoms, one all-reduce (sum) makes it global, and the
+rest of the evaluation (reciprocal forces, direct space with a full neighbour list,
+exclusions, chain rule) is local to the owned, molecule-aligned atom range
+(SURVEY.md §8(e)).  Positions are replicated; an MD driver re-replicates them after
+integrating its owned atoms (`replicate_positions`).
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+from .kernel import HipCalcCoulForceKernel
+
+
+class _DeviceArray:
+    """Zero-copy view of a raw device pointer for torch (CUDA array interface)."""
+
+    def __init__(self, ptr: int, count: int):
+        self.__cuda_array_interface__ = {"shape": (count,), "typestr": "<f8", "data": (ptr, False), "version": 2,
+                                         "strides": None}
+
+
+def device_buffer_as_tensor(ptr: int, count: int, device) -> torch.Tensor:
+    return torch.as_tensor(_DeviceArray(ptr, count), device=device)
+
+
+class ShardedCoulKernel:
+    """CalcCoulForceKernel over `world_size` ranks.  execute() returns the GLOBAL energy
+    (device scalar) and adds forces for this rank's owned atoms into `forces`."""
+
+    def __init__(self, system, force, device: int, group=None, kspace_algo: int = 0):
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.device = torch.device("cuda", device)
+        stream = torch.cuda.current_stream(self.device).cuda_stream
+        self.kernel = HipCalcCoulForceKernel(device=device, stream=stream, rank=self.rank, world_size=self.world,
+                                             kspace_algo=kspace_algo).initialize(system, force)
+        self.lo, self.hi = self.kernel.owned_range()
+        self.energy = torch.zeros(1, dtype=torch.float64, device=self.device)
+        ptr, n = self.kernel.kspace_buffer()
+        self._sbuf = device_buffer_as_tensor(ptr, n, self.device) if n else None
+
+    def execute(self, positions: torch.Tensor, box, forces: torch.Tensor | None, include_energy: bool = True):
+        k = self.kernel
+        k.begin(positions, box, forces is not None, include_energy)
+        if self.world > 1 and self._sbuf is not None:
+            dist.all_reduce(self._sbuf, op=dist.ReduceOp.SUM, group=self.group)
+        k.end(forces, self.energy)
+        if self.world > 1 and include_energy:
+            dist.all_reduce(self.energy, op=dist.ReduceOp.SUM, group=self.group)
+        return self.energy
+
+    def replicate_positions(self, positions: torch.Tensor):
+        """After each rank updated positions[lo:hi], make every rank's copy identical."""
+        if self.world == 1:
+            return positions
+        mask = torch.zeros_like(positions)
+        mask[self.lo:self.hi] = positions[self.lo:self.hi]
+        dist.all_reduce(mask, op=dist.ReduceOp.SUM, group=self.group)
+        positions.copy_(mask)
+        return positions

@@ -1,0 +1,261 @@
+"""The HIP implementation of CalcCoulForceKernel, plus a minimal OpenMM-shaped
+System/Context/State so the force can be driven (and tested) the way the reference is
+driven from OpenMM.
+
+Reference interfaces mirrored:
+  CalcCoulForceKernel::{Name, initialize, execute}   openmmapi/include/CoulKernels.h:15-38
+  CoulForceImpl::{initialize, calcForcesAndEnergy}   openmmapi/src/CoulForceImpl.cpp:16-27
+  System::getDefaultPeriodicBoxVectors               (used at ReferenceCoulKernels.cpp:399-400)
+
+Device arrays are torch tensors (PyTorch is plumbing here: device memory and streams);
+host arrays are numpy.  Every evaluation runs in libchargeflux_hip.so — there is no
+Python or CPU compute path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _cabi
+from .force import CoulForce
+
+DP = C.POINTER(C.c_double)
+
+
+def _dp(a: np.ndarray):
+    return a.ctypes.data_as(DP)
+
+
+class System:
+    """Minimal stand-in for openmm.System (particle count + default box + forces)."""
+
+    def __init__(self):
+        self._masses: list[float] = []
+        self._box = np.diag([2.0, 2.0, 2.0]).astype(np.float64)
+        self._forces: list = []
+
+    def addParticle(self, mass):
+        self._masses.append(float(mass))
+        return len(self._masses) - 1
+
+    def getNumParticles(self):
+        return len(self._masses)
+
+    def setDefaultPeriodicBoxVectors(self, a, b, c):
+        self._box = np.array([a, b, c], dtype=np.float64).reshape(3, 3)
+
+    def getDefaultPeriodicBoxVectors(self):
+        return [self._box[0].copy(), self._box[1].copy(), self._box[2].copy()]
+
+    def addForce(self, force):
+        self._forces.append(force)
+        return len(self._forces) - 1
+
+    def getForces(self):
+        return list(self._forces)
+
+
+def _box9(box) -> np.ndarray:
+    if box is None:
+        return np.zeros(9)
+    return np.ascontiguousarray(np.asarray(box, dtype=np.float64).reshape(9))
+
+
+class HipCalcCoulForceKernel:
+    """CalcCoulForceKernel on MI355X.  initialize() ~ ReferenceCalcCoulForceKernel::initialize
+    (ReferenceCoulKernels.cpp:230-422); execute() ~ ...::execute (:424-636)."""
+
+    @staticmethod
+    def Name():
+        return "CalcCoulForce"
+
+    def __init__(self, device: int = 0, stream=None, rank: int = 0, world_size: int = 1, kspace_algo: int = 0):
+        self._lib = _cabi.load_library()
+        self._h = C.c_void_p()
+        self._device = device
+        self._stream = stream
+        self._rank, self._world = rank, world_size
+        self._algo = kspace_algo
+        self._n = 0
+        self._pbc = False
+
+    # -------------------------------------------------------------------------------
+    def initialize(self, system, force: CoulForce):
+        if system.getNumParticles() != force.getNumParticles():
+            raise _cabi.ChargeFluxError(_cabi.CF_ERR_INVALID,
+                                        "System and CoulForce have different numbers of particles")
+        a, b, c = system.getDefaultPeriodicBoxVectors()
+        box = np.array([a, b, c], dtype=np.float64).reshape(9)
+        params, keep = force.to_cparams(box)
+        opt = _cabi.cf_options()
+        opt.device = self._device
+        opt.stream = C.c_void_p(self._stream) if self._stream else None
+        opt.rank, opt.world_size, opt.kspace_algo = self._rank, self._world, self._algo
+        self.destroy()
+        _cabi.check(self._lib.cf_create(C.byref(params), C.byref(opt), C.byref(self._h)), self._lib)
+        del keep
+        self._n = force.getNumParticles()
+        self._pbc = force.usesPeriodicBoundaryConditions()
+        return self
+
+    def destroy(self):
+        if self._h:
+            self._lib.cf_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.destroy()
+        except Exception:
+            pass
+
+    # -------------------------------------------------------------------------------
+    def ewald_params(self):
+        alpha = C.c_double()
+        kmax = (C.c_int32 * 3)()
+        _cabi.check(self._lib.cf_get_ewald_params(self._h, C.byref(alpha), kmax), self._lib)
+        return alpha.value, tuple(kmax)
+
+    def owned_range(self):
+        lo, hi = C.c_int32(), C.c_int32()
+        _cabi.check(self._lib.cf_get_owned_range(self._h, C.byref(lo), C.byref(hi)), self._lib)
+        return lo.value, hi.value
+
+    @staticmethod
+    def _flags(include_forces, include_energy):
+        return (_cabi.CF_INCLUDE_FORCES if include_forces else 0) | (_cabi.CF_INCLUDE_ENERGY if include_energy else 0)
+
+    def execute_host(self, positions, box=None, includeForces=True, includeEnergy=True, forces=None):
+        """Host-memory execute: positions (N,3) nm; forces (N,3) float64 array ADDED to
+        (created if None).  Returns (energy, forces)."""
+        pos = np.ascontiguousarray(np.asarray(positions, dtype=np.float64).reshape(self._n, 3))
+        if forces is None:
+            forces = np.zeros((self._n, 3))
+        if forces.dtype != np.float64 or not forces.flags.c_contiguous or forces.shape != (self._n, 3):
+            raise ValueError("forces must be a C-contiguous float64 (N,3) array")
+        e = C.c_double()
+        b9 = _box9(box)
+        _cabi.check(self._lib.cf_compute_host(self._h, _dp(pos), _dp(b9), self._flags(includeForces, includeEnergy),
+                                              _dp(forces), C.byref(e)), self._lib)
+        return e.value, forces
+
+    def execute_device(self, positions, box=None, includeForces=True, includeEnergy=True, forces=None, energy=None):
+        """Device execute on torch tensors (float64, cuda): forces (N,3) ADDED to, energy
+        (1,) overwritten.  Asynchronous on the kernel's stream."""
+        b9 = _box9(box)
+        fptr = forces.data_ptr() if forces is not None else None
+        eptr = energy.data_ptr() if energy is not None else None
+        _cabi.check(self._lib.cf_compute(self._h, C.c_void_p(positions.data_ptr()), _dp(b9),
+                                         self._flags(includeForces, includeEnergy), C.c_void_p(fptr),
+                                         C.c_void_p(eptr)), self._lib)
+
+    # split-phase (multi-GPU): begin -> all-reduce kspace_buffer -> end
+    def begin(self, positions, box=None, includeForces=True, includeEnergy=True):
+        self._b9 = _box9(box)
+        _cabi.check(self._lib.cf_compute_begin(self._h, C.c_void_p(positions.data_ptr()), _dp(self._b9),
+                                               self._flags(includeForces, includeEnergy)), self._lib)
+
+    def kspace_buffer(self):
+        ptr, n = C.c_void_p(), C.c_int64()
+        _cabi.check(self._lib.cf_kspace_buffer(self._h, C.byref(ptr), C.byref(n)), self._lib)
+        return ptr.value, n.value
+
+    def end(self, forces=None, energy=None):
+        fptr = forces.data_ptr() if forces is not None else None
+        eptr = energy.data_ptr() if energy is not None else None
+        _cabi.check(self._lib.cf_compute_end(self._h, C.c_void_p(fptr), C.c_void_p(eptr)), self._lib)
+
+    def execute(self, context, includeForces, includeEnergy):
+        """OpenMM-style execute(ContextImpl&, bool, bool) -> energy (ReferenceCoulKernels.cpp:424)."""
+        return context._execute_kernel(self, includeForces, includeEnergy)
+
+    # diagnostics ----------------------------------------------------------------------
+    def charges(self):
+        out = np.zeros(self._n)
+        _cabi.check(self._lib.cf_get_charges(self._h, _dp(out)), self._lib)
+        return out
+
+    def dedq(self):
+        out = np.zeros(self._n)
+        _cabi.check(self._lib.cf_get_dedq(self._h, _dp(out)), self._lib)
+        return out
+
+    def energy_terms(self):
+        out = np.zeros(4)
+        _cabi.check(self._lib.cf_get_energy_terms(self._h, _dp(out)), self._lib)
+        return out
+
+    def set_timing(self, enable=True):
+        _cabi.check(self._lib.cf_set_timing(self._h, 1 if enable else 0), self._lib)
+
+    def timing(self):
+        """{phase: (total_ms, launches)} recorded since set_timing(True)."""
+        nmax = 32
+        names = C.create_string_buffer(16 * nmax)
+        tot = (C.c_double * nmax)()
+        calls = (C.c_int32 * nmax)()
+        nph = C.c_int32()
+        _cabi.check(self._lib.cf_get_timing(self._h, nmax, names, tot, calls, C.byref(nph)), self._lib)
+        out = {}
+        for p in range(nph.value):
+            nm = names.raw[16 * p:16 * p + 16].split(b"\0")[0].decode()
+            out[nm] = (tot[p], calls[p])
+        return out
+
+    def synchronize(self):
+        _cabi.check(self._lib.cf_synchronize(self._h), self._lib)
+
+
+class State:
+    def __init__(self, energy, forces):
+        self._e, self._f = energy, forces
+
+    def getPotentialEnergy(self):
+        return self._e
+
+    def getForces(self, asNumpy=True):
+        return self._f
+
+
+class Context:
+    """Minimal OpenMM-Context mirror: owns one HipCalcCoulForceKernel per CoulForce in the
+    System (CoulForceImpl::initialize, CoulForceImpl.cpp:16-21) and evaluates them with the
+    force-group test of CoulForceImpl::calcForcesAndEnergy (CoulForceImpl.cpp:23-27)."""
+
+    def __init__(self, system: System, device: int = 0, kspace_algo: int = 0):
+        self._system = system
+        self._n = system.getNumParticles()
+        self._pos = np.zeros((self._n, 3))
+        a, b, c = system.getDefaultPeriodicBoxVectors()
+        self._box = np.array([a, b, c], dtype=np.float64)
+        self._impls = []
+        for f in system.getForces():
+            if isinstance(f, CoulForce):
+                k = HipCalcCoulForceKernel(device=device, kspace_algo=kspace_algo).initialize(system, f)
+                self._impls.append((f, k))
+
+    def setPositions(self, positions):
+        self._pos = np.ascontiguousarray(np.asarray(positions, dtype=np.float64).reshape(self._n, 3))
+
+    def setPeriodicBoxVectors(self, a, b, c):
+        self._box = np.array([a, b, c], dtype=np.float64)
+
+    def kernels(self):
+        return [k for _, k in self._impls]
+
+    def _execute_kernel(self, kernel, include_forces, include_energy):
+        forces = np.zeros((self._n, 3))
+        e, _ = kernel.execute_host(self._pos, self._box, include_forces, include_energy, forces)
+        self._last_forces = forces
+        return e
+
+    def getState(self, getEnergy=False, getForces=False, groups=-1):
+        energy = 0.0
+        forces = np.zeros((self._n, 3))
+        for f, k in self._impls:
+            if (groups & (1 << f.getForceGroup())) == 0:
+                continue
+            e, _ = k.execute_host(self._pos, self._box, bool(getForces), bool(getEnergy), forces)
+            energy += e
+        return State(energy if getEnergy else None, forces if getForces else None)

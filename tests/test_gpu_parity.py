@@ -1,0 +1,190 @@
+"""GPU parity tests: the HIP path (through the C-ABI) against the oracle restatement of
+ReferenceCoulKernels.cpp on identical inputs.
+
+Tolerances (fp64 everywhere; north star: forces within 1e-5 kJ/mol/nm):
+  forces   max |dF|            <= 1e-5 kJ/mol/nm   (typically ~1e-9)
+  energy   |dE|                <= 1e-9 |E| + 1e-8 kJ/mol
+  charges  max |dq|            <= 1e-12 e
+  dE/dq    max |d(dE/dq)|      <= 1e-9 max|dE/dq| + 1e-9
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+from oracle import Oracle  # noqa: E402
+from openmmcoul import HipCalcCoulForceKernel, ChargeFluxError  # noqa: E402
+from openmmcoul import testsystems as ts  # noqa: E402
+from openmmcoul.distributed import device_buffer_as_tensor  # noqa: E402
+
+F_TOL = 1e-5
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+
+
+def _compare(got, ref, f_tol=F_TOL, e_rel=1e-9):
+    e, f, q, dq, terms = got
+    assert abs(e - ref["energy"]) <= e_rel * abs(ref["energy"]) + 1e-8, (e, ref["energy"])
+    assert np.abs(f - ref["forces"]).max() <= f_tol, np.abs(f - ref["forces"]).max()
+    assert np.abs(q - ref["charges"]).max() <= 1e-12
+    if dq is not None:
+        scale = np.abs(ref["dedq"]).max()
+        assert np.abs(dq - ref["dedq"]).max() <= 1e-9 * scale + 1e-9
+    for a, b in zip(terms, ref["terms"]):
+        assert abs(a - b) <= e_rel * max(abs(b), 1.0) + 1e-8, (terms, ref["terms"])
+
+
+def _run(kernel, pos, box, fl=True, en=True):
+    e, f = kernel.execute_host(pos, box, fl, en)
+    return e, f, kernel.charges(), (kernel.dedq() if fl else None), kernel.energy_terms()
+
+
+def test_c1_cluster_no_pbc():
+    system, force, pos, box = ts.cluster_c1()
+    k = HipCalcCoulForceKernel().initialize(system, force)
+    o = Oracle(force)
+    for fl, en in ((True, True), (True, False), (False, True)):
+        ref = o.execute(pos, None, fl, en)
+        got = _run(k, pos, None, fl, en)
+        _compare(got, ref)
+
+
+@pytest.mark.parametrize("algo", [0, 1])
+@pytest.mark.parametrize("nw,rc,tol", [(100, 0.6, 1e-5), (400, 0.7, 1e-4)])
+def test_small_pbc_boxes(algo, nw, rc, tol):
+    # 100 waters: 2 cells/dim -> brute-force neighbour path; 400 waters: 3 cells/dim -> cell list
+    system, force, pos, box = ts.water_box(nw, cutoff=rc, ewald_tol=tol, every_bond_angle=3)
+    k = HipCalcCoulForceKernel(kspace_algo=algo).initialize(system, force)
+    o = Oracle(force, box)
+    assert k.ewald_params()[1] == o.ewald()[1]
+    for fl, en in ((True, True), (True, False), (False, True)):
+        _compare(_run(k, pos, box, fl, en), o.execute(pos, box, fl, en))
+
+
+@pytest.mark.parametrize("algo", [0, 1])
+def test_c2_parity(algo):
+    system, force, pos, box = ts.make("C2")
+    k = HipCalcCoulForceKernel(kspace_algo=algo).initialize(system, force)
+    assert k.ewald_params()[1] == (7, 7, 7)
+    _compare(_run(k, pos, box), Oracle(force, box).execute(pos, box))
+
+
+def test_c2_golden_fixture():
+    import os
+    d = np.load(os.path.join(os.path.dirname(__file__), "golden", "c2.npz"))
+    system, force, pos, box = ts.make("C2")
+    assert np.array_equal(pos, d["pos"])
+    k = HipCalcCoulForceKernel().initialize(system, force)
+    e, f, q, dq, terms = _run(k, pos, box)
+    assert abs(e - float(d["energy"])) <= 1e-9 * abs(float(d["energy"]))
+    assert np.abs(f - d["forces"]).max() <= F_TOL
+
+
+def test_nacl_madelung_gpu():
+    system, force, pos, box = ts.nacl_crystal(cells=4, a=0.5, cutoff=1.0, ewald_tol=1e-10)
+    k = HipCalcCoulForceKernel().initialize(system, force)
+    e, f = k.execute_host(pos, box)
+    expect = -(len(pos) / 2) * 1.747564594633182 * 138.935456 / 0.25
+    assert e == pytest.approx(expect, rel=2e-9)
+    assert np.abs(f).max() < 1e-6
+
+
+def test_moved_box_and_wrapped_positions():
+    # atoms outside the box, current box != default box (kmax stays from the default box)
+    system, force, pos, box = ts.water_box(400, cutoff=0.7, ewald_tol=1e-4)
+    p2 = pos + np.array([3.1, -7.4, 12.0])
+    box2 = box * 1.02
+    k = HipCalcCoulForceKernel().initialize(system, force)
+    _compare(_run(k, p2, box2), Oracle(force, box).execute(p2, box2))
+
+
+def test_device_api_matches_host_api_and_is_deterministic():
+    system, force, pos, box = ts.water_box(1500, cutoff=1.0, ewald_tol=1e-4)
+    stream = torch.cuda.current_stream().cuda_stream
+    k = HipCalcCoulForceKernel(stream=stream).initialize(system, force)
+    e_h, f_h = k.execute_host(pos, box)
+    pt = torch.tensor(pos, dtype=torch.float64, device="cuda")
+    outs = []
+    for _ in range(2):
+        f = torch.zeros_like(pt)
+        e = torch.zeros(1, dtype=torch.float64, device="cuda")
+        k.execute_device(pt, box, True, True, f, e)
+        torch.cuda.synchronize()
+        outs.append((e.item(), f.cpu().numpy()))
+    assert outs[0][0] == outs[1][0] and np.array_equal(outs[0][1], outs[1][1])  # bitwise reproducible
+    assert outs[0][0] == e_h and np.array_equal(outs[0][1], f_h)
+
+
+def test_forces_accumulate_and_untouched_without_forces():
+    system, force, pos, box = ts.water_box(100, cutoff=0.6)
+    k = HipCalcCoulForceKernel().initialize(system, force)
+    _, f1 = k.execute_host(pos, box)
+    f = np.ones_like(f1)
+    k.execute_host(pos, box, True, True, f)
+    assert np.allclose(f, f1 + 1.0, atol=1e-12)
+    g = np.full_like(f1, 3.0)
+    k.execute_host(pos, box, False, True, g)
+    assert np.all(g == 3.0)
+
+
+def test_two_rank_decomposition_on_one_gpu():
+    system, force, pos, box = ts.water_box(1200, cutoff=1.0, ewald_tol=1e-4, every_bond_angle=4)
+    stream = torch.cuda.current_stream().cuda_stream
+    pt = torch.tensor(pos, dtype=torch.float64, device="cuda")
+    single = HipCalcCoulForceKernel(stream=stream).initialize(system, force)
+    e1, f1 = single.execute_host(pos, box)
+    ks = [HipCalcCoulForceKernel(stream=stream, rank=r, world_size=2).initialize(system, force) for r in range(2)]
+    ranges = [k.owned_range() for k in ks]
+    assert ranges[0][0] == 0 and ranges[0][1] == ranges[1][0] and ranges[1][1] == len(pos)
+    for k in ks:
+        k.begin(pt, box, True, True)
+    bufs = [device_buffer_as_tensor(*k.kspace_buffer(), "cuda") for k in ks]
+    total = bufs[0] + bufs[1]
+    for b in bufs:
+        b.copy_(total)
+    f = torch.zeros_like(pt)
+    es = []
+    for k in ks:
+        e = torch.zeros(1, dtype=torch.float64, device="cuda")
+        k.end(f, e)
+        es.append(e)
+    torch.cuda.synchronize()
+    assert (es[0] + es[1]).item() == pytest.approx(e1, rel=1e-11)
+    assert np.abs(f.cpu().numpy() - f1).max() < 1e-8
+
+
+def test_c3_mfma_matches_direct_path():
+    # full-size C3 (96k atoms, kmax 31): the MFMA separable path against the independent
+    # direct-sincos VALU path (the oracle would take ~10 minutes here)
+    system, force, pos, box = ts.make("C3")
+    ka = HipCalcCoulForceKernel(kspace_algo=0).initialize(system, force)
+    kb = HipCalcCoulForceKernel(kspace_algo=1).initialize(system, force)
+    assert ka.ewald_params()[1] == (31, 31, 31)
+    ea, fa = ka.execute_host(pos, box)
+    eb, fb = kb.execute_host(pos, box)
+    assert ea == pytest.approx(eb, rel=1e-11)
+    assert np.abs(fa - fb).max() < 1e-7
+    q = ka.charges()
+    assert q.sum() == pytest.approx(force.arrays()["charges"].sum(), abs=1e-9)
+    ta, tb = ka.energy_terms(), kb.energy_terms()
+    assert np.allclose(ta, tb, rtol=1e-11, atol=1e-8)
+
+
+def test_error_behaviour():
+    system, force, pos, box = ts.water_box(100, cutoff=0.6)
+    k = HipCalcCoulForceKernel().initialize(system, force)
+    with pytest.raises(ChargeFluxError) as ei:
+        k.execute_host(pos, box * 0.8)  # cutoff > L/2
+    assert ei.value.code == -1
+    with pytest.raises(ChargeFluxError) as ei:
+        k.end()
+    assert ei.value.code == -3
+    force.setCutoffDistance(0.9)
+    with pytest.raises(ChargeFluxError):
+        HipCalcCoulForceKernel().initialize(system, force)
