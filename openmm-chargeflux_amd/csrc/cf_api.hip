@@ -23,11 +23,11 @@
 // Per-kernel HIP-event timing (cf_set_timing / cf_get_timing): start/stop events are
 // recorded on the handle's stream around every launch, so bench.py can report kernel
 // durations measured on the stream the kernels actually run on.
-enum Phase { PH_FLUX, PH_PREP, PH_CELLS, PH_TABLES, PH_SFAC, PH_COEFFS, PH_FORCE, PH_DIRECT, PH_ASSEMBLE,
-             PH_ENERGY, PH_COUNT };
-static const char* kPhaseNames[PH_COUNT] = {"flux_terms", "atoms_prep", "cell_sort", "kspace_tables",
-                                            "kspace_sfac", "kspace_coeffs", "kspace_force", "direct",
-                                            "assemble", "energy"};
+enum Phase { PH_FLUX, PH_PREP, PH_CELLS, PH_NLIST, PH_TABLES, PH_SFAC, PH_COEFFS, PH_FORCE, PH_DIRECT,
+             PH_ASSEMBLE, PH_ENERGY, PH_COUNT };
+static const char* kPhaseNames[PH_COUNT] = {"flux_terms", "atoms_prep", "cell_sort", "neighbor_list",
+                                            "kspace_tables", "kspace_sfac", "kspace_coeffs", "kspace_force",
+                                            "direct_pairs", "assemble", "energy"};
 constexpr int kMaxTimed = 8192;
 
 struct cf_handle {
@@ -247,12 +247,7 @@ CF_EXPORT int cf_create(const cf_params* p, const cf_options* opt, cf_handle** o
         h.rank = o.rank;
         h.world = world;
         h.kspace_algo = o.kspace_algo == 1 ? 1 : 0;
-        if (o.stream) {
-            h.stream = (hipStream_t)o.stream;
-        } else {
-            check_hip(hipStreamCreateWithFlags(&h.stream, hipStreamNonBlocking), "stream");
-            h.own_stream = true;
-        }
+        h.stream = (hipStream_t)o.stream;  // NULL = the null stream (orders with torch's default stream)
 
         // ---- particles: q0, LJ (sigma/2, 2 sqrt(eps))   RCK:234-240
         std::vector<double> q0(n);
@@ -418,6 +413,15 @@ CF_EXPORT int cf_create(const cf_params* p, const cf_options* opt, cf_handle** o
                       "sort temp query");
             h.sort_tmp_bytes = tmp;
             h.sort_tmp = dalloc<char>(H, tmp);
+            // neighbour-list capacity: 1.5x the mean count at the default-box density + margin
+            // (k_pairs rescans the cells for any atom that overflows, so this is a speed knob)
+            {
+                double V = p->default_box[0] * p->default_box[4] * p->default_box[8];
+                double mean = 4.0 / 3.0 * M_PI * h.cutoff * h.cutoff * h.cutoff * n / V;
+                h.nb_cap = (int)std::min<double>(n, 1.5 * mean + 64);
+                h.nl = dalloc<int>(H, (size_t)h.nb_cap * n);
+                h.nl_cnt = dalloc<int>(H, n);
+            }
             if (h.kspace_algo == 0) {
                 // phase tables: padded rows stay zero forever (memset once)
                 h.tab_xq = dalloc<double2>(H, (size_t)h.npad * g.KX);
@@ -506,6 +510,7 @@ CF_EXPORT int cf_compute_begin(cf_handle* H, const double* pos_dev, const double
         { Timed t(H, PH_PREP); cf::launch_atoms_prep(h, pos_dev); }
         if (h.pbc) {
             { Timed t(H, PH_CELLS); cf::launch_cell_sort(h, pos_dev); }
+            if (h.hi > h.lo) { Timed t(H, PH_NLIST); cf::launch_nlist(h, pos_dev); }
             if ((forces || energy) && h.hi > h.lo) {
                 if (h.kspace_algo == 0) {
                     { Timed t(H, PH_TABLES); cf::launch_kspace_tables(h, pos_dev); }

@@ -107,6 +107,9 @@ struct Handle {
     double4* pos4s = nullptr;   // [N] sorted wrapped (x,y,z,q)
     double2* ljs = nullptr;     // [N] sorted LJ
     void* sort_tmp = nullptr; size_t sort_tmp_bytes = 0;
+    int nb_cap = 0;             // neighbour-list capacity per atom
+    int* nl = nullptr;          // [nb_cap][N] transposed neighbour list (sorted index | shift<<26)
+    int* nl_cnt = nullptr;      // [N]
     // k-space (MFMA path)
     int npad = 0;               // owned rows of the phase tables, padded to the S-pass tile
     double2* tab_xq = nullptr;  // [Nown][KX]
@@ -136,6 +139,7 @@ struct Handle {
 void launch_flux_terms(Handle& h, const double* pos);
 void launch_atoms_prep(Handle& h, const double* pos);
 void launch_cell_sort(Handle& h, const double* pos);
+void launch_nlist(Handle& h, const double* pos);
 void launch_direct(Handle& h, const double* pos, int include_forces);
 void launch_nopbc(Handle& h, const double* pos, int include_forces, int include_energy);
 void launch_assemble(Handle& h, double* forces_out);

@@ -170,17 +170,27 @@ __global__ void __launch_bounds__(256) k_cell_gather(int n, const int* __restric
 }
 
 // ---------------------------------------------------------------------------------
-// 4. direct space + exclusion correction, one lane per owned atom i (full neighbour
-//    list: each pair is evaluated from both sides, every per-atom sum is a gather).
+// 4. direct space + exclusion correction (full neighbour list: every pair is evaluated
+//    from both sides, so every per-atom sum is a gather and no atomics are needed).
 //    Real-space pair RCK:562-593, exclusion erf correction RCK:596-622.
-//    Finishes dE/dq_i (self + recip + direct + excl) and the non-chain forces.
+//
+//    4a k_nlist: one lane per owned atom (cell-sorted order) scans the 27 neighbour cells
+//       and appends every non-excluded partner with r^2 <= rc^2 (the reference's voxel-hash
+//       list, RCK:559) to a transposed list nl[k*N + s] = t | shift<<26.  Only ~12% of the
+//       candidates pass the cutoff, so the expensive erfc/exp math is kept out of this
+//       divergent loop.
+//    4b k_pairs: one lane per owned atom walks its list with every lane busy, then the
+//       exclusion correction, and finishes dE/dq_i and the non-chain forces.
 // ---------------------------------------------------------------------------------
 constexpr int kMaxRegExcl = 8;
+constexpr int kShiftBits = 26;
+constexpr int kBruteShift = 31;  // shift code: minimum image by floor (brute-force path)
 
 struct DirectArgs {
     int n, lo, hi, include_forces;
     double3 L; int3 nc; int brute;
     double rc2, alpha;
+    int nb_cap;
     const int* atom_sorted; const int* key_sorted;
     const int* cstart; const int* cend;
     const double4* pos4s; const double2* ljs;
@@ -188,6 +198,7 @@ struct DirectArgs {
     const int* ex_start; const int* ex_list;
     const double* dedq_self;
     const double* t_part; int nparts; int nown;  // reciprocal partials [p][nown][4]
+    int* nl; int* nl_cnt;
     double* dedq; double* f_part; double* e_atom;
 };
 
@@ -201,7 +212,168 @@ __device__ __forceinline__ bool in_excl(int j, const int* reg, int cnt, const in
     return false;
 }
 
-__global__ void __launch_bounds__(256) k_direct(DirectArgs a) {
+__device__ __forceinline__ double3 shift_of(int code, double3 L) {
+    int ox = code / 9 - 1, oy = (code / 3) % 3 - 1, oz = code % 3 - 1;
+    return make_double3(ox * L.x, oy * L.y, oz * L.z);
+}
+
+// Visit the 27 neighbour cells of sorted atom s; fn(t, code, dx, dy, dz, r2) for every
+// candidate t != s within the cutoff (exclusions are left to the caller).
+template <class F>
+__device__ __forceinline__ void scan_cells(const DirectArgs& a, int s, double4 pi, F&& fn) {
+    if (!a.brute) {
+        int key = a.key_sorted[s];
+        int cz = key % a.nc.z, cy = (key / a.nc.z) % a.nc.y, cx = key / (a.nc.y * a.nc.z);
+        for (int ox = -1; ox <= 1; ox++) {
+            int x = cx + ox; double sx = 0; int kx = ox + 1;
+            if (x < 0) { x += a.nc.x; sx = -a.L.x; kx = 0; } else if (x >= a.nc.x) { x -= a.nc.x; sx = a.L.x; kx = 2; } else kx = 1;
+            for (int oy = -1; oy <= 1; oy++) {
+                int y = cy + oy; double sy = 0; int ky;
+                if (y < 0) { y += a.nc.y; sy = -a.L.y; ky = 0; } else if (y >= a.nc.y) { y -= a.nc.y; sy = a.L.y; ky = 2; } else ky = 1;
+                for (int oz = -1; oz <= 1; oz++) {
+                    int z = cz + oz; double sz = 0; int kz;
+                    if (z < 0) { z += a.nc.z; sz = -a.L.z; kz = 0; } else if (z >= a.nc.z) { z -= a.nc.z; sz = a.L.z; kz = 2; } else kz = 1;
+                    int code = kx * 9 + ky * 3 + kz;
+                    int c = (x * a.nc.y + y) * a.nc.z + z;
+                    int t1 = a.cend[c];
+                    for (int t = a.cstart[c]; t < t1; t++) {
+                        double4 pj = a.pos4s[t];
+                        double dx = pi.x - (pj.x + sx), dy = pi.y - (pj.y + sy), dz = pi.z - (pj.z + sz);
+                        double r2 = dx * dx + dy * dy + dz * dz;
+                        if (r2 > a.rc2 || t == s) continue;
+                        fn(t, code, dx, dy, dz, r2);
+                    }
+                }
+            }
+        }
+    } else {
+        for (int t = 0; t < a.n; t++) {
+            if (t == s) continue;
+            double4 pj = a.pos4s[t];
+            double3 d = delta_r(make_double3(pj.x, pj.y, pj.z), make_double3(pi.x, pi.y, pi.z), a.L, 1);
+            double r2 = d.x * d.x + d.y * d.y + d.z * d.z;
+            if (r2 > a.rc2) continue;
+            fn(t, kBruteShift, d.x, d.y, d.z, r2);
+        }
+    }
+}
+
+__global__ void __launch_bounds__(256) k_nlist(DirectArgs a) {
+    int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= a.n) return;
+    int i = a.atom_sorted[s];
+    if (i < a.lo || i >= a.hi) return;
+    const double4 pi = a.pos4s[s];
+    const int ex0 = a.ex_start[i], exc = a.ex_start[i + 1] - ex0;
+    int reg[kMaxRegExcl];
+#pragma unroll
+    for (int k = 0; k < kMaxRegExcl; k++) reg[k] = k < exc ? a.ex_list[ex0 + k] : -1;
+    int cnt = 0;
+    scan_cells(a, s, pi, [&](int t, int code, double, double, double, double) {
+        if (exc && in_excl(a.atom_sorted[t], reg, exc, a.ex_list, ex0)) return;
+        if (cnt < a.nb_cap) a.nl[(size_t)cnt * a.n + s] = t | (code << kShiftBits);
+        cnt++;
+    });
+    a.nl_cnt[s] = cnt;
+}
+
+// Wave-cooperative list build (the fast path): one 64-lane workgroup owns 64 consecutive
+// cell-sorted atoms.  The union of their 27-cell neighbourhoods is a small box of cells in
+// unwrapped cell coordinates; candidates of each cell are loaded coalesced (one per lane),
+// shifted to the image adjacent to the block, staged in LDS and tested by every lane with
+// broadcast LDS reads.  Falls back to the per-lane scan when the box would wrap onto itself.
+constexpr int kWaveNL = 64;
+
+__global__ void __launch_bounds__(kWaveNL) k_nlist_wave(DirectArgs a) {
+    __shared__ double4 cand[kWaveNL];
+    __shared__ int cand_t[kWaveNL];
+    const int lane = threadIdx.x;
+    const int base = blockIdx.x * kWaveNL;
+    const int s = base + lane;
+    const bool valid = s < a.n;
+    const int ss = valid ? s : a.n - 1;
+    const int i = a.atom_sorted[ss];
+    const bool active = valid && i >= a.lo && i < a.hi;
+    const double4 pi = a.pos4s[ss];
+    const int key = a.key_sorted[ss];
+    int c[3] = {key / (a.nc.y * a.nc.z), (key / a.nc.z) % a.nc.y, key % a.nc.z};
+    const int key0 = a.key_sorted[base];
+    const int c0[3] = {key0 / (a.nc.y * a.nc.z), (key0 / a.nc.z) % a.nc.y, key0 % a.nc.z};
+    const int ncs[3] = {a.nc.x, a.nc.y, a.nc.z};
+    int lo3[3], hi3[3];
+    bool fits = true;
+#pragma unroll
+    for (int d = 0; d < 3; d++) {
+        int dd = c[d] - c0[d];
+        if (dd > ncs[d] / 2) dd -= ncs[d];
+        if (dd < -(ncs[d] / 2)) dd += ncs[d];
+        int u = c0[d] + dd;  // unwrapped cell coordinate of this lane
+        int mn = u, mx = u;
+        for (int off = 32; off > 0; off >>= 1) {
+            mn = min(mn, __shfl_xor(mn, off));
+            mx = max(mx, __shfl_xor(mx, off));
+        }
+        lo3[d] = mn - 1; hi3[d] = mx + 1;
+        if (hi3[d] - lo3[d] + 1 > ncs[d]) fits = false;
+    }
+    const int ex0 = a.ex_start[i], exc = a.ex_start[i + 1] - ex0;
+    int reg[kMaxRegExcl];
+#pragma unroll
+    for (int k = 0; k < kMaxRegExcl; k++) reg[k] = k < exc ? a.ex_list[ex0 + k] : -1;
+    // exclusion lists are sorted: a candidate outside [ex_min, ex_max] needs no lookup
+    const int ex_min = exc ? a.ex_list[ex0] : 1, ex_max = exc ? a.ex_list[ex0 + exc - 1] : 0;
+    int cnt = 0;
+    auto emit = [&](int t, int j, int code) {
+        if (j >= ex_min && j <= ex_max && in_excl(j, reg, exc, a.ex_list, ex0)) return;
+        if (cnt < a.nb_cap) a.nl[(size_t)cnt * a.n + s] = t | (code << kShiftBits);
+        cnt++;
+    };
+    if (!fits) {  // wave-uniform
+        if (active)
+            scan_cells(a, s, pi, [&](int t, int code, double, double, double, double) { emit(t, a.atom_sorted[t], code); });
+    } else {
+        const double Ls[3] = {a.L.x, a.L.y, a.L.z};
+        for (int ux = lo3[0]; ux <= hi3[0]; ux++) {
+            int wx = (ux % ncs[0] + ncs[0]) % ncs[0];
+            int kx = ux < 0 ? 0 : (ux >= ncs[0] ? 2 : 1);
+            double sx = (kx - 1) * Ls[0];
+            for (int uy = lo3[1]; uy <= hi3[1]; uy++) {
+                int wy = (uy % ncs[1] + ncs[1]) % ncs[1];
+                int ky = uy < 0 ? 0 : (uy >= ncs[1] ? 2 : 1);
+                double sy = (ky - 1) * Ls[1];
+                for (int uz = lo3[2]; uz <= hi3[2]; uz++) {
+                    int wz = (uz % ncs[2] + ncs[2]) % ncs[2];
+                    int kz = uz < 0 ? 0 : (uz >= ncs[2] ? 2 : 1);
+                    double sz = (kz - 1) * Ls[2];
+                    const int code = kx * 9 + ky * 3 + kz;
+                    const int cc = (wx * a.nc.y + wy) * a.nc.z + wz;
+                    const int t0 = a.cstart[cc], t1 = a.cend[cc];
+                    for (int tb = t0; tb < t1; tb += kWaveNL) {
+                        const int m = min(kWaveNL, t1 - tb);
+                        __syncthreads();
+                        if (lane < m) {
+                            double4 pj = a.pos4s[tb + lane];
+                            cand[lane] = make_double4(pj.x + sx, pj.y + sy, pj.z + sz, 0.0);
+                            cand_t[lane] = a.atom_sorted[tb + lane];
+                        }
+                        __syncthreads();
+                        if (active) {
+                            for (int u = 0; u < m; u++) {
+                                double4 pj = cand[u];
+                                double dx = pi.x - pj.x, dy = pi.y - pj.y, dz = pi.z - pj.z;
+                                double r2 = dx * dx + dy * dy + dz * dz;
+                                if (r2 <= a.rc2 && tb + u != s) emit(tb + u, cand_t[u], code);
+                            }
+                        }
+                    }
+                }
+            }
+        }
+    }
+    if (active) a.nl_cnt[s] = cnt;
+}
+
+__global__ void __launch_bounds__(256) k_pairs(DirectArgs a) {
     int s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= a.n) return;
     int i = a.atom_sorted[s];
@@ -209,15 +381,14 @@ __global__ void __launch_bounds__(256) k_direct(DirectArgs a) {
     const double4 pi = a.pos4s[s];
     const double2 li = a.ljs[s];
     const int ex0 = a.ex_start[i], exc = a.ex_start[i + 1] - ex0;
-    int reg[kMaxRegExcl];
-#pragma unroll
-    for (int k = 0; k < kMaxRegExcl; k++) reg[k] = k < exc ? a.ex_list[ex0 + k] : -1;
 
     const double ke = kOne4PiEps0;
     const double two_over_sqrtpi = 2.0 / sqrt(kPi);
     double fx = 0, fy = 0, fz = 0, dq = 0, e = 0;
 
-    auto pair = [&](const double4& pj, const double2& lj2, double dx, double dy, double dz, double r2) {
+    auto pair = [&](int t, double dx, double dy, double dz, double r2) {
+        const double4 pj = a.pos4s[t];
+        const double2 lj2 = a.ljs[t];
         double r = sqrt(r2);
         double inv_r = 1.0 / r, ar = a.alpha * r;
         double ec = erfc(ar);
@@ -235,43 +406,31 @@ __global__ void __launch_bounds__(256) k_direct(DirectArgs a) {
         e += 0.5 * (qq * ec + es6 * (sig6 - 1));
     };
 
-    if (!a.brute) {
-        int key = a.key_sorted[s];
-        int cz = key % a.nc.z, cy = (key / a.nc.z) % a.nc.y, cx = key / (a.nc.y * a.nc.z);
-        for (int ox = -1; ox <= 1; ox++) {
-            int x = cx + ox; double sx = 0;
-            if (x < 0) { x += a.nc.x; sx = -a.L.x; } else if (x >= a.nc.x) { x -= a.nc.x; sx = a.L.x; }
-            for (int oy = -1; oy <= 1; oy++) {
-                int y = cy + oy; double sy = 0;
-                if (y < 0) { y += a.nc.y; sy = -a.L.y; } else if (y >= a.nc.y) { y -= a.nc.y; sy = a.L.y; }
-                for (int oz = -1; oz <= 1; oz++) {
-                    int z = cz + oz; double sz = 0;
-                    if (z < 0) { z += a.nc.z; sz = -a.L.z; } else if (z >= a.nc.z) { z -= a.nc.z; sz = a.L.z; }
-                    int c = (x * a.nc.y + y) * a.nc.z + z;
-                    int t1 = a.cend[c];
-                    for (int t = a.cstart[c]; t < t1; t++) {
-                        double4 pj = a.pos4s[t];
-                        double dx = pi.x - (pj.x + sx), dy = pi.y - (pj.y + sy), dz = pi.z - (pj.z + sz);
-                        double r2 = dx * dx + dy * dy + dz * dz;
-                        if (r2 > a.rc2 || t == s) continue;
-                        int j = a.atom_sorted[t];
-                        if (exc && in_excl(j, reg, exc, a.ex_list, ex0)) continue;
-                        pair(pj, a.ljs[t], dx, dy, dz, r2);
-                    }
-                }
+    const int cnt = a.nl_cnt[s];
+    if (cnt <= a.nb_cap) {
+        for (int k = 0; k < cnt; k++) {
+            int v = a.nl[(size_t)k * a.n + s];
+            int t = v & ((1 << kShiftBits) - 1), code = v >> kShiftBits;
+            double4 pj = a.pos4s[t];
+            double dx, dy, dz;
+            if (code != kBruteShift) {
+                double3 sh = shift_of(code, a.L);
+                dx = pi.x - (pj.x + sh.x); dy = pi.y - (pj.y + sh.y); dz = pi.z - (pj.z + sh.z);
+            } else {
+                double3 d = delta_r(make_double3(pj.x, pj.y, pj.z), make_double3(pi.x, pi.y, pi.z), a.L, 1);
+                dx = d.x; dy = d.y; dz = d.z;
             }
+            pair(t, dx, dy, dz, dx * dx + dy * dy + dz * dz);
         }
     } else {
-        for (int t = 0; t < a.n; t++) {
-            if (t == s) continue;
-            double4 pj = a.pos4s[t];
-            double3 d = delta_r(make_double3(pj.x, pj.y, pj.z), make_double3(pi.x, pi.y, pi.z), a.L, 1);
-            double r2 = d.x * d.x + d.y * d.y + d.z * d.z;
-            if (r2 > a.rc2) continue;
-            int j = a.atom_sorted[t];
-            if (exc && in_excl(j, reg, exc, a.ex_list, ex0)) continue;
-            pair(pj, a.ljs[t], d.x, d.y, d.z, r2);
-        }
+        // list overflow (denser than planned): rescan the cells directly
+        int reg[kMaxRegExcl];
+#pragma unroll
+        for (int k = 0; k < kMaxRegExcl; k++) reg[k] = k < exc ? a.ex_list[ex0 + k] : -1;
+        scan_cells(a, s, pi, [&](int t, int, double dx, double dy, double dz, double r2) {
+            if (exc && in_excl(a.atom_sorted[t], reg, exc, a.ex_list, ex0)) return;
+            pair(t, dx, dy, dz, r2);
+        });
     }
 
     // exclusion correction: subtract the erf (Gaussian-screened) part for EVERY excluded
@@ -466,13 +625,14 @@ void launch_cell_sort(Handle& h, const double* pos) {
                        h.atom_sorted, pos, h.q, h.lj, L, h.cell_start, h.cell_end, h.pos4s, h.ljs);
 }
 
-void launch_direct(Handle& h, const double* pos, int include_forces) {
+static DirectArgs direct_args(Handle& h, const double* pos, int include_forces) {
     DirectArgs a;
     a.n = h.n; a.lo = h.lo; a.hi = h.hi; a.include_forces = include_forces;
     a.L = make_double3(h.box_L[0], h.box_L[1], h.box_L[2]);
     a.nc = make_int3(h.nc[0], h.nc[1], h.nc[2]);
     a.brute = (h.nc[0] < 3 || h.nc[1] < 3 || h.nc[2] < 3) ? 1 : 0;
     a.rc2 = h.cutoff * h.cutoff; a.alpha = h.alpha;
+    a.nb_cap = h.nb_cap;
     a.atom_sorted = h.atom_sorted; a.key_sorted = h.cell_key_sorted;
     a.cstart = h.cell_start; a.cend = h.cell_end;
     a.pos4s = h.pos4s; a.ljs = h.ljs;
@@ -480,9 +640,23 @@ void launch_direct(Handle& h, const double* pos, int include_forces) {
     a.dedq_self = h.dedq_self;
     a.nparts = h.kspace_algo == 1 ? 1 : h.fp.nparts();
     a.t_part = h.t_part; a.nown = h.hi - h.lo;
+    a.nl = h.nl; a.nl_cnt = h.nl_cnt;
     a.dedq = h.dedq; a.f_part = h.f_part; a.e_atom = h.e_atom;
     a.pos = pos;
-    hipLaunchKernelGGL(k_direct, dim3(nblk(h.n, 256)), dim3(256), 0, h.stream, a);
+    return a;
+}
+
+void launch_nlist(Handle& h, const double* pos) {
+    DirectArgs a = direct_args(h, pos, 0);
+    if (a.brute || h.nc[0] < 4 || h.nc[1] < 4 || h.nc[2] < 4)
+        hipLaunchKernelGGL(k_nlist, dim3(nblk(h.n, 256)), dim3(256), 0, h.stream, a);
+    else
+        hipLaunchKernelGGL(k_nlist_wave, dim3(nblk(h.n, kWaveNL)), dim3(kWaveNL), 0, h.stream, a);
+}
+
+void launch_direct(Handle& h, const double* pos, int include_forces) {
+    DirectArgs a = direct_args(h, pos, include_forces);
+    hipLaunchKernelGGL(k_pairs, dim3(nblk(h.n, 256)), dim3(256), 0, h.stream, a);
 }
 
 void launch_nopbc(Handle& h, const double* pos, int include_forces, int include_energy) {

@@ -29,9 +29,13 @@ def _need_gpu():
 
 
 def _compare(got, ref, f_tol=F_TOL, e_rel=1e-9):
+    # forces are compared only when requested: without includeForces the reference still
+    # applies its chain rule with the self-term dE/dq (ReferenceCoulKernels.cpp:509,626)
+    # to a force buffer OpenMM then ignores; the HIP path leaves forces untouched.
     e, f, q, dq, terms = got
     assert abs(e - ref["energy"]) <= e_rel * abs(ref["energy"]) + 1e-8, (e, ref["energy"])
-    assert np.abs(f - ref["forces"]).max() <= f_tol, np.abs(f - ref["forces"]).max()
+    if dq is not None:
+        assert np.abs(f - ref["forces"]).max() <= f_tol, np.abs(f - ref["forces"]).max()
     assert np.abs(q - ref["charges"]).max() <= 1e-12
     if dq is not None:
         scale = np.abs(ref["dedq"]).max()
