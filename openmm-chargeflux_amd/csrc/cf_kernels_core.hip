@@ -294,6 +294,7 @@ __global__ void __launch_bounds__(kWaveNL) k_nlist_wave(DirectArgs a) {
     const int ss = valid ? s : a.n - 1;
     const int i = a.atom_sorted[ss];
     const bool active = valid && i >= a.lo && i < a.hi;
+    if (__ballot(active) == 0) return;  // no owned atom in this block (multi-GPU): skip it whole
     const double4 pi = a.pos4s[ss];
     const int key = a.key_sorted[ss];
     int c[3] = {key / (a.nc.y * a.nc.z), (key / a.nc.z) % a.nc.y, key % a.nc.z};

@@ -32,18 +32,21 @@ class ShardedCoulKernel:
     """CalcCoulForceKernel over `world_size` ranks.  execute() returns the GLOBAL energy
     (device scalar) and adds forces for this rank's owned atoms into `forces`."""
 
-    def __init__(self, system, force, device: int, group=None, kspace_algo: int = 0):
+    def __init__(self, system, force, device: int, group=None, kspace_algo: int = 0, kernel=None):
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
-        self.device = torch.device("cuda", device)
-        stream = torch.cuda.current_stream(self.device).cuda_stream
-        self.kernel = HipCalcCoulForceKernel(device=device, stream=stream, rank=self.rank, world_size=self.world,
-                                             kspace_algo=kspace_algo).initialize(system, force)
+        if kernel is None:
+            self.device = torch.device("cuda", device)
+            stream = torch.cuda.current_stream(self.device).cuda_stream
+            kernel = HipCalcCoulForceKernel(device=device, stream=stream, rank=self.rank, world_size=self.world,
+                                            kspace_algo=kspace_algo).initialize(system, force)
+        else:  # any object with the split-phase kernel interface (tests drive this on CPU/gloo)
+            self.device = torch.device(device) if not isinstance(device, torch.device) else device
+        self.kernel = kernel
         self.lo, self.hi = self.kernel.owned_range()
         self.energy = torch.zeros(1, dtype=torch.float64, device=self.device)
-        ptr, n = self.kernel.kspace_buffer()
-        self._sbuf = device_buffer_as_tensor(ptr, n, self.device) if n else None
+        self._sbuf = self.kernel.kspace_tensor(self.device)
 
     def execute(self, positions: torch.Tensor, box, forces: torch.Tensor | None, include_energy: bool = True):
         k = self.kernel

@@ -161,6 +161,14 @@ class HipCalcCoulForceKernel:
         _cabi.check(self._lib.cf_kspace_buffer(self._h, C.byref(ptr), C.byref(n)), self._lib)
         return ptr.value, n.value
 
+    def kspace_tensor(self, device):
+        """The structure-factor buffer as a zero-copy torch tensor (None without PBC)."""
+        ptr, n = self.kspace_buffer()
+        if not n:
+            return None
+        from .distributed import device_buffer_as_tensor
+        return device_buffer_as_tensor(ptr, n, device)
+
     def end(self, forces=None, energy=None):
         fptr = forces.data_ptr() if forces is not None else None
         eptr = energy.data_ptr() if energy is not None else None
