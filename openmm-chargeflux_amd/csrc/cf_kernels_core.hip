@@ -285,8 +285,8 @@ __global__ void __launch_bounds__(256) k_nlist(DirectArgs a) {
 constexpr int kWaveNL = 64;
 
 __global__ void __launch_bounds__(kWaveNL) k_nlist_wave(DirectArgs a) {
-    __shared__ double4 cand[kWaveNL];
-    __shared__ int cand_t[kWaveNL];
+    __shared__ float4 cand[kWaveNL + 8];
+    __shared__ int cand_t[kWaveNL + 8];
     const int lane = threadIdx.x;
     const int base = blockIdx.x * kWaveNL;
     const int s = base + lane;
@@ -301,14 +301,15 @@ __global__ void __launch_bounds__(kWaveNL) k_nlist_wave(DirectArgs a) {
     const int key0 = a.key_sorted[base];
     const int c0[3] = {key0 / (a.nc.y * a.nc.z), (key0 / a.nc.z) % a.nc.y, key0 % a.nc.z};
     const int ncs[3] = {a.nc.x, a.nc.y, a.nc.z};
-    int lo3[3], hi3[3];
+    int lo3[3], hi3[3], lsh[3];
     bool fits = true;
 #pragma unroll
     for (int d = 0; d < 3; d++) {
         int dd = c[d] - c0[d];
         if (dd > ncs[d] / 2) dd -= ncs[d];
         if (dd < -(ncs[d] / 2)) dd += ncs[d];
-        int u = c0[d] + dd;  // unwrapped cell coordinate of this lane
+        int u = c0[d] + dd;  // unwrapped cell coordinate of this lane in the block frame
+        lsh[d] = u < 0 ? -1 : (u >= ncs[d] ? 1 : 0);  // image of this lane's (wrapped) position
         int mn = u, mx = u;
         for (int off = 32; off > 0; off >>= 1) {
             mn = min(mn, __shfl_xor(mn, off));
@@ -317,6 +318,12 @@ __global__ void __launch_bounds__(kWaveNL) k_nlist_wave(DirectArgs a) {
         lo3[d] = mn - 1; hi3[d] = mx + 1;
         if (hi3[d] - lo3[d] + 1 > ncs[d]) fits = false;
     }
+    // block frame: every lane's position moved to the image of its unwrapped cell; origin =
+    // lane 0 (lsh = 0 there), so all frame coordinates are within a few cells of 0
+    const double3 pu = make_double3(pi.x + lsh[0] * a.L.x, pi.y + lsh[1] * a.L.y, pi.z + lsh[2] * a.L.z);
+    const double4 org = make_double4(__shfl(pu.x, 0), __shfl(pu.y, 0), __shfl(pu.z, 0), 0.0);
+    const float3 pf = make_float3((float)(pu.x - org.x), (float)(pu.y - org.y), (float)(pu.z - org.z));
+    const float rc2f = (float)(a.rc2 * (1.0 + 1e-5)) + 1e-6f;
     const int ex0 = a.ex_start[i], exc = a.ex_start[i + 1] - ex0;
     int reg[kMaxRegExcl];
 #pragma unroll
@@ -346,24 +353,39 @@ __global__ void __launch_bounds__(kWaveNL) k_nlist_wave(DirectArgs a) {
                     int wz = (uz % ncs[2] + ncs[2]) % ncs[2];
                     int kz = uz < 0 ? 0 : (uz >= ncs[2] ? 2 : 1);
                     double sz = (kz - 1) * Ls[2];
-                    const int code = kx * 9 + ky * 3 + kz;
+                    // code of the candidate image relative to this lane's image (hits: -1..1)
+                    const int code = (kx - lsh[0]) * 9 + (ky - lsh[1]) * 3 + (kz - lsh[2]);
                     const int cc = (wx * a.nc.y + wy) * a.nc.z + wz;
                     const int t0 = a.cstart[cc], t1 = a.cend[cc];
                     for (int tb = t0; tb < t1; tb += kWaveNL) {
                         const int m = min(kWaveNL, t1 - tb);
                         __syncthreads();
                         if (lane < m) {
+                            // candidate in the block's frame (fp32, |coords| < a few nm)
                             double4 pj = a.pos4s[tb + lane];
-                            cand[lane] = make_double4(pj.x + sx, pj.y + sy, pj.z + sz, 0.0);
+                            cand[lane] = make_float4((float)(pj.x + sx - org.x), (float)(pj.y + sy - org.y),
+                                                     (float)(pj.z + sz - org.z), 0.0f);
                             cand_t[lane] = a.atom_sorted[tb + lane];
                         }
                         __syncthreads();
                         if (active) {
-                            for (int u = 0; u < m; u++) {
-                                double4 pj = cand[u];
-                                double dx = pi.x - pj.x, dy = pi.y - pj.y, dz = pi.z - pj.z;
-                                double r2 = dx * dx + dy * dy + dz * dz;
-                                if (r2 <= a.rc2 && tb + u != s) emit(tb + u, cand_t[u], code);
+                            // fp32 prefilter with a margin; k_pairs applies the exact fp64
+                            // r <= rc test, so borderline extras are harmless
+                            for (int u0 = 0; u0 < m; u0 += 8) {
+                                unsigned bits = 0;
+#pragma unroll
+                                for (int v = 0; v < 8; v++) {
+                                    const float4 c = cand[u0 + v];
+                                    float dx = pf.x - c.x, dy = pf.y - c.y, dz = pf.z - c.z;
+                                    float r2 = fmaf(dx, dx, fmaf(dy, dy, dz * dz));
+                                    bits |= (r2 <= rc2f && u0 + v < m) ? (1u << v) : 0u;
+                                }
+                                if (s >= tb + u0 && s < tb + u0 + 8) bits &= ~(1u << (s - tb - u0));
+                                while (bits) {
+                                    int v = __builtin_ctz(bits);
+                                    bits &= bits - 1;
+                                    emit(tb + u0 + v, cand_t[u0 + v], code);
+                                }
                             }
                         }
                     }
@@ -374,68 +396,47 @@ __global__ void __launch_bounds__(kWaveNL) k_nlist_wave(DirectArgs a) {
     if (active) a.nl_cnt[s] = cnt;
 }
 
-__global__ void __launch_bounds__(256) k_pairs(DirectArgs a) {
-    int s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= a.n) return;
-    int i = a.atom_sorted[s];
-    if (i < a.lo || i >= a.hi) return;
-    const double4 pi = a.pos4s[s];
-    const double2 li = a.ljs[s];
-    const int ex0 = a.ex_start[i], exc = a.ex_start[i + 1] - ex0;
+// 1/sqrt(r2) to full fp64 accuracy: hardware v_rsq_f64 estimate + two Newton steps
+__device__ __forceinline__ double rsqrt_fp64(double r2) {
+    double y = __builtin_amdgcn_rsq(r2);
+    double h = 0.5 * r2;
+    y = y * fma(-h * y, y, 1.5);
+    y = y * fma(-h * y, y, 1.5);
+    return y;
+}
 
-    const double ke = kOne4PiEps0;
-    const double two_over_sqrtpi = 2.0 / sqrt(kPi);
+struct PairAcc {
     double fx = 0, fy = 0, fz = 0, dq = 0, e = 0;
+};
 
-    auto pair = [&](int t, double dx, double dy, double dz, double r2) {
-        const double4 pj = a.pos4s[t];
-        const double2 lj2 = a.ljs[t];
-        double r = sqrt(r2);
-        double inv_r = 1.0 / r, ar = a.alpha * r;
-        double ec = erfc(ar);
-        double sig = li.x + lj2.x;
-        double s2 = inv_r * sig; s2 *= s2;
-        double sig6 = s2 * s2 * s2;
-        double es6 = sig6 * li.y * lj2.y;
-        double qq = ke * pi.w * pj.w * inv_r;
-        if (a.include_forces) {
-            double dEdR = qq * inv_r * inv_r * (ec + ar * exp(-ar * ar) * two_over_sqrtpi);
-            dEdR += es6 * (12 * sig6 - 6) * inv_r * inv_r;
-            fx += dEdR * dx; fy += dEdR * dy; fz += dEdR * dz;
-            dq += ke * pj.w * inv_r * ec;
-        }
-        e += 0.5 * (qq * ec + es6 * (sig6 - 1));
-    };
-
-    const int cnt = a.nl_cnt[s];
-    if (cnt <= a.nb_cap) {
-        for (int k = 0; k < cnt; k++) {
-            int v = a.nl[(size_t)k * a.n + s];
-            int t = v & ((1 << kShiftBits) - 1), code = v >> kShiftBits;
-            double4 pj = a.pos4s[t];
-            double dx, dy, dz;
-            if (code != kBruteShift) {
-                double3 sh = shift_of(code, a.L);
-                dx = pi.x - (pj.x + sh.x); dy = pi.y - (pj.y + sh.y); dz = pi.z - (pj.z + sh.z);
-            } else {
-                double3 d = delta_r(make_double3(pj.x, pj.y, pj.z), make_double3(pi.x, pi.y, pi.z), a.L, 1);
-                dx = d.x; dy = d.y; dz = d.z;
-            }
-            pair(t, dx, dy, dz, dx * dx + dy * dy + dz * dz);
-        }
-    } else {
-        // list overflow (denser than planned): rescan the cells directly
-        int reg[kMaxRegExcl];
-#pragma unroll
-        for (int k = 0; k < kMaxRegExcl; k++) reg[k] = k < exc ? a.ex_list[ex0 + k] : -1;
-        scan_cells(a, s, pi, [&](int t, int, double dx, double dy, double dz, double r2) {
-            if (exc && in_excl(a.atom_sorted[t], reg, exc, a.ex_list, ex0)) return;
-            pair(t, dx, dy, dz, r2);
-        });
+// real-space Ewald + LJ pair (RCK:567-592), d = pos_i - pos_j (minimum image)
+__device__ __forceinline__ void pair_term(PairAcc& acc, const DirectArgs& a, double4 pi, double2 li, double4 pj,
+                                          double2 lj2, double dx, double dy, double dz, double r2) {
+    const double ke = kOne4PiEps0;
+    const double two_over_sqrtpi = 1.1283791670955126;
+    double inv_r = rsqrt_fp64(r2);
+    double r = r2 * inv_r;
+    double ar = a.alpha * r;
+    double ec = erfc(ar);
+    double sig = li.x + lj2.x;
+    double s2 = inv_r * sig; s2 *= s2;
+    double sig6 = s2 * s2 * s2;
+    double es6 = sig6 * li.y * lj2.y;
+    double qq = ke * pi.w * pj.w * inv_r;
+    if (a.include_forces) {
+        double inv_r2 = inv_r * inv_r;
+        double dEdR = qq * inv_r2 * (ec + ar * exp(-ar * ar) * two_over_sqrtpi);
+        dEdR += es6 * (12 * sig6 - 6) * inv_r2;
+        acc.fx += dEdR * dx; acc.fy += dEdR * dy; acc.fz += dEdR * dz;
+        acc.dq += ke * pj.w * inv_r * ec;
     }
+    acc.e += 0.5 * (qq * ec + es6 * (sig6 - 1));
+}
 
-    // exclusion correction: subtract the erf (Gaussian-screened) part for EVERY excluded
-    // pair, no cutoff test, no LJ (RCK:596-622).  d = pos_i - pos_j minimum image.
+// exclusion correction of atom i (RCK:596-622) + finish dE/dq and the non-chain forces
+__device__ __forceinline__ void finish_atom(PairAcc acc, const DirectArgs& a, int i, int ex0, int exc) {
+    const double ke = kOne4PiEps0;
+    const double two_over_sqrtpi = 1.1283791670955126;
     double ex_e = 0;
     if (exc) {
         double3 xi = ld3(a.pos, i);
@@ -449,13 +450,13 @@ __global__ void __launch_bounds__(256) k_pairs(DirectArgs a) {
             double qj = a.q[j];
             if (a.include_forces) {
                 double g = ke * qi * qj * inv_r * inv_r * inv_r * (ef - ar * exp(-ar * ar) * two_over_sqrtpi);
-                fx -= g * d.x; fy -= g * d.y; fz -= g * d.z;
-                dq -= ke * qj * inv_r * ef;
+                acc.fx -= g * d.x; acc.fy -= g * d.y; acc.fz -= g * d.z;
+                acc.dq -= ke * qj * inv_r * ef;
             }
             ex_e -= 0.5 * ke * qi * qj * inv_r * ef;
         }
     }
-    a.e_atom[3 * i + 1] = e;
+    a.e_atom[3 * i + 1] = acc.e;
     a.e_atom[3 * i + 2] = ex_e;
     if (a.include_forces) {
         double dr = 0, rx = 0, ry = 0, rz = 0;
@@ -464,11 +465,63 @@ __global__ void __launch_bounds__(256) k_pairs(DirectArgs a) {
             const double* tp = a.t_part + ((size_t)p * a.nown + io) * 4;
             dr += tp[0]; rx += tp[1]; ry += tp[2]; rz += tp[3];
         }
-        a.dedq[i] = a.dedq_self[i] + dr + dq;
-        a.f_part[3 * i] = rx + fx;
-        a.f_part[3 * i + 1] = ry + fy;
-        a.f_part[3 * i + 2] = rz + fz;
+        a.dedq[i] = a.dedq_self[i] + dr + acc.dq;
+        a.f_part[3 * i] = rx + acc.fx;
+        a.f_part[3 * i + 1] = ry + acc.fy;
+        a.f_part[3 * i + 2] = rz + acc.fz;
     }
+}
+
+// 4b: walk the list (atoms whose list overflowed are left to k_pairs_overflow)
+__global__ void __launch_bounds__(256) k_pairs(DirectArgs a) {
+    int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= a.n) return;
+    int i = a.atom_sorted[s];
+    if (i < a.lo || i >= a.hi) return;
+    const int cnt = a.nl_cnt[s];
+    if (cnt > a.nb_cap) return;
+    const double4 pi = a.pos4s[s];
+    const double2 li = a.ljs[s];
+    PairAcc acc;
+    for (int k = 0; k < cnt; k++) {
+        int v = a.nl[(size_t)k * a.n + s];
+        int t = v & ((1 << kShiftBits) - 1), code = v >> kShiftBits;
+        double4 pj = a.pos4s[t];
+        double2 lj2 = a.ljs[t];
+        double dx, dy, dz;
+        if (code != kBruteShift) {
+            double3 sh = shift_of(code, a.L);
+            dx = pi.x - (pj.x + sh.x); dy = pi.y - (pj.y + sh.y); dz = pi.z - (pj.z + sh.z);
+        } else {
+            double3 d = delta_r(make_double3(pj.x, pj.y, pj.z), make_double3(pi.x, pi.y, pi.z), a.L, 1);
+            dx = d.x; dy = d.y; dz = d.z;
+        }
+        double r2 = dx * dx + dy * dy + dz * dz;
+        if (r2 <= a.rc2) pair_term(acc, a, pi, li, pj, lj2, dx, dy, dz, r2);  // exact voxel-hash test
+    }
+    const int ex0 = a.ex_start[i], exc = a.ex_start[i + 1] - ex0;
+    finish_atom(acc, a, i, ex0, exc);
+}
+
+// 4c: atoms whose neighbour list overflowed (denser than planned): rescan the cells
+__global__ void __launch_bounds__(256) k_pairs_overflow(DirectArgs a) {
+    int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= a.n) return;
+    if (a.nl_cnt[s] <= a.nb_cap) return;
+    int i = a.atom_sorted[s];
+    if (i < a.lo || i >= a.hi) return;
+    const double4 pi = a.pos4s[s];
+    const double2 li = a.ljs[s];
+    const int ex0 = a.ex_start[i], exc = a.ex_start[i + 1] - ex0;
+    int reg[kMaxRegExcl];
+#pragma unroll
+    for (int k = 0; k < kMaxRegExcl; k++) reg[k] = k < exc ? a.ex_list[ex0 + k] : -1;
+    PairAcc acc;
+    scan_cells(a, s, pi, [&](int t, int, double dx, double dy, double dz, double r2) {
+        if (exc && in_excl(a.atom_sorted[t], reg, exc, a.ex_list, ex0)) return;
+        pair_term(acc, a, pi, li, a.pos4s[t], a.ljs[t], dx, dy, dz, r2);
+    });
+    finish_atom(acc, a, i, ex0, exc);
 }
 
 // ---------------------------------------------------------------------------------
@@ -658,6 +711,7 @@ void launch_nlist(Handle& h, const double* pos) {
 void launch_direct(Handle& h, const double* pos, int include_forces) {
     DirectArgs a = direct_args(h, pos, include_forces);
     hipLaunchKernelGGL(k_pairs, dim3(nblk(h.n, 256)), dim3(256), 0, h.stream, a);
+    hipLaunchKernelGGL(k_pairs_overflow, dim3(nblk(h.n, 256)), dim3(256), 0, h.stream, a);
 }
 
 void launch_nopbc(Handle& h, const double* pos, int include_forces, int include_energy) {

@@ -505,6 +505,11 @@ double cfo_execute(cfo_state* s, const double* pos, const double* box9, int incl
     return e;
 }
 
+double cfo_execute_klimit(cfo_state* s, const double* pos, const double* box9, int include_forces,
+                          int include_energy, double* forces, double terms[4], int64_t k_count) {
+    return execute_impl(s, pos, box9, include_forces, include_energy, forces, terms, NULL, k_count, NULL, NULL);
+}
+
 int cfo_time_sample(cfo_state* s, const double* pos, const double* box9, int64_t k_count,
                     double* t_nonrecip, double* t_recip_sample, int64_t* k_total) {
     if (!s->pbc) return -1;

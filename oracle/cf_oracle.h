@@ -34,6 +34,11 @@ double cfo_execute(cfo_state* s, const double* pos, const double* box9, int incl
                    int include_energy, double* forces, double terms[4], double* q_out,
                    double* dedq_out);
 
+/* execute with the reciprocal loop cut after k_count k-vectors (k_count = 0: none) —
+ * used to check the non-reciprocal terms at sizes where the full k-sum is too slow. */
+double cfo_execute_klimit(cfo_state* s, const double* pos, const double* box9, int include_forces,
+                          int include_energy, double* forces, double terms[4], int64_t k_count);
+
 /* CPU-baseline sampling: time the real-space + flux + chain part of one evaluation
  * fully and the reciprocal half-space loop over only its first k_count k-vectors
  * (same per-k work as the reference: 2 passes x cos+sin per atom).  Returns

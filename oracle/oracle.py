@@ -39,6 +39,8 @@ def lib():
         L.cfo_ewald.argtypes = [C.c_void_p, DP, C.POINTER(C.c_int32)]
         L.cfo_execute.restype = C.c_double
         L.cfo_execute.argtypes = [C.c_void_p, DP, DP, C.c_int, C.c_int, DP, DP, DP, DP]
+        L.cfo_execute_klimit.restype = C.c_double
+        L.cfo_execute_klimit.argtypes = [C.c_void_p, DP, DP, C.c_int, C.c_int, DP, DP, C.c_int64]
         L.cfo_time_sample.restype = C.c_int
         L.cfo_time_sample.argtypes = [C.c_void_p, DP, DP, C.c_int64, DP, DP, C.POINTER(C.c_int64)]
         _lib = L
@@ -85,6 +87,15 @@ class Oracle:
         e = lib().cfo_execute(self._h, _dp(pos), _dp(b9), int(include_forces), int(include_energy), _dp(f),
                               _dp(terms), _dp(q), _dp(dedq))
         return {"energy": e, "forces": f, "terms": terms, "charges": q, "dedq": dedq}
+
+    def terms_without_recip(self, pos, box):
+        """Energy terms (self, 0, direct, exclusion) with the reciprocal loop skipped."""
+        pos = np.ascontiguousarray(np.asarray(pos, np.float64).reshape(self.n, 3))
+        b9 = np.ascontiguousarray(np.asarray(box, np.float64).reshape(9))
+        f = np.zeros((self.n, 3))
+        terms = np.zeros(4)
+        lib().cfo_execute_klimit(self._h, _dp(pos), _dp(b9), 0, 1, _dp(f), _dp(terms), 0)
+        return terms
 
     def time_sample(self, pos, box, k_count):
         """CPU-baseline sample: (t_nonrecip, t_recip_for_k_count, k_total)."""

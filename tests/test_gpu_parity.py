@@ -138,7 +138,8 @@ def test_forces_accumulate_and_untouched_without_forces():
 
 
 def test_two_rank_decomposition_on_one_gpu():
-    system, force, pos, box = ts.water_box(1200, cutoff=1.0, ewald_tol=1e-4, every_bond_angle=4)
+    # 2400 waters: 4 cells/dim -> the wave-cooperative neighbour path with unowned blocks
+    system, force, pos, box = ts.water_box(2400, cutoff=1.0, ewald_tol=1e-4, every_bond_angle=4)
     stream = torch.cuda.current_stream().cuda_stream
     pt = torch.tensor(pos, dtype=torch.float64, device="cuda")
     single = HipCalcCoulForceKernel(stream=stream).initialize(system, force)
@@ -161,6 +162,25 @@ def test_two_rank_decomposition_on_one_gpu():
     torch.cuda.synchronize()
     assert (es[0] + es[1]).item() == pytest.approx(e1, rel=1e-11)
     assert np.abs(f.cpu().numpy() - f1).max() < 1e-8
+
+
+def test_wave_neighbour_path_full_parity():
+    # 4000 waters, L = 4.93 nm: 4 cells/dim -> k_nlist_wave (blocks straddling periodic seams)
+    system, force, pos, box = ts.water_box(4000, cutoff=1.0, ewald_tol=1e-3, every_bond_angle=5)
+    k = HipCalcCoulForceKernel().initialize(system, force)
+    _compare(_run(k, pos, box), Oracle(force, box).execute(pos, box))
+
+
+def test_c3_direct_space_terms_vs_oracle():
+    # full C3: self, direct (erfc + LJ) and exclusion energies against the oracle with its
+    # reciprocal loop skipped (the full oracle k-sum would take ~6 minutes)
+    system, force, pos, box = ts.make("C3")
+    k = HipCalcCoulForceKernel().initialize(system, force)
+    k.execute_host(pos, box, False, True)
+    got = k.energy_terms()
+    ref = Oracle(force, box).terms_without_recip(pos, box)
+    for c in (0, 2, 3):
+        assert got[c] == pytest.approx(ref[c], rel=1e-10), (c, got, ref)
 
 
 def test_c3_mfma_matches_direct_path():

@@ -1,23 +1,25 @@
 // fp64 throughput microbenchmark for the roofline denominator (MI355X_MICROARCH.md lists
-// no FP64 matrix rate): v_mfma_f64_16x16x4_f64 and v_fma_f64 on every CU, random data.
+// no FP64 matrix rate): v_mfma_f64_16x16x4_f64 with NACC independent accumulators per
+// wave and v_fma_f64 with 16 chains, at 1/2/4 waves per SIMD, on every CU.
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <vector>
 
 typedef double d4 __attribute__((ext_vector_type(4)));
 
+template <int NACC>
 __global__ void __launch_bounds__(256) mfma_loop(const double* in, double* out, int iters) {
     double a = in[threadIdx.x], b = in[threadIdx.x + 256];
-    d4 acc[8];
+    d4 acc[NACC];
 #pragma unroll
-    for (int k = 0; k < 8; k++) acc[k] = (d4){in[k], in[k + 1], in[k + 2], in[k + 3]};
+    for (int k = 0; k < NACC; k++) acc[k] = (d4){in[k], in[k + 1], in[k + 2], in[k + 3]};
     for (int it = 0; it < iters; it++) {
 #pragma unroll
-        for (int k = 0; k < 8; k++) acc[k] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[k], 0, 0, 0);
+        for (int k = 0; k < NACC; k++) acc[k] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[k], 0, 0, 0);
     }
     double s = 0;
 #pragma unroll
-    for (int k = 0; k < 8; k++) s += acc[k][0] + acc[k][1] + acc[k][2] + acc[k][3];
+    for (int k = 0; k < NACC; k++) s += acc[k][0] + acc[k][1] + acc[k][2] + acc[k][3];
     out[blockIdx.x * 256 + threadIdx.x] = s;
 }
 
@@ -36,39 +38,49 @@ __global__ void __launch_bounds__(256) fma_loop(const double* in, double* out, i
     out[blockIdx.x * 256 + threadIdx.x] = s;
 }
 
+static hipEvent_t ea, eb;
+
+template <int NACC>
+void run_mfma(const double* in, double* out, int ncu, int bpc) {
+    int blocks = ncu * bpc, iters = 160000 / NACC;
+    float ms = 0;
+    for (int rep = 0; rep < 2; rep++) {
+        (void)hipEventRecord(ea);
+        hipLaunchKernelGGL(mfma_loop<NACC>, dim3(blocks), dim3(256), 0, 0, in, out, iters);
+        (void)hipEventRecord(eb);
+        (void)hipEventSynchronize(eb);
+        (void)hipEventElapsedTime(&ms, ea, eb);
+    }
+    double flops = (double)blocks * 4 * iters * NACC * 2048.0;
+    printf("waves/SIMD=%d mfma_f64_16x16x4 acc=%2d: %6.2f TFLOP/s\n", bpc, NACC, flops / ms / 1e9);
+}
+
 int main() {
-    int dev = 0, ncu = 0;
-    hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    int ncu = 0;
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0);
     std::vector<double> h(1024);
     for (int i = 0; i < 1024; i++) h[i] = 0.5 + 1e-3 * ((i * 7919) % 1000) / 1000.0;
     double *in, *out;
-    hipMalloc(&in, 1024 * 8);
-    hipMalloc(&out, (size_t)ncu * 8 * 256 * 8);
-    hipMemcpy(in, h.data(), 1024 * 8, hipMemcpyHostToDevice);
-    hipEvent_t a, b;
-    hipEventCreate(&a); hipEventCreate(&b);
-    for (int bpc = 1; bpc <= 4; bpc *= 2) {  // 4-wave blocks per CU = waves per SIMD
-        int blocks = ncu * bpc;
-        int iters = 20000;
-        float ms;
+    (void)hipMalloc(&in, 1024 * 8);
+    (void)hipMalloc(&out, (size_t)ncu * 8 * 256 * 8);
+    (void)hipMemcpy(in, h.data(), 1024 * 8, hipMemcpyHostToDevice);
+    (void)hipEventCreate(&ea); (void)hipEventCreate(&eb);
+    for (int bpc = 1; bpc <= 4; bpc *= 2) {
+        run_mfma<2>(in, out, ncu, bpc);
+        run_mfma<4>(in, out, ncu, bpc);
+        run_mfma<8>(in, out, ncu, bpc);
+        run_mfma<16>(in, out, ncu, bpc);
+        int blocks = ncu * bpc, iters = 20000;
+        float ms = 0;
         for (int rep = 0; rep < 2; rep++) {
-            hipEventRecord(a);
-            hipLaunchKernelGGL(mfma_loop, dim3(blocks), dim3(256), 0, 0, in, out, iters);
-            hipEventRecord(b);
-            hipEventSynchronize(b);
-            hipEventElapsedTime(&ms, a, b);
-        }
-        double flops = (double)blocks * 4 /*waves*/ * iters * 8 * 2048.0;
-        printf("waves/SIMD=%d mfma_f64_16x16x4 (8 acc): %.2f TFLOP/s\n", bpc, flops / ms / 1e9);
-        for (int rep = 0; rep < 2; rep++) {
-            hipEventRecord(a);
+            (void)hipEventRecord(ea);
             hipLaunchKernelGGL(fma_loop, dim3(blocks), dim3(256), 0, 0, in, out, iters);
-            hipEventRecord(b);
-            hipEventSynchronize(b);
-            hipEventElapsedTime(&ms, a, b);
+            (void)hipEventRecord(eb);
+            (void)hipEventSynchronize(eb);
+            (void)hipEventElapsedTime(&ms, ea, eb);
         }
-        flops = (double)blocks * 256 * iters * 16 * 2.0;
-        printf("waves/SIMD=%d v_fma_f64 (16 chains):     %.2f TFLOP/s\n", bpc, flops / ms / 1e9);
+        double flops = (double)blocks * 256 * iters * 16 * 2.0;
+        printf("waves/SIMD=%d v_fma_f64 16 chains:     %6.2f TFLOP/s\n", bpc, flops / ms / 1e9);
     }
     return 0;
 }
