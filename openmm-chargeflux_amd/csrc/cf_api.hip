@@ -418,9 +418,10 @@ CF_EXPORT int cf_create(const cf_params* p, const cf_options* opt, cf_handle** o
             {
                 double V = p->default_box[0] * p->default_box[4] * p->default_box[8];
                 double mean = 4.0 / 3.0 * M_PI * h.cutoff * h.cutoff * h.cutoff * n / V;
-                h.nb_cap = (int)std::min<double>(n, 1.5 * mean + 64);
-                h.nl = dalloc<int>(H, (size_t)h.nb_cap * n);
-                h.nl_cnt = dalloc<int>(H, n);
+                // kSeg = 4 sub-lists per atom, each sized for a quarter of the neighbours
+                h.nb_cap = (int)std::min<double>(n, 0.5 * mean + 64);
+                h.nl = dalloc<int>(H, (size_t)4 * h.nb_cap * n);
+                h.nl_cnt = dalloc<int>(H, (size_t)4 * n);
             }
             if (h.kspace_algo == 0) {
                 // phase tables: padded rows stay zero forever (memset once)

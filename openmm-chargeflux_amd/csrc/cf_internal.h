@@ -107,9 +107,9 @@ struct Handle {
     double4* pos4s = nullptr;   // [N] sorted wrapped (x,y,z,q)
     double2* ljs = nullptr;     // [N] sorted LJ
     void* sort_tmp = nullptr; size_t sort_tmp_bytes = 0;
-    int nb_cap = 0;             // neighbour-list capacity per atom
-    int* nl = nullptr;          // [nb_cap][N] transposed neighbour list (sorted index | shift<<26)
-    int* nl_cnt = nullptr;      // [N]
+    int nb_cap = 0;             // capacity of each of the 4 neighbour sub-lists of an atom
+    int* nl = nullptr;          // [4][nb_cap][N] transposed sub-lists (sorted index | shift<<26)
+    int* nl_cnt = nullptr;      // [4][N]
     // k-space (MFMA path)
     int npad = 0;               // owned rows of the phase tables, padded to the S-pass tile
     double2* tab_xq = nullptr;  // [Nown][KX]

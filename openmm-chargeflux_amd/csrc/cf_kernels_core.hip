@@ -183,6 +183,7 @@ __global__ void __launch_bounds__(256) k_cell_gather(int n, const int* __restric
 //       exclusion correction, and finishes dE/dq_i and the non-chain forces.
 // ---------------------------------------------------------------------------------
 constexpr int kMaxRegExcl = 8;
+constexpr int kSeg = 4;          // neighbour sub-lists per atom (one per scanning wave / pair lane)
 constexpr int kShiftBits = 26;
 constexpr int kBruteShift = 31;  // shift code: minimum image by floor (brute-force path)
 
@@ -190,7 +191,7 @@ struct DirectArgs {
     int n, lo, hi, include_forces;
     double3 L; int3 nc; int brute;
     double rc2, alpha;
-    int nb_cap;
+    int nb_cap;                 // capacity of ONE of the kSeg sub-lists
     const int* atom_sorted; const int* key_sorted;
     const int* cstart; const int* cend;
     const double4* pos4s; const double2* ljs;
@@ -220,8 +221,10 @@ __device__ __forceinline__ double3 shift_of(int code, double3 L) {
 // Visit the 27 neighbour cells of sorted atom s; fn(t, code, dx, dy, dz, r2) for every
 // candidate t != s within the cutoff (exclusions are left to the caller).
 template <class F>
-__device__ __forceinline__ void scan_cells(const DirectArgs& a, int s, double4 pi, F&& fn) {
+__device__ __forceinline__ void scan_cells(const DirectArgs& a, int s, double4 pi, F&& fn, int part = 0,
+                                           int nparts = 1) {
     if (!a.brute) {
+        int ord = 0;
         int key = a.key_sorted[s];
         int cz = key % a.nc.z, cy = (key / a.nc.z) % a.nc.y, cx = key / (a.nc.y * a.nc.z);
         for (int ox = -1; ox <= 1; ox++) {
@@ -235,6 +238,7 @@ __device__ __forceinline__ void scan_cells(const DirectArgs& a, int s, double4 p
                     if (z < 0) { z += a.nc.z; sz = -a.L.z; kz = 0; } else if (z >= a.nc.z) { z -= a.nc.z; sz = a.L.z; kz = 2; } else kz = 1;
                     int code = kx * 9 + ky * 3 + kz;
                     int c = (x * a.nc.y + y) * a.nc.z + z;
+                    if (ord++ % nparts != part) continue;
                     int t1 = a.cend[c];
                     for (int t = a.cstart[c]; t < t1; t++) {
                         double4 pj = a.pos4s[t];
@@ -247,7 +251,7 @@ __device__ __forceinline__ void scan_cells(const DirectArgs& a, int s, double4 p
             }
         }
     } else {
-        for (int t = 0; t < a.n; t++) {
+        for (int t = part; t < a.n; t += nparts) {
             if (t == s) continue;
             double4 pj = a.pos4s[t];
             double3 d = delta_r(make_double3(pj.x, pj.y, pj.z), make_double3(pi.x, pi.y, pi.z), a.L, 1);
@@ -268,13 +272,15 @@ __global__ void __launch_bounds__(256) k_nlist(DirectArgs a) {
     int reg[kMaxRegExcl];
 #pragma unroll
     for (int k = 0; k < kMaxRegExcl; k++) reg[k] = k < exc ? a.ex_list[ex0 + k] : -1;
-    int cnt = 0;
-    scan_cells(a, s, pi, [&](int t, int code, double, double, double, double) {
-        if (exc && in_excl(a.atom_sorted[t], reg, exc, a.ex_list, ex0)) return;
-        if (cnt < a.nb_cap) a.nl[(size_t)cnt * a.n + s] = t | (code << kShiftBits);
-        cnt++;
-    });
-    a.nl_cnt[s] = cnt;
+    for (int seg = 0; seg < kSeg; seg++) {
+        int cnt = 0;
+        scan_cells(a, s, pi, [&](int t, int code, double, double, double, double) {
+            if (exc && in_excl(a.atom_sorted[t], reg, exc, a.ex_list, ex0)) return;
+            if (cnt < a.nb_cap) a.nl[((size_t)seg * a.nb_cap + cnt) * a.n + s] = t | (code << kShiftBits);
+            cnt++;
+        }, seg, kSeg);
+        a.nl_cnt[(size_t)seg * a.n + s] = cnt;
+    }
 }
 
 // Wave-cooperative list build (the fast path): one 64-lane workgroup owns 64 consecutive
@@ -282,12 +288,23 @@ __global__ void __launch_bounds__(256) k_nlist(DirectArgs a) {
 // unwrapped cell coordinates; candidates of each cell are loaded coalesced (one per lane),
 // shifted to the image adjacent to the block, staged in LDS and tested by every lane with
 // broadcast LDS reads.  Falls back to the per-lane scan when the box would wrap onto itself.
+// Wave-cooperative list build (the fast path): one 64-lane workgroup owns 64 consecutive
+// cell-sorted atoms.  The union of their 27-cell neighbourhoods is a small box of cells in
+// unwrapped cell coordinates.  Each cell's candidates (up to 256 per step) are loaded
+// coalesced, moved to the block frame (fp64 shift, then fp32), staged in LDS and tested by
+// every lane with broadcast reads; the next cell is prefetched into registers meanwhile.
+// The fp32 test uses a margin; k_pairs applies the exact fp64 r <= rc test.  Falls back to
+// the per-lane scan when the box would wrap onto itself.
 constexpr int kWaveNL = 64;
+constexpr int kStage = 4 * kWaveNL;
 
-__global__ void __launch_bounds__(kWaveNL) k_nlist_wave(DirectArgs a) {
-    __shared__ float4 cand[kWaveNL + 8];
-    __shared__ int cand_t[kWaveNL + 8];
-    const int lane = threadIdx.x;
+__global__ void __launch_bounds__(kWaveNL * kSeg) k_nlist_wave(DirectArgs a) {
+    __shared__ float4 cand_all[kSeg][kStage + 8];
+    __shared__ int cand_j_all[kSeg][kStage + 8];
+    const int lane = threadIdx.x & 63;
+    const int seg = threadIdx.x >> 6;   // this wave's share of the cell box and its sub-list
+    float4* cand = cand_all[seg];
+    int* cand_j = cand_j_all[seg];
     const int base = blockIdx.x * kWaveNL;
     const int s = base + lane;
     const bool valid = s < a.n;
@@ -297,10 +314,12 @@ __global__ void __launch_bounds__(kWaveNL) k_nlist_wave(DirectArgs a) {
     if (__ballot(active) == 0) return;  // no owned atom in this block (multi-GPU): skip it whole
     const double4 pi = a.pos4s[ss];
     const int key = a.key_sorted[ss];
-    int c[3] = {key / (a.nc.y * a.nc.z), (key / a.nc.z) % a.nc.y, key % a.nc.z};
+    const size_t seg_off = (size_t)seg * a.nb_cap;
+    const int c[3] = {key / (a.nc.y * a.nc.z), (key / a.nc.z) % a.nc.y, key % a.nc.z};
     const int key0 = a.key_sorted[base];
     const int c0[3] = {key0 / (a.nc.y * a.nc.z), (key0 / a.nc.z) % a.nc.y, key0 % a.nc.z};
     const int ncs[3] = {a.nc.x, a.nc.y, a.nc.z};
+    const double Ls[3] = {a.L.x, a.L.y, a.L.z};
     int lo3[3], hi3[3], lsh[3];
     bool fits = true;
 #pragma unroll
@@ -318,12 +337,6 @@ __global__ void __launch_bounds__(kWaveNL) k_nlist_wave(DirectArgs a) {
         lo3[d] = mn - 1; hi3[d] = mx + 1;
         if (hi3[d] - lo3[d] + 1 > ncs[d]) fits = false;
     }
-    // block frame: every lane's position moved to the image of its unwrapped cell; origin =
-    // lane 0 (lsh = 0 there), so all frame coordinates are within a few cells of 0
-    const double3 pu = make_double3(pi.x + lsh[0] * a.L.x, pi.y + lsh[1] * a.L.y, pi.z + lsh[2] * a.L.z);
-    const double4 org = make_double4(__shfl(pu.x, 0), __shfl(pu.y, 0), __shfl(pu.z, 0), 0.0);
-    const float3 pf = make_float3((float)(pu.x - org.x), (float)(pu.y - org.y), (float)(pu.z - org.z));
-    const float rc2f = (float)(a.rc2 * (1.0 + 1e-5)) + 1e-6f;
     const int ex0 = a.ex_start[i], exc = a.ex_start[i + 1] - ex0;
     int reg[kMaxRegExcl];
 #pragma unroll
@@ -333,67 +346,130 @@ __global__ void __launch_bounds__(kWaveNL) k_nlist_wave(DirectArgs a) {
     int cnt = 0;
     auto emit = [&](int t, int j, int code) {
         if (j >= ex_min && j <= ex_max && in_excl(j, reg, exc, a.ex_list, ex0)) return;
-        if (cnt < a.nb_cap) a.nl[(size_t)cnt * a.n + s] = t | (code << kShiftBits);
+        if (cnt < a.nb_cap) a.nl[(seg_off + cnt) * a.n + s] = t | (code << kShiftBits);
         cnt++;
     };
-    if (!fits) {  // wave-uniform
+    if (!fits) {  // wave-uniform (and block-uniform: every wave sees the same 64 atoms)
         if (active)
-            scan_cells(a, s, pi, [&](int t, int code, double, double, double, double) { emit(t, a.atom_sorted[t], code); });
-    } else {
-        const double Ls[3] = {a.L.x, a.L.y, a.L.z};
-        for (int ux = lo3[0]; ux <= hi3[0]; ux++) {
-            int wx = (ux % ncs[0] + ncs[0]) % ncs[0];
-            int kx = ux < 0 ? 0 : (ux >= ncs[0] ? 2 : 1);
-            double sx = (kx - 1) * Ls[0];
-            for (int uy = lo3[1]; uy <= hi3[1]; uy++) {
-                int wy = (uy % ncs[1] + ncs[1]) % ncs[1];
-                int ky = uy < 0 ? 0 : (uy >= ncs[1] ? 2 : 1);
-                double sy = (ky - 1) * Ls[1];
-                for (int uz = lo3[2]; uz <= hi3[2]; uz++) {
-                    int wz = (uz % ncs[2] + ncs[2]) % ncs[2];
-                    int kz = uz < 0 ? 0 : (uz >= ncs[2] ? 2 : 1);
-                    double sz = (kz - 1) * Ls[2];
-                    // code of the candidate image relative to this lane's image (hits: -1..1)
-                    const int code = (kx - lsh[0]) * 9 + (ky - lsh[1]) * 3 + (kz - lsh[2]);
-                    const int cc = (wx * a.nc.y + wy) * a.nc.z + wz;
-                    const int t0 = a.cstart[cc], t1 = a.cend[cc];
-                    for (int tb = t0; tb < t1; tb += kWaveNL) {
-                        const int m = min(kWaveNL, t1 - tb);
-                        __syncthreads();
-                        if (lane < m) {
-                            // candidate in the block's frame (fp32, |coords| < a few nm)
-                            double4 pj = a.pos4s[tb + lane];
-                            cand[lane] = make_float4((float)(pj.x + sx - org.x), (float)(pj.y + sy - org.y),
-                                                     (float)(pj.z + sz - org.z), 0.0f);
-                            cand_t[lane] = a.atom_sorted[tb + lane];
-                        }
-                        __syncthreads();
-                        if (active) {
-                            // fp32 prefilter with a margin; k_pairs applies the exact fp64
-                            // r <= rc test, so borderline extras are harmless
-                            for (int u0 = 0; u0 < m; u0 += 8) {
-                                unsigned bits = 0;
+            scan_cells(a, s, pi, [&](int t, int code, double, double, double, double) { emit(t, a.atom_sorted[t], code); },
+                       seg, kSeg);
+        if (active) a.nl_cnt[(size_t)seg * a.n + s] = cnt;
+        return;
+    }
+
+    // block frame: every lane's position moved to the image of its unwrapped cell; origin =
+    // lane 0 (lsh = 0 there), so frame coordinates stay within a few cells of 0
+    const double3 pu = make_double3(pi.x + lsh[0] * Ls[0], pi.y + lsh[1] * Ls[1], pi.z + lsh[2] * Ls[2]);
+    const double3 org = make_double3(__shfl(pu.x, 0), __shfl(pu.y, 0), __shfl(pu.z, 0));
+    const float3 pf = make_float3((float)(pu.x - org.x), (float)(pu.y - org.y), (float)(pu.z - org.z));
+    const float rc2f = (float)(a.rc2 * (1.0 + 1e-5)) + 1e-6f;
+
+    const int by = hi3[1] - lo3[1] + 1, bz = hi3[2] - lo3[2] + 1;
+    const int ncell = (hi3[0] - lo3[0] + 1) * by * bz;
+    // cell q of the box -> storage index, image code, frame offset (shift - origin)
+    auto cell_of = [&](int q, int& code, double3& off) {
+        int w[3] = {lo3[0] + q / (by * bz), lo3[1] + (q / bz) % by, lo3[2] + q % bz}, k[3];
 #pragma unroll
-                                for (int v = 0; v < 8; v++) {
-                                    const float4 c = cand[u0 + v];
-                                    float dx = pf.x - c.x, dy = pf.y - c.y, dz = pf.z - c.z;
-                                    float r2 = fmaf(dx, dx, fmaf(dy, dy, dz * dz));
-                                    bits |= (r2 <= rc2f && u0 + v < m) ? (1u << v) : 0u;
-                                }
-                                if (s >= tb + u0 && s < tb + u0 + 8) bits &= ~(1u << (s - tb - u0));
-                                while (bits) {
-                                    int v = __builtin_ctz(bits);
-                                    bits &= bits - 1;
-                                    emit(tb + u0 + v, cand_t[u0 + v], code);
-                                }
-                            }
-                        }
-                    }
-                }
+        for (int d = 0; d < 3; d++) {
+            k[d] = w[d] < 0 ? 0 : (w[d] >= ncs[d] ? 2 : 1);
+            w[d] -= (k[d] - 1) * ncs[d];
+        }
+        code = (k[0] - lsh[0]) * 9 + (k[1] - lsh[1]) * 3 + (k[2] - lsh[2]);  // relative to this lane's image
+        off = make_double3((k[0] - 1) * Ls[0] - org.x, (k[1] - 1) * Ls[1] - org.y, (k[2] - 1) * Ls[2] - org.z);
+        return (w[0] * a.nc.y + w[1]) * a.nc.z + w[2];
+    };
+    double4 rp[4];
+    int rj[4];
+    auto fetch = [&](int t0, int t1) {
+#pragma unroll
+        for (int v = 0; v < 4; v++) {
+            int t = t0 + v * kWaveNL + lane;
+            if (t < t1) { rp[v] = a.pos4s[t]; rj[v] = a.atom_sorted[t]; }
+        }
+    };
+    auto stage = [&](int t0, int t1, double3 off) {
+#pragma unroll
+        for (int v = 0; v < 4; v++) {
+            int u = v * kWaveNL + lane;
+            if (t0 + u < t1) {
+                cand[u] = make_float4((float)(rp[v].x + off.x), (float)(rp[v].y + off.y), (float)(rp[v].z + off.z), 0.f);
+                cand_j[u] = rj[v];
             }
         }
+    };
+    auto test = [&](int t0, int m, int code) {
+        if (!active) return;
+        for (int u0 = 0; u0 < m; u0 += 8) {
+            unsigned bits = 0;
+#pragma unroll
+            for (int v = 0; v < 8; v++) {
+                const float4 cv = cand[u0 + v];
+                float dx = pf.x - cv.x, dy = pf.y - cv.y, dz = pf.z - cv.z;
+                float r2 = fmaf(dx, dx, fmaf(dy, dy, dz * dz));
+                bits |= (r2 <= rc2f && u0 + v < m) ? (1u << v) : 0u;
+            }
+            if (s >= t0 + u0 && s < t0 + u0 + 8) bits &= ~(1u << (s - t0 - u0));
+            while (bits) {
+                int v = __builtin_ctz(bits);
+                bits &= bits - 1;
+                emit(t0 + u0 + v, cand_j[u0 + v], code);
+            }
+        }
+    };
+
+    // every wave visits every cell of the box but takes only its contiguous quarter of the
+    // cell's atoms, so the kSeg sub-lists of an atom are statistically balanced.
+    // (LDS regions are per wave: wave barriers only.)
+    auto quarter = [&](int cc_, int& t0_, int& t1_) {
+        int b = a.cstart[cc_], e = a.cend[cc_];
+        int qs = (e - b + kSeg - 1) / kSeg;
+        t0_ = min(e, b + seg * qs);
+        t1_ = min(e, t0_ + qs);
+    };
+    int code_n; double3 off_n;
+    int cc = cell_of(0, code_n, off_n);
+    int t0_n, end_n;
+    quarter(cc, t0_n, end_n);
+    int t1_n = min(end_n, t0_n + kStage);
+    fetch(t0_n, t1_n);
+    for (int q = 0; q < ncell; q++) {
+        const int code = code_n, t0 = t0_n, t1 = t1_n, cend = end_n;
+        const double3 off = off_n;
+        __builtin_amdgcn_wave_barrier();
+        stage(t0, t1, off);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (q + 1 < ncell) {  // prefetch the next cell while this one is tested
+            cc = cell_of(q + 1, code_n, off_n);
+            quarter(cc, t0_n, end_n);
+            t1_n = min(end_n, t0_n + kStage);
+            fetch(t0_n, t1_n);
+        }
+        test(t0, t1 - t0, code);
+        // rare: a quarter cell with more than kStage atoms (synchronous remainder)
+        for (int tb = t0 + kStage; tb < cend; tb += kStage) {
+            const int te = min(cend, tb + kStage);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+#pragma unroll
+            for (int v = 0; v < 4; v++) {
+                int t = tb + v * kWaveNL + lane;
+                if (t < te) {
+                    double4 pj = a.pos4s[t];
+                    cand[v * kWaveNL + lane] = make_float4((float)(pj.x + off.x), (float)(pj.y + off.y),
+                                                           (float)(pj.z + off.z), 0.f);
+                    cand_j[v * kWaveNL + lane] = a.atom_sorted[t];
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            test(tb, te - tb, code);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     }
-    if (active) a.nl_cnt[s] = cnt;
+    if (active) a.nl_cnt[(size_t)seg * a.n + s] = cnt;
 }
 
 // 1/sqrt(r2) to full fp64 accuracy: hardware v_rsq_f64 estimate + two Newton steps
@@ -472,33 +548,49 @@ __device__ __forceinline__ void finish_atom(PairAcc acc, const DirectArgs& a, in
     }
 }
 
-// 4b: walk the list (atoms whose list overflowed are left to k_pairs_overflow)
+// 4b: walk the list — kSeg adjacent lanes per atom, lane g walks sub-list g; partial sums
+// are combined with two xor-shuffles (fixed order: deterministic).  Atoms with an
+// overflowed sub-list are left to k_pairs_overflow.
 __global__ void __launch_bounds__(256) k_pairs(DirectArgs a) {
-    int s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= a.n) return;
-    int i = a.atom_sorted[s];
-    if (i < a.lo || i >= a.hi) return;
-    const int cnt = a.nl_cnt[s];
-    if (cnt > a.nb_cap) return;
-    const double4 pi = a.pos4s[s];
-    const double2 li = a.ljs[s];
+    const int gt = blockIdx.x * blockDim.x + threadIdx.x;
+    const int s = gt / kSeg, g = gt % kSeg;
+    const bool valid = s < a.n;
+    const int ss = valid ? s : a.n - 1;
+    const int i = a.atom_sorted[ss];
+    bool active = valid && i >= a.lo && i < a.hi;
+    int cnt = active ? a.nl_cnt[(size_t)g * a.n + ss] : 0;
+    bool over = cnt > a.nb_cap;
+    over = __shfl_xor(over, 1) || over;
+    over = __shfl_xor(over, 2) || over;
+    if (over) active = false;
     PairAcc acc;
-    for (int k = 0; k < cnt; k++) {
-        int v = a.nl[(size_t)k * a.n + s];
-        int t = v & ((1 << kShiftBits) - 1), code = v >> kShiftBits;
-        double4 pj = a.pos4s[t];
-        double2 lj2 = a.ljs[t];
-        double dx, dy, dz;
-        if (code != kBruteShift) {
-            double3 sh = shift_of(code, a.L);
-            dx = pi.x - (pj.x + sh.x); dy = pi.y - (pj.y + sh.y); dz = pi.z - (pj.z + sh.z);
-        } else {
-            double3 d = delta_r(make_double3(pj.x, pj.y, pj.z), make_double3(pi.x, pi.y, pi.z), a.L, 1);
-            dx = d.x; dy = d.y; dz = d.z;
+    if (active) {
+        const double4 pi = a.pos4s[ss];
+        const double2 li = a.ljs[ss];
+        const int* nl = a.nl + (size_t)g * a.nb_cap * a.n + ss;
+        for (int k = 0; k < cnt; k++) {
+            int v = nl[(size_t)k * a.n];
+            int t = v & ((1 << kShiftBits) - 1), code = v >> kShiftBits;
+            double4 pj = a.pos4s[t];
+            double2 lj2 = a.ljs[t];
+            double dx, dy, dz;
+            if (code != kBruteShift) {
+                double3 sh = shift_of(code, a.L);
+                dx = pi.x - (pj.x + sh.x); dy = pi.y - (pj.y + sh.y); dz = pi.z - (pj.z + sh.z);
+            } else {
+                double3 d = delta_r(make_double3(pj.x, pj.y, pj.z), make_double3(pi.x, pi.y, pi.z), a.L, 1);
+                dx = d.x; dy = d.y; dz = d.z;
+            }
+            double r2 = dx * dx + dy * dy + dz * dz;
+            if (r2 <= a.rc2) pair_term(acc, a, pi, li, pj, lj2, dx, dy, dz, r2);  // exact voxel-hash test
         }
-        double r2 = dx * dx + dy * dy + dz * dz;
-        if (r2 <= a.rc2) pair_term(acc, a, pi, li, pj, lj2, dx, dy, dz, r2);  // exact voxel-hash test
     }
+#pragma unroll
+    for (int m = 1; m < kSeg; m <<= 1) {
+        acc.fx += __shfl_xor(acc.fx, m); acc.fy += __shfl_xor(acc.fy, m); acc.fz += __shfl_xor(acc.fz, m);
+        acc.dq += __shfl_xor(acc.dq, m); acc.e += __shfl_xor(acc.e, m);
+    }
+    if (!active || g != 0) return;
     const int ex0 = a.ex_start[i], exc = a.ex_start[i + 1] - ex0;
     finish_atom(acc, a, i, ex0, exc);
 }
@@ -507,7 +599,9 @@ __global__ void __launch_bounds__(256) k_pairs(DirectArgs a) {
 __global__ void __launch_bounds__(256) k_pairs_overflow(DirectArgs a) {
     int s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= a.n) return;
-    if (a.nl_cnt[s] <= a.nb_cap) return;
+    bool over = false;
+    for (int g = 0; g < kSeg; g++) over = over || a.nl_cnt[(size_t)g * a.n + s] > a.nb_cap;
+    if (!over) return;
     int i = a.atom_sorted[s];
     if (i < a.lo || i >= a.hi) return;
     const double4 pi = a.pos4s[s];
@@ -705,12 +799,12 @@ void launch_nlist(Handle& h, const double* pos) {
     if (a.brute || h.nc[0] < 4 || h.nc[1] < 4 || h.nc[2] < 4)
         hipLaunchKernelGGL(k_nlist, dim3(nblk(h.n, 256)), dim3(256), 0, h.stream, a);
     else
-        hipLaunchKernelGGL(k_nlist_wave, dim3(nblk(h.n, kWaveNL)), dim3(kWaveNL), 0, h.stream, a);
+        hipLaunchKernelGGL(k_nlist_wave, dim3(nblk(h.n, kWaveNL)), dim3(kWaveNL * kSeg), 0, h.stream, a);
 }
 
 void launch_direct(Handle& h, const double* pos, int include_forces) {
     DirectArgs a = direct_args(h, pos, include_forces);
-    hipLaunchKernelGGL(k_pairs, dim3(nblk(h.n, 256)), dim3(256), 0, h.stream, a);
+    hipLaunchKernelGGL(k_pairs, dim3(nblk((int64_t)h.n * kSeg, 256)), dim3(256), 0, h.stream, a);
     hipLaunchKernelGGL(k_pairs_overflow, dim3(nblk(h.n, 256)), dim3(256), 0, h.stream, a);
 }
 
