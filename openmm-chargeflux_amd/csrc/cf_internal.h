@@ -26,13 +26,14 @@ struct KGeom {
     int NY = 0;    // 2KY-1
     int NYB = 0;   // ceil(NY/16)  (S-pass combo groups per nx)
     int NYP = 0;   // 16*NYB
-    int NYB4 = 0;  // ceil(NY/4)   (force-pass m-tiles per nx)
+    int NYB4 = 0;  // ceil(NY/4)
+    int NMT = 0;   // force-pass m-tiles: ceil(KX*NY/4), combos flattened (no per-row padding)
     int NZP = 0;   // 2KZ rounded up to 16
     int NB = 0;    // column blocks of <= 64 (CS table blocks, S-pass n-blocks, force K-chunks)
     int CSW = 0;   // CS table block width: min(64, NZP)
     __host__ __device__ int nslots() const { return KX * NYP; }
     __host__ __device__ int ngroups() const { return KX * NYB; }
-    __host__ __device__ int nmtiles() const { return KX * NYB4; }
+    __host__ __device__ int nmtiles() const { return NMT; }
     __host__ __device__ int nksteps() const { return NZP / 4; }
     __host__ __device__ int64_t k_half() const {
         return (int64_t)(KZ - 1) + (int64_t)(KY - 1) * (2 * KZ - 1) +

@@ -290,8 +290,9 @@ __global__ void __launch_bounds__(256) k_coeffs(KGeom g, double3 rec, double cst
         double Qr = -Di, Qi = Dr;                 // Q  = i D
         double Pzr = nz * Dr, Pzi = nz * Di;      // Pz = nz D
         double Qzr = -nz * Pi, Qzi = nz * Pr;     // Qz = i nz P
-        // A fragment: m-tile mt = nx*NYB4 + iy/4, row = (iy%4) + 4*part, k = j
-        int mt = nx * g.NYB4 + iy / 4, qrow = iy % 4;
+        // A fragment: combos flattened c = nx*NY + iy, m-tile mt = c/4, row = (c%4) + 4*part, k = j
+        int cflat = nx * g.NY + iy;
+        int mt = cflat / 4, qrow = cflat % 4;
         int KS = g.nksteps();
         double vc[4] = {Pr, Pi, Pzr, Pzi}, vs[4] = {Qr, Qi, Qzr, Qzi};
 #pragma unroll
@@ -413,8 +414,11 @@ __global__ void __launch_bounds__(kFThreads) k_force(FArgs a) {
         for (int mloc = 0; mloc < kFMB; mloc++) {
             const int mt = m_lo + st * kFMB + mloc;
             if (mt >= m_hi) break;
-            const int nx = mt / g.NYB4, b4 = mt % g.NYB4;
-            const int ny = 4 * b4 + qg - (g.KY - 1);
+            // this lane-group's combo (flattened): c = 4 mt + qg -> (nx, ny); padding combos
+            // past KX*NY have zero coefficients
+            const int cfl = 4 * mt + qg;
+            const int nx = cfl / g.NY;
+            const int ny = cfl - nx * g.NY - (g.KY - 1);
             const double* A = &alds[buf][mloc * 16 * 64];
             d4 acc[NA];
 #pragma unroll
@@ -427,8 +431,8 @@ __global__ void __launch_bounds__(kFThreads) k_force(FArgs a) {
                     for (int at = 0; at < NA; at++) acc[at] = mfma64(av, b[at][t], acc[at]);
                 }
             }
-            // phase w = e^{i(nx gx x + ny gy y)}: direct at the start of an nx row, then
-            // advanced by e^{i 4 gy y} per m-tile.
+            // phase w = e^{i(nx gx x + ny gy y)}: direct when this lane's nx row changes
+            // (divergent only across the 16-lane combo groups), else advanced by e^{i 4 gy y}.
             if (nx != cur_nx) {
 #pragma unroll
                 for (int at = 0; at < NA; at++) {
@@ -488,6 +492,7 @@ void kspace_plan(Handle& h) {
     g.NYB = (g.NY + 15) / 16;
     g.NYP = 16 * g.NYB;
     g.NYB4 = (g.NY + 3) / 4;
+    g.NMT = (g.KX * g.NY + 3) / 4;
     g.NZP = ((2 * g.KZ + 15) / 16) * 16;
     g.NB = (g.NZP + 63) / 64;
     g.CSW = std::min(64, g.NZP);
