@@ -61,6 +61,9 @@ int guarded(F&& f) {
     } catch (const CfError& e) {
         g_err = e.what();
         return e.code;
+    } catch (const std::invalid_argument& e) {
+        g_err = e.what();
+        return CF_ERR_INVALID;
     } catch (const std::bad_alloc&) {
         g_err = "host allocation failed";
         return CF_ERR_NOMEM;

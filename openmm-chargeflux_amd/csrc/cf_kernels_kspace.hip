@@ -18,12 +18,16 @@
 // (complex products, phase recurrences) beside the matrix pipe.
 #include <algorithm>
 #include <cmath>
+#include <stdexcept>
 
 #include "cf_internal.h"
 
 namespace cf {
 
 typedef double d4 __attribute__((ext_vector_type(4)));
+// native 2-vector for staging registers (HIP's double2 struct copies lower to memcpy
+// through a private alloca, i.e. scratch memory, when the source address is a select)
+typedef double v2d __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ d4 mfma64(double a, double b, d4 c) {
     return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
@@ -94,17 +98,20 @@ __host__ __device__ inline int cs_lds_stride(int csw) {
 
 struct SArgs {
     KGeom g;
-    int nown, npad, chunk_atoms, tile_atoms, wg_groups;
+    int nown, npad, chunk_atoms, wg_groups, nbk0;
     const double* cs; const double2* ty; const double2* xq;
     double* slab;
 };
 
+// NT column tiles (16 columns each) of column block nbk0 + blockIdx.x / wg_groups; TA
+// atoms per LDS tile.  Both compile-time so the k-step loop is straight-line code and
+// the scheduler can issue the next k-step's LDS operands under the current MFMAs.
+template <int NT, int TA>
 __global__ void __launch_bounds__(kSThreads) k_sfac(SArgs a) {
     extern __shared__ __attribute__((aligned(16))) double lds[];
     const KGeom g = a.g;
-    const int TA = a.tile_atoms;
     const int wgx = blockIdx.x % a.wg_groups;
-    const int nbk = blockIdx.x / a.wg_groups;
+    const int nbk = a.nbk0 + blockIdx.x / a.wg_groups;
     const int chunk = blockIdx.y;
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
@@ -113,7 +120,6 @@ __global__ void __launch_bounds__(kSThreads) k_sfac(SArgs a) {
     const int ngroups = g.ngroups();
     const int g0 = wgx * 16;
     const int col0 = nbk * 64;
-    const int NTv = min(4, (g.NZP - col0) / 16);
     const int a_begin = chunk * a.chunk_atoms;                 // owned index, multiple of TA
     const int a_end = min(a.nown, a_begin + a.chunk_atoms);
     if (a_begin >= a_end) return;  // whole workgroup uniform
@@ -127,84 +133,93 @@ __global__ void __launch_bounds__(kSThreads) k_sfac(SArgs a) {
     const int half = g.CSW / 2;
     const int ncs2 = TA * half, ny2 = TA * g.NYP, nxq2 = TA * g.KX;
 
-    auto stage_load = [&](int tile_a0, double2 (&reg)[kSMaxV]) {
-        const double2* csb = reinterpret_cast<const double2*>(a.cs + ((size_t)nbk * a.npad + tile_a0) * g.CSW);
-        const double2* yb = a.ty + (size_t)tile_a0 * g.NYP;
-        const double2* xb = a.xq + (size_t)tile_a0 * g.KX;
-#pragma unroll
-        for (int v = 0; v < kSMaxV; v++) {
-            int e = threadIdx.x + v * kSThreads;
-            double2 val = make_double2(0, 0);
-            if (e < ncs2) val = csb[e];
-            else if (e < ncs2 + ny2) val = yb[e - ncs2];
-            else if (e < ncs2 + ny2 + nxq2) val = xb[e - ncs2 - ny2];
-            reg[v] = val;
-        }
-    };
-    auto stage_store = [&](int buf, const double2 (&reg)[kSMaxV]) {
-        double* base = lds + buf * buf_d;
-#pragma unroll
-        for (int v = 0; v < kSMaxV; v++) {
-            int e = threadIdx.x + v * kSThreads;
-            int dst;
-            if (e < ncs2) { int at = e / half; dst = at * csl + 2 * (e - at * half); }
-            else if (e < ncs2 + ny2 + nxq2) dst = cs_d + 2 * (e - ncs2);
-            else continue;
-            *reinterpret_cast<double2*>(base + dst) = reg[v];
-        }
-    };
+    const int n_el = ncs2 + ny2 + nxq2;
+    // branch-free staging: every lane loads a valid address (elements past the tile
+    // re-read the last XQ entry and are never stored), so the loads issue back to back
+#define CF_STAGE_LOAD(tile_a0, h)                                                                           \
+    {                                                                                                       \
+        const double2* csb = reinterpret_cast<const double2*>(a.cs + ((size_t)nbk * a.npad + (tile_a0)) * g.CSW); \
+        const double2* yb = a.ty + (size_t)(tile_a0) * g.NYP;                                               \
+        const double2* xb = a.xq + (size_t)(tile_a0) * g.KX;                                                \
+        _Pragma("unroll") for (int u = 0; u < kSMaxV / 2; u++) {                                            \
+            int e = threadIdx.x + ((h) * (kSMaxV / 2) + u) * kSThreads;                                     \
+            const double2* src = e < ncs2 ? csb + e                                                         \
+                               : (e < ncs2 + ny2 ? yb + (e - ncs2) : xb + min(e - ncs2 - ny2, nxq2 - 1));   \
+            reg[u] = *reinterpret_cast<const v2d*>(src);                                                    \
+        }                                                                                                   \
+    }
+#define CF_STAGE_STORE(buf, h)                                                                              \
+    {                                                                                                       \
+        double* base = lds + (buf) * buf_d;                                                                 \
+        _Pragma("unroll") for (int u = 0; u < kSMaxV / 2; u++) {                                            \
+            int e = threadIdx.x + ((h) * (kSMaxV / 2) + u) * kSThreads;                                     \
+            int at = e / half;                                                                              \
+            int dst = e < ncs2 ? at * csl + 2 * (e - at * half) : cs_d + 2 * (e - ncs2);                    \
+            if (e < n_el) *reinterpret_cast<v2d*>(base + dst) = reg[u];                                     \
+        }                                                                                                   \
+    }
 
-    // wave's combo groups
-    int gq[2]; bool gv[2]; int gnx[2], giy[2];
+    // wave's combo groups; a group past ngroups reads row 0 and contributes zero weight
+    int gq[2], gnx[2], giy[2];
+    double gm[2];
 #pragma unroll
     for (int gi = 0; gi < 2; gi++) {
         gq[gi] = g0 + 2 * wave + gi;
-        gv[gi] = gq[gi] < ngroups;
-        gnx[gi] = gv[gi] ? gq[gi] / g.NYB : 0;
-        giy[gi] = gv[gi] ? (gq[gi] % g.NYB) * 16 + r : 0;
+        bool v = gq[gi] < ngroups;
+        gm[gi] = v ? 1.0 : 0.0;
+        gnx[gi] = v ? gq[gi] / g.NYB : 0;
+        giy[gi] = v ? (gq[gi] % g.NYB) * 16 + r : 0;
     }
 
-    d4 acc[2][2][4];
+    d4 acc[2][2][NT];
 #pragma unroll
     for (int gi = 0; gi < 2; gi++)
 #pragma unroll
         for (int p = 0; p < 2; p++)
 #pragma unroll
-            for (int nt = 0; nt < 4; nt++) acc[gi][p][nt] = (d4){0, 0, 0, 0};
+            for (int nt = 0; nt < NT; nt++) acc[gi][p][nt] = (d4){0, 0, 0, 0};
 
     const int ntiles = (a_end - a_begin + TA - 1) / TA;
-    double2 reg[kSMaxV];
-    stage_load(a_begin, reg);
-    stage_store(0, reg);
+    // staging of the next tile runs in two halves, each loaded before and stored after
+    // half of the current tile's k-steps (16 staging VGPRs instead of 32)
+    v2d reg[kSMaxV / 2];
+    CF_STAGE_LOAD(a_begin, 0);
+    CF_STAGE_STORE(0, 0);
+    CF_STAGE_LOAD(a_begin, 1);
+    CF_STAGE_STORE(0, 1);
     __syncthreads();
+    constexpr int KSTEPS = TA / 4;
     for (int tt = 0; tt < ntiles; tt++) {
         const int buf = tt & 1;
-        if (tt + 1 < ntiles) stage_load(a_begin + (tt + 1) * TA, reg);
+        const bool more = tt + 1 < ntiles;
+        const int next_a0 = a_begin + (tt + 1) * TA;
         const double* cs_l = lds + buf * buf_d;
         const double2* y_l = reinterpret_cast<const double2*>(cs_l + cs_d);
         const double2* xq_l = reinterpret_cast<const double2*>(cs_l + cs_d + y_d);
-        for (int t = 0; t < TA / 4; t++) {
-            const int at = 4 * t + kq;
-            double b[4];
 #pragma unroll
-            for (int nt = 0; nt < 4; nt++) b[nt] = nt < NTv ? cs_l[at * csl + nt * 16 + r] : 0.0;
+        for (int h = 0; h < 2; h++) {
+            if (more) CF_STAGE_LOAD(next_a0, h);
 #pragma unroll
-            for (int gi = 0; gi < 2; gi++) {
-                if (!gv[gi]) continue;
-                double2 x = xq_l[at * g.KX + gnx[gi]];
-                double2 y = y_l[at * g.NYP + giy[gi]];
-                double wr = x.x * y.x - x.y * y.y;
-                double wi = x.x * y.y + x.y * y.x;
+            for (int t = h * (KSTEPS / 2); t < (h ? KSTEPS : KSTEPS / 2); t++) {
+                const int at = 4 * t + kq;
+                double b[NT];
 #pragma unroll
-                for (int nt = 0; nt < 4; nt++) {
-                    if (nt < NTv) {
+                for (int nt = 0; nt < NT; nt++) b[nt] = cs_l[at * csl + nt * 16 + r];
+#pragma unroll
+                for (int gi = 0; gi < 2; gi++) {
+                    double2 x = xq_l[at * g.KX + gnx[gi]];
+                    double2 y = y_l[at * g.NYP + giy[gi]];
+                    double wr = (x.x * y.x - x.y * y.y) * gm[gi];
+                    double wi = (x.x * y.y + x.y * y.x) * gm[gi];
+#pragma unroll
+                    for (int nt = 0; nt < NT; nt++) {
                         acc[gi][0][nt] = mfma64(wr, b[nt], acc[gi][0][nt]);
                         acc[gi][1][nt] = mfma64(wi, b[nt], acc[gi][1][nt]);
                     }
                 }
             }
+            if (more) CF_STAGE_STORE(buf ^ 1, h);
         }
-        if (tt + 1 < ntiles) stage_store(buf ^ 1, reg);
         __syncthreads();
     }
 
@@ -212,12 +227,11 @@ __global__ void __launch_bounds__(kSThreads) k_sfac(SArgs a) {
     const int nslots = g.nslots();
 #pragma unroll
     for (int gi = 0; gi < 2; gi++) {
-        if (!gv[gi]) continue;
+        if (gq[gi] >= ngroups) continue;
 #pragma unroll
         for (int p = 0; p < 2; p++)
 #pragma unroll
-            for (int nt = 0; nt < 4; nt++) {
-                if (nt >= NTv) continue;
+            for (int nt = 0; nt < NT; nt++) {
 #pragma unroll
                 for (int v = 0; v < 4; v++) {
                     int row = kq + 4 * v;
@@ -228,6 +242,9 @@ __global__ void __launch_bounds__(kSThreads) k_sfac(SArgs a) {
             }
     }
 }
+
+#undef CF_STAGE_LOAD
+#undef CF_STAGE_STORE
 
 __global__ void __launch_bounds__(256) k_sfac_reduce(int64_t count, int nchunks, const double* __restrict__ slab,
                                                      double* __restrict__ out) {
@@ -243,6 +260,12 @@ __global__ void __launch_bounds__(256) k_sfac_reduce(int64_t count, int nchunks,
 // weights w = 2*c*exp(-k^2/4a^2)/k^2 (RCK:517,528), the energy c*eak*|S|^2
 // (RCK:549-551) and the force-pass MFMA A-fragments (P, Q, Pz, Qz).
 // ---------------------------------------------------------------------------------
+// coefficient element (m-tile mt, k-step ks, A-lane l) in the k_coeffs output
+__host__ __device__ inline size_t coef_index(int mt, int ks, int l, int KS) {
+    // k-step pair p = ks/2 of m-tile mt is the 64-lane double2 block (mt*KS/2 + p)
+    return (((size_t)mt * KS + (ks & ~1)) * 32 + l) * 2 + (ks & 1);
+}
+
 __device__ __forceinline__ bool in_half_space(int nx, int ny, int nz) {
     // RCK:519-556: nx=0 -> ny>=0, and ny=0 -> nz>=1
     if (nx > 0) return true;
@@ -291,6 +314,7 @@ __global__ void __launch_bounds__(256) k_coeffs(KGeom g, double3 rec, double cst
         double Pzr = nz * Dr, Pzi = nz * Di;      // Pz = nz D
         double Qzr = -nz * Pi, Qzi = nz * Pr;     // Qz = i nz P
         // A fragment: combos flattened c = nx*NY + iy, m-tile mt = c/4, row = (c%4) + 4*part, k = j
+        // (k-step pairs interleaved per lane, coef_index)
         int cflat = nx * g.NY + iy;
         int mt = cflat / 4, qrow = cflat % 4;
         int KS = g.nksteps();
@@ -299,8 +323,8 @@ __global__ void __launch_bounds__(256) k_coeffs(KGeom g, double3 rec, double cst
         for (int part = 0; part < 4; part++) {
             int row = qrow + 4 * part;
             int jc = 2 * nz, js = 2 * nz + 1;
-            coef[((size_t)mt * KS + jc / 4) * 64 + (jc % 4) * 16 + row] = vc[part];
-            coef[((size_t)mt * KS + js / 4) * 64 + (js % 4) * 16 + row] = vs[part];
+            coef[coef_index(mt, jc / 4, (jc % 4) * 16 + row, KS)] = vc[part];
+            coef[coef_index(mt, js / 4, (js % 4) * 16 + row, KS)] = vs[part];
         }
     }
     red[threadIdx.x] = e;
@@ -317,13 +341,18 @@ __global__ void __launch_bounds__(256) k_coeffs(KGeom g, double3 rec, double cst
 // Ta = Im sum S^ n_a e^{ik.r} (-> F_a = q g_a Ta), RCK:538-547.
 //   workgroup = 8 waves; wave owns NA 16-atom tiles; B operand (CS columns of its
 //   atoms) lives in registers for the whole kernel; the A operand (coefficients) is
-//   streamed per m-tile through an LDS double buffer shared by the 8 waves.
-//   Accumulator lane (qg, atom) receives the 4 parts (U0r,U0i,Uzr,Uzi) of combo
-//   (nx, 4*b4+qg) -> epilogue multiplies by X Y in registers.
+//   streamed through an LDS double buffer shared by the 8 waves (kFMB m-tiles per
+//   stage), and each wave prefetches the next m-tile's A fragments into registers
+//   while the MFMAs of the current one run (no LDS latency on the MFMA chain).
+//   Coefficients hold k-step pairs interleaved per lane -> one ds_read_b128 feeds
+//   two k-steps.  Accumulator lane (qg, atom) receives the 4 parts (U0r,U0i,Uzr,Uzi)
+//   of combo 4*mt+qg -> epilogue multiplies by X Y in registers.
 // ---------------------------------------------------------------------------------
 constexpr int kFWaves = 8;
 constexpr int kFThreads = kFWaves * 64;
-constexpr int kFMB = 2;  // m-tiles per LDS stage
+constexpr int kFMB = 4;                   // m-tiles per LDS stage (must be even)
+constexpr int kFStageD2 = kFMB * 8 * 64;  // double2 per stage
+constexpr int kFStageV = kFStageD2 / kFThreads;
 
 struct FArgs {
     KGeom g;
@@ -335,17 +364,16 @@ struct FArgs {
 
 template <int NA>
 __global__ void __launch_bounds__(kFThreads) k_force(FArgs a) {
-    __shared__ __attribute__((aligned(16))) double alds[2][kFMB * 16 * 64];
+    __shared__ __attribute__((aligned(16))) double2 alds[2][kFStageD2];
     const KGeom g = a.g;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int col = lane & 15, qg = lane >> 4;
     const int kc = blockIdx.y / a.msplit, ms = blockIdx.y % a.msplit;
     const int KS = g.nksteps();
     const int ks0 = kc * 16;
-    const int NKS = min(16, KS - ks0);
+    const int NKS = min(16, KS - ks0);    // k-steps past NKS carry zero A and B
     const int M = g.nmtiles();
     const int m_lo = (int)((int64_t)M * ms / a.msplit), m_hi = (int)((int64_t)M * (ms + 1) / a.msplit);
-    const int nparts = gridDim.y;
     const int part = blockIdx.y;
 
     // atoms and B operand
@@ -377,88 +405,96 @@ __global__ void __launch_bounds__(kFThreads) k_force(FArgs a) {
         wr[at] = wi[at] = 0;
     }
 
-    // LDS staging of coefficient m-tiles: stage = kFMB m-tiles x 16 ksteps x 64 doubles
-    auto load_stage = [&](int m0, double2 (&reg)[2]) {
+    // stage = kFMB m-tiles x 8 k-step pairs x 64 lanes (double2), a linear copy of 8 KB
+    // per m-tile; k-step pairs past NKS and m-tiles past m_hi are zero-filled.
+    auto load_stage = [&](int m0, double2 (&reg)[kFStageV]) {
 #pragma unroll
-        for (int v = 0; v < 2; v++) {
-            int e = threadIdx.x + v * kFThreads;    // double2 index within stage (0..1023)
-            int mloc = e / (16 * 32), rem = e % (16 * 32);
-            int t = rem / 32, l2 = rem % 32;
+        for (int v = 0; v < kFStageV; v++) {
+            int e = threadIdx.x + v * kFThreads;
+            int mloc = e >> 9, rem = e & 511;  // rem = tp*64 + lane
             int mt = m0 + mloc;
-            double2 val = make_double2(0, 0);
-            if (mt < m_hi && t < NKS)
-                val = *reinterpret_cast<const double2*>(a.coef + ((size_t)mt * KS + ks0 + t) * 64 + 2 * l2);
-            reg[v] = val;
+            bool ok = mt < m_hi && 2 * (rem >> 6) < NKS;
+            // unconditional load from a clamped address, then select (no branch per load)
+            double2 val = reinterpret_cast<const double2*>(a.coef)[ok ? ((size_t)mt * KS + ks0) * 32 + rem : 0];
+            reg[v] = ok ? val : make_double2(0, 0);
         }
     };
-    auto store_stage = [&](int buf, const double2 (&reg)[2]) {
+    auto store_stage = [&](int buf, const double2 (&reg)[kFStageV]) {
 #pragma unroll
-        for (int v = 0; v < 2; v++) {
-            int e = threadIdx.x + v * kFThreads;
-            reinterpret_cast<double2*>(&alds[buf][0])[e] = reg[v];
+        for (int v = 0; v < kFStageV; v++) alds[buf][threadIdx.x + v * kFThreads] = reg[v];
+    };
+    auto read_a = [&](int buf, int mloc, double2 (&av)[8]) {
+#pragma unroll
+        for (int tp = 0; tp < 8; tp++) av[tp] = alds[buf][mloc * 512 + tp * 64 + lane];
+    };
+
+    int cur_nx = -1;
+    auto mtile = [&](int mt, const double2 (&av)[8]) {
+        if (mt >= m_hi) return;  // wave-uniform
+        d4 acc[NA];
+#pragma unroll
+        for (int at = 0; at < NA; at++) acc[at] = (d4){0, 0, 0, 0};
+#pragma unroll
+        for (int tp = 0; tp < 8; tp++) {
+#pragma unroll
+            for (int at = 0; at < NA; at++) acc[at] = mfma64(av[tp].x, b[at][2 * tp], acc[at]);
+#pragma unroll
+            for (int at = 0; at < NA; at++) acc[at] = mfma64(av[tp].y, b[at][2 * tp + 1], acc[at]);
+        }
+        // this lane-group's combo (flattened): c = 4 mt + qg -> (nx, ny); padding combos
+        // past KX*NY have zero coefficients.  Phase w = e^{i(nx gx x + ny gy y)}: direct
+        // when this lane's nx row changes (divergent only across the 16-lane combo
+        // groups), else advanced by e^{i 4 gy y}.
+        const int cfl = 4 * mt + qg;
+        const int nx = cfl / g.NY;
+        const int ny = cfl - nx * g.NY - (g.KY - 1);
+        if (nx != cur_nx) {
+#pragma unroll
+            for (int at = 0; at < NA; at++) {
+                double s, c;
+                sincos((nx * a.rec.x) * px[at] + (ny * a.rec.y) * py[at], &s, &c);
+                wr[at] = c; wi[at] = s;
+            }
+            cur_nx = nx;
+        } else {
+#pragma unroll
+            for (int at = 0; at < NA; at++) {
+                double nr = wr[at] * sr[at] - wi[at] * si[at];
+                double ni = wr[at] * si[at] + wi[at] * sr[at];
+                wr[at] = nr; wi[at] = ni;
+            }
+        }
+#pragma unroll
+        for (int at = 0; at < NA; at++) {
+            double re0 = wr[at] * acc[at][0] - wi[at] * acc[at][1];
+            double im0 = wr[at] * acc[at][1] + wi[at] * acc[at][0];
+            double imz = wr[at] * acc[at][3] + wi[at] * acc[at][2];
+            T0[at] += re0;
+            Tx[at] += nx * im0;
+            Ty[at] += ny * im0;
+            Tz[at] += imz;
         }
     };
 
     const int nstages = (m_hi - m_lo + kFMB - 1) / kFMB;
-    double2 reg[2];
+    double2 reg[kFStageV];
     if (nstages > 0) {
         load_stage(m_lo, reg);
         store_stage(0, reg);
     }
     __syncthreads();
-    int cur_nx = -1;
     for (int st = 0; st < nstages; st++) {
         const int buf = st & 1;
-        if (st + 1 < nstages) load_stage(m_lo + (st + 1) * kFMB, reg);
+        const int m0 = m_lo + st * kFMB;
+        if (st + 1 < nstages) load_stage(m0 + kFMB, reg);
+        double2 aA[8], aB[8];
+        read_a(buf, 0, aA);
 #pragma unroll
-        for (int mloc = 0; mloc < kFMB; mloc++) {
-            const int mt = m_lo + st * kFMB + mloc;
-            if (mt >= m_hi) break;
-            // this lane-group's combo (flattened): c = 4 mt + qg -> (nx, ny); padding combos
-            // past KX*NY have zero coefficients
-            const int cfl = 4 * mt + qg;
-            const int nx = cfl / g.NY;
-            const int ny = cfl - nx * g.NY - (g.KY - 1);
-            const double* A = &alds[buf][mloc * 16 * 64];
-            d4 acc[NA];
-#pragma unroll
-            for (int at = 0; at < NA; at++) acc[at] = (d4){0, 0, 0, 0};
-#pragma unroll
-            for (int t = 0; t < 16; t++) {
-                if (t < NKS) {
-                    double av = A[t * 64 + lane];
-#pragma unroll
-                    for (int at = 0; at < NA; at++) acc[at] = mfma64(av, b[at][t], acc[at]);
-                }
-            }
-            // phase w = e^{i(nx gx x + ny gy y)}: direct when this lane's nx row changes
-            // (divergent only across the 16-lane combo groups), else advanced by e^{i 4 gy y}.
-            if (nx != cur_nx) {
-#pragma unroll
-                for (int at = 0; at < NA; at++) {
-                    double s, c;
-                    sincos((nx * a.rec.x) * px[at] + (ny * a.rec.y) * py[at], &s, &c);
-                    wr[at] = c; wi[at] = s;
-                }
-                cur_nx = nx;
-            } else {
-#pragma unroll
-                for (int at = 0; at < NA; at++) {
-                    double nr = wr[at] * sr[at] - wi[at] * si[at];
-                    double ni = wr[at] * si[at] + wi[at] * sr[at];
-                    wr[at] = nr; wi[at] = ni;
-                }
-            }
-#pragma unroll
-            for (int at = 0; at < NA; at++) {
-                double re0 = wr[at] * acc[at][0] - wi[at] * acc[at][1];
-                double im0 = wr[at] * acc[at][1] + wi[at] * acc[at][0];
-                double imz = wr[at] * acc[at][3] + wi[at] * acc[at][2];
-                T0[at] += re0;
-                Tx[at] += nx * im0;
-                Ty[at] += ny * im0;
-                Tz[at] += imz;
-            }
+        for (int mloc = 0; mloc < kFMB; mloc += 2) {
+            read_a(buf, mloc + 1, aB);
+            mtile(m0 + mloc, aA);
+            if (mloc + 2 < kFMB) read_a(buf, mloc + 2, aA);
+            mtile(m0 + mloc + 1, aB);
         }
         if (st + 1 < nstages) store_stage(buf ^ 1, reg);
         __syncthreads();
@@ -479,12 +515,32 @@ __global__ void __launch_bounds__(kFThreads) k_force(FArgs a) {
             o[3] = qi * a.rec.z * v3;
         }
     }
-    (void)nparts;
 }
 
 // ---------------------------------------------------------------------------------
 // plan + launchers
 // ---------------------------------------------------------------------------------
+typedef void (*SfacKernel)(SArgs);
+
+template <int NT>
+static SfacKernel sfac_kernel_nt(int ta) {
+    switch (ta) {
+        case 32: return k_sfac<NT, 32>;
+        case 16: return k_sfac<NT, 16>;
+        case 8: return k_sfac<NT, 8>;
+        default: return k_sfac<NT, 4>;
+    }
+}
+
+static SfacKernel sfac_kernel(int nt, int ta) {
+    switch (nt) {
+        case 4: return sfac_kernel_nt<4>(ta);
+        case 3: return sfac_kernel_nt<3>(ta);
+        case 2: return sfac_kernel_nt<2>(ta);
+        default: return sfac_kernel_nt<1>(ta);
+    }
+}
+
 void kspace_plan(Handle& h) {
     KGeom& g = h.kg;
     g.KX = h.kmax[0]; g.KY = h.kmax[1]; g.KZ = h.kmax[2];
@@ -506,8 +562,17 @@ void kspace_plan(Handle& h) {
         int elems = TA * (g.CSW / 2 + g.NYP + g.KX);
         return 2 * tile_bytes(TA) <= 150 * 1024 && elems <= kSMaxV * kSThreads;
     };
+    if (!tile_fits(4))
+        throw std::invalid_argument("reciprocal-space grid too large for the S-pass LDS tile (kmax)");
     sp.tile_atoms = tile_fits(32) ? 32 : (tile_fits(16) ? 16 : (tile_fits(8) ? 8 : 4));
     sp.lds_bytes = 2 * tile_bytes(sp.tile_atoms);
+    // dynamic-LDS permission (a limit, not an allocation) for the S-pass variants used
+    for (int nt : {4, (g.NZP % 64) / 16}) {
+        if (nt == 0) continue;
+        check_hip(hipFuncSetAttribute((const void*)sfac_kernel(nt, sp.tile_atoms),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024),
+                  "k_sfac LDS attribute");
+    }
     h.npad = ((nown + sp.tile_atoms - 1) / sp.tile_atoms) * sp.tile_atoms;
     int wg_per_chunk = sp.wg_groups * g.NB;
     int target = std::max(1, (256 + wg_per_chunk - 1) / wg_per_chunk);  // ~one workgroup per CU
@@ -564,18 +629,21 @@ void launch_kspace_sfac(Handle& h) {
     const KGeom& g = h.kg;
     SArgs a;
     a.g = g; a.nown = h.hi - h.lo; a.npad = h.npad;
-    a.chunk_atoms = h.sp.chunk_atoms; a.tile_atoms = h.sp.tile_atoms;
+    a.chunk_atoms = h.sp.chunk_atoms;
     a.wg_groups = h.sp.wg_groups;
     a.cs = h.tab_cs; a.ty = h.tab_y; a.xq = h.tab_xq; a.slab = h.s_slab;
-    static size_t lds_attr = 0;
-    if (h.sp.lds_bytes > lds_attr) {
-        check_hip(hipFuncSetAttribute((const void*)k_sfac, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                      (int)h.sp.lds_bytes),
-                  "k_sfac LDS attribute");
-        lds_attr = h.sp.lds_bytes;
+    // column blocks 0..NB-1 hold 64 columns except the last (NZP % 64 if nonzero):
+    // full blocks in one launch, the ragged one in a second with fewer column tiles
+    const int nfull = g.NZP / 64;
+    const int rem_nt = (g.NZP % 64) / 16;
+    struct L { int nt, nbk0, nblocks; } launches[2] = {{4, 0, nfull}, {rem_nt, nfull, rem_nt > 0 ? 1 : 0}};
+    for (const L& l : launches) {
+        if (l.nblocks == 0) continue;
+        SfacKernel k = sfac_kernel(l.nt, h.sp.tile_atoms);
+        a.nbk0 = l.nbk0;
+        dim3 grid(h.sp.wg_groups * l.nblocks, h.sp.nchunks);
+        hipLaunchKernelGGL(k, grid, dim3(kSThreads), h.sp.lds_bytes, h.stream, a);
     }
-    dim3 grid(h.sp.wg_groups * g.NB, h.sp.nchunks);
-    hipLaunchKernelGGL(k_sfac, grid, dim3(kSThreads), h.sp.lds_bytes, h.stream, a);
     int64_t count = (int64_t)2 * g.nslots() * g.NZP;
     hipLaunchKernelGGL(k_sfac_reduce, dim3(nblk(count, 256)), dim3(256), 0, h.stream, count, h.sp.nchunks, h.s_slab,
                        h.s_red);
