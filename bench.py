@@ -79,6 +79,27 @@ def cpu_baseline(force, pos, box, k_sample):
     }
 
 
+# rocprofv3 kernel names of the library's timing phases (k-space MFMA kernels at C3)
+PMC_KERNEL = {"kspace_force": "cf::k_force<2>", "kspace_sfac": "cf::k_sfac<4, 32>"}
+
+
+def pmc_traffic(config, world, phase):
+    """HBM bytes per launch of the dominant kernel from the newest committed PMC summary
+    (profiles/r*_c3_pmc_summary_*.json, written by tools/profile_round.sh from separate
+    rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this same bench command, with the
+    gfx950 FETCH_SIZE x2 correction).  None when no profile matches this workload."""
+    if config != "C3" or world != 1:
+        return None, None
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_c3_pmc_summary_*.json")))
+    if not files:
+        return None, None
+    e = json.load(open(files[-1])).get(PMC_KERNEL[phase], {})
+    if "hbm_read_bytes_est" not in e or "hbm_write_bytes" not in e:
+        return None, None
+    return int(e["hbm_read_bytes_est"] + e["hbm_write_bytes"]), os.path.relpath(files[-1], ROOT)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -89,6 +110,8 @@ def main():
     ap.add_argument("--cpu-k-sample", type=int, default=1500)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dt", type=float, default=0.001, help="ps")
+    ap.add_argument("--neighbor-skin", type=float, default=0.1,
+                    help="nm; persistent list rebuilt when an atom moved > skin/2 (0 = every step)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -103,7 +126,7 @@ def main():
     system, force, pos_np, box = ts.make(args.config)
     n = len(pos_np)
     n_waters = force.getNumFluxWaters() + force.getNumFluxAngles()
-    kern = ShardedCoulKernel(system, force, local, kspace_algo=args.kspace_algo)
+    kern = ShardedCoulKernel(system, force, local, kspace_algo=args.kspace_algo, neighbor_skin=args.neighbor_skin)
     lo, hi = kern.lo, kern.hi
     alpha, kmax = kern.kernel.ewald_params()
     k_half = (kmax[2] - 1) + (kmax[1] - 1) * (2 * kmax[2] - 1) + (kmax[0] - 1) * (2 * kmax[1] - 1) * (2 * kmax[2] - 1)
@@ -147,6 +170,7 @@ def main():
         energy = step(False)
     torch.cuda.synchronize()
     kern.kernel.set_timing(True)
+    builds0, evals0 = kern.kernel.neighbor_stats()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -162,23 +186,33 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
     timing = kern.kernel.timing()
+    builds1, evals1 = kern.kernel.neighbor_stats()
     kern.kernel.set_timing(False)
     ms_eval = float(np.mean([a.elapsed_time(b) for a, b in ev])) if ev else float("nan")
     e_final = energy.item()
     ms_step = elapsed / args.steps * 1e3
     ns_day = 86.4 / ms_step * (dt / 0.001)
 
-    kernels = {k: (v[0] / v[1] if v[1] else 0.0) for k, v in timing.items()}
+    per_launch = {k: (v[0] / v[1] if v[1] else 0.0) for k, v in timing.items()}
+    per_step = {k: v[0] / args.steps for k, v in timing.items()}   # amortized (list phases are not every step)
+    kernels = per_launch
     n_own = hi - lo
     units = float(n_own) * k_half
+    # algorithmic fp64 flops per (atom, half-space k-vector) of the separable GEMM form
+    # (DESIGN.md §4.3): S-pass 4 (w x (cos, sin), re and im), force pass 8 (4 outputs x
+    # (cos, sin)).  SURVEY §8(d) prices the direct VALU form at 10 / 20 per unit.
     alg = {"kspace_sfac": 4.0 * units, "kspace_force": 8.0 * units}
+    survey = {"kspace_sfac": 10.0 * units, "kspace_force": 20.0 * units}
     dom = max(alg, key=lambda k: kernels.get(k, 0.0))
     t_dom = kernels.get(dom, 0.0) * 1e-3
     achieved = alg[dom] / t_dom / 1e12 if t_dom > 0 else 0.0
+    traffic, traffic_src = pmc_traffic(args.config, world, dom)
     roofline = {"kernel": dom, "bound": "mfma", "achieved": round(achieved, 3), "peak": FP64_MFMA_PEAK_TFLOPS,
-                "unit": "TFLOP/s", "frac": round(achieved / FP64_MFMA_PEAK_TFLOPS, 4), "traffic": None,
+                "unit": "TFLOP/s", "frac": round(achieved / FP64_MFMA_PEAK_TFLOPS, 4), "traffic": traffic,
+                "traffic_source": traffic_src,
                 "alg_flops_per_launch": alg[dom], "avg_launch_ms": kernels.get(dom, 0.0),
-                "per_unit": "4 (S-pass) / 8 (force pass) fp64 flops per atom x half-space k-vector"}
+                "per_unit": "4 (S-pass) / 8 (force pass) fp64 flops per atom x half-space k-vector (GEMM form)",
+                "survey_equiv_tflops": round(survey[dom] / t_dom / 1e12, 3) if t_dom > 0 else 0.0}
 
     if rank == 0:
         cpu = None
@@ -194,10 +228,12 @@ def main():
                                    f"(alpha {alpha:.5f}, kmax {kmax[0]}, K_half {k_half}), velocity Verlet dt="
                                    f"{dt * 1000:g} fs, fp64",
                        "atoms": n, "kmax": list(kmax), "k_half": k_half,
+                       "neighbor_skin_nm": args.neighbor_skin,
+                       "nlist_builds_in_timed_steps": f"{builds1 - builds0}/{evals1 - evals0}",
                        "parallelism": f"atom-decomposition x{world}" + (" (RCCL all-reduce of S(k))" if world > 1 else "")},
             "ms_per_force_eval": round(ms_eval, 4),
             "energy_kj_mol": e_final,
-            "kernels_ms": {k: round(v, 4) for k, v in kernels.items()},
+            "kernels_ms_per_step": {k: round(v, 4) for k, v in per_step.items()},
             "roofline": roofline,
             "cpu_baseline": cpu,
         }

@@ -104,6 +104,18 @@ CF_EXPORT int cf_get_owned_range(const cf_handle* h, int32_t* lo, int32_t* hi);
  * contiguous and never split a molecule (connected component of flux terms + exceptions). */
 CF_EXPORT int cf_partition(const cf_params* params, int32_t world_size, int32_t rank, int32_t* lo, int32_t* hi);
 
+/* Persistent neighbour list (the reference rebuilds its voxel-hash list on
+ * every call, ReferenceCoulKernels.cpp:559).  skin = 0 (default): rebuild on every
+ * evaluation.  skin > 0 (nm): the list holds pairs within cutoff + skin and is kept while
+ * the box is unchanged and no atom has moved more than skin/2 since the last build (decided
+ * on the device).  The evaluated pair set is identical either way (every pair is tested
+ * against the exact cutoff); only the fp64 summation order can differ.  Positions must be
+ * continuous between calls (a re-wrapped atom just triggers a rebuild).  The skin is capped
+ * at half the smallest box length minus the cutoff. */
+CF_EXPORT int cf_set_neighbor_skin(cf_handle* h, double skin);
+/* Number of neighbour-list builds and evaluations since cf_create. */
+CF_EXPORT int cf_get_neighbor_stats(const cf_handle* h, int64_t* builds, int64_t* evaluations);
+
 /*
  * Replaces ReferenceCalcCoulForceKernel::execute (ReferenceCoulKernels.cpp:424-636).
  * Device-resident, asynchronous on the handle's stream:

@@ -39,6 +39,7 @@ struct cf_handle {
     double* pos_host_dev = nullptr;   // cf_compute_host staging
     double* frc_host_dev = nullptr;
     double* ene_host_dev = nullptr;
+    double default_box[9] = {};
     const double* pos_pending = nullptr;
 };
 
@@ -90,6 +91,31 @@ T* dupload(cf_handle* H, const std::vector<T>& v) {
     return p;
 }
 
+void dfree(cf_handle* H, void* p) {
+    if (!p) return;
+    auto it = std::find(H->allocs.begin(), H->allocs.end(), p);
+    if (it != H->allocs.end()) H->allocs.erase(it);
+    (void)hipFree(p);
+}
+
+// neighbour-list capacity: the mean count within rc + skin at the default-box density,
+// split over kSeg = 4 sub-lists, x2 + margin (k_pairs_overflow rescans the cells for any
+// atom that overflows, so this is a speed knob, not a correctness limit)
+void alloc_nlist(cf_handle* H, double skin) {
+    cf::Handle& h = H->h;
+    const double* b = H->default_box;
+    double V = b[0] * b[4] * b[8];
+    double r = h.cutoff + skin;
+    double mean = 4.0 / 3.0 * M_PI * r * r * r * h.n / V;
+    int cap = (int)std::min<double>(h.n, 0.5 * mean + 64);
+    if (h.nl && cap <= h.nb_cap) return;
+    dfree(H, h.nl);
+    h.nl = nullptr;
+    h.nb_cap = cap;
+    h.nl = dalloc<int>(H, (size_t)4 * h.nb_cap * h.n);
+    if (!h.nl_cnt) h.nl_cnt = dalloc<int>(H, (size_t)4 * h.n);
+}
+
 // getEwaldParamValue, ReferenceCoulKernels.cpp:32-35
 double ewald_param_value(int kmax, double width, double alpha) {
     double t = kmax * M_PI / (width * alpha);
@@ -111,7 +137,7 @@ void set_cells(cf_handle* H, const double L[3]) {
     cf::Handle& h = H->h;
     int nc[3];
     for (int d = 0; d < 3; d++) {
-        double v = std::floor(L[d] / h.cutoff);
+        double v = std::floor(L[d] / (h.cutoff + h.list_skin));
         nc[d] = (int)std::max(1.0, std::min(v, 1024.0));
     }
     int64_t ncell = (int64_t)nc[0] * nc[1] * nc[2];
@@ -135,7 +161,6 @@ void set_box(cf_handle* H, const double* box9) {
         if (h.cutoff > 0.5 * L[d] * (1 + 1e-12))
             fail(CF_ERR_INVALID, "cutoff exceeds half the periodic box (minimum image would be ambiguous)");
     h.box_L[0] = L[0]; h.box_L[1] = L[1]; h.box_L[2] = L[2];
-    set_cells(H, L);
 }
 
 // Atom decomposition: contiguous owned ranges [lo,hi), cut only where no molecule
@@ -416,16 +441,8 @@ CF_EXPORT int cf_create(const cf_params* p, const cf_options* opt, cf_handle** o
                       "sort temp query");
             h.sort_tmp_bytes = tmp;
             h.sort_tmp = dalloc<char>(H, tmp);
-            // neighbour-list capacity: 1.5x the mean count at the default-box density + margin
-            // (k_pairs rescans the cells for any atom that overflows, so this is a speed knob)
-            {
-                double V = p->default_box[0] * p->default_box[4] * p->default_box[8];
-                double mean = 4.0 / 3.0 * M_PI * h.cutoff * h.cutoff * h.cutoff * n / V;
-                // kSeg = 4 sub-lists per atom, each sized for a quarter of the neighbours
-                h.nb_cap = (int)std::min<double>(n, 0.5 * mean + 64);
-                h.nl = dalloc<int>(H, (size_t)4 * h.nb_cap * n);
-                h.nl_cnt = dalloc<int>(H, (size_t)4 * n);
-            }
+            std::copy(p->default_box, p->default_box + 9, H->default_box);
+            alloc_nlist(H, 0.0);
             if (h.kspace_algo == 0) {
                 // phase tables: padded rows stay zero forever (memset once)
                 h.tab_xq = dalloc<double2>(H, (size_t)h.npad * g.KX);
@@ -471,6 +488,8 @@ CF_EXPORT int cf_destroy(cf_handle* H) {
             for (hipEvent_t e : v) (void)hipEventDestroy(e);
         if (H->h.cell_start) (void)hipFree(H->h.cell_start);
         if (H->h.cell_end) (void)hipFree(H->h.cell_end);
+        if (H->h.skin_flag_host) (void)hipHostFree(H->h.skin_flag_host);
+        if (H->h.skin_event) (void)hipEventDestroy(H->h.skin_event);
         if (H->h.own_stream) (void)hipStreamDestroy(H->h.stream);
         delete H;
     });
@@ -486,6 +505,34 @@ CF_EXPORT int cf_partition(const cf_params* p, int32_t world_size, int32_t rank,
         partition(p, world, rank, &l, &h);
         *lo = l; *hi = h;
     });
+}
+
+CF_EXPORT int cf_set_neighbor_skin(cf_handle* H, double skin) {
+    return guarded([&] {
+        if (!H) fail(CF_ERR_INVALID, "null handle");
+        if (!(skin >= 0 && skin < 1e3)) fail(CF_ERR_INVALID, "skin must be finite and >= 0");
+        cf::Handle& h = H->h;
+        if (h.pending_flags >= 0) fail(CF_ERR_STATE, "cf_set_neighbor_skin during a begun evaluation");
+        check_hip(hipSetDevice(h.device), "hipSetDevice");
+        check_hip(hipStreamSynchronize(h.stream), "stream sync");
+        h.skin = skin;
+        h.list_valid = false;
+        if (!h.pbc) return;
+        alloc_nlist(H, skin);
+        if (skin > 0 && !h.pos_ref) {
+            h.pos_ref = dalloc<double>(H, (size_t)3 * h.n);
+            h.skin_flag = dalloc<int>(H, 1);
+            check_hip(hipHostMalloc((void**)&h.skin_flag_host, sizeof(int)), "pinned flag");
+            check_hip(hipEventCreateWithFlags(&h.skin_event, hipEventDisableTiming), "skin event");
+        }
+    });
+}
+
+CF_EXPORT int cf_get_neighbor_stats(const cf_handle* H, int64_t* builds, int64_t* evaluations) {
+    if (!H) { g_err = "null handle"; return CF_ERR_INVALID; }
+    if (builds) *builds = H->h.n_builds;
+    if (evaluations) *evaluations = H->h.n_evals;
+    return CF_OK;
 }
 
 CF_EXPORT int cf_get_ewald_params(const cf_handle* H, double* alpha, int32_t kmax[3]) {
@@ -513,8 +560,15 @@ CF_EXPORT int cf_compute_begin(cf_handle* H, const double* pos_dev, const double
         { Timed t(H, PH_FLUX); cf::launch_flux_terms(h, pos_dev); }
         { Timed t(H, PH_PREP); cf::launch_atoms_prep(h, pos_dev); }
         if (h.pbc) {
-            { Timed t(H, PH_CELLS); cf::launch_cell_sort(h, pos_dev); }
-            if (h.hi > h.lo) { Timed t(H, PH_NLIST); cf::launch_nlist(h, pos_dev); }
+            // neighbour list: rebuilt on every call (skin 0, the reference's behaviour,
+            // RCK:559), or kept while no atom has moved more than half the skin.  The
+            // device-side displacement check is queued first; the host reads its flag only
+            // after the k-space work is queued, so the GPU never idles on the decision.
+            const double Lmin = std::min(h.box_L[0], std::min(h.box_L[1], h.box_L[2]));
+            const double s_call = h.skin > 0 ? std::max(0.0, std::min(h.skin, 0.5 * Lmin - h.cutoff)) : 0.0;
+            const bool reusable = h.skin > 0 && h.list_valid && s_call == h.list_skin &&
+                                  h.list_L[0] == h.box_L[0] && h.list_L[1] == h.box_L[1] && h.list_L[2] == h.box_L[2];
+            if (reusable) { Timed t(H, PH_CELLS); cf::launch_skin_check(h, pos_dev); }
             if ((forces || energy) && h.hi > h.lo) {
                 if (h.kspace_algo == 0) {
                     { Timed t(H, PH_TABLES); cf::launch_kspace_tables(h, pos_dev); }
@@ -528,7 +582,25 @@ CF_EXPORT int cf_compute_begin(cf_handle* H, const double* pos_dev, const double
                 double* buf = cf::kspace_reduce_buffer(h, &cnt);
                 check_hip(hipMemsetAsync(buf, 0, sizeof(double) * cnt, h.stream), "memset S");
             }
+            bool rebuild = true;
+            if (reusable) {
+                check_hip(hipEventSynchronize(h.skin_event), "skin flag wait");
+                rebuild = *h.skin_flag_host != 0;
+            }
+            if (rebuild) {
+                h.list_skin = s_call;
+                set_cells(H, h.box_L);
+                { Timed t(H, PH_CELLS); cf::launch_cell_sort(h, pos_dev); }
+                if (h.hi > h.lo) { Timed t(H, PH_NLIST); cf::launch_nlist(h, pos_dev); }
+                h.list_valid = h.skin > 0;
+                std::copy(h.box_L, h.box_L + 3, h.list_L);
+                h.n_builds++;
+            } else {
+                Timed t(H, PH_CELLS);
+                cf::launch_pos_refresh(h, pos_dev);
+            }
         }
+        h.n_evals++;
         launch_check("compute_begin");
         h.pending_flags = flags;
         H->pos_pending = pos_dev;

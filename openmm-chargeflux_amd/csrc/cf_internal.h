@@ -108,6 +108,17 @@ struct Handle {
     double4* pos4s = nullptr;   // [N] sorted wrapped (x,y,z,q)
     double2* ljs = nullptr;     // [N] sorted LJ
     void* sort_tmp = nullptr; size_t sort_tmp_bytes = 0;
+    // persistent list with skin: pairs within rc + list_skin at the last
+    // build; reused while every atom has moved <= list_skin/2 and the box is unchanged
+    double skin = 0.0;          // requested skin (nm); 0 = rebuild on every evaluation
+    double list_skin = 0.0;     // skin the current list was built with
+    double list_L[3] = {0, 0, 0};
+    bool list_valid = false;
+    double* pos_ref = nullptr;  // [N*3] positions at the last build
+    int* skin_flag = nullptr;   // [1] device: some atom moved > list_skin/2
+    int* skin_flag_host = nullptr;  // pinned copy
+    hipEvent_t skin_event = nullptr;
+    int64_t n_builds = 0, n_evals = 0;
     int nb_cap = 0;             // capacity of each of the 4 neighbour sub-lists of an atom
     int* nl = nullptr;          // [4][nb_cap][N] transposed sub-lists (sorted index | shift<<26)
     int* nl_cnt = nullptr;      // [4][N]
@@ -140,6 +151,8 @@ struct Handle {
 void launch_flux_terms(Handle& h, const double* pos);
 void launch_atoms_prep(Handle& h, const double* pos);
 void launch_cell_sort(Handle& h, const double* pos);
+void launch_skin_check(Handle& h, const double* pos);   // -> skin_flag, skin_flag_host, skin_event
+void launch_pos_refresh(Handle& h, const double* pos);  // sorted positions/charges, list kept
 void launch_nlist(Handle& h, const double* pos);
 void launch_direct(Handle& h, const double* pos, int include_forces);
 void launch_nopbc(Handle& h, const double* pos, int include_forces, int include_energy);

@@ -156,7 +156,8 @@ __global__ void __launch_bounds__(256) k_cell_gather(int n, const int* __restric
                                                      const double* __restrict__ pos, const double* __restrict__ q,
                                                      const double2* __restrict__ lj, double3 L,
                                                      int* __restrict__ cstart, int* __restrict__ cend,
-                                                     double4* __restrict__ pos4s, double2* __restrict__ ljs) {
+                                                     double4* __restrict__ pos4s, double2* __restrict__ ljs,
+                                                     double* __restrict__ pos_ref) {
     int s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= n) return;
     int k = key_s[s];
@@ -167,6 +168,36 @@ __global__ void __launch_bounds__(256) k_cell_gather(int n, const int* __restric
     pos4s[s] = make_double4(x.x - floor(x.x / L.x) * L.x, x.y - floor(x.y / L.y) * L.y,
                             x.z - floor(x.z / L.z) * L.z, q[i]);
     ljs[s] = lj[i];
+    if (pos_ref) { pos_ref[3 * i] = x.x; pos_ref[3 * i + 1] = x.y; pos_ref[3 * i + 2] = x.z; }
+}
+
+// Between list rebuilds (skin > 0): the sorted order and every atom's periodic image are
+// kept from the last build (wrap offsets recomputed from the build positions, so they are
+// bit-identical to k_cell_gather's), only coordinates and flux charges are refreshed.
+__global__ void __launch_bounds__(256) k_pos_refresh(int n, const int* __restrict__ idx_s,
+                                                     const double* __restrict__ pos, const double* __restrict__ pos_ref,
+                                                     const double* __restrict__ q, double3 L,
+                                                     double4* __restrict__ pos4s) {
+    int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= n) return;
+    int i = idx_s[s];
+    double3 x = ld3(pos, i), r = ld3(pos_ref, i);
+    pos4s[s] = make_double4(x.x - floor(r.x / L.x) * L.x, x.y - floor(r.y / L.y) * L.y,
+                            x.z - floor(r.z / L.z) * L.z, q[i]);
+}
+
+// list validity: flag = 1 if any atom moved more than half the skin since the last build
+__global__ void __launch_bounds__(256) k_skin_check(int n, const double* __restrict__ pos,
+                                                    const double* __restrict__ pos_ref, double lim2,
+                                                    int* __restrict__ flag) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    bool moved = false;
+    if (i < n) {
+        double3 x = ld3(pos, i), r = ld3(pos_ref, i);
+        double dx = x.x - r.x, dy = x.y - r.y, dz = x.z - r.z;
+        moved = !(dx * dx + dy * dy + dz * dz <= lim2);  // NaN counts as moved
+    }
+    if (__ballot(moved) && (threadIdx.x & 63) == 0) atomicOr(flag, 1);
 }
 
 // ---------------------------------------------------------------------------------
@@ -191,6 +222,7 @@ struct DirectArgs {
     int n, lo, hi, include_forces;
     double3 L; int3 nc; int brute;
     double rc2, alpha;
+    double rl2;                 // list radius^2: (rc + list skin)^2
     int nb_cap;                 // capacity of ONE of the kSeg sub-lists
     const int* atom_sorted; const int* key_sorted;
     const int* cstart; const int* cend;
@@ -221,8 +253,8 @@ __device__ __forceinline__ double3 shift_of(int code, double3 L) {
 // Visit the 27 neighbour cells of sorted atom s; fn(t, code, dx, dy, dz, r2) for every
 // candidate t != s within the cutoff (exclusions are left to the caller).
 template <class F>
-__device__ __forceinline__ void scan_cells(const DirectArgs& a, int s, double4 pi, F&& fn, int part = 0,
-                                           int nparts = 1) {
+__device__ __forceinline__ void scan_cells(const DirectArgs& a, int s, double4 pi, double r2max, F&& fn,
+                                           int part = 0, int nparts = 1) {
     if (!a.brute) {
         int ord = 0;
         int key = a.key_sorted[s];
@@ -244,7 +276,7 @@ __device__ __forceinline__ void scan_cells(const DirectArgs& a, int s, double4 p
                         double4 pj = a.pos4s[t];
                         double dx = pi.x - (pj.x + sx), dy = pi.y - (pj.y + sy), dz = pi.z - (pj.z + sz);
                         double r2 = dx * dx + dy * dy + dz * dz;
-                        if (r2 > a.rc2 || t == s) continue;
+                        if (r2 > r2max || t == s) continue;
                         fn(t, code, dx, dy, dz, r2);
                     }
                 }
@@ -256,7 +288,7 @@ __device__ __forceinline__ void scan_cells(const DirectArgs& a, int s, double4 p
             double4 pj = a.pos4s[t];
             double3 d = delta_r(make_double3(pj.x, pj.y, pj.z), make_double3(pi.x, pi.y, pi.z), a.L, 1);
             double r2 = d.x * d.x + d.y * d.y + d.z * d.z;
-            if (r2 > a.rc2) continue;
+            if (r2 > r2max) continue;
             fn(t, kBruteShift, d.x, d.y, d.z, r2);
         }
     }
@@ -274,7 +306,7 @@ __global__ void __launch_bounds__(256) k_nlist(DirectArgs a) {
     for (int k = 0; k < kMaxRegExcl; k++) reg[k] = k < exc ? a.ex_list[ex0 + k] : -1;
     for (int seg = 0; seg < kSeg; seg++) {
         int cnt = 0;
-        scan_cells(a, s, pi, [&](int t, int code, double, double, double, double) {
+        scan_cells(a, s, pi, a.rl2, [&](int t, int code, double, double, double, double) {
             if (exc && in_excl(a.atom_sorted[t], reg, exc, a.ex_list, ex0)) return;
             if (cnt < a.nb_cap) a.nl[((size_t)seg * a.nb_cap + cnt) * a.n + s] = t | (code << kShiftBits);
             cnt++;
@@ -351,7 +383,7 @@ __global__ void __launch_bounds__(kWaveNL * kSeg) k_nlist_wave(DirectArgs a) {
     };
     if (!fits) {  // wave-uniform (and block-uniform: every wave sees the same 64 atoms)
         if (active)
-            scan_cells(a, s, pi, [&](int t, int code, double, double, double, double) { emit(t, a.atom_sorted[t], code); },
+            scan_cells(a, s, pi, a.rl2, [&](int t, int code, double, double, double, double) { emit(t, a.atom_sorted[t], code); },
                        seg, kSeg);
         if (active) a.nl_cnt[(size_t)seg * a.n + s] = cnt;
         return;
@@ -362,7 +394,7 @@ __global__ void __launch_bounds__(kWaveNL * kSeg) k_nlist_wave(DirectArgs a) {
     const double3 pu = make_double3(pi.x + lsh[0] * Ls[0], pi.y + lsh[1] * Ls[1], pi.z + lsh[2] * Ls[2]);
     const double3 org = make_double3(__shfl(pu.x, 0), __shfl(pu.y, 0), __shfl(pu.z, 0));
     const float3 pf = make_float3((float)(pu.x - org.x), (float)(pu.y - org.y), (float)(pu.z - org.z));
-    const float rc2f = (float)(a.rc2 * (1.0 + 1e-5)) + 1e-6f;
+    const float rc2f = (float)(a.rl2 * (1.0 + 1e-5)) + 1e-6f;
 
     const int by = hi3[1] - lo3[1] + 1, bz = hi3[2] - lo3[2] + 1;
     const int ncell = (hi3[0] - lo3[0] + 1) * by * bz;
@@ -611,7 +643,7 @@ __global__ void __launch_bounds__(256) k_pairs_overflow(DirectArgs a) {
 #pragma unroll
     for (int k = 0; k < kMaxRegExcl; k++) reg[k] = k < exc ? a.ex_list[ex0 + k] : -1;
     PairAcc acc;
-    scan_cells(a, s, pi, [&](int t, int, double dx, double dy, double dz, double r2) {
+    scan_cells(a, s, pi, a.rc2, [&](int t, int, double dx, double dy, double dz, double r2) {
         if (exc && in_excl(a.atom_sorted[t], reg, exc, a.ex_list, ex0)) return;
         pair_term(acc, a, pi, li, a.pos4s[t], a.ljs[t], dx, dy, dz, r2);
     });
@@ -770,7 +802,23 @@ void launch_cell_sort(Handle& h, const double* pos) {
     check_hip(hipMemsetAsync(h.cell_start, 0, sizeof(int) * ncell, h.stream), "memset cell_start");
     check_hip(hipMemsetAsync(h.cell_end, 0, sizeof(int) * ncell, h.stream), "memset cell_end");
     hipLaunchKernelGGL(k_cell_gather, dim3(nblk(h.n, 256)), dim3(256), 0, h.stream, h.n, h.cell_key_sorted,
-                       h.atom_sorted, pos, h.q, h.lj, L, h.cell_start, h.cell_end, h.pos4s, h.ljs);
+                       h.atom_sorted, pos, h.q, h.lj, L, h.cell_start, h.cell_end, h.pos4s, h.ljs, h.pos_ref);
+}
+
+void launch_skin_check(Handle& h, const double* pos) {
+    check_hip(hipMemsetAsync(h.skin_flag, 0, sizeof(int), h.stream), "memset skin flag");
+    const double lim = 0.5 * h.list_skin;
+    hipLaunchKernelGGL(k_skin_check, dim3(nblk(h.n, 256)), dim3(256), 0, h.stream, h.n, pos, h.pos_ref, lim * lim,
+                       h.skin_flag);
+    check_hip(hipMemcpyAsync(h.skin_flag_host, h.skin_flag, sizeof(int), hipMemcpyDeviceToHost, h.stream),
+              "skin flag copy");
+    check_hip(hipEventRecord(h.skin_event, h.stream), "skin event");
+}
+
+void launch_pos_refresh(Handle& h, const double* pos) {
+    double3 L = make_double3(h.box_L[0], h.box_L[1], h.box_L[2]);
+    hipLaunchKernelGGL(k_pos_refresh, dim3(nblk(h.n, 256)), dim3(256), 0, h.stream, h.n, h.atom_sorted, pos,
+                       h.pos_ref, h.q, L, h.pos4s);
 }
 
 static DirectArgs direct_args(Handle& h, const double* pos, int include_forces) {
@@ -780,6 +828,7 @@ static DirectArgs direct_args(Handle& h, const double* pos, int include_forces) 
     a.nc = make_int3(h.nc[0], h.nc[1], h.nc[2]);
     a.brute = (h.nc[0] < 3 || h.nc[1] < 3 || h.nc[2] < 3) ? 1 : 0;
     a.rc2 = h.cutoff * h.cutoff; a.alpha = h.alpha;
+    a.rl2 = (h.cutoff + h.list_skin) * (h.cutoff + h.list_skin);
     a.nb_cap = h.nb_cap;
     a.atom_sorted = h.atom_sorted; a.key_sorted = h.cell_key_sorted;
     a.cstart = h.cell_start; a.cend = h.cell_end;

@@ -83,6 +83,8 @@ SIGNATURES = [
                                 C.POINTER(C.c_int32)]),
     ("cf_partition", C.c_int, [C.POINTER(cf_params), C.c_int32, C.c_int32, C.POINTER(C.c_int32),
                                C.POINTER(C.c_int32)]),
+    ("cf_set_neighbor_skin", C.c_int, [C.c_void_p, C.c_double]),
+    ("cf_get_neighbor_stats", C.c_int, [C.c_void_p, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
 ]
 
 _lib = None

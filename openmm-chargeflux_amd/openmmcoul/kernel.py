@@ -117,6 +117,18 @@ class HipCalcCoulForceKernel:
         _cabi.check(self._lib.cf_get_ewald_params(self._h, C.byref(alpha), kmax), self._lib)
         return alpha.value, tuple(kmax)
 
+    def set_neighbor_skin(self, skin: float):
+        """Persistent neighbour list with a skin (nm); 0 = rebuild on every execute (the
+        reference's behaviour, ReferenceCoulKernels.cpp:559).  See include/chargeflux.h."""
+        _cabi.check(self._lib.cf_set_neighbor_skin(self._h, float(skin)), self._lib)
+        return self
+
+    def neighbor_stats(self):
+        """(list builds, evaluations) since initialize."""
+        b, e = C.c_int64(), C.c_int64()
+        _cabi.check(self._lib.cf_get_neighbor_stats(self._h, C.byref(b), C.byref(e)), self._lib)
+        return b.value, e.value
+
     def owned_range(self):
         lo, hi = C.c_int32(), C.c_int32()
         _cabi.check(self._lib.cf_get_owned_range(self._h, C.byref(lo), C.byref(hi)), self._lib)
