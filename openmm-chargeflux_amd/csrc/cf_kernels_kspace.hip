@@ -18,6 +18,7 @@
 // (complex products, phase recurrences) beside the matrix pipe.
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <stdexcept>
 
 #include "cf_internal.h"
@@ -348,11 +349,8 @@ __global__ void __launch_bounds__(256) k_coeffs(KGeom g, double3 rec, double cst
 //   two k-steps.  Accumulator lane (qg, atom) receives the 4 parts (U0r,U0i,Uzr,Uzi)
 //   of combo 4*mt+qg -> epilogue multiplies by X Y in registers.
 // ---------------------------------------------------------------------------------
-constexpr int kFWaves = 8;
-constexpr int kFThreads = kFWaves * 64;
 constexpr int kFMB = 4;                   // m-tiles per LDS stage (must be even)
 constexpr int kFStageD2 = kFMB * 8 * 64;  // double2 per stage
-constexpr int kFStageV = kFStageD2 / kFThreads;
 
 struct FArgs {
     KGeom g;
@@ -362,8 +360,12 @@ struct FArgs {
     double* t_part;
 };
 
-template <int NA>
-__global__ void __launch_bounds__(kFThreads) k_force(FArgs a) {
+// WAVES waves per workgroup (8: 2 per SIMD, 256 registers each; 4: 1 per SIMD, 512),
+// NA 16-atom tiles per wave (independent MFMA accumulator chains).
+template <int NA, int WAVES>
+__global__ void __launch_bounds__(WAVES * 64) k_force(FArgs a) {
+    constexpr int kFThreads = WAVES * 64;
+    constexpr int kFStageV = kFStageD2 / kFThreads;
     __shared__ __attribute__((aligned(16))) double2 alds[2][kFStageD2];
     const KGeom g = a.g;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -382,7 +384,7 @@ __global__ void __launch_bounds__(kFThreads) k_force(FArgs a) {
     int atom[NA];
 #pragma unroll
     for (int at = 0; at < NA; at++) {
-        int ia = ((blockIdx.x * kFWaves + wave) * NA + at) * 16 + col;  // owned index
+        int ia = ((blockIdx.x * WAVES + wave) * NA + at) * 16 + col;  // owned index
         atom[at] = ia;
         bool ok = ia < a.nown;
         int i = a.lo + (ok ? ia : 0);
@@ -394,15 +396,27 @@ __global__ void __launch_bounds__(kFThreads) k_force(FArgs a) {
             b[at][t] = (ok && t < NKS) ? a.cs[((size_t)kc * a.npad + ia) * g.CSW + 4 * t + qg] : 0.0;
     }
 
+    // This lane group's combo walks c = 4 mt + qg -> (nx, ny), one m-tile at a time.  The
+    // phase w = e^{i(nx gx x + ny gy y)} follows by recurrence: x e^{i 4 gy y} per m-tile,
+    // and x e^{i(gx x - NY gy y)} per row wrap (ny past KY-1): sincos only here, once.
+    int nx, ny;
+    {
+        const int c0 = 4 * m_lo + qg;
+        nx = c0 / g.NY;
+        ny = c0 - nx * g.NY - (g.KY - 1);
+    }
     double T0[NA], Tx[NA], Ty[NA], Tz[NA];
-    double wr[NA], wi[NA], sr[NA], si[NA];
+    double wr[NA], wi[NA], sr[NA], si[NA], rr[NA], ri[NA];
 #pragma unroll
     for (int at = 0; at < NA; at++) {
         T0[at] = Tx[at] = Ty[at] = Tz[at] = 0;
         double s, c;
         sincos((4.0 * a.rec.y) * py[at], &s, &c);  // step e^{i 4 gy y}
         sr[at] = c; si[at] = s;
-        wr[at] = wi[at] = 0;
+        sincos(a.rec.x * px[at] - (g.NY * a.rec.y) * py[at], &s, &c);  // row wrap
+        rr[at] = c; ri[at] = s;
+        sincos((nx * a.rec.x) * px[at] + (ny * a.rec.y) * py[at], &s, &c);
+        wr[at] = c; wi[at] = s;
     }
 
     // stage = kFMB m-tiles x 8 k-step pairs x 64 lanes (double2), a linear copy of 8 KB
@@ -428,7 +442,6 @@ __global__ void __launch_bounds__(kFThreads) k_force(FArgs a) {
         for (int tp = 0; tp < 8; tp++) av[tp] = alds[buf][mloc * 512 + tp * 64 + lane];
     };
 
-    int cur_nx = -1;
     auto mtile = [&](int mt, const double2 (&av)[8]) {
         if (mt >= m_hi) return;  // wave-uniform
         d4 acc[NA];
@@ -441,38 +454,35 @@ __global__ void __launch_bounds__(kFThreads) k_force(FArgs a) {
 #pragma unroll
             for (int at = 0; at < NA; at++) acc[at] = mfma64(av[tp].y, b[at][2 * tp + 1], acc[at]);
         }
-        // this lane-group's combo (flattened): c = 4 mt + qg -> (nx, ny); padding combos
-        // past KX*NY have zero coefficients.  Phase w = e^{i(nx gx x + ny gy y)}: direct
-        // when this lane's nx row changes (divergent only across the 16-lane combo
-        // groups), else advanced by e^{i 4 gy y}.
-        const int cfl = 4 * mt + qg;
-        const int nx = cfl / g.NY;
-        const int ny = cfl - nx * g.NY - (g.KY - 1);
-        if (nx != cur_nx) {
-#pragma unroll
-            for (int at = 0; at < NA; at++) {
-                double s, c;
-                sincos((nx * a.rec.x) * px[at] + (ny * a.rec.y) * py[at], &s, &c);
-                wr[at] = c; wi[at] = s;
-            }
-            cur_nx = nx;
-        } else {
-#pragma unroll
-            for (int at = 0; at < NA; at++) {
-                double nr = wr[at] * sr[at] - wi[at] * si[at];
-                double ni = wr[at] * si[at] + wi[at] * sr[at];
-                wr[at] = nr; wi[at] = ni;
-            }
-        }
+        // padding combos past KX*NY have zero coefficients
+        const double nxd = nx, nyd = ny;
 #pragma unroll
         for (int at = 0; at < NA; at++) {
             double re0 = wr[at] * acc[at][0] - wi[at] * acc[at][1];
             double im0 = wr[at] * acc[at][1] + wi[at] * acc[at][0];
             double imz = wr[at] * acc[at][3] + wi[at] * acc[at][2];
             T0[at] += re0;
-            Tx[at] += nx * im0;
-            Ty[at] += ny * im0;
+            Tx[at] += nxd * im0;
+            Ty[at] += nyd * im0;
             Tz[at] += imz;
+        }
+        // advance to combo c + 4
+        ny += 4;
+#pragma unroll
+        for (int at = 0; at < NA; at++) {
+            double nr = wr[at] * sr[at] - wi[at] * si[at];
+            double ni = wr[at] * si[at] + wi[at] * sr[at];
+            wr[at] = nr; wi[at] = ni;
+        }
+        while (ny > g.KY - 1) {  // at most once per m-tile when NY >= 4
+            ny -= g.NY;
+            nx += 1;
+#pragma unroll
+            for (int at = 0; at < NA; at++) {
+                double nr = wr[at] * rr[at] - wi[at] * ri[at];
+                double ni = wr[at] * ri[at] + wi[at] * rr[at];
+                wr[at] = nr; wi[at] = ni;
+            }
         }
     };
 
@@ -583,9 +593,14 @@ void kspace_plan(Handle& h) {
     sp.nchunks = std::max(1, (nown + sp.chunk_atoms - 1) / sp.chunk_atoms);
     // ---- force pass
     FPassPlan& fp = h.fp;
+    // variant (NA, waves): (2, 8) default; CF_FORCE_VARIANT=1 -> (4, 4), 2 -> (2, 4)
     fp.na = 2;
-    fp.waves = kFWaves;
-    int atoms_per_wg = fp.na * 16 * kFWaves;
+    fp.waves = 8;
+    if (const char* v = getenv("CF_FORCE_VARIANT")) {
+        if (atoi(v) == 1) { fp.na = 4; fp.waves = 4; }
+        if (atoi(v) == 2) { fp.na = 2; fp.waves = 4; }
+    }
+    int atoms_per_wg = fp.na * 16 * fp.waves;
     fp.natom_groups = std::max(1, (nown + atoms_per_wg - 1) / atoms_per_wg);
     fp.kchunks = g.NB;
     // split the m-tile range so the number of workgroups is close to a multiple of the CU count
@@ -674,7 +689,12 @@ void launch_kspace_force(Handle& h, const double* pos) {
     a.lo = h.lo; a.nown = h.hi - h.lo; a.npad = h.npad; a.msplit = h.fp.msplit;
     a.cs = h.tab_cs; a.coef = h.coef_a; a.pos = pos; a.q = h.q; a.t_part = h.t_part;
     dim3 grid(h.fp.natom_groups, h.fp.kchunks * h.fp.msplit);
-    hipLaunchKernelGGL(k_force<2>, grid, dim3(kFThreads), 0, h.stream, a);
+    if (h.fp.na == 4 && h.fp.waves == 4)
+        hipLaunchKernelGGL((k_force<4, 4>), grid, dim3(256), 0, h.stream, a);
+    else if (h.fp.na == 2 && h.fp.waves == 4)
+        hipLaunchKernelGGL((k_force<2, 4>), grid, dim3(256), 0, h.stream, a);
+    else
+        hipLaunchKernelGGL((k_force<2, 8>), grid, dim3(512), 0, h.stream, a);
 }
 
 // =================================================================================
