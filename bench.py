@@ -43,22 +43,33 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def water_restraints(pos, n_waters, lo, hi):
-    """Harmonic O-H1, O-H2, H1-H2 forces (flexible water harness); owned atoms only."""
-    x = pos[: 3 * n_waters].view(n_waters, 3, 3)
-    f = torch.zeros_like(x)
-    for a, b, k, r0 in ((0, 1, K_OH, R_OH0), (0, 2, K_OH, R_OH0), (1, 2, K_HH, R_HH0)):
-        d = x[:, b] - x[:, a]
-        r = d.norm(dim=1, keepdim=True)
-        g = (k * (r - r0) / r) * d
-        f[:, a] += g
-        f[:, b] -= g
-    f = f.view(-1, 3)
-    if lo > 0:
-        f[:lo] = 0
-    if hi < f.shape[0]:
-        f[hi:] = 0
-    return f
+class MDHarness:
+    """Velocity Verlet + flexible-water restraints as two fused HIP kernels per step
+    (libcf_mdharness.so, csrc/md_harness.hip; not part of the CoulForce path)."""
+
+    def __init__(self, n_waters, lo, hi, dt, inv_mass, stream):
+        import ctypes as C
+        path = os.path.join(ROOT, "openmm-chargeflux_amd", "libcf_mdharness.so")
+        if not os.path.exists(path):
+            raise RuntimeError(f"{path} missing: run __graft_entry__.build() (make -C openmm-chargeflux_amd/csrc)")
+        L = C.CDLL(path)
+        vp, d, i = C.c_void_p, C.c_double, C.c_int
+        L.md_kick_drift.argtypes = [i, i, d, vp, vp, vp, vp, vp]
+        L.md_restrain_kick.argtypes = [i, i, i, d, d, d, d, d, vp, vp, vp, vp, vp]
+        self.L, self.C = L, C
+        self.nw, self.lo, self.hi, self.dt = n_waters, lo, hi, dt
+        self.inv_m = inv_mass
+        self.stream = C.c_void_p(stream)
+
+    def kick_drift(self, pos, vel, frc):
+        rc = self.L.md_kick_drift(self.lo, self.hi, self.dt, pos.data_ptr(), vel.data_ptr(), frc.data_ptr(),
+                                  self.inv_m.data_ptr(), self.stream)
+        assert rc == 0
+
+    def restrain_kick(self, pos, vel, frc, kick=True):
+        rc = self.L.md_restrain_kick(self.lo, self.hi, self.nw, K_OH, R_OH0, K_HH, R_HH0, self.dt if kick else 0.0,
+                                     pos.data_ptr(), vel.data_ptr(), frc.data_ptr(), self.inv_m.data_ptr(), self.stream)
+        assert rc == 0
 
 
 def cpu_baseline(force, pos, box, k_sample):
@@ -136,34 +147,29 @@ def main():
     rng = np.random.default_rng(ts.SEED + 1)
     v0 = rng.normal(size=(n, 3)) * np.sqrt(KB * 300.0 / masses.cpu().numpy())
     vel = torch.tensor(v0, dtype=torch.float64, device=dev)
-    owned = torch.zeros(n, 1, dtype=torch.float64, device=dev)
-    owned[lo:hi] = 1.0
     frc = torch.zeros_like(pos)
     dt = args.dt
     log(f"[rank {rank}] setup {time.time() - t_setup:.1f}s  N={n} owned=[{lo},{hi}) alpha={alpha:.5f} "
         f"kmax={kmax} K_half={k_half}")
 
-    def forces_now():
-        frc.zero_()
-        e = kern.execute(pos, box, frc, include_energy=True)
-        frc.add_(water_restraints(pos, n_waters, lo, hi))
-        return e
-
-    energy = forces_now()
+    md = MDHarness(n_waters, lo, hi, dt, (1.0 / masses).contiguous(), torch.cuda.current_stream(dev).cuda_stream)
+    frc.zero_()
+    energy = kern.execute(pos, box, frc, include_energy=True)
+    md.restrain_kick(pos, vel, frc, kick=False)
     ev = []
 
     def step(record):
-        vel.add_(0.5 * dt * frc / masses * owned)
-        pos.add_(dt * vel * owned)
+        md.kick_drift(pos, vel, frc)            # v += dt/2 f/m ; x += dt v  (owned atoms)
         kern.replicate_positions(pos)
         if record:
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             a.record()
-        e = forces_now()
+        frc.zero_()
+        e = kern.execute(pos, box, frc, include_energy=True)
         if record:
             b.record()
             ev.append((a, b))
-        vel.add_(0.5 * dt * frc / masses * owned)
+        md.restrain_kick(pos, vel, frc)         # f += restraints ; v += dt/2 f/m
         return e
 
     for _ in range(args.warmup):

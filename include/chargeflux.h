@@ -136,6 +136,11 @@ CF_EXPORT int cf_compute(cf_handle* h, const double* pos_dev, const double* box9
  * cf_kspace_buffer (fp64, on device, on the handle's stream ordering); end finishes. */
 CF_EXPORT int cf_compute_begin(cf_handle* h, const double* pos_dev, const double* box9, int flags);
 CF_EXPORT int cf_kspace_buffer(cf_handle* h, double** buf_dev, int64_t* count);
+/* Optional, between cf_compute_begin and cf_compute_end: launch the direct-space and
+ * exclusion kernels now.  They do not depend on the structure factors, so a multi-rank
+ * caller launches them after starting the S(k) all-reduce and before waiting for it (the
+ * two overlap).  cf_compute_end runs them itself if this was not called. */
+CF_EXPORT int cf_compute_direct(cf_handle* h);
 CF_EXPORT int cf_compute_end(cf_handle* h, double* forces_dev, double* energy_dev);
 
 /* Synchronous host-memory convenience (H2D positions, D2H forces/energy): what an

@@ -109,11 +109,12 @@ void alloc_nlist(cf_handle* H, double skin) {
     double mean = 4.0 / 3.0 * M_PI * r * r * r * h.n / V;
     int cap = (int)std::min<double>(h.n, 0.5 * mean + 64);
     if (h.nl && cap <= h.nb_cap) return;
+    const size_t rows = std::max(h.hi - h.lo, 1);  // one row per owned atom
     dfree(H, h.nl);
     h.nl = nullptr;
     h.nb_cap = cap;
-    h.nl = dalloc<int>(H, (size_t)4 * h.nb_cap * h.n);
-    if (!h.nl_cnt) h.nl_cnt = dalloc<int>(H, (size_t)4 * h.n);
+    h.nl = dalloc<int>(H, (size_t)4 * h.nb_cap * rows);
+    if (!h.nl_cnt) h.nl_cnt = dalloc<int>(H, (size_t)4 * rows);
 }
 
 // getEwaldParamValue, ReferenceCoulKernels.cpp:32-35
@@ -441,6 +442,21 @@ CF_EXPORT int cf_create(const cf_params* p, const cf_options* opt, cf_handle** o
                       "sort temp query");
             h.sort_tmp_bytes = tmp;
             h.sort_tmp = dalloc<char>(H, tmp);
+            h.key_tmp = dalloc<int>(H, n);
+            h.atom_tmp = dalloc<int>(H, n);
+            h.skin_flag = dalloc<int>(H, 1);
+            h.n_builds_dev = dalloc<long long>(H, 1);
+            check_hip(hipMemset(h.n_builds_dev, 0, sizeof(long long)), "memset");
+            if (h.world > 1) {  // owned atoms compacted in cell-sorted order
+                h.own_s = dalloc<int>(H, std::max(nown, 1));
+                h.own_flag = dalloc<int>(H, n);
+                h.own_pre = dalloc<int>(H, n);
+                size_t sb = 0;
+                check_hip(hipcub::DeviceScan::ExclusiveSum(nullptr, sb, h.own_flag, h.own_pre, n, h.stream),
+                          "scan temp query");
+                h.scan_tmp_bytes = sb;
+                h.scan_tmp = dalloc<char>(H, sb);
+            }
             std::copy(p->default_box, p->default_box + 9, H->default_box);
             alloc_nlist(H, 0.0);
             if (h.kspace_algo == 0) {
@@ -488,8 +504,6 @@ CF_EXPORT int cf_destroy(cf_handle* H) {
             for (hipEvent_t e : v) (void)hipEventDestroy(e);
         if (H->h.cell_start) (void)hipFree(H->h.cell_start);
         if (H->h.cell_end) (void)hipFree(H->h.cell_end);
-        if (H->h.skin_flag_host) (void)hipHostFree(H->h.skin_flag_host);
-        if (H->h.skin_event) (void)hipEventDestroy(H->h.skin_event);
         if (H->h.own_stream) (void)hipStreamDestroy(H->h.stream);
         delete H;
     });
@@ -519,18 +533,23 @@ CF_EXPORT int cf_set_neighbor_skin(cf_handle* H, double skin) {
         h.list_valid = false;
         if (!h.pbc) return;
         alloc_nlist(H, skin);
-        if (skin > 0 && !h.pos_ref) {
-            h.pos_ref = dalloc<double>(H, (size_t)3 * h.n);
-            h.skin_flag = dalloc<int>(H, 1);
-            check_hip(hipHostMalloc((void**)&h.skin_flag_host, sizeof(int)), "pinned flag");
-            check_hip(hipEventCreateWithFlags(&h.skin_event, hipEventDisableTiming), "skin event");
-        }
+        if (skin > 0 && !h.pos_ref) h.pos_ref = dalloc<double>(H, (size_t)3 * h.n);
     });
 }
 
 CF_EXPORT int cf_get_neighbor_stats(const cf_handle* H, int64_t* builds, int64_t* evaluations) {
     if (!H) { g_err = "null handle"; return CF_ERR_INVALID; }
-    if (builds) *builds = H->h.n_builds;
+    if (builds) {
+        long long b = 0;
+        if (H->h.n_builds_dev) {
+            (void)hipSetDevice(H->h.device);
+            if (hipMemcpy(&b, H->h.n_builds_dev, sizeof(b), hipMemcpyDeviceToHost) != hipSuccess) {
+                g_err = "hipMemcpy failed";
+                return CF_ERR_HIP;
+            }
+        }
+        *builds = b;
+    }
     if (evaluations) *evaluations = H->h.n_evals;
     return CF_OK;
 }
@@ -561,14 +580,28 @@ CF_EXPORT int cf_compute_begin(cf_handle* H, const double* pos_dev, const double
         { Timed t(H, PH_PREP); cf::launch_atoms_prep(h, pos_dev); }
         if (h.pbc) {
             // neighbour list: rebuilt on every call (skin 0, the reference's behaviour,
-            // RCK:559), or kept while no atom has moved more than half the skin.  The
-            // device-side displacement check is queued first; the host reads its flag only
-            // after the k-space work is queued, so the GPU never idles on the decision.
+            // RCK:559), or kept while no atom has moved more than half the skin.  The host
+            // forces a rebuild (first call, new box, skin change); otherwise k_skin_check
+            // decides on the device and the cell commit / list kernels follow its flag, so
+            // nothing waits on the host and the sequence is graph-capturable.
             const double Lmin = std::min(h.box_L[0], std::min(h.box_L[1], h.box_L[2]));
             const double s_call = h.skin > 0 ? std::max(0.0, std::min(h.skin, 0.5 * Lmin - h.cutoff)) : 0.0;
             const bool reusable = h.skin > 0 && h.list_valid && s_call == h.list_skin &&
                                   h.list_L[0] == h.box_L[0] && h.list_L[1] == h.box_L[1] && h.list_L[2] == h.box_L[2];
-            if (reusable) { Timed t(H, PH_CELLS); cf::launch_skin_check(h, pos_dev); }
+            {
+                Timed t(H, PH_CELLS);
+                if (reusable) {
+                    cf::launch_skin_check(h, pos_dev);
+                } else {
+                    h.list_skin = s_call;
+                    set_cells(H, h.box_L);
+                    cf::launch_force_rebuild(h);
+                    h.list_valid = h.skin > 0;
+                    std::copy(h.box_L, h.box_L + 3, h.list_L);
+                }
+                cf::launch_cell_sort(h, pos_dev);
+            }
+            if (h.hi > h.lo) { Timed t(H, PH_NLIST); cf::launch_nlist(h, pos_dev); }
             if ((forces || energy) && h.hi > h.lo) {
                 if (h.kspace_algo == 0) {
                     { Timed t(H, PH_TABLES); cf::launch_kspace_tables(h, pos_dev); }
@@ -582,27 +615,11 @@ CF_EXPORT int cf_compute_begin(cf_handle* H, const double* pos_dev, const double
                 double* buf = cf::kspace_reduce_buffer(h, &cnt);
                 check_hip(hipMemsetAsync(buf, 0, sizeof(double) * cnt, h.stream), "memset S");
             }
-            bool rebuild = true;
-            if (reusable) {
-                check_hip(hipEventSynchronize(h.skin_event), "skin flag wait");
-                rebuild = *h.skin_flag_host != 0;
-            }
-            if (rebuild) {
-                h.list_skin = s_call;
-                set_cells(H, h.box_L);
-                { Timed t(H, PH_CELLS); cf::launch_cell_sort(h, pos_dev); }
-                if (h.hi > h.lo) { Timed t(H, PH_NLIST); cf::launch_nlist(h, pos_dev); }
-                h.list_valid = h.skin > 0;
-                std::copy(h.box_L, h.box_L + 3, h.list_L);
-                h.n_builds++;
-            } else {
-                Timed t(H, PH_CELLS);
-                cf::launch_pos_refresh(h, pos_dev);
-            }
         }
         h.n_evals++;
         launch_check("compute_begin");
         h.pending_flags = flags;
+        h.direct_done = false;
         H->pos_pending = pos_dev;
     });
 }
@@ -615,14 +632,39 @@ CF_EXPORT int cf_kspace_buffer(cf_handle* H, double** buf, int64_t* count) {
     });
 }
 
+// direct space + exclusion correction of a begun evaluation: independent of the
+// structure factors, so a multi-rank caller can run it while S(k) is being all-reduced
+static void run_direct(cf_handle* H) {
+    cf::Handle& h = H->h;
+    if (h.direct_done) return;
+    h.direct_done = true;
+    if (h.hi <= h.lo) return;
+    const int flags = h.pending_flags;
+    const int forces = flags & CF_INCLUDE_FORCES, energy = flags & CF_INCLUDE_ENERGY;
+    Timed t(H, PH_DIRECT);
+    if (h.pbc) cf::launch_direct(h, H->pos_pending, forces);
+    else cf::launch_nopbc(h, H->pos_pending, forces, energy);
+}
+
+CF_EXPORT int cf_compute_direct(cf_handle* H) {
+    return guarded([&] {
+        if (!H) fail(CF_ERR_INVALID, "null handle");
+        if (H->h.pending_flags < 0) fail(CF_ERR_STATE, "cf_compute_direct without cf_compute_begin");
+        check_hip(hipSetDevice(H->h.device), "hipSetDevice");
+        run_direct(H);
+        launch_check("compute_direct");
+    });
+}
+
 CF_EXPORT int cf_compute_end(cf_handle* H, double* forces_dev, double* energy_dev) {
     return guarded([&] {
         if (!H) fail(CF_ERR_INVALID, "null handle");
         cf::Handle& h = H->h;
         if (h.pending_flags < 0) fail(CF_ERR_STATE, "cf_compute_end without cf_compute_begin");
+        check_hip(hipSetDevice(h.device), "hipSetDevice");
+        run_direct(H);
         const int flags = h.pending_flags;
         h.pending_flags = -1;
-        check_hip(hipSetDevice(h.device), "hipSetDevice");
         const int forces = flags & CF_INCLUDE_FORCES, energy = flags & CF_INCLUDE_ENERGY;
         const double* pos = H->pos_pending;
         if (h.hi > h.lo) {
@@ -636,11 +678,8 @@ CF_EXPORT int cf_compute_end(cf_handle* H, double* forces_dev, double* energy_de
                     Timed t(H, PH_FORCE);
                     if (h.kspace_algo == 0) cf::launch_kspace_force(h, pos);
                     else cf::launch_kspace_direct_force(h, pos);
+                    cf::launch_recip_add(h);
                 }
-                { Timed t(H, PH_DIRECT); cf::launch_direct(h, pos, forces); }
-            } else {
-                Timed t(H, PH_DIRECT);
-                cf::launch_nopbc(h, pos, forces, energy);
             }
             if (forces && forces_dev) { Timed t(H, PH_ASSEMBLE); cf::launch_assemble(h, forces_dev); }
         }

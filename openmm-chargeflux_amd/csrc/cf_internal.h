@@ -114,11 +114,17 @@ struct Handle {
     double list_skin = 0.0;     // skin the current list was built with
     double list_L[3] = {0, 0, 0};
     bool list_valid = false;
-    double* pos_ref = nullptr;  // [N*3] positions at the last build
-    int* skin_flag = nullptr;   // [1] device: some atom moved > list_skin/2
-    int* skin_flag_host = nullptr;  // pinned copy
-    hipEvent_t skin_event = nullptr;
-    int64_t n_builds = 0, n_evals = 0;
+    double* pos_ref = nullptr;  // [N*3] positions at the last build (skin > 0)
+    int* skin_flag = nullptr;   // [1] device: rebuild this evaluation (host-forced or moved > skin/2)
+    long long* n_builds_dev = nullptr;  // [1] list builds (device counter)
+    int64_t n_evals = 0;
+    // every evaluation sorts into scratch; k_cell_commit copies it to the live arrays only
+    // when the flag is set (the decision never leaves the device)
+    int* key_tmp = nullptr; int* atom_tmp = nullptr;
+    // multi-rank: owned atoms compacted in cell-sorted order (list rows)
+    int* own_s = nullptr;       // [N_own] (null on one rank: identity)
+    int* own_flag = nullptr; int* own_pre = nullptr;  // [N]
+    void* scan_tmp = nullptr; size_t scan_tmp_bytes = 0;
     int nb_cap = 0;             // capacity of each of the 4 neighbour sub-lists of an atom
     int* nl = nullptr;          // [4][nb_cap][N] transposed sub-lists (sorted index | shift<<26)
     int* nl_cnt = nullptr;      // [4][N]
@@ -144,6 +150,7 @@ struct Handle {
     double* energy_dev = nullptr;// [1] internal
     // state
     int pending_flags = -1;     // flags of a begun evaluation
+    bool direct_done = false;   // cf_compute_direct already ran for the begun evaluation
     double box_L[3] = {0, 0, 0};
 };
 
@@ -151,10 +158,11 @@ struct Handle {
 void launch_flux_terms(Handle& h, const double* pos);
 void launch_atoms_prep(Handle& h, const double* pos);
 void launch_cell_sort(Handle& h, const double* pos);
-void launch_skin_check(Handle& h, const double* pos);   // -> skin_flag, skin_flag_host, skin_event
-void launch_pos_refresh(Handle& h, const double* pos);  // sorted positions/charges, list kept
+void launch_skin_check(Handle& h, const double* pos);   // skin_flag = some atom moved > list_skin/2
+void launch_force_rebuild(Handle& h);                   // skin_flag = 1
 void launch_nlist(Handle& h, const double* pos);
 void launch_direct(Handle& h, const double* pos, int include_forces);
+void launch_recip_add(Handle& h);   // dedq, f_part += reciprocal partials
 void launch_nopbc(Handle& h, const double* pos, int include_forces, int include_energy);
 void launch_assemble(Handle& h, double* forces_out);
 void launch_energy(Handle& h, int include_energy, double* energy_out);

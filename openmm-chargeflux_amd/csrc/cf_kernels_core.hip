@@ -152,38 +152,60 @@ __global__ void __launch_bounds__(256) k_cell_keys(int n, const double* __restri
     val[i] = i;
 }
 
-__global__ void __launch_bounds__(256) k_cell_gather(int n, const int* __restrict__ key_s, const int* __restrict__ idx_s,
+// rebuild (flag set): commit the freshly sorted order (scratch -> live), cell bounds,
+// sorted wrapped (x,y,z,q) + LJ, build positions, owned-atom compaction.
+// no rebuild: the sorted order and every atom's periodic image are kept from the last
+// build (wrap offsets recomputed from the build positions, so bit-identical to the commit),
+// only coordinates and flux charges are refreshed.
+__global__ void __launch_bounds__(256) k_cell_commit(int n, const int* __restrict__ flag,
+                                                     const int* __restrict__ key_tmp, const int* __restrict__ idx_tmp,
+                                                     const int* __restrict__ own_pre, int lo, int hi,
                                                      const double* __restrict__ pos, const double* __restrict__ q,
                                                      const double2* __restrict__ lj, double3 L,
+                                                     int* __restrict__ key_s, int* __restrict__ idx_s,
                                                      int* __restrict__ cstart, int* __restrict__ cend,
                                                      double4* __restrict__ pos4s, double2* __restrict__ ljs,
-                                                     double* __restrict__ pos_ref) {
+                                                     double* __restrict__ pos_ref, int* __restrict__ own_s,
+                                                     long long* __restrict__ n_builds) {
     int s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= n) return;
-    int k = key_s[s];
-    if (s == 0 || key_s[s - 1] != k) cstart[k] = s;
-    if (s == n - 1 || key_s[s + 1] != k) cend[k] = s + 1;
-    int i = idx_s[s];
-    double3 x = ld3(pos, i);
-    pos4s[s] = make_double4(x.x - floor(x.x / L.x) * L.x, x.y - floor(x.y / L.y) * L.y,
-                            x.z - floor(x.z / L.z) * L.z, q[i]);
-    ljs[s] = lj[i];
-    if (pos_ref) { pos_ref[3 * i] = x.x; pos_ref[3 * i + 1] = x.y; pos_ref[3 * i + 2] = x.z; }
+    if (*flag) {
+        int k = key_tmp[s];
+        if (s == 0 || key_tmp[s - 1] != k) cstart[k] = s;
+        if (s == n - 1 || key_tmp[s + 1] != k) cend[k] = s + 1;
+        int i = idx_tmp[s];
+        key_s[s] = k;
+        idx_s[s] = i;
+        double3 x = ld3(pos, i);
+        pos4s[s] = make_double4(x.x - floor(x.x / L.x) * L.x, x.y - floor(x.y / L.y) * L.y,
+                                x.z - floor(x.z / L.z) * L.z, q[i]);
+        ljs[s] = lj[i];
+        if (pos_ref) { pos_ref[3 * i] = x.x; pos_ref[3 * i + 1] = x.y; pos_ref[3 * i + 2] = x.z; }
+        if (own_s && i >= lo && i < hi) own_s[own_pre[s]] = s;
+        if (s == 0) *n_builds += 1;
+    } else {
+        int i = idx_s[s];
+        double3 x = ld3(pos, i), r = ld3(pos_ref, i);
+        pos4s[s] = make_double4(x.x - floor(r.x / L.x) * L.x, x.y - floor(r.y / L.y) * L.y,
+                                x.z - floor(r.z / L.z) * L.z, q[i]);
+    }
 }
 
-// Between list rebuilds (skin > 0): the sorted order and every atom's periodic image are
-// kept from the last build (wrap offsets recomputed from the build positions, so they are
-// bit-identical to k_cell_gather's), only coordinates and flux charges are refreshed.
-__global__ void __launch_bounds__(256) k_pos_refresh(int n, const int* __restrict__ idx_s,
-                                                     const double* __restrict__ pos, const double* __restrict__ pos_ref,
-                                                     const double* __restrict__ q, double3 L,
-                                                     double4* __restrict__ pos4s) {
+__global__ void __launch_bounds__(256) k_cell_clear(int ncell, const int* __restrict__ flag, int* __restrict__ cstart,
+                                                    int* __restrict__ cend) {
+    int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= ncell || !*flag) return;
+    cstart[c] = 0;
+    cend[c] = 0;
+}
+
+// owned flags of the freshly sorted order (multi-rank): prefix sum -> compact row index
+__global__ void __launch_bounds__(256) k_own_flags(int n, const int* __restrict__ idx_tmp, int lo, int hi,
+                                                   int* __restrict__ f) {
     int s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= n) return;
-    int i = idx_s[s];
-    double3 x = ld3(pos, i), r = ld3(pos_ref, i);
-    pos4s[s] = make_double4(x.x - floor(r.x / L.x) * L.x, x.y - floor(r.y / L.y) * L.y,
-                            x.z - floor(r.z / L.z) * L.z, q[i]);
+    int i = idx_tmp[s];
+    f[s] = (i >= lo && i < hi) ? 1 : 0;
 }
 
 // list validity: flag = 1 if any atom moved more than half the skin since the last build
@@ -224,16 +246,20 @@ struct DirectArgs {
     double rc2, alpha;
     double rl2;                 // list radius^2: (rc + list skin)^2
     int nb_cap;                 // capacity of ONE of the kSeg sub-lists
+    int nlr;                    // list rows = owned atoms; row c <-> sorted slot own_slot(c)
+    const int* own_s;           // [nlr] cell-sorted slots of the owned atoms (null: identity)
+    const int* flag;            // rebuild flag (list kernels exit when 0)
     const int* atom_sorted; const int* key_sorted;
     const int* cstart; const int* cend;
     const double4* pos4s; const double2* ljs;
     const double* pos; const double* q;
     const int* ex_start; const int* ex_list;
     const double* dedq_self;
-    const double* t_part; int nparts; int nown;  // reciprocal partials [p][nown][4]
     int* nl; int* nl_cnt;
     double* dedq; double* f_part; double* e_atom;
 };
+
+__device__ __forceinline__ int own_slot(const DirectArgs& a, int c) { return a.own_s ? a.own_s[c] : c; }
 
 __device__ __forceinline__ bool in_excl(int j, const int* reg, int cnt, const int* ex_list, int ex0) {
     int m = cnt < kMaxRegExcl ? cnt : kMaxRegExcl;
@@ -295,10 +321,10 @@ __device__ __forceinline__ void scan_cells(const DirectArgs& a, int s, double4 p
 }
 
 __global__ void __launch_bounds__(256) k_nlist(DirectArgs a) {
-    int s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= a.n) return;
+    int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= a.nlr || !*a.flag) return;
+    int s = own_slot(a, c);
     int i = a.atom_sorted[s];
-    if (i < a.lo || i >= a.hi) return;
     const double4 pi = a.pos4s[s];
     const int ex0 = a.ex_start[i], exc = a.ex_start[i + 1] - ex0;
     int reg[kMaxRegExcl];
@@ -308,10 +334,10 @@ __global__ void __launch_bounds__(256) k_nlist(DirectArgs a) {
         int cnt = 0;
         scan_cells(a, s, pi, a.rl2, [&](int t, int code, double, double, double, double) {
             if (exc && in_excl(a.atom_sorted[t], reg, exc, a.ex_list, ex0)) return;
-            if (cnt < a.nb_cap) a.nl[((size_t)seg * a.nb_cap + cnt) * a.n + s] = t | (code << kShiftBits);
+            if (cnt < a.nb_cap) a.nl[((size_t)seg * a.nb_cap + cnt) * a.nlr + c] = t | (code << kShiftBits);
             cnt++;
         }, seg, kSeg);
-        a.nl_cnt[(size_t)seg * a.n + s] = cnt;
+        a.nl_cnt[(size_t)seg * a.nlr + c] = cnt;
     }
 }
 
@@ -337,18 +363,17 @@ __global__ void __launch_bounds__(kWaveNL * kSeg) k_nlist_wave(DirectArgs a) {
     const int seg = threadIdx.x >> 6;   // this wave's share of the cell box and its sub-list
     float4* cand = cand_all[seg];
     int* cand_j = cand_j_all[seg];
+    if (!*a.flag) return;  // list still valid (skin): nothing to build
     const int base = blockIdx.x * kWaveNL;
-    const int s = base + lane;
-    const bool valid = s < a.n;
-    const int ss = valid ? s : a.n - 1;
-    const int i = a.atom_sorted[ss];
-    const bool active = valid && i >= a.lo && i < a.hi;
-    if (__ballot(active) == 0) return;  // no owned atom in this block (multi-GPU): skip it whole
-    const double4 pi = a.pos4s[ss];
-    const int key = a.key_sorted[ss];
+    const int c = base + lane;  // list row (owned atom, cell-sorted order)
+    const bool active = c < a.nlr;
+    const int s = own_slot(a, active ? c : a.nlr - 1);
+    const int i = a.atom_sorted[s];
+    const double4 pi = a.pos4s[s];
+    const int key = a.key_sorted[s];
     const size_t seg_off = (size_t)seg * a.nb_cap;
-    const int c[3] = {key / (a.nc.y * a.nc.z), (key / a.nc.z) % a.nc.y, key % a.nc.z};
-    const int key0 = a.key_sorted[base];
+    const int cl[3] = {key / (a.nc.y * a.nc.z), (key / a.nc.z) % a.nc.y, key % a.nc.z};
+    const int key0 = a.key_sorted[__shfl(s, 0)];
     const int c0[3] = {key0 / (a.nc.y * a.nc.z), (key0 / a.nc.z) % a.nc.y, key0 % a.nc.z};
     const int ncs[3] = {a.nc.x, a.nc.y, a.nc.z};
     const double Ls[3] = {a.L.x, a.L.y, a.L.z};
@@ -356,7 +381,7 @@ __global__ void __launch_bounds__(kWaveNL * kSeg) k_nlist_wave(DirectArgs a) {
     bool fits = true;
 #pragma unroll
     for (int d = 0; d < 3; d++) {
-        int dd = c[d] - c0[d];
+        int dd = cl[d] - c0[d];
         if (dd > ncs[d] / 2) dd -= ncs[d];
         if (dd < -(ncs[d] / 2)) dd += ncs[d];
         int u = c0[d] + dd;  // unwrapped cell coordinate of this lane in the block frame
@@ -378,14 +403,14 @@ __global__ void __launch_bounds__(kWaveNL * kSeg) k_nlist_wave(DirectArgs a) {
     int cnt = 0;
     auto emit = [&](int t, int j, int code) {
         if (j >= ex_min && j <= ex_max && in_excl(j, reg, exc, a.ex_list, ex0)) return;
-        if (cnt < a.nb_cap) a.nl[(seg_off + cnt) * a.n + s] = t | (code << kShiftBits);
+        if (cnt < a.nb_cap) a.nl[(seg_off + cnt) * a.nlr + c] = t | (code << kShiftBits);
         cnt++;
     };
     if (!fits) {  // wave-uniform (and block-uniform: every wave sees the same 64 atoms)
         if (active)
             scan_cells(a, s, pi, a.rl2, [&](int t, int code, double, double, double, double) { emit(t, a.atom_sorted[t], code); },
                        seg, kSeg);
-        if (active) a.nl_cnt[(size_t)seg * a.n + s] = cnt;
+        if (active) a.nl_cnt[(size_t)seg * a.nlr + c] = cnt;
         return;
     }
 
@@ -501,7 +526,7 @@ __global__ void __launch_bounds__(kWaveNL * kSeg) k_nlist_wave(DirectArgs a) {
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     }
-    if (active) a.nl_cnt[(size_t)seg * a.n + s] = cnt;
+    if (active) a.nl_cnt[(size_t)seg * a.nlr + c] = cnt;
 }
 
 // 1/sqrt(r2) to full fp64 accuracy: hardware v_rsq_f64 estimate + two Newton steps
@@ -566,42 +591,57 @@ __device__ __forceinline__ void finish_atom(PairAcc acc, const DirectArgs& a, in
     }
     a.e_atom[3 * i + 1] = acc.e;
     a.e_atom[3 * i + 2] = ex_e;
-    if (a.include_forces) {
-        double dr = 0, rx = 0, ry = 0, rz = 0;
-        int io = i - a.lo;
-        for (int p = 0; p < a.nparts; p++) {
-            const double* tp = a.t_part + ((size_t)p * a.nown + io) * 4;
-            dr += tp[0]; rx += tp[1]; ry += tp[2]; rz += tp[3];
-        }
-        a.dedq[i] = a.dedq_self[i] + dr + acc.dq;
-        a.f_part[3 * i] = rx + acc.fx;
-        a.f_part[3 * i + 1] = ry + acc.fy;
-        a.f_part[3 * i + 2] = rz + acc.fz;
+    if (a.include_forces) {  // reciprocal partials are added by k_recip_add after the k-space pass
+        a.dedq[i] = a.dedq_self[i] + acc.dq;
+        a.f_part[3 * i] = acc.fx;
+        a.f_part[3 * i + 1] = acc.fy;
+        a.f_part[3 * i + 2] = acc.fz;
     }
+}
+
+// dE/dq and non-chain forces += reciprocal partials (fixed part order: deterministic)
+__global__ void __launch_bounds__(256) k_recip_add(int lo, int nown, int nparts, const double* __restrict__ t_part,
+                                                   double* __restrict__ dedq, double* __restrict__ f_part) {
+    int io = blockIdx.x * blockDim.x + threadIdx.x;
+    if (io >= nown) return;
+    double dr = 0, rx = 0, ry = 0, rz = 0;
+    for (int p = 0; p < nparts; p++) {
+        const double* tp = t_part + ((size_t)p * nown + io) * 4;
+        dr += tp[0]; rx += tp[1]; ry += tp[2]; rz += tp[3];
+    }
+    int i = lo + io;
+    dedq[i] += dr;
+    f_part[3 * i] += rx;
+    f_part[3 * i + 1] += ry;
+    f_part[3 * i + 2] += rz;
 }
 
 // 4b: walk the list — kSeg adjacent lanes per atom, lane g walks sub-list g; partial sums
 // are combined with two xor-shuffles (fixed order: deterministic).  Atoms with an
 // overflowed sub-list are left to k_pairs_overflow.
+// LPA lanes per atom (4, 8 or 16; more when few atoms are owned, so the grid still fills
+// the chip): lane g walks entries g/4, g/4 + LPA/4, ... of sub-list g%4.
+template <int LPA>
 __global__ void __launch_bounds__(256) k_pairs(DirectArgs a) {
     const int gt = blockIdx.x * blockDim.x + threadIdx.x;
-    const int s = gt / kSeg, g = gt % kSeg;
-    const bool valid = s < a.n;
-    const int ss = valid ? s : a.n - 1;
+    const int c = gt / LPA, g = gt % LPA;
+    const int seg = g % kSeg, part = g / kSeg;
+    bool active = c < a.nlr;
+    const int cc = active ? c : a.nlr - 1;
+    const int ss = own_slot(a, cc);
     const int i = a.atom_sorted[ss];
-    bool active = valid && i >= a.lo && i < a.hi;
-    int cnt = active ? a.nl_cnt[(size_t)g * a.n + ss] : 0;
+    int cnt = active ? a.nl_cnt[(size_t)seg * a.nlr + cc] : 0;
     bool over = cnt > a.nb_cap;
-    over = __shfl_xor(over, 1) || over;
-    over = __shfl_xor(over, 2) || over;
+#pragma unroll
+    for (int m = 1; m < LPA; m <<= 1) over = __shfl_xor(over, m) || over;
     if (over) active = false;
     PairAcc acc;
     if (active) {
         const double4 pi = a.pos4s[ss];
         const double2 li = a.ljs[ss];
-        const int* nl = a.nl + (size_t)g * a.nb_cap * a.n + ss;
-        for (int k = 0; k < cnt; k++) {
-            int v = nl[(size_t)k * a.n];
+        const int* nl = a.nl + (size_t)seg * a.nb_cap * a.nlr + cc;
+        for (int k = part; k < cnt; k += LPA / kSeg) {
+            int v = nl[(size_t)k * a.nlr];
             int t = v & ((1 << kShiftBits) - 1), code = v >> kShiftBits;
             double4 pj = a.pos4s[t];
             double2 lj2 = a.ljs[t];
@@ -618,7 +658,7 @@ __global__ void __launch_bounds__(256) k_pairs(DirectArgs a) {
         }
     }
 #pragma unroll
-    for (int m = 1; m < kSeg; m <<= 1) {
+    for (int m = 1; m < LPA; m <<= 1) {
         acc.fx += __shfl_xor(acc.fx, m); acc.fy += __shfl_xor(acc.fy, m); acc.fz += __shfl_xor(acc.fz, m);
         acc.dq += __shfl_xor(acc.dq, m); acc.e += __shfl_xor(acc.e, m);
     }
@@ -629,13 +669,13 @@ __global__ void __launch_bounds__(256) k_pairs(DirectArgs a) {
 
 // 4c: atoms whose neighbour list overflowed (denser than planned): rescan the cells
 __global__ void __launch_bounds__(256) k_pairs_overflow(DirectArgs a) {
-    int s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= a.n) return;
+    int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= a.nlr) return;
     bool over = false;
-    for (int g = 0; g < kSeg; g++) over = over || a.nl_cnt[(size_t)g * a.n + s] > a.nb_cap;
+    for (int g = 0; g < kSeg; g++) over = over || a.nl_cnt[(size_t)g * a.nlr + c] > a.nb_cap;
     if (!over) return;
+    int s = own_slot(a, c);
     int i = a.atom_sorted[s];
-    if (i < a.lo || i >= a.hi) return;
     const double4 pi = a.pos4s[s];
     const double2 li = a.ljs[s];
     const int ex0 = a.ex_start[i], exc = a.ex_start[i + 1] - ex0;
@@ -796,13 +836,20 @@ void launch_cell_sort(Handle& h, const double* pos) {
     int end_bit = 1;
     while ((1 << end_bit) < ncell) end_bit++;
     size_t bytes = h.sort_tmp_bytes;
-    check_hip(hipcub::DeviceRadixSort::SortPairs(h.sort_tmp, bytes, h.cell_key, h.cell_key_sorted, h.atom_val,
-                                                 h.atom_sorted, h.n, 0, end_bit, h.stream),
+    check_hip(hipcub::DeviceRadixSort::SortPairs(h.sort_tmp, bytes, h.cell_key, h.key_tmp, h.atom_val, h.atom_tmp,
+                                                 h.n, 0, end_bit, h.stream),
               "radix sort");
-    check_hip(hipMemsetAsync(h.cell_start, 0, sizeof(int) * ncell, h.stream), "memset cell_start");
-    check_hip(hipMemsetAsync(h.cell_end, 0, sizeof(int) * ncell, h.stream), "memset cell_end");
-    hipLaunchKernelGGL(k_cell_gather, dim3(nblk(h.n, 256)), dim3(256), 0, h.stream, h.n, h.cell_key_sorted,
-                       h.atom_sorted, pos, h.q, h.lj, L, h.cell_start, h.cell_end, h.pos4s, h.ljs, h.pos_ref);
+    if (h.own_s) {
+        hipLaunchKernelGGL(k_own_flags, dim3(nblk(h.n, 256)), dim3(256), 0, h.stream, h.n, h.atom_tmp, h.lo, h.hi,
+                           h.own_flag);
+        size_t sb = h.scan_tmp_bytes;
+        check_hip(hipcub::DeviceScan::ExclusiveSum(h.scan_tmp, sb, h.own_flag, h.own_pre, h.n, h.stream), "scan");
+    }
+    hipLaunchKernelGGL(k_cell_clear, dim3(nblk(ncell, 256)), dim3(256), 0, h.stream, ncell, h.skin_flag,
+                       h.cell_start, h.cell_end);
+    hipLaunchKernelGGL(k_cell_commit, dim3(nblk(h.n, 256)), dim3(256), 0, h.stream, h.n, h.skin_flag, h.key_tmp,
+                       h.atom_tmp, h.own_pre, h.lo, h.hi, pos, h.q, h.lj, L, h.cell_key_sorted, h.atom_sorted,
+                       h.cell_start, h.cell_end, h.pos4s, h.ljs, h.pos_ref, h.own_s, h.n_builds_dev);
 }
 
 void launch_skin_check(Handle& h, const double* pos) {
@@ -810,15 +857,10 @@ void launch_skin_check(Handle& h, const double* pos) {
     const double lim = 0.5 * h.list_skin;
     hipLaunchKernelGGL(k_skin_check, dim3(nblk(h.n, 256)), dim3(256), 0, h.stream, h.n, pos, h.pos_ref, lim * lim,
                        h.skin_flag);
-    check_hip(hipMemcpyAsync(h.skin_flag_host, h.skin_flag, sizeof(int), hipMemcpyDeviceToHost, h.stream),
-              "skin flag copy");
-    check_hip(hipEventRecord(h.skin_event, h.stream), "skin event");
 }
 
-void launch_pos_refresh(Handle& h, const double* pos) {
-    double3 L = make_double3(h.box_L[0], h.box_L[1], h.box_L[2]);
-    hipLaunchKernelGGL(k_pos_refresh, dim3(nblk(h.n, 256)), dim3(256), 0, h.stream, h.n, h.atom_sorted, pos,
-                       h.pos_ref, h.q, L, h.pos4s);
+void launch_force_rebuild(Handle& h) {
+    check_hip(hipMemsetD32Async(h.skin_flag, 1, 1, h.stream), "set rebuild flag");
 }
 
 static DirectArgs direct_args(Handle& h, const double* pos, int include_forces) {
@@ -830,13 +872,14 @@ static DirectArgs direct_args(Handle& h, const double* pos, int include_forces) 
     a.rc2 = h.cutoff * h.cutoff; a.alpha = h.alpha;
     a.rl2 = (h.cutoff + h.list_skin) * (h.cutoff + h.list_skin);
     a.nb_cap = h.nb_cap;
+    a.nlr = h.hi - h.lo;
+    a.own_s = h.own_s;
+    a.flag = h.skin_flag;
     a.atom_sorted = h.atom_sorted; a.key_sorted = h.cell_key_sorted;
     a.cstart = h.cell_start; a.cend = h.cell_end;
     a.pos4s = h.pos4s; a.ljs = h.ljs;
     a.q = h.q; a.ex_start = h.ex_start; a.ex_list = h.ex_list;
     a.dedq_self = h.dedq_self;
-    a.nparts = h.kspace_algo == 1 ? 1 : h.fp.nparts();
-    a.t_part = h.t_part; a.nown = h.hi - h.lo;
     a.nl = h.nl; a.nl_cnt = h.nl_cnt;
     a.dedq = h.dedq; a.f_part = h.f_part; a.e_atom = h.e_atom;
     a.pos = pos;
@@ -846,15 +889,29 @@ static DirectArgs direct_args(Handle& h, const double* pos, int include_forces) 
 void launch_nlist(Handle& h, const double* pos) {
     DirectArgs a = direct_args(h, pos, 0);
     if (a.brute || h.nc[0] < 4 || h.nc[1] < 4 || h.nc[2] < 4)
-        hipLaunchKernelGGL(k_nlist, dim3(nblk(h.n, 256)), dim3(256), 0, h.stream, a);
+        hipLaunchKernelGGL(k_nlist, dim3(nblk(a.nlr, 256)), dim3(256), 0, h.stream, a);
     else
-        hipLaunchKernelGGL(k_nlist_wave, dim3(nblk(h.n, kWaveNL)), dim3(kWaveNL * kSeg), 0, h.stream, a);
+        hipLaunchKernelGGL(k_nlist_wave, dim3(nblk(a.nlr, kWaveNL)), dim3(kWaveNL * kSeg), 0, h.stream, a);
 }
 
 void launch_direct(Handle& h, const double* pos, int include_forces) {
     DirectArgs a = direct_args(h, pos, include_forces);
-    hipLaunchKernelGGL(k_pairs, dim3(nblk((int64_t)h.n * kSeg, 256)), dim3(256), 0, h.stream, a);
-    hipLaunchKernelGGL(k_pairs_overflow, dim3(nblk(h.n, 256)), dim3(256), 0, h.stream, a);
+    // lanes per atom: enough threads for ~2 waves per SIMD on 256 CUs
+    const int64_t want = 256LL * 4 * 2 * 64;
+    if ((int64_t)a.nlr * 4 >= want)
+        hipLaunchKernelGGL(k_pairs<4>, dim3(nblk((int64_t)a.nlr * 4, 256)), dim3(256), 0, h.stream, a);
+    else if ((int64_t)a.nlr * 8 >= want)
+        hipLaunchKernelGGL(k_pairs<8>, dim3(nblk((int64_t)a.nlr * 8, 256)), dim3(256), 0, h.stream, a);
+    else
+        hipLaunchKernelGGL(k_pairs<16>, dim3(nblk((int64_t)a.nlr * 16, 256)), dim3(256), 0, h.stream, a);
+    hipLaunchKernelGGL(k_pairs_overflow, dim3(nblk(a.nlr, 256)), dim3(256), 0, h.stream, a);
+}
+
+void launch_recip_add(Handle& h) {
+    int nown = h.hi - h.lo;
+    int nparts = h.kspace_algo == 1 ? 1 : h.fp.nparts();
+    hipLaunchKernelGGL(k_recip_add, dim3(nblk(nown, 256)), dim3(256), 0, h.stream, h.lo, nown, nparts, h.t_part,
+                       h.dedq, h.f_part);
 }
 
 void launch_nopbc(Handle& h, const double* pos, int include_forces, int include_energy) {

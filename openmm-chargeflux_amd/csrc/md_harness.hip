@@ -1,0 +1,85 @@
+// md_harness.hip — the benchmark's MD harness (NOT part of the CoulForce path): velocity
+// Verlet for the owned atoms and the flexible-water harmonic restraints (O-H, O-H, H-H),
+// fused into two kernels per step so the harness does not dominate small per-rank steps.
+// Built into its own library (libcf_mdharness.so) and driven by bench.py.
+//
+// Step:  md_kick_drift   v += dt/2 f/m ; x += dt v            (owned atoms)
+//        <positions replicated, forces zeroed, CoulForce adds its forces>
+//        md_restrain_kick f += restraint(x) ; v += dt/2 f/m   (owned atoms)
+// Waters are atoms 3w, 3w+1, 3w+2 (O, H, H) for w < n_waters; every atom recomputes the
+// three bonds of its own water, so there are no atomics and the result is deterministic.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#define MD_EXPORT extern "C" __attribute__((visibility("default")))
+
+namespace {
+
+__global__ void __launch_bounds__(256) k_kick_drift(int lo, int hi, double dt, double* __restrict__ x,
+                                                    double* __restrict__ v, const double* __restrict__ f,
+                                                    const double* __restrict__ inv_m) {
+    int i = lo + blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= hi) return;
+    double h = 0.5 * dt * inv_m[i];
+#pragma unroll
+    for (int d = 0; d < 3; d++) {
+        double vv = v[3 * i + d] + h * f[3 * i + d];
+        v[3 * i + d] = vv;
+        x[3 * i + d] += dt * vv;
+    }
+}
+
+__device__ __forceinline__ void bond(const double* x, int a, int b, double k, double r0, double g[3]) {
+    double d[3] = {x[3 * b] - x[3 * a], x[3 * b + 1] - x[3 * a + 1], x[3 * b + 2] - x[3 * a + 2]};
+    double r = sqrt(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]);
+    double c = k * (r - r0) / r;
+    g[0] = c * d[0]; g[1] = c * d[1]; g[2] = c * d[2];  // force on a; -g on b
+}
+
+__global__ void __launch_bounds__(256) k_restrain_kick(int lo, int hi, int n_waters, double k_oh, double r_oh,
+                                                       double k_hh, double r_hh, double dt,
+                                                       const double* __restrict__ x, double* __restrict__ v,
+                                                       double* __restrict__ f, const double* __restrict__ inv_m) {
+    int i = lo + blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= hi) return;
+    double fi[3] = {f[3 * i], f[3 * i + 1], f[3 * i + 2]};
+    if (i < 3 * n_waters) {
+        int o = 3 * (i / 3), r = i - o;
+        double g1[3], g2[3], g3[3];
+        bond(x, o, o + 1, k_oh, r_oh, g1);
+        bond(x, o, o + 2, k_oh, r_oh, g2);
+        bond(x, o + 1, o + 2, k_hh, r_hh, g3);
+#pragma unroll
+        for (int d = 0; d < 3; d++) {
+            double add = r == 0 ? g1[d] + g2[d] : (r == 1 ? -g1[d] + g3[d] : -g2[d] - g3[d]);
+            fi[d] += add;
+        }
+    }
+    double h = 0.5 * dt * inv_m[i];
+#pragma unroll
+    for (int d = 0; d < 3; d++) {
+        f[3 * i + d] = fi[d];
+        v[3 * i + d] += h * fi[d];
+    }
+}
+
+inline int nblk(int n) { return (n + 255) / 256; }
+
+}  // namespace
+
+MD_EXPORT int md_kick_drift(int lo, int hi, double dt, double* x, double* v, const double* f, const double* inv_m,
+                            void* stream) {
+    if (hi <= lo) return 0;
+    hipLaunchKernelGGL(k_kick_drift, dim3(nblk(hi - lo)), dim3(256), 0, (hipStream_t)stream, lo, hi, dt, x, v, f,
+                       inv_m);
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+MD_EXPORT int md_restrain_kick(int lo, int hi, int n_waters, double k_oh, double r_oh, double k_hh, double r_hh,
+                               double dt, const double* x, double* v, double* f, const double* inv_m, void* stream) {
+    if (hi <= lo) return 0;
+    hipLaunchKernelGGL(k_restrain_kick, dim3(nblk(hi - lo)), dim3(256), 0, (hipStream_t)stream, lo, hi, n_waters,
+                       k_oh, r_oh, k_hh, r_hh, dt, x, v, f, inv_m);
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+}

@@ -72,6 +72,7 @@ SIGNATURES = [
     ("cf_compute", C.c_int, [C.c_void_p, C.c_void_p, DP, C.c_int, C.c_void_p, C.c_void_p]),
     ("cf_compute_begin", C.c_int, [C.c_void_p, C.c_void_p, DP, C.c_int]),
     ("cf_kspace_buffer", C.c_int, [C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_int64)]),
+    ("cf_compute_direct", C.c_int, [C.c_void_p]),
     ("cf_compute_end", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
     ("cf_compute_host", C.c_int, [C.c_void_p, DP, DP, C.c_int, DP, DP]),
     ("cf_get_charges", C.c_int, [C.c_void_p, DP]),

@@ -50,23 +50,42 @@ class ShardedCoulKernel:
         self.lo, self.hi = self.kernel.owned_range()
         self.energy = torch.zeros(1, dtype=torch.float64, device=self.device)
         self._sbuf = self.kernel.kspace_tensor(self.device)
+        self._gidx = None
+        if self.world > 1:
+            # every rank's owned range -> padded all-gather layout for position replication
+            mine = torch.tensor([self.lo, self.hi], dtype=torch.int64, device=self.device)
+            allr = [torch.zeros_like(mine) for _ in range(self.world)]
+            dist.all_gather(allr, mine, group=self.group)
+            ranges = [tuple(int(v) for v in t.cpu()) for t in allr]
+            self._maxown = max(1, max(h - l for l, h in ranges))
+            rows = []
+            for r, (l, h) in enumerate(ranges):
+                rows.extend(range(r * self._maxown, r * self._maxown + (h - l)))
+            self._gidx = torch.tensor(rows, dtype=torch.int64, device=self.device)
+            self._send = torch.zeros(self._maxown, 3, dtype=torch.float64, device=self.device)
+            self._recv = torch.zeros(self.world * self._maxown, 3, dtype=torch.float64, device=self.device)
 
     def execute(self, positions: torch.Tensor, box, forces: torch.Tensor | None, include_energy: bool = True):
         k = self.kernel
         k.begin(positions, box, forces is not None, include_energy)
         if self.world > 1 and self._sbuf is not None:
-            dist.all_reduce(self._sbuf, op=dist.ReduceOp.SUM, group=self.group)
+            # the direct-space kernels do not need S(k): they run while it is all-reduced
+            work = dist.all_reduce(self._sbuf, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+            if hasattr(k, "direct"):
+                k.direct()
+            work.wait()
         k.end(forces, self.energy)
         if self.world > 1 and include_energy:
             dist.all_reduce(self.energy, op=dist.ReduceOp.SUM, group=self.group)
         return self.energy
 
     def replicate_positions(self, positions: torch.Tensor):
-        """After each rank updated positions[lo:hi], make every rank's copy identical."""
+        """After each rank updated positions[lo:hi], make every rank's copy identical
+        (one all-gather of the owned slices, padded to the largest)."""
         if self.world == 1:
             return positions
-        mask = torch.zeros_like(positions)
-        mask[self.lo:self.hi] = positions[self.lo:self.hi]
-        dist.all_reduce(mask, op=dist.ReduceOp.SUM, group=self.group)
-        positions.copy_(mask)
+        p = positions.view(-1, 3)
+        self._send[: self.hi - self.lo].copy_(p[self.lo:self.hi])
+        dist.all_gather_into_tensor(self._recv, self._send, group=self.group)
+        torch.index_select(self._recv, 0, self._gidx, out=p)
         return positions

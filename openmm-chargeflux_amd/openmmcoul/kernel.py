@@ -181,6 +181,11 @@ class HipCalcCoulForceKernel:
         from .distributed import device_buffer_as_tensor
         return device_buffer_as_tensor(ptr, n, device)
 
+    def direct(self):
+        """Launch the direct-space kernels of the begun evaluation now (optional; lets a
+        multi-rank caller overlap them with the S(k) all-reduce)."""
+        _cabi.check(self._lib.cf_compute_direct(self._h), self._lib)
+
     def end(self, forces=None, energy=None):
         fptr = forces.data_ptr() if forces is not None else None
         eptr = energy.data_ptr() if energy is not None else None

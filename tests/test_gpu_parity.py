@@ -171,6 +171,13 @@ def test_wave_neighbour_path_full_parity():
     _compare(_run(k, pos, box), Oracle(force, box).execute(pos, box))
 
 
+def test_pair_kernel_8_lanes_per_atom():
+    # 7000 waters = 21000 owned atoms: k_pairs runs 8 lanes per atom (4 at C3, 16 below 16k)
+    system, force, pos, box = ts.water_box(7000, cutoff=1.0, ewald_tol=1e-3, every_bond_angle=6)
+    k = HipCalcCoulForceKernel().initialize(system, force)
+    _compare(_run(k, pos, box), Oracle(force, box).execute(pos, box))
+
+
 def test_c3_direct_space_terms_vs_oracle():
     # full C3: self, direct (erfc + LJ) and exclusion energies against the oracle with its
     # reciprocal loop skipped (the full oracle k-sum would take ~6 minutes)
