@@ -9,7 +9,6 @@
 // for host outputs), so it can be captured into a hipGraph.
 #include <hip/hip_runtime.h>
 
-#include <hipcub/hipcub.hpp>
 #include <algorithm>
 #include <cmath>
 #include <cstring>
@@ -144,9 +143,10 @@ void set_cells(cf_handle* H, const double L[3]) {
     int64_t ncell = (int64_t)nc[0] * nc[1] * nc[2];
     if (ncell > h.ncell_alloc) {
         // grow (not graph-capture safe; only happens when the box grows past the initial grid)
-        if (h.cell_start) { (void)hipFree(h.cell_start); (void)hipFree(h.cell_end); }
+        if (h.cell_start) { (void)hipFree(h.cell_start); (void)hipFree(h.cell_end); (void)hipFree(h.cell_cnt); }
         cf::check_hip(hipMalloc(&h.cell_start, sizeof(int) * ncell), "cells");
         cf::check_hip(hipMalloc(&h.cell_end, sizeof(int) * ncell), "cells");
+        cf::check_hip(hipMalloc(&h.cell_cnt, sizeof(int) * ncell), "cells");
         h.ncell_alloc = (int)ncell;
     }
     h.nc[0] = nc[0]; h.nc[1] = nc[1]; h.nc[2] = nc[2];
@@ -436,27 +436,12 @@ CF_EXPORT int cf_create(const cf_params* p, const cf_options* opt, cf_handle** o
             h.atom_val = dalloc<int>(H, n); h.atom_sorted = dalloc<int>(H, n);
             h.pos4s = dalloc<double4>(H, n);
             h.ljs = dalloc<double2>(H, n);
-            size_t tmp = 0;
-            check_hip(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, h.cell_key, h.cell_key_sorted, h.atom_val,
-                                                         h.atom_sorted, n, 0, 31, h.stream),
-                      "sort temp query");
-            h.sort_tmp_bytes = tmp;
-            h.sort_tmp = dalloc<char>(H, tmp);
             h.key_tmp = dalloc<int>(H, n);
             h.atom_tmp = dalloc<int>(H, n);
             h.skin_flag = dalloc<int>(H, 1);
             h.n_builds_dev = dalloc<long long>(H, 1);
             check_hip(hipMemset(h.n_builds_dev, 0, sizeof(long long)), "memset");
-            if (h.world > 1) {  // owned atoms compacted in cell-sorted order
-                h.own_s = dalloc<int>(H, std::max(nown, 1));
-                h.own_flag = dalloc<int>(H, n);
-                h.own_pre = dalloc<int>(H, n);
-                size_t sb = 0;
-                check_hip(hipcub::DeviceScan::ExclusiveSum(nullptr, sb, h.own_flag, h.own_pre, n, h.stream),
-                          "scan temp query");
-                h.scan_tmp_bytes = sb;
-                h.scan_tmp = dalloc<char>(H, sb);
-            }
+            if (h.world > 1) h.own_s = dalloc<int>(H, std::max(nown, 1));  // owned atoms, cell-sorted
             std::copy(p->default_box, p->default_box + 9, H->default_box);
             alloc_nlist(H, 0.0);
             if (h.kspace_algo == 0) {
@@ -504,6 +489,7 @@ CF_EXPORT int cf_destroy(cf_handle* H) {
             for (hipEvent_t e : v) (void)hipEventDestroy(e);
         if (H->h.cell_start) (void)hipFree(H->h.cell_start);
         if (H->h.cell_end) (void)hipFree(H->h.cell_end);
+        if (H->h.cell_cnt) (void)hipFree(H->h.cell_cnt);
         if (H->h.own_stream) (void)hipStreamDestroy(H->h.stream);
         delete H;
     });

@@ -104,10 +104,9 @@ struct Handle {
     int nc[3] = {0, 0, 0};
     int* cell_key = nullptr; int* cell_key_sorted = nullptr;
     int* atom_val = nullptr; int* atom_sorted = nullptr;
-    int* cell_start = nullptr; int* cell_end = nullptr;
+    int* cell_start = nullptr; int* cell_end = nullptr; int* cell_cnt = nullptr;
     double4* pos4s = nullptr;   // [N] sorted wrapped (x,y,z,q)
     double2* ljs = nullptr;     // [N] sorted LJ
-    void* sort_tmp = nullptr; size_t sort_tmp_bytes = 0;
     // persistent list with skin: pairs within rc + list_skin at the last
     // build; reused while every atom has moved <= list_skin/2 and the box is unchanged
     double skin = 0.0;          // requested skin (nm); 0 = rebuild on every evaluation
@@ -118,13 +117,11 @@ struct Handle {
     int* skin_flag = nullptr;   // [1] device: rebuild this evaluation (host-forced or moved > skin/2)
     long long* n_builds_dev = nullptr;  // [1] list builds (device counter)
     int64_t n_evals = 0;
-    // every evaluation sorts into scratch; k_cell_commit copies it to the live arrays only
-    // when the flag is set (the decision never leaves the device)
+    // cell-sort scratch (the sort kernels run only when the device flag asks for a rebuild;
+    // k_cell_commit then copies the new order to the live arrays)
     int* key_tmp = nullptr; int* atom_tmp = nullptr;
     // multi-rank: owned atoms compacted in cell-sorted order (list rows)
     int* own_s = nullptr;       // [N_own] (null on one rank: identity)
-    int* own_flag = nullptr; int* own_pre = nullptr;  // [N]
-    void* scan_tmp = nullptr; size_t scan_tmp_bytes = 0;
     int nb_cap = 0;             // capacity of each of the 4 neighbour sub-lists of an atom
     int* nl = nullptr;          // [4][nb_cap][N] transposed sub-lists (sorted index | shift<<26)
     int* nl_cnt = nullptr;      // [4][N]

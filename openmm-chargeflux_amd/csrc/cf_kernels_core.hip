@@ -3,8 +3,6 @@
 // gathers in a fixed order (no atomics), so results are bitwise reproducible.
 //
 // Reference semantics: platforms/reference/src/ReferenceCoulKernels.cpp (RCK).
-#include <hipcub/hipcub.hpp>
-
 #include "cf_internal.h"
 
 namespace cf {
@@ -131,13 +129,24 @@ __global__ void __launch_bounds__(256) k_atoms_prep(int n, const double* __restr
 }
 
 // ---------------------------------------------------------------------------------
-// 3. cell list (replaces OpenMM computeNeighborListVoxelHash, RCK:559): wrap, bin,
-//    stable radix sort by cell, cell bounds, gather sorted (x,y,z,q) and LJ.
+// 3. cell list (replaces OpenMM computeNeighborListVoxelHash, RCK:559): wrap, bin, sort
+//    by cell (atom index within a cell: the order of a stable sort), cell bounds, sorted
+//    wrapped (x,y,z,q) and LJ.  A deterministic counting sort whose kernels all return at
+//    once when the device rebuild flag is clear, so a kept list costs only launches:
+//      clear counts -> keys + histogram -> scan (bounds) -> scatter -> order within cells
+//      -> [owned compaction] -> commit (or refresh of the kept list's coordinates)
 // ---------------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) k_cell_keys(int n, const double* __restrict__ pos, double3 L, int3 nc,
-                                                   int* __restrict__ key, int* __restrict__ val) {
+__global__ void __launch_bounds__(256) k_cell_zero(int ncell, const int* __restrict__ flag, int* __restrict__ cnt) {
+    int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= ncell || !*flag) return;
+    cnt[c] = 0;
+}
+
+__global__ void __launch_bounds__(256) k_cell_hist(int n, const int* __restrict__ flag, const double* __restrict__ pos,
+                                                   double3 L, int3 nc, int* __restrict__ key, int* __restrict__ rank,
+                                                   int* __restrict__ cnt) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
+    if (i >= n || !*flag) return;
     double3 x = ld3(pos, i);
     double w[3] = {x.x - floor(x.x / L.x) * L.x, x.y - floor(x.y / L.y) * L.y, x.z - floor(x.z / L.z) * L.z};
     double Ls[3] = {L.x, L.y, L.z};
@@ -148,40 +157,151 @@ __global__ void __launch_bounds__(256) k_cell_keys(int n, const double* __restri
         int ci = (int)(w[d] / Ls[d] * ncs[d]);
         c[d] = ci < 0 ? 0 : (ci >= ncs[d] ? ncs[d] - 1 : ci);
     }
-    key[i] = (c[0] * nc.y + c[1]) * nc.z + c[2];
-    val[i] = i;
+    int k = (c[0] * nc.y + c[1]) * nc.z + c[2];
+    key[i] = k;
+    rank[i] = atomicAdd(&cnt[k], 1);  // provisional slot; k_cell_order fixes the order
 }
 
-// rebuild (flag set): commit the freshly sorted order (scratch -> live), cell bounds,
-// sorted wrapped (x,y,z,q) + LJ, build positions, owned-atom compaction.
-// no rebuild: the sorted order and every atom's periodic image are kept from the last
-// build (wrap offsets recomputed from the build positions, so bit-identical to the commit),
-// only coordinates and flux charges are refreshed.
+// one workgroup: exclusive scan of m counts (chunked per thread); bounds -> start/end
+constexpr int kScanThreads = 1024;
+
+__device__ __forceinline__ int block_exclusive_scan(int v, int* sh) {
+    const int t = threadIdx.x;
+    sh[t] = v;
+    __syncthreads();
+    for (int off = 1; off < kScanThreads; off <<= 1) {
+        int u = t >= off ? sh[t - off] : 0;
+        __syncthreads();
+        sh[t] += u;
+        __syncthreads();
+    }
+    int incl = sh[t];
+    __syncthreads();
+    return incl - v;
+}
+
+__global__ void __launch_bounds__(kScanThreads) k_cell_scan(int ncell, const int* __restrict__ flag,
+                                                            const int* __restrict__ cnt, int* __restrict__ cstart,
+                                                            int* __restrict__ cend) {
+    __shared__ int sh[kScanThreads];
+    if (!*flag) return;
+    const int per = (ncell + kScanThreads - 1) / kScanThreads;
+    const int c0 = min(ncell, threadIdx.x * per), c1 = min(ncell, c0 + per);
+    int sum = 0;
+    for (int c = c0; c < c1; c++) sum += cnt[c];
+    int run = block_exclusive_scan(sum, sh);
+    for (int c = c0; c < c1; c++) {
+        cstart[c] = run;
+        run += cnt[c];
+        cend[c] = run;
+    }
+}
+
+__global__ void __launch_bounds__(256) k_cell_scatter(int n, const int* __restrict__ flag, const int* __restrict__ key,
+                                                      const int* __restrict__ rank, const int* __restrict__ cstart,
+                                                      int* __restrict__ tmp) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n || !*flag) return;
+    tmp[cstart[key[i]] + rank[i]] = i;
+}
+
+// one wave per cell: final position of each member = cell start + number of members with
+// a smaller atom index (members staged in LDS and read by broadcast)
+constexpr int kOrderLds = 1024;
+
+__global__ void __launch_bounds__(256) k_cell_order(int ncell, const int* __restrict__ flag,
+                                                    const int* __restrict__ cstart, const int* __restrict__ cend,
+                                                    const int* __restrict__ tmp, int* __restrict__ out) {
+    __shared__ int mem[4][kOrderLds];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int c = blockIdx.x * 4 + w;
+    if (c >= ncell || !*flag) return;
+    const int b = cstart[c], m = cend[c] - b;
+    const int* src = tmp + b;
+    if (m <= kOrderLds) {
+        for (int e = lane; e < m; e += 64) mem[w][e] = src[e];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        src = mem[w];
+    }
+    for (int e = lane; e < m; e += 64) {
+        const int v = src[e];
+        int r = 0;
+        for (int j = 0; j < m; j++) r += src[j] < v;
+        out[b + r] = v;
+    }
+}
+
+// multi-rank: owned atoms of the new order compacted, in cell-sorted order.  Three
+// coalesced passes over 1024-slot blocks: owned count per block, exclusive scan of the
+// block counts (one workgroup), in-block ballot prefix + write.
+__global__ void __launch_bounds__(kScanThreads) k_own_count(int n, const int* __restrict__ flag,
+                                                            const int* __restrict__ idx, int lo, int hi,
+                                                            int* __restrict__ bsum) {
+    if (!*flag) return;
+    int s = blockIdx.x * kScanThreads + threadIdx.x;
+    int i = s < n ? idx[s] : -1;
+    int c = __syncthreads_count(i >= lo && i < hi);
+    if (threadIdx.x == 0) bsum[blockIdx.x] = c;
+}
+
+__global__ void __launch_bounds__(kScanThreads) k_own_scan(int nb, const int* __restrict__ flag,
+                                                           int* __restrict__ bsum) {
+    __shared__ int sh[kScanThreads];
+    if (!*flag) return;
+    const int per = (nb + kScanThreads - 1) / kScanThreads;
+    const int b0 = min(nb, threadIdx.x * per), b1 = min(nb, b0 + per);
+    int sum = 0;
+    for (int b = b0; b < b1; b++) sum += bsum[b];
+    int run = block_exclusive_scan(sum, sh);
+    for (int b = b0; b < b1; b++) {
+        int v = bsum[b];
+        bsum[b] = run;  // in place: counts -> offsets
+        run += v;
+    }
+}
+
+__global__ void __launch_bounds__(kScanThreads) k_own_write(int n, const int* __restrict__ flag,
+                                                            const int* __restrict__ idx, int lo, int hi,
+                                                            const int* __restrict__ boff, int* __restrict__ own_s) {
+    __shared__ int wsum[kScanThreads / 64];
+    if (!*flag) return;
+    const int s = blockIdx.x * kScanThreads + threadIdx.x;
+    const int i = s < n ? idx[s] : -1;
+    const bool own = i >= lo && i < hi;
+    const unsigned long long m = __ballot(own);
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int pre = __popcll(m & ((1ull << lane) - 1));
+    if (lane == 0) wsum[w] = __popcll(m);
+    __syncthreads();
+    int off = boff[blockIdx.x];
+    for (int k = 0; k < w; k++) off += wsum[k];
+    if (own) own_s[off + pre] = s;
+}
+
+// rebuild (flag set): commit the new order (scratch -> live), sorted wrapped (x,y,z,q) +
+// LJ, build positions.  No rebuild: the sorted order and every atom's periodic image are
+// kept from the last build (wrap offsets recomputed from the build positions, so
+// bit-identical to the commit); only coordinates and flux charges are refreshed.
 __global__ void __launch_bounds__(256) k_cell_commit(int n, const int* __restrict__ flag,
-                                                     const int* __restrict__ key_tmp, const int* __restrict__ idx_tmp,
-                                                     const int* __restrict__ own_pre, int lo, int hi,
+                                                     const int* __restrict__ key, const int* __restrict__ idx_new,
                                                      const double* __restrict__ pos, const double* __restrict__ q,
                                                      const double2* __restrict__ lj, double3 L,
                                                      int* __restrict__ key_s, int* __restrict__ idx_s,
-                                                     int* __restrict__ cstart, int* __restrict__ cend,
                                                      double4* __restrict__ pos4s, double2* __restrict__ ljs,
-                                                     double* __restrict__ pos_ref, int* __restrict__ own_s,
-                                                     long long* __restrict__ n_builds) {
+                                                     double* __restrict__ pos_ref, long long* __restrict__ n_builds) {
     int s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= n) return;
     if (*flag) {
-        int k = key_tmp[s];
-        if (s == 0 || key_tmp[s - 1] != k) cstart[k] = s;
-        if (s == n - 1 || key_tmp[s + 1] != k) cend[k] = s + 1;
-        int i = idx_tmp[s];
-        key_s[s] = k;
+        int i = idx_new[s];
+        key_s[s] = key[i];
         idx_s[s] = i;
         double3 x = ld3(pos, i);
         pos4s[s] = make_double4(x.x - floor(x.x / L.x) * L.x, x.y - floor(x.y / L.y) * L.y,
                                 x.z - floor(x.z / L.z) * L.z, q[i]);
         ljs[s] = lj[i];
         if (pos_ref) { pos_ref[3 * i] = x.x; pos_ref[3 * i + 1] = x.y; pos_ref[3 * i + 2] = x.z; }
-        if (own_s && i >= lo && i < hi) own_s[own_pre[s]] = s;
         if (s == 0) *n_builds += 1;
     } else {
         int i = idx_s[s];
@@ -189,23 +309,6 @@ __global__ void __launch_bounds__(256) k_cell_commit(int n, const int* __restric
         pos4s[s] = make_double4(x.x - floor(r.x / L.x) * L.x, x.y - floor(r.y / L.y) * L.y,
                                 x.z - floor(r.z / L.z) * L.z, q[i]);
     }
-}
-
-__global__ void __launch_bounds__(256) k_cell_clear(int ncell, const int* __restrict__ flag, int* __restrict__ cstart,
-                                                    int* __restrict__ cend) {
-    int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= ncell || !*flag) return;
-    cstart[c] = 0;
-    cend[c] = 0;
-}
-
-// owned flags of the freshly sorted order (multi-rank): prefix sum -> compact row index
-__global__ void __launch_bounds__(256) k_own_flags(int n, const int* __restrict__ idx_tmp, int lo, int hi,
-                                                   int* __restrict__ f) {
-    int s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= n) return;
-    int i = idx_tmp[s];
-    f[s] = (i >= lo && i < hi) ? 1 : 0;
 }
 
 // list validity: flag = 1 if any atom moved more than half the skin since the last build
@@ -831,25 +934,29 @@ void launch_cell_sort(Handle& h, const double* pos) {
     double3 L = make_double3(h.box_L[0], h.box_L[1], h.box_L[2]);
     int3 nc = make_int3(h.nc[0], h.nc[1], h.nc[2]);
     int ncell = nc.x * nc.y * nc.z;
-    hipLaunchKernelGGL(k_cell_keys, dim3(nblk(h.n, 256)), dim3(256), 0, h.stream, h.n, pos, L, nc, h.cell_key,
-                       h.atom_val);
-    int end_bit = 1;
-    while ((1 << end_bit) < ncell) end_bit++;
-    size_t bytes = h.sort_tmp_bytes;
-    check_hip(hipcub::DeviceRadixSort::SortPairs(h.sort_tmp, bytes, h.cell_key, h.key_tmp, h.atom_val, h.atom_tmp,
-                                                 h.n, 0, end_bit, h.stream),
-              "radix sort");
+    const int* f = h.skin_flag;
+    // scratch: cell_key = per-atom key, atom_val = provisional rank, key_tmp = per-cell
+    // counts, atom_tmp = scattered order, cell_key_sorted's partner atom_new = final order
+    hipLaunchKernelGGL(k_cell_zero, dim3(nblk(ncell, 256)), dim3(256), 0, h.stream, ncell, f, h.cell_cnt);
+    hipLaunchKernelGGL(k_cell_hist, dim3(nblk(h.n, 256)), dim3(256), 0, h.stream, h.n, f, pos, L, nc, h.cell_key,
+                       h.atom_val, h.cell_cnt);
+    hipLaunchKernelGGL(k_cell_scan, dim3(1), dim3(kScanThreads), 0, h.stream, ncell, f, h.cell_cnt, h.cell_start,
+                       h.cell_end);
+    hipLaunchKernelGGL(k_cell_scatter, dim3(nblk(h.n, 256)), dim3(256), 0, h.stream, h.n, f, h.cell_key, h.atom_val,
+                       h.cell_start, h.atom_tmp);
+    hipLaunchKernelGGL(k_cell_order, dim3(nblk(ncell, 4)), dim3(256), 0, h.stream, ncell, f, h.cell_start,
+                       h.cell_end, h.atom_tmp, h.key_tmp);
     if (h.own_s) {
-        hipLaunchKernelGGL(k_own_flags, dim3(nblk(h.n, 256)), dim3(256), 0, h.stream, h.n, h.atom_tmp, h.lo, h.hi,
-                           h.own_flag);
-        size_t sb = h.scan_tmp_bytes;
-        check_hip(hipcub::DeviceScan::ExclusiveSum(h.scan_tmp, sb, h.own_flag, h.own_pre, h.n, h.stream), "scan");
+        const int nb = nblk(h.n, kScanThreads);  // block sums live in atom_val (free after the scatter)
+        hipLaunchKernelGGL(k_own_count, dim3(nb), dim3(kScanThreads), 0, h.stream, h.n, f, h.key_tmp, h.lo, h.hi,
+                           h.atom_val);
+        hipLaunchKernelGGL(k_own_scan, dim3(1), dim3(kScanThreads), 0, h.stream, nb, f, h.atom_val);
+        hipLaunchKernelGGL(k_own_write, dim3(nb), dim3(kScanThreads), 0, h.stream, h.n, f, h.key_tmp, h.lo, h.hi,
+                           h.atom_val, h.own_s);
     }
-    hipLaunchKernelGGL(k_cell_clear, dim3(nblk(ncell, 256)), dim3(256), 0, h.stream, ncell, h.skin_flag,
-                       h.cell_start, h.cell_end);
-    hipLaunchKernelGGL(k_cell_commit, dim3(nblk(h.n, 256)), dim3(256), 0, h.stream, h.n, h.skin_flag, h.key_tmp,
-                       h.atom_tmp, h.own_pre, h.lo, h.hi, pos, h.q, h.lj, L, h.cell_key_sorted, h.atom_sorted,
-                       h.cell_start, h.cell_end, h.pos4s, h.ljs, h.pos_ref, h.own_s, h.n_builds_dev);
+    hipLaunchKernelGGL(k_cell_commit, dim3(nblk(h.n, 256)), dim3(256), 0, h.stream, h.n, f, h.cell_key, h.key_tmp,
+                       pos, h.q, h.lj, L, h.cell_key_sorted, h.atom_sorted, h.pos4s, h.ljs, h.pos_ref,
+                       h.n_builds_dev);
 }
 
 void launch_skin_check(Handle& h, const double* pos) {
