@@ -78,8 +78,13 @@ typedef struct cf_options {
     void* stream;        /* hipStream_t to enqueue on (NULL = the null stream)             */
     int32_t rank;        /* atom-decomposition rank (0..world_size-1)                       */
     int32_t world_size;  /* 0 or 1 = single GPU                                            */
-    int32_t kspace_algo; /* 0 = default (MFMA fp64 separable), 1 = direct VALU (check path) */
-    int32_t reserved[7];
+    int32_t kspace_algo; /* reciprocal sum of ReferenceCoulKernels.cpp:513-556:
+                            0 = default: exact k-sum, fp64 MFMA separable form
+                            1 = exact k-sum, direct VALU sincos (check path)
+                            2 = grid: the same k-sum through ES-kernel spreading, pruned DFT
+                                and interpolation (error set by grid_width) */
+    int32_t grid_width;  /* kspace_algo 2: ES kernel width in grid points, 4..16 (0 = 14) */
+    int32_t reserved[6];
 } cf_options;
 
 /* compute flags */

@@ -23,10 +23,11 @@
 // recorded on the handle's stream around every launch, so bench.py can report kernel
 // durations measured on the stream the kernels actually run on.
 enum Phase { PH_FLUX, PH_PREP, PH_CELLS, PH_NLIST, PH_TABLES, PH_SFAC, PH_COEFFS, PH_FORCE, PH_DIRECT,
-             PH_ASSEMBLE, PH_ENERGY, PH_COUNT };
+             PH_ASSEMBLE, PH_ENERGY, PH_GSORT, PH_GSPREAD, PH_GDFTF, PH_GDFTI, PH_GINTERP, PH_COUNT };
 static const char* kPhaseNames[PH_COUNT] = {"flux_terms", "atoms_prep", "cell_sort", "neighbor_list",
                                             "kspace_tables", "kspace_sfac", "kspace_coeffs", "kspace_force",
-                                            "direct_pairs", "assemble", "energy"};
+                                            "direct_pairs", "assemble", "energy", "grid_sort", "grid_spread",
+                                            "grid_dft_fwd", "grid_dft_inv", "grid_interp"};
 constexpr int kMaxTimed = 8192;
 
 struct cf_handle {
@@ -275,7 +276,10 @@ CF_EXPORT int cf_create(const cf_params* p, const cf_options* opt, cf_handle** o
         h.device = o.device;
         h.rank = o.rank;
         h.world = world;
-        h.kspace_algo = o.kspace_algo == 1 ? 1 : 0;
+        if (o.kspace_algo < 0 || o.kspace_algo > 2) fail(CF_ERR_INVALID, "kspace_algo must be 0, 1 or 2");
+        if (o.grid_width != 0 && (o.grid_width < 4 || o.grid_width > 16))
+            fail(CF_ERR_INVALID, "grid_width must be 0 (default) or in [4, 16]");
+        h.kspace_algo = o.kspace_algo;
         h.stream = (hipStream_t)o.stream;  // NULL = the null stream (orders with torch's default stream)
 
         // ---- particles: q0, LJ (sigma/2, 2 sqrt(eps))   RCK:234-240
@@ -402,6 +406,7 @@ CF_EXPORT int cf_create(const cf_params* p, const cf_options* opt, cf_handle** o
             h.kg.KX = h.kmax[0];
             cf::kspace_plan(h);
             h.khalf = h.kg.k_half();
+            if (h.kspace_algo == 2) cf::grid_plan(h, o.grid_width, 2.0);
         }
 
         // ---- device allocation + upload
@@ -459,6 +464,30 @@ CF_EXPORT int cf_create(const cf_params* p, const cf_options* opt, cf_handle** o
                 check_hip(hipMemset(h.coef_a, 0, sizeof(double) * ncoef), "memset coef");
                 h.t_part = dalloc<double>(H, (size_t)h.fp.nparts() * nown * 4);
                 h.e_rec_part = dalloc<double>(H, (size_t)(g.KX * g.NY * g.KZ + 255) / 256 + 1);
+            } else if (h.kspace_algo == 2) {
+                const cf::GridPlan& gp = h.gp;
+                const size_t npts = (size_t)gp.ng[0] * gp.ng[1] * gp.ng[2];
+                std::vector<double2> tw[3], twz;
+                std::vector<double> dc[3];
+                cf::grid_tables(h, tw, twz, dc);
+                for (int d = 0; d < 3; d++) { h.g_tw[d] = dupload(H, tw[d]); h.g_deconv[d] = dupload(H, dc[d]); }
+                h.g_twz = dupload(H, twz);
+                h.g_grid = dalloc<double>(H, npts);
+                h.g_t1 = dalloc<double2>(H, (size_t)gp.ng[0] * gp.ng[1] * gp.KZ);
+                h.g_t2 = dalloc<double2>(H, (size_t)gp.ng[0] * gp.NY * gp.KZ);
+                h.g_b = dalloc<double2>(H, (size_t)gp.NX * gp.NY * gp.KZ);
+                h.g_cnt = dalloc<int>(H, gp.nbins);
+                h.g_start = dalloc<int>(H, gp.nbins + 1);
+                const size_t no = std::max(nown, 1);
+                h.g_srec = dalloc<double4>(H, no);
+                h.g_g0u = dalloc<int4>(H, no);
+                h.g_rank = dalloc<int>(H, no);
+                h.g_tmp = dalloc<int>(H, no);
+                h.g_order = dalloc<int>(H, no);
+                h.g_g0s = dalloc<int4>(H, no);
+                h.g_taps = dalloc<double>(H, no * 72);
+                h.t_part = dalloc<double>(H, no * 4);
+                h.e_rec_part = dalloc<double>(H, (size_t)(gp.NX * gp.NY * gp.KZ + 255) / 256 + 1);
             } else {
                 int blocks_k = (int)((h.khalf + 255) / 256);
                 h.sk_nchunk = std::max(1, std::min((2048 + blocks_k - 1) / blocks_k, std::max(1, nown / 256)));
@@ -592,6 +621,10 @@ CF_EXPORT int cf_compute_begin(cf_handle* H, const double* pos_dev, const double
                 if (h.kspace_algo == 0) {
                     { Timed t(H, PH_TABLES); cf::launch_kspace_tables(h, pos_dev); }
                     { Timed t(H, PH_SFAC); cf::launch_kspace_sfac(h); }
+                } else if (h.kspace_algo == 2) {
+                    { Timed t(H, PH_GSORT); cf::launch_grid_sort(h, pos_dev); }
+                    { Timed t(H, PH_GSPREAD); cf::launch_grid_spread(h); }
+                    { Timed t(H, PH_GDFTF); cf::launch_grid_dft_fwd(h); }
                 } else {
                     Timed t(H, PH_SFAC);
                     cf::launch_kspace_direct_sfac(h, pos_dev);
@@ -658,9 +691,13 @@ CF_EXPORT int cf_compute_end(cf_handle* H, double* forces_dev, double* energy_de
                 if (forces || energy) {
                     Timed t(H, PH_COEFFS);
                     if (h.kspace_algo == 0) cf::launch_kspace_coeffs(h, energy);
+                    else if (h.kspace_algo == 2) cf::launch_grid_coeffs(h, energy);
                     else cf::launch_kspace_direct_coeffs(h, energy);
                 }
-                if (forces) {
+                if (forces && h.kspace_algo == 2) {
+                    { Timed t(H, PH_GDFTI); cf::launch_grid_dft_inv(h); }
+                    { Timed t(H, PH_GINTERP); cf::launch_grid_interp(h); cf::launch_recip_add(h); }
+                } else if (forces) {
                     Timed t(H, PH_FORCE);
                     if (h.kspace_algo == 0) cf::launch_kspace_force(h, pos);
                     else cf::launch_kspace_direct_force(h, pos);

@@ -60,6 +60,21 @@ struct FPassPlan {
     int nparts() const { return kchunks * msplit; }
 };
 
+// grid path (kspace_algo = 2, cf_kernels_grid.hip): ES-kernel spreading on an oversampled
+// grid of ng points per axis (multiple of 8; 8^3-point tiles = sort bins), pruned DFT to
+// the reference's mode box |n_a| < K_a, interpolation
+struct GridPlan {
+    int W = 0;               // kernel width (grid points)
+    double beta = 0;         // ES shape parameter
+    double sigma = 0;        // effective oversampling min_a ng_a / (2K_a - 1)
+    int ng[3] = {0, 0, 0};
+    int nb[3] = {0, 0, 0};   // tiles per axis (ng/8)
+    int nbins = 0;
+    int KX = 0, KY = 0, KZ = 0;
+    int NX = 0, NY = 0;      // 2KX-1, 2KY-1 (mode rows nx, ny in (-K, K)); nz in [0, KZ)
+    int KZP = 0;             // KZ padded for the forward z stage
+};
+
 struct Handle {
     // ---- configuration -------------------------------------------------------
     int n = 0;
@@ -136,6 +151,24 @@ struct Handle {
     double* t_part = nullptr;   // [nparts][Nown][4]
     double* e_rec_part = nullptr; // [nblk]
     int e_rec_nblk = 0;
+    // k-space (grid path)
+    GridPlan gp;
+    double* g_grid = nullptr;   // [ngx][ngy][ngz] spread charges, later the potential grid
+    double2* g_t1 = nullptr;    // [ngx][ngy][KZ]
+    double2* g_t2 = nullptr;    // [ngx][NY][KZ]
+    double2* g_b = nullptr;     // [NX][NY][KZ] B(n) (all-reduced), then coefficients f(n)
+    double2* g_tw[3] = {nullptr, nullptr, nullptr};  // [2K-1][ng] e^{i 2pi n g/ng}
+    double2* g_twz = nullptr;   // [ngz][KZP] e^{i 2pi nz z/ngz}, nz >= 0
+    double* g_deconv[3] = {nullptr, nullptr, nullptr};  // [K] 1/phih(n/ng)
+    int* g_cnt = nullptr;       // [nbins]
+    int* g_start = nullptr;     // [nbins+1]
+    double4* g_srec = nullptr;  // [Nown] (s_x, s_y, s_z, q), s = grid coordinate
+    int4* g_g0u = nullptr;      // [Nown] first tap (unwrapped) per axis, bin
+    int* g_rank = nullptr;      // [Nown]
+    int* g_tmp = nullptr;       // [Nown]
+    int* g_order = nullptr;     // [Nown] sorted slot -> owned index
+    int4* g_g0s = nullptr;      // [Nown] wrapped first taps per sorted slot
+    double* g_taps = nullptr;   // [Nown][48]
     // k-space (direct VALU check path)
     int64_t khalf = 0;
     double* sk_slab = nullptr;  // [nchunk][2][khalf]
@@ -176,6 +209,17 @@ void launch_kspace_force(Handle& h, const double* pos);
 void launch_kspace_direct_sfac(Handle& h, const double* pos);
 void launch_kspace_direct_coeffs(Handle& h, int include_energy);
 void launch_kspace_direct_force(Handle& h, const double* pos);
+
+// grid path (kspace_algo = 2)
+void grid_plan(Handle& h, int width, double sigma);
+void grid_tables(const Handle& h, std::vector<double2> tw[3], std::vector<double2>& twz, std::vector<double> deconv[3]);
+void launch_grid_sort(Handle& h, const double* pos);
+void launch_grid_spread(Handle& h);
+void launch_grid_dft_fwd(Handle& h);
+double* grid_reduce_buffer(Handle& h, int64_t* count);
+void launch_grid_coeffs(Handle& h, int include_energy);
+void launch_grid_dft_inv(Handle& h);
+void launch_grid_interp(Handle& h);
 
 void check_hip(hipError_t e, const char* what);
 

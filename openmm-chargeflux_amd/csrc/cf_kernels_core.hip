@@ -1016,7 +1016,7 @@ void launch_direct(Handle& h, const double* pos, int include_forces) {
 
 void launch_recip_add(Handle& h) {
     int nown = h.hi - h.lo;
-    int nparts = h.kspace_algo == 1 ? 1 : h.fp.nparts();
+    int nparts = h.kspace_algo == 0 ? h.fp.nparts() : 1;
     hipLaunchKernelGGL(k_recip_add, dim3(nblk(nown, 256)), dim3(256), 0, h.stream, h.lo, nown, nparts, h.t_part,
                        h.dedq, h.f_part);
 }

@@ -1,0 +1,755 @@
+// cf_kernels_grid.hip — reciprocal-space Ewald sum on a grid (kspace_algo = 2).
+//
+// Reference: the half-space k loop of ReferenceCoulKernels.cpp:513-556 (RCK), O(N*K)
+// with cos/sin twice per (atom, k).  The same truncated k-sum (identical k-set,
+// weights and box) is evaluated here as a type-1 / type-2 non-uniform DFT pair with an
+// exponential-of-semicircle (ES) kernel of width W on an oversampled grid:
+//
+//   b[g]   = sum_j q_j phi(g - s_j)                    spread        (N W^3)
+//   B(n)   = sum_g b[g] e^{+i 2pi n.g/ng}             pruned DFT, |n_a| < K_a
+//   S(n)   = B(n) / (phih_x phih_y phih_z)(n)           = sum_j q_j e^{i k.r_j}  (to ~1e-13)
+//   E      = 1/2 sum_{n != 0} c a_k |S(n)|^2            (RCK:549-551, half space doubled)
+//   f(n)   = c a_k conj(S(n)) / phih(n)                 (RCK:528, 546)
+//   G[g]   = sum_n f(n) e^{+i 2pi n.g/ng}              pruned inverse DFT
+//   dE/dq_j = sum_g G[g] phi(g - s_j),   F_j = -q_j grad_j (same sum)   interpolation
+//
+// s_j = ng * frac(x_j / L) (grid units), phi(t) = exp(beta (sqrt(1 - (2t/W)^2) - 1)).
+// The error is set by W and the oversampling ng/(2K-1) (tools/nufft_proto.py: W = 14,
+// ng ~ 2(2K-1) -> |dF| ~ 5e-9 kJ/mol/nm at C2 and 12k atoms).  Every sum is a gather in a
+// fixed order (atoms are sorted by grid tile each evaluation with a deterministic counting
+// sort), so results are bitwise reproducible.  All fp64.
+#include <algorithm>
+#include <cmath>
+#include <vector>
+
+#include "cf_internal.h"
+
+namespace cf {
+
+static inline int nblk(int64_t n, int b) { return (int)((n + b - 1) / b); }
+
+// native 2-vector for register staging (HIP's double2 struct arrays stay in scratch memory)
+typedef double v2d __attribute__((ext_vector_type(2)));
+
+// wave index within the workgroup as a wave-uniform (SGPR) value, so that everything
+// derived from it is scalar (the compiler treats threadIdx.x >> 6 as divergent)
+__device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
+
+__device__ __forceinline__ double readlane_d(double v, int lane) {
+    int2 p = *reinterpret_cast<int2*>(&v);
+    p.x = __builtin_amdgcn_readlane(p.x, lane);
+    p.y = __builtin_amdgcn_readlane(p.y, lane);
+    return *reinterpret_cast<double*>(&p);
+}
+
+// phi(t) and d/ds phi(g - s) (= -phi'(t)) at t = g - s; zero outside the open support
+__device__ __forceinline__ void es_tap(double t, double hw_inv, double beta, double& v, double& dv) {
+    const double z = t * hw_inv;
+    const double u = 1.0 - z * z;
+    if (u > 0.0) {
+        const double r = sqrt(u);
+        v = exp(beta * (r - 1.0));
+        dv = v * beta * z / r * hw_inv;
+    } else {
+        v = 0.0;
+        dv = 0.0;
+    }
+}
+
+__device__ __forceinline__ double es_val(double t, double hw_inv, double beta) {
+    const double z = t * hw_inv;
+    const double u = 1.0 - z * z;
+    return u > 0.0 ? exp(beta * (sqrt(u) - 1.0)) : 0.0;
+}
+
+// ---------------------------------------------------------------------------------
+// 1. bin owned atoms by the 8^3 grid tile holding their first tap; deterministic counting
+//    sort (atomic provisional rank, then the order of a stable sort by atom index)
+// ---------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_g_bin(int lo, int nown, const double* __restrict__ pos,
+                                               const double* __restrict__ q, double3 L, int3 ng, int W, int3 nb,
+                                               double4* __restrict__ srec, int4* __restrict__ g0u,
+                                               int* __restrict__ rank, int* __restrict__ cnt) {
+    const int io = blockIdx.x * blockDim.x + threadIdx.x;
+    if (io >= nown) return;
+    const int i = lo + io;
+    const double x[3] = {pos[3 * i], pos[3 * i + 1], pos[3 * i + 2]};
+    const double Ls[3] = {L.x, L.y, L.z};
+    const int n[3] = {ng.x, ng.y, ng.z};
+    double s[3];
+    int g[3], gw[3];
+#pragma unroll
+    for (int d = 0; d < 3; d++) {
+        double u = x[d] / Ls[d];
+        u -= floor(u);
+        double sd = u * n[d];
+        if (sd >= n[d]) sd -= n[d];
+        s[d] = sd;
+        g[d] = (int)ceil(sd - 0.5 * W);
+        gw[d] = g[d] < 0 ? g[d] + n[d] : g[d];
+    }
+    const int bin = ((gw[0] >> 3) * nb.y + (gw[1] >> 3)) * nb.z + (gw[2] >> 3);
+    srec[io] = make_double4(s[0], s[1], s[2], q[i]);
+    g0u[io] = make_int4(g[0], g[1], g[2], bin);
+    rank[io] = atomicAdd(&cnt[bin], 1);
+}
+
+constexpr int kGScan = 1024;
+
+__global__ void __launch_bounds__(kGScan) k_g_scan(int nbins, const int* __restrict__ cnt, int* __restrict__ start) {
+    __shared__ int sh[kGScan];
+    const int t = threadIdx.x;
+    const int per = (nbins + kGScan - 1) / kGScan;
+    const int b0 = min(nbins, t * per), b1 = min(nbins, b0 + per);
+    int sum = 0;
+    for (int b = b0; b < b1; b++) sum += cnt[b];
+    sh[t] = sum;
+    __syncthreads();
+    for (int off = 1; off < kGScan; off <<= 1) {
+        int u = t >= off ? sh[t - off] : 0;
+        __syncthreads();
+        sh[t] += u;
+        __syncthreads();
+    }
+    int run = sh[t] - sum;
+    for (int b = b0; b < b1; b++) {
+        start[b] = run;
+        run += cnt[b];
+    }
+    if (t == kGScan - 1) start[nbins] = sh[t];
+}
+
+__global__ void __launch_bounds__(256) k_g_scatter(int nown, const int4* __restrict__ g0u, const int* __restrict__ rank,
+                                                   const int* __restrict__ start, int* __restrict__ tmp) {
+    const int io = blockIdx.x * blockDim.x + threadIdx.x;
+    if (io >= nown) return;
+    tmp[start[g0u[io].w] + rank[io]] = io;
+}
+
+// one wave per bin: slot of each member = bin start + number of members with a smaller index
+__global__ void __launch_bounds__(256) k_g_order(int nbins, const int* __restrict__ start,
+                                                 const int* __restrict__ tmp, int* __restrict__ order) {
+    __shared__ int mem[4][256];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int b = blockIdx.x * 4 + w;
+    if (b >= nbins) return;
+    const int b0 = start[b], m = start[b + 1] - b0;
+    const int* src = tmp + b0;
+    if (m <= 256) {
+        for (int e = lane; e < m; e += 64) mem[w][e] = src[e];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        src = mem[w];
+    }
+    for (int e = lane; e < m; e += 64) {
+        const int v = src[e];
+        int r = 0;
+        for (int j = 0; j < m; j++) r += src[j] < v;
+        order[b0 + r] = v;
+    }
+}
+
+// taps of every sorted atom in bin-aligned rows: taps[slot][d][p], p in [0, 24), is the
+// kernel weight of grid point 8*bin_d + p (tap m = p - (g0_d mod 8); zero outside 0 <= m < W),
+// q folded into the x row.  A tile db tiles ahead of the atom's bin then reads the fixed
+// window p = 8*db + i, so no per-atom offset is needed to address the taps.
+constexpr int kRow = 24;
+constexpr int kTapStride = 3 * kRow;
+
+__global__ void __launch_bounds__(256) k_g_taps(int nown, int W, double beta, int3 ng, const int* __restrict__ order,
+                                                const double4* __restrict__ srec, const int4* __restrict__ g0u,
+                                                double* __restrict__ taps, int4* __restrict__ g0s) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= (int64_t)nown * kTapStride) return;
+    const int slot = (int)(t / kTapStride), r = (int)(t % kTapStride);
+    const int d = r / kRow, p = r % kRow;
+    const int io = order[slot];
+    const double4 sr = srec[io];
+    const int4 g = g0u[io];
+    const double sd = d == 0 ? sr.x : (d == 1 ? sr.y : sr.z);
+    const int g0 = d == 0 ? g.x : (d == 1 ? g.y : g.z);
+    const int m = p - (g0 & 7);   // g0 & 7 == wrapped g0 mod 8 (ng is a multiple of 8)
+    double v = (m >= 0 && m < W) ? es_val((double)(g0 + m) - sd, 2.0 / W, beta) : 0.0;
+    if (d == 0) v *= sr.w;
+    taps[t] = v;
+    if (r == 0)
+        g0s[slot] = make_int4(g.x < 0 ? g.x + ng.x : g.x, g.y < 0 ? g.y + ng.y : g.y, g.z < 0 ? g.z + ng.z : g.z, io);
+}
+
+// ---------------------------------------------------------------------------------
+// 2. spread: a gather per 8^3 grid tile.  A workgroup of 8 waves owns a 2x2x2 block of
+//    tiles, one per wave.  The block's 4x4x4 source bins (a first tap in bin B reaches
+//    tiles B..B+2 for W <= 17) are walked as 16 (x, y) columns of 4 z-bins whose tap rows
+//    are staged in LDS (shared by the 8 tiles), double-buffered: the next pass's global
+//    loads are in flight in registers while the current pass is computed.  Each wave takes
+//    the 27 bins within 0..2 tiles behind its own tile, 8 atoms at a time: lane (a, k)
+//    holds atom a's x and y windows and z tap k and accumulates the 8x8 (i, j) points of
+//    its z column (8 muls + 64 FMAs per atom).  The 8 atom lanes of a column are summed
+//    in fixed order through LDS at the end -> deterministic.
+// ---------------------------------------------------------------------------------
+constexpr int kSpreadCap = 112;                         // atoms staged per pass (63 KB)
+constexpr int kSpreadU = (kSpreadCap * (kTapStride / 2) + 511) / 512;   // double2 per thread
+
+struct SpreadPass {
+    int col;          // (sx, sy) = (col >> 2, col & 3); 16 = done
+    int base, nst;    // atoms [base, base + nst) of the column's concatenated z-bins
+    int cs[4], cn[4];
+};
+
+__device__ __forceinline__ int wrapb(int b, int n) { return b < 0 ? b + n : (b >= n ? b - n : b); }
+
+__device__ __forceinline__ void spread_column(SpreadPass& p, int3 nb, int BX, int BY, int BZ,
+                                              const int* __restrict__ start) {
+    const int bx = wrapb(2 * BX - 2 + (p.col >> 2), nb.x), by = wrapb(2 * BY - 2 + (p.col & 3), nb.y);
+#pragma unroll
+    for (int sz = 0; sz < 4; sz++) {
+        const int b = (bx * nb.y + by) * nb.z + wrapb(2 * BZ - 2 + sz, nb.z);
+        p.cs[sz] = start[b];
+        p.cn[sz] = start[b + 1] - p.cs[sz];
+    }
+}
+
+// advance to the next non-empty pass; false when the columns are exhausted
+__device__ __forceinline__ bool spread_next(SpreadPass& p, int3 nb, int BX, int BY, int BZ,
+                                            const int* __restrict__ start) {
+    int tot = p.cn[0] + p.cn[1] + p.cn[2] + p.cn[3];
+    if (p.col < 16 && p.base + kSpreadCap < tot) {
+        p.base += kSpreadCap;
+    } else {
+        do {
+            if (++p.col >= 16) return false;
+            spread_column(p, nb, BX, BY, BZ, start);
+            tot = p.cn[0] + p.cn[1] + p.cn[2] + p.cn[3];
+        } while (tot == 0);
+        p.base = 0;
+    }
+    p.nst = min(kSpreadCap, tot - p.base);
+    return true;
+}
+
+__device__ __forceinline__ void spread_fetch(const SpreadPass& p, const double* __restrict__ taps,
+                                             v2d (&r)[kSpreadU]) {
+    const int c1 = p.cn[0], c2 = c1 + p.cn[1], c3 = c2 + p.cn[2];
+#pragma unroll
+    for (int q = 0; q < kSpreadU; q++) {
+        const int e = threadIdx.x + 512 * q;
+        const int a = e / (kTapStride / 2), c = e - a * (kTapStride / 2);
+        const int u = p.base + min(a, p.nst - 1);
+        const int slot = u < c1 ? p.cs[0] + u : (u < c2 ? p.cs[1] + u - c1 : (u < c3 ? p.cs[2] + u - c2 : p.cs[3] + u - c3));
+        r[q] = reinterpret_cast<const v2d*>(taps + (size_t)slot * kTapStride)[c];
+    }
+}
+
+__device__ __forceinline__ void spread_store(const SpreadPass& p, double* __restrict__ buf, const v2d (&r)[kSpreadU]) {
+#pragma unroll
+    for (int q = 0; q < kSpreadU; q++) {
+        const int e = threadIdx.x + 512 * q;
+        if (e < p.nst * (kTapStride / 2)) reinterpret_cast<v2d*>(buf)[e] = r[q];
+    }
+}
+
+__global__ void __launch_bounds__(512) k_g_spread(int3 ng, int3 nb, const int* __restrict__ start,
+                                                  const double* __restrict__ taps, double* __restrict__ grid) {
+    extern __shared__ double st[];   // 2 x [kSpreadCap][kTapStride]
+    const int lane = threadIdx.x & 63, w = wave_id();
+    const int ka = lane >> 3, k = lane & 7;   // atom-in-group, z column
+    const int nbbz = (nb.z + 1) >> 1, nbby = (nb.y + 1) >> 1;
+    const int BZ = blockIdx.x % nbbz, BY = (blockIdx.x / nbbz) % nbby, BX = blockIdx.x / (nbbz * nbby);
+    const int wx = (w >> 2) & 1, wy = (w >> 1) & 1, wz = w & 1;
+    const int tx = 2 * BX + wx, ty = 2 * BY + wy, tz = 2 * BZ + wz;
+    const bool active = tx < nb.x && ty < nb.y && tz < nb.z;
+    double acc[8][8];
+#pragma unroll
+    for (int i = 0; i < 8; i++)
+#pragma unroll
+        for (int jj = 0; jj < 8; jj++) acc[i][jj] = 0.0;
+    SpreadPass p;
+    p.col = -1; p.base = 0;
+    p.cn[0] = p.cn[1] = p.cn[2] = p.cn[3] = 0;
+    bool have = spread_next(p, nb, BX, BY, BZ, start);
+    v2d r[kSpreadU];
+    int cur = 0;
+    if (have) {
+        spread_fetch(p, taps, r);
+        spread_store(p, st, r);
+    }
+    __syncthreads();
+    while (have) {
+        SpreadPass pn = p;
+        const bool more = spread_next(pn, nb, BX, BY, BZ, start);
+        if (more) spread_fetch(pn, taps, r);   // in flight during the compute below
+        const double* buf = st + (size_t)cur * kSpreadCap * kTapStride;
+        const int dbx = wx + 2 - (p.col >> 2), dby = wy + 2 - (p.col & 3);
+        if (active && dbx >= 0 && dbx <= 2 && dby >= 0 && dby <= 2) {
+            const int ox = 8 * dbx, oy = kRow + 8 * dby;
+            int off = 0;
+#pragma unroll
+            for (int sz = 0; sz < 4; sz++) {
+                const int dbz = wz + 2 - sz;
+                const int lo = max(off, p.base) - p.base, hi = min(off + p.cn[sz], p.base + p.nst) - p.base;
+                off += p.cn[sz];
+                if (dbz < 0 || dbz > 2 || lo >= hi) continue;
+                const int oz = 2 * kRow + 8 * dbz + k;
+                for (int u0 = lo; u0 < hi; u0 += 8) {
+                    const int u = min(u0 + ka, hi - 1);
+                    const double* rr = buf + (size_t)u * kTapStride;
+                    const double zq = u0 + ka < hi ? rr[oz] : 0.0;
+                    double yz[8];
+#pragma unroll
+                    for (int jj = 0; jj < 8; jj++) yz[jj] = rr[oy + jj] * zq;
+#pragma unroll
+                    for (int i = 0; i < 8; i++) {
+                        const double xi = rr[ox + i];
+#pragma unroll
+                        for (int jj = 0; jj < 8; jj++) acc[i][jj] += xi * yz[jj];
+                    }
+                }
+            }
+        }
+        if (!more) break;
+        cur ^= 1;
+        spread_store(pn, st + (size_t)cur * kSpreadCap * kTapStride, r);
+        p = pn;
+        __syncthreads();
+    }
+    // sum the 8 atom lanes of each z column in fixed order through LDS, one x row at a time
+    __syncthreads();
+    double* red = st + (size_t)w * 512;   // [ka][jj][k] of this wave
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+#pragma unroll
+        for (int jj = 0; jj < 8; jj++) red[(ka * 8 + jj) * 8 + k] = acc[i][jj];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const int jl = lane >> 3;   // lane = (jl, k) sums the 8 atom partials of point (i, jl, k)
+        double v = red[jl * 8 + k];
+#pragma unroll
+        for (int a2 = 1; a2 < 8; a2++) v += red[(a2 * 8 + jl) * 8 + k];
+        if (active) grid[((size_t)(8 * tx + i) * ng.y + 8 * ty + jl) * ng.z + 8 * tz + k] = v;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+}
+
+// ---------------------------------------------------------------------------------
+// 3. pruned DFT stages (VALU)
+// ---------------------------------------------------------------------------------
+// z, real -> half spectrum:  t1[row][nz] = sum_z grid[row][z] e^{i th nz z}, nz < KZ.
+// lane = row; twiddles (uniform) from twz[z][KZP].
+constexpr int kNZB = 4;
+
+__global__ void __launch_bounds__(256) k_g_dftz_fwd(int rows, int ngz, int KZ, int KZP, const double* __restrict__ grid,
+                                                    const double2* __restrict__ twz, double2* __restrict__ t1) {
+    const int row = blockIdx.x * blockDim.x + threadIdx.x;
+    const int nz0 = blockIdx.y * kNZB;
+    const bool ok = row < rows;
+    const double* gr = grid + (size_t)(ok ? row : 0) * ngz;
+    double re[kNZB], im[kNZB];
+#pragma unroll
+    for (int u = 0; u < kNZB; u++) { re[u] = 0; im[u] = 0; }
+#pragma unroll 8
+    for (int z = 0; z < ngz; z++) {
+        const double gv = gr[z];
+        const double2* w = twz + (size_t)z * KZP + nz0;
+#pragma unroll
+        for (int u = 0; u < kNZB; u++) {
+            const double2 c = w[u];
+            re[u] += gv * c.x;
+            im[u] += gv * c.y;
+        }
+    }
+    if (!ok) return;
+#pragma unroll
+    for (int u = 0; u < kNZB; u++)
+        if (nz0 + u < KZ) t1[(size_t)row * KZ + nz0 + u] = make_double2(re[u], im[u]);
+}
+
+// middle-axis complex contraction: out[o][ap][i] = sum_a in[o][a][i] * tw[ap*sap + a*sa]
+// lanes over the flattened (o, i) pairs, kAP consecutive ap per thread (uniform twiddles)
+constexpr int kAP = 2;
+
+__global__ void __launch_bounds__(256) k_g_contract(int O, int A, int APn, int inner, const double2* __restrict__ in,
+                                                    const double2* __restrict__ tw, int sap, int sa,
+                                                    double2* __restrict__ out) {
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    const int ap0 = blockIdx.y * kAP;
+    const bool ok = p < O * inner;
+    const int o = ok ? p / inner : 0, i = ok ? p % inner : 0;
+    const double2* src = in + (size_t)o * A * inner + i;
+    double re[kAP], im[kAP];
+    const double2* twp[kAP];
+#pragma unroll
+    for (int u = 0; u < kAP; u++) {
+        re[u] = 0; im[u] = 0;
+        twp[u] = tw + (size_t)min(ap0 + u, APn - 1) * sap;
+    }
+#pragma unroll 8
+    for (int a = 0; a < A; a++) {
+        const double2 v = src[(size_t)a * inner];
+#pragma unroll
+        for (int u = 0; u < kAP; u++) {
+            const double2 w = twp[u][(size_t)a * sa];
+            re[u] += v.x * w.x - v.y * w.y;
+            im[u] += v.x * w.y + v.y * w.x;
+        }
+    }
+    if (!ok) return;
+#pragma unroll
+    for (int u = 0; u < kAP; u++)
+        if (ap0 + u < APn) out[((size_t)o * APn + ap0 + u) * inner + i] = make_double2(re[u], im[u]);
+}
+
+// half spectrum -> real z rows: grid[row][z] = sum_{nz<KZ} Re(u2[row][nz] e^{i th nz z})
+// (the x2 weight of nz > 0 is folded into the coefficients).  lane = z (64-wide chunk),
+// 4 waves x kRW rows; the block's rows of u2 are staged in LDS (broadcast reads).
+constexpr int kRW = 8;
+
+__global__ void __launch_bounds__(256) k_g_dftz_inv(int rows, int ngz, int KZ, const double2* __restrict__ u2,
+                                                    const double2* __restrict__ twnz, double* __restrict__ grid) {
+    extern __shared__ double2 su[];   // [4*kRW][KZ]
+    const int zchunks = (ngz + 63) / 64;
+    const int rb = blockIdx.x / zchunks, zc = blockIdx.x % zchunks;
+    const int row0 = rb * 4 * kRW;
+    const int nrows = min(4 * kRW, rows - row0);
+    for (int e = threadIdx.x; e < nrows * KZ; e += 256) su[e] = u2[(size_t)row0 * KZ + e];
+    __syncthreads();
+    const int lane = threadIdx.x & 63, w = wave_id();
+    const int z = zc * 64 + lane;
+    const int zz = z < ngz ? z : 0;
+    const int r0 = w * kRW;
+    if (r0 >= nrows) return;
+    double acc[kRW];
+#pragma unroll
+    for (int r = 0; r < kRW; r++) acc[r] = 0;
+#pragma unroll 4
+    for (int nz = 0; nz < KZ; nz++) {
+        const double2 t = twnz[(size_t)nz * ngz + zz];
+#pragma unroll
+        for (int r = 0; r < kRW; r++) {
+            const double2 uv = su[min(r0 + r, nrows - 1) * KZ + nz];
+            acc[r] += uv.x * t.x - uv.y * t.y;
+        }
+    }
+    if (z >= ngz) return;
+#pragma unroll
+    for (int r = 0; r < kRW; r++)
+        if (r0 + r < nrows) grid[(size_t)(row0 + r0 + r) * ngz + z] = acc[r];
+}
+
+// ---------------------------------------------------------------------------------
+// 4. coefficients: S = B/phih, energy c a |S|^2 (x1/2 for the nz = 0 plane, which holds
+//    both members of each +-n pair), f = w_z c a conj(S)/phih written in place.
+// ---------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_g_coeffs(int KX, int KY, int KZ, double3 rec, double cst, double one_4a2,
+                                                  const double* __restrict__ dx, const double* __restrict__ dy,
+                                                  const double* __restrict__ dz, double2* __restrict__ buf,
+                                                  double* __restrict__ e_part, int include_energy) {
+    __shared__ double red[256];
+    const int NY = 2 * KY - 1;
+    const int total = (2 * KX - 1) * NY * KZ;
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    double e = 0;
+    if (t < total) {
+        const int nz = t % KZ, r = t / KZ;
+        const int ny = r % NY - (KY - 1), nx = r / NY - (KX - 1);
+        const double kx = nx * rec.x, ky = ny * rec.y, kz = nz * rec.z;
+        const double k2 = kx * kx + ky * ky + kz * kz;
+        const double a = k2 > 0 ? exp(-k2 * 0.25 * one_4a2) / k2 : 0.0;   // RCK:528
+        const double D = dx[abs(nx)] * dy[abs(ny)] * dz[nz];
+        const double2 B = buf[t];
+        const double sr = B.x * D, si = B.y * D;
+        const double wz = nz > 0 ? 2.0 : 1.0;
+        if (include_energy) e = 0.5 * wz * cst * a * (sr * sr + si * si);   // RCK:549-551
+        const double c = wz * cst * a * D;
+        buf[t] = make_double2(c * sr, -c * si);
+    }
+    red[threadIdx.x] = e;
+    __syncthreads();
+    for (int s = 128; s > 0; s >>= 1) {
+        if (threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) e_part[blockIdx.x] = red[0];
+}
+
+// ---------------------------------------------------------------------------------
+// 5. interpolation, one workgroup per 8^3 tile: the potential grid over the tile plus the
+//    W-1 halo (R = 7 + W points per axis, wrapped) is staged in LDS, then each wave takes
+//    atoms of the tile's bin.  Per atom: lane (d, m) evaluates tap m of axis d and its
+//    derivative; lane (jg, k) accumulates t0 = sum_i G X_i and t1 = sum_i G dX_i over its
+//    (j = 4jj + jg, k) columns (2 FMAs per LDS read, x taps as wave-uniform scalars), then
+//    pot = sum t0 Y Z, grad = (t1 Y Z, t0 dY Z, t0 Y dZ) in a fixed-order wave reduction.
+// ---------------------------------------------------------------------------------
+template <int W>
+__global__ void __launch_bounds__(256) k_g_interp(int3 ng, int3 nb, const int* __restrict__ start,
+                                                  const int4* __restrict__ g0s, const double4* __restrict__ srec,
+                                                  double beta, double3 gscale, const double* __restrict__ G,
+                                                  double* __restrict__ t_part) {
+    constexpr int R = 7 + W;
+    constexpr int NJ = (W + 3) / 4;
+    extern __shared__ double sg[];   // [R][R][R]
+    const int tile = blockIdx.x;
+    const int s0 = start[tile], s1 = start[tile + 1];
+    if (s0 == s1) return;
+    const int tz = tile % nb.z, ty = (tile / nb.z) % nb.y, tx = tile / (nb.z * nb.y);
+    // rows of R consecutive z: thread t loads element c = t % R... of rows r = t / R, ...
+#pragma unroll 4
+    for (int e = threadIdx.x; e < R * R * R; e += 256) {
+        const int row = e / R, c = e - row * R;
+        const int b = row % R, a = row / R;
+        int x = 8 * tx + a, y = 8 * ty + b, z = 8 * tz + c;
+        x -= x >= ng.x ? ng.x : 0; y -= y >= ng.y ? ng.y : 0; z -= z >= ng.z ? ng.z : 0;
+        sg[e] = G[((size_t)x * ng.y + y) * ng.z + z];
+    }
+    __syncthreads();
+    const int lane = threadIdx.x & 63, w = wave_id();
+    const int d = lane >> 4, m = lane & 15;
+    const int k = lane & 15, jg = lane >> 4;
+    for (int s = s0 + w; s < s1; s += 4) {
+        const int4 g = g0s[s];
+        const double4 sr = srec[g.w];
+        // taps: lane (d, m)
+        // tap m at t = g0 + m - s, g0 = ceil(s - W/2) (the unwrapped first tap of k_g_bin)
+        const double sd = d == 0 ? sr.x : (d == 1 ? sr.y : sr.z);
+        double v = 0, dv = 0;
+        if (d < 3 && m < W) es_tap(ceil(sd - 0.5 * W) + m - sd, 2.0 / W, beta, v, dv);
+        const int rx = g.x & 7, ry = g.y & 7, rz = g.z & 7;
+        const double zt = __shfl(v, 32 + k), dzt = __shfl(dv, 32 + k);
+        double t0[NJ], t1[NJ];
+#pragma unroll
+        for (int jj = 0; jj < NJ; jj++) { t0[jj] = 0; t1[jj] = 0; }
+        const int kk = k < W ? k : 0;
+        const double* base = sg + (rx * R + ry) * R + rz + kk;
+#pragma unroll
+        for (int i = 0; i < W; i++) {
+            const double xi = readlane_d(v, i), dxi = readlane_d(dv, i);
+#pragma unroll
+            for (int jj = 0; jj < NJ; jj++) {
+                const int j = 4 * jj + jg;
+                const double gv = base[(i * R + (j < W ? j : 0)) * R];
+                t0[jj] += gv * xi;
+                t1[jj] += gv * dxi;
+            }
+        }
+        double pv = 0, px = 0, py = 0, pz = 0;
+#pragma unroll
+        for (int jj = 0; jj < NJ; jj++) {
+            const int j = 4 * jj + jg;
+            const int jl = 16 + (j < 16 ? j : 15);
+            double yt = __shfl(v, jl), dyt = __shfl(dv, jl);
+            if (j >= W) { yt = 0; dyt = 0; }
+            pv += t0[jj] * yt;
+            px += t1[jj] * yt;
+            py += t0[jj] * dyt;
+        }
+        pz = pv * dzt;
+        pv *= zt; px *= zt; py *= zt;
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            pv += __shfl_xor(pv, off); px += __shfl_xor(px, off);
+            py += __shfl_xor(py, off); pz += __shfl_xor(pz, off);
+        }
+        if (lane == 0) {
+            double* o = t_part + (size_t)g.w * 4;
+            o[0] = pv;
+            o[1] = -sr.w * gscale.x * px;
+            o[2] = -sr.w * gscale.y * py;
+            o[3] = -sr.w * gscale.z * pz;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------------
+static double es_host(double t, int W, double beta) {
+    double z = 2.0 * t / W, u = 1.0 - z * z;
+    return u > 0 ? std::exp(beta * (std::sqrt(u) - 1.0)) : 0.0;
+}
+
+// Gauss-Legendre nodes/weights on [-1, 1] (Newton on P_n)
+static void gauss_legendre(int n, std::vector<double>& x, std::vector<double>& w) {
+    x.assign(n, 0.0);
+    w.assign(n, 0.0);
+    for (int i = 0; i < (n + 1) / 2; i++) {
+        double z = std::cos(kPi * (i + 0.75) / (n + 0.5)), pp = 0;
+        for (int it = 0; it < 100; it++) {
+            double p1 = 1, p2 = 0;
+            for (int j = 1; j <= n; j++) {
+                double p3 = p2;
+                p2 = p1;
+                p1 = ((2.0 * j - 1) * z * p2 - (j - 1.0) * p3) / j;
+            }
+            pp = n * (z * p1 - p2) / (z * z - 1);
+            double dz = p1 / pp;
+            z -= dz;
+            if (std::fabs(dz) < 1e-16) break;
+        }
+        x[i] = -z; x[n - 1 - i] = z;
+        w[i] = w[n - 1 - i] = 2.0 / ((1 - z * z) * pp * pp);
+    }
+}
+
+static int round8(int v) { return (v + 7) / 8 * 8; }
+
+void grid_plan(Handle& h, int width, double sigma) {
+    GridPlan& p = h.gp;
+    p.W = width > 0 ? width : 14;
+    if (p.W < 4 || p.W > 16) throw std::invalid_argument("grid kernel width must be in [4, 16]");
+    if (!(sigma > 1.0)) sigma = 2.0;
+    double sig_eff = 1e30;
+    for (int d = 0; d < 3; d++) {
+        const int K = h.kmax[d];
+        int n = round8((int)std::ceil(sigma * (2 * K - 1)));
+        n = std::max(n, std::max(24, round8(p.W + 8)));
+        p.ng[d] = n;
+        p.nb[d] = n / 8;
+        sig_eff = std::min(sig_eff, (double)n / (2 * K - 1));
+    }
+    p.sigma = sig_eff;
+    p.beta = 0.97 * kPi * (1.0 - 0.5 / sig_eff) * p.W;   // ES shape for this oversampling
+    p.nbins = p.nb[0] * p.nb[1] * p.nb[2];
+    p.KX = h.kmax[0]; p.KY = h.kmax[1]; p.KZ = h.kmax[2];
+    p.NX = 2 * p.KX - 1; p.NY = 2 * p.KY - 1;
+    p.KZP = (p.KZ + kNZB - 1) / kNZB * kNZB;
+}
+
+void grid_tables(const Handle& h, std::vector<double2> tw[3], std::vector<double2>& twz, std::vector<double> deconv[3]) {
+    const GridPlan& p = h.gp;
+    std::vector<double> gx, gw;
+    gauss_legendre(200, gx, gw);
+    for (int d = 0; d < 3; d++) {
+        const int ng = p.ng[d], K = h.kmax[d];
+        tw[d].resize((size_t)(2 * K - 1) * ng);
+        for (int ni = 0; ni < 2 * K - 1; ni++) {
+            const long n = ni - (K - 1);
+            for (int g = 0; g < ng; g++) {
+                long r = (n * g) % ng;
+                if (r < 0) r += ng;
+                const double th = 2.0 * kPi * (double)r / ng;
+                tw[d][(size_t)ni * ng + g] = make_double2(std::cos(th), std::sin(th));
+            }
+        }
+        deconv[d].resize(K);
+        for (int n = 0; n < K; n++) {
+            const double xi = (double)n / ng;
+            double s = 0;
+            for (size_t q = 0; q < gx.size(); q++) {
+                const double t = 0.5 * p.W * gx[q];
+                s += 0.5 * p.W * gw[q] * es_host(t, p.W, p.beta) * std::cos(2.0 * kPi * xi * t);
+            }
+            deconv[d][n] = 1.0 / s;
+        }
+    }
+    twz.assign((size_t)p.ng[2] * p.KZP, make_double2(0, 0));
+    for (int z = 0; z < p.ng[2]; z++)
+        for (int nz = 0; nz < p.KZ; nz++) twz[(size_t)z * p.KZP + nz] = tw[2][(size_t)(nz + p.KZ - 1) * p.ng[2] + z];
+}
+
+static double3 recip_vec(const Handle& h) {
+    return make_double3(2 * kPi / h.box_L[0], 2 * kPi / h.box_L[1], 2 * kPi / h.box_L[2]);
+}
+
+void launch_grid_sort(Handle& h, const double* pos) {
+    const GridPlan& p = h.gp;
+    const int nown = h.hi - h.lo;
+    const int3 ng = make_int3(p.ng[0], p.ng[1], p.ng[2]), nb = make_int3(p.nb[0], p.nb[1], p.nb[2]);
+    const double3 L = make_double3(h.box_L[0], h.box_L[1], h.box_L[2]);
+    check_hip(hipMemsetAsync(h.g_cnt, 0, sizeof(int) * p.nbins, h.stream), "memset bins");
+    hipLaunchKernelGGL(k_g_bin, dim3(nblk(nown, 256)), dim3(256), 0, h.stream, h.lo, nown, pos, h.q, L, ng, p.W,
+                       nb, h.g_srec, h.g_g0u, h.g_rank, h.g_cnt);
+    hipLaunchKernelGGL(k_g_scan, dim3(1), dim3(kGScan), 0, h.stream, p.nbins, h.g_cnt, h.g_start);
+    hipLaunchKernelGGL(k_g_scatter, dim3(nblk(nown, 256)), dim3(256), 0, h.stream, nown, h.g_g0u, h.g_rank, h.g_start,
+                       h.g_tmp);
+    hipLaunchKernelGGL(k_g_order, dim3(nblk(p.nbins, 4)), dim3(256), 0, h.stream, p.nbins, h.g_start, h.g_tmp,
+                       h.g_order);
+    hipLaunchKernelGGL(k_g_taps, dim3(nblk((int64_t)nown * kTapStride, 256)), dim3(256), 0, h.stream, nown, p.W, p.beta,
+                       ng, h.g_order, h.g_srec, h.g_g0u, h.g_taps, h.g_g0s);
+}
+
+#define CF_GRID_W_DISPATCH(W_, CALL) \
+    switch (W_) {                    \
+        case 4: CALL(4); break;      \
+        case 5: CALL(5); break;      \
+        case 6: CALL(6); break;      \
+        case 7: CALL(7); break;      \
+        case 8: CALL(8); break;      \
+        case 9: CALL(9); break;      \
+        case 10: CALL(10); break;    \
+        case 11: CALL(11); break;    \
+        case 12: CALL(12); break;    \
+        case 13: CALL(13); break;    \
+        case 14: CALL(14); break;    \
+        case 15: CALL(15); break;    \
+        default: CALL(16); break;    \
+    }
+
+void launch_grid_spread(Handle& h) {
+    const GridPlan& p = h.gp;
+    const int3 ng = make_int3(p.ng[0], p.ng[1], p.ng[2]), nb = make_int3(p.nb[0], p.nb[1], p.nb[2]);
+    const int nblocks = ((p.nb[0] + 1) / 2) * ((p.nb[1] + 1) / 2) * ((p.nb[2] + 1) / 2);
+    hipLaunchKernelGGL(k_g_spread, dim3(nblocks), dim3(512), sizeof(double) * 2 * kSpreadCap * kTapStride, h.stream, ng,
+                       nb, h.g_start, h.g_taps, h.g_grid);
+}
+
+void launch_grid_dft_fwd(Handle& h) {
+    const GridPlan& p = h.gp;
+    const int rows = p.ng[0] * p.ng[1];
+    hipLaunchKernelGGL(k_g_dftz_fwd, dim3(nblk(rows, 256), p.KZP / kNZB), dim3(256), 0, h.stream, rows, p.ng[2], p.KZ,
+                       p.KZP, h.g_grid, h.g_twz, h.g_t1);
+    // y: [X][ngy][KZ] -> [X][NY][KZ]
+    hipLaunchKernelGGL(k_g_contract, dim3(nblk(p.ng[0] * p.KZ, 256), nblk(p.NY, kAP)), dim3(256), 0, h.stream, p.ng[0],
+                       p.ng[1], p.NY, p.KZ, h.g_t1, h.g_tw[1], p.ng[1], 1, h.g_t2);
+    // x: [ngx][NY*KZ] -> [NX][NY*KZ]
+    hipLaunchKernelGGL(k_g_contract, dim3(nblk(p.NY * p.KZ, 256), nblk(p.NX, kAP)), dim3(256), 0, h.stream, 1, p.ng[0],
+                       p.NX, p.NY * p.KZ, h.g_t2, h.g_tw[0], p.ng[0], 1, h.g_b);
+}
+
+double* grid_reduce_buffer(Handle& h, int64_t* count) {
+    *count = (int64_t)2 * h.gp.NX * h.gp.NY * h.gp.KZ;
+    return reinterpret_cast<double*>(h.g_b);
+}
+
+void launch_grid_coeffs(Handle& h, int include_energy) {
+    const GridPlan& p = h.gp;
+    const double V = h.box_L[0] * h.box_L[1] * h.box_L[2];
+    const double cst = 4.0 / V * kPi * kOne4PiEps0;   // RCK:517
+    const int total = p.NX * p.NY * p.KZ;
+    h.e_rec_nblk = nblk(total, 256);
+    hipLaunchKernelGGL(k_g_coeffs, dim3(h.e_rec_nblk), dim3(256), 0, h.stream, p.KX, p.KY, p.KZ, recip_vec(h), cst,
+                       1.0 / (h.alpha * h.alpha), h.g_deconv[0], h.g_deconv[1], h.g_deconv[2], h.g_b, h.e_rec_part,
+                       include_energy);
+}
+
+void launch_grid_dft_inv(Handle& h) {
+    const GridPlan& p = h.gp;
+    // x: [NX][NY*KZ] -> [ngx][NY*KZ]
+    hipLaunchKernelGGL(k_g_contract, dim3(nblk(p.NY * p.KZ, 256), nblk(p.ng[0], kAP)), dim3(256), 0, h.stream, 1, p.NX,
+                       p.ng[0], p.NY * p.KZ, h.g_b, h.g_tw[0], 1, p.ng[0], h.g_t2);
+    // y: [ngx][NY][KZ] -> [ngx][ngy][KZ]
+    hipLaunchKernelGGL(k_g_contract, dim3(nblk(p.ng[0] * p.KZ, 256), nblk(p.ng[1], kAP)), dim3(256), 0, h.stream,
+                       p.ng[0], p.NY, p.ng[1], p.KZ, h.g_t2, h.g_tw[1], 1, p.ng[1], h.g_t1);
+    // z: half spectrum -> real rows
+    const int rows = p.ng[0] * p.ng[1];
+    const int nblocks = nblk(rows, 4 * kRW) * ((p.ng[2] + 63) / 64);
+    hipLaunchKernelGGL(k_g_dftz_inv, dim3(nblocks), dim3(256), sizeof(double2) * 4 * kRW * p.KZ, h.stream, rows,
+                       p.ng[2], p.KZ, h.g_t1, h.g_tw[2] + (size_t)(p.KZ - 1) * p.ng[2], h.g_grid);
+}
+
+void launch_grid_interp(Handle& h) {
+    const GridPlan& p = h.gp;
+    const int3 ng = make_int3(p.ng[0], p.ng[1], p.ng[2]), nb = make_int3(p.nb[0], p.nb[1], p.nb[2]);
+    const double3 gs = make_double3(p.ng[0] / h.box_L[0], p.ng[1] / h.box_L[1], p.ng[2] / h.box_L[2]);
+    const size_t R = 7 + p.W;
+    const size_t lds = R * R * R * sizeof(double);
+#define CF_INTERP(W_)                                                                                               \
+    hipLaunchKernelGGL(k_g_interp<W_>, dim3(p.nbins), dim3(256), lds, h.stream, ng, nb, h.g_start, h.g_g0s, h.g_srec, \
+                       p.beta, gs, h.g_grid, h.t_part)
+    CF_GRID_W_DISPATCH(p.W, CF_INTERP)
+#undef CF_INTERP
+}
+
+}  // namespace cf

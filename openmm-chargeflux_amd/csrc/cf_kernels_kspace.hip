@@ -665,6 +665,7 @@ void launch_kspace_sfac(Handle& h) {
 }
 
 double* kspace_reduce_buffer(Handle& h, int64_t* count) {
+    if (h.kspace_algo == 2) return grid_reduce_buffer(h, count);
     if (h.kspace_algo == 1) {
         *count = 2 * h.khalf;
         return h.sk_red;

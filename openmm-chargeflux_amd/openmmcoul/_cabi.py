@@ -55,7 +55,8 @@ class cf_options(C.Structure):
         ("rank", C.c_int32),
         ("world_size", C.c_int32),
         ("kspace_algo", C.c_int32),
-        ("reserved", C.c_int32 * 7),
+        ("grid_width", C.c_int32),
+        ("reserved", C.c_int32 * 6),
     ]
 
 

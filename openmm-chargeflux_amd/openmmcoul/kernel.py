@@ -70,8 +70,15 @@ class HipCalcCoulForceKernel:
     def Name():
         return "CalcCoulForce"
 
-    def __init__(self, device: int = 0, stream=None, rank: int = 0, world_size: int = 1, kspace_algo: int = 0):
+    # reciprocal-sum algorithms (cf_options.kspace_algo, include/chargeflux.h)
+    KSPACE_EXACT_MFMA = 0   # exact k-sum, fp64 MFMA separable form
+    KSPACE_EXACT_VALU = 1   # exact k-sum, direct sincos (check path)
+    KSPACE_GRID = 2         # same k-sum via ES-kernel grid (spread, pruned DFT, interpolate)
+
+    def __init__(self, device: int = 0, stream=None, rank: int = 0, world_size: int = 1, kspace_algo: int = 0,
+                 grid_width: int = 0):
         self._lib = _cabi.load_library()
+        self._grid_width = grid_width
         self._h = C.c_void_p()
         self._device = device
         self._stream = stream
@@ -92,6 +99,7 @@ class HipCalcCoulForceKernel:
         opt.device = self._device
         opt.stream = C.c_void_p(self._stream) if self._stream else None
         opt.rank, opt.world_size, opt.kspace_algo = self._rank, self._world, self._algo
+        opt.grid_width = self._grid_width
         self.destroy()
         _cabi.check(self._lib.cf_create(C.byref(params), C.byref(opt), C.byref(self._h)), self._lib)
         del keep
@@ -248,7 +256,7 @@ class Context:
     System (CoulForceImpl::initialize, CoulForceImpl.cpp:16-21) and evaluates them with the
     force-group test of CoulForceImpl::calcForcesAndEnergy (CoulForceImpl.cpp:23-27)."""
 
-    def __init__(self, system: System, device: int = 0, kspace_algo: int = 0):
+    def __init__(self, system: System, device: int = 0, kspace_algo: int = 0, grid_width: int = 0):
         self._system = system
         self._n = system.getNumParticles()
         self._pos = np.zeros((self._n, 3))
@@ -257,7 +265,8 @@ class Context:
         self._impls = []
         for f in system.getForces():
             if isinstance(f, CoulForce):
-                k = HipCalcCoulForceKernel(device=device, kspace_algo=kspace_algo).initialize(system, f)
+                k = HipCalcCoulForceKernel(device=device, kspace_algo=kspace_algo,
+                                           grid_width=grid_width).initialize(system, f)
                 self._impls.append((f, k))
 
     def setPositions(self, positions):

@@ -1,0 +1,171 @@
+"""GPU parity of the grid reciprocal path (kspace_algo = 2: ES-kernel spreading, pruned
+DFT, interpolation) against the oracle restatement of
+ReferenceCoulKernels.cpp:513-556 and against the exact fp64-MFMA k-sum.
+
+The grid evaluates the reference's own truncated k-sum (same k-set, weights and current
+box); its only error is the ES-kernel quadrature error, set by the kernel width W.
+Tolerances (written here; north star: forces within 1e-5 kJ/mol/nm):
+  forces   max |dF|         <= 1e-6 kJ/mol/nm   (W = 14 observed ~1e-8, W = 12 ~5e-7)
+  energy   |dE|             <= 1e-9 |E| + 1e-8 kJ/mol
+  dE/dq    max |d(dE/dq)|   <= 1e-9 max|dE/dq| + 1e-9
+  charges  max |dq|         <= 1e-12 e (untouched by the k-space method)
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+from oracle import Oracle  # noqa: E402
+from openmmcoul import HipCalcCoulForceKernel, ChargeFluxError  # noqa: E402
+from openmmcoul import testsystems as ts  # noqa: E402
+from openmmcoul.distributed import device_buffer_as_tensor  # noqa: E402
+
+GRID = HipCalcCoulForceKernel.KSPACE_GRID
+F_TOL = 1e-6
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+
+
+def _compare(got, ref, f_tol=F_TOL, e_rel=1e-9):
+    e, f, q, dq, terms = got
+    assert abs(e - ref["energy"]) <= e_rel * abs(ref["energy"]) + 1e-8, (e, ref["energy"])
+    if dq is not None:
+        assert np.abs(f - ref["forces"]).max() <= f_tol, np.abs(f - ref["forces"]).max()
+        scale = np.abs(ref["dedq"]).max()
+        assert np.abs(dq - ref["dedq"]).max() <= 1e-9 * scale + 1e-9, np.abs(dq - ref["dedq"]).max()
+    assert np.abs(q - ref["charges"]).max() <= 1e-12
+    for a, b in zip(terms, ref["terms"]):
+        assert abs(a - b) <= e_rel * max(abs(b), 1.0) + 1e-8, (terms, ref["terms"])
+
+
+def _run(kernel, pos, box, fl=True, en=True):
+    e, f = kernel.execute_host(pos, box, fl, en)
+    return e, f, kernel.charges(), (kernel.dedq() if fl else None), kernel.energy_terms()
+
+
+@pytest.mark.parametrize("nw,rc,tol", [(100, 0.6, 1e-5), (400, 0.7, 1e-4)])
+def test_grid_small_boxes(nw, rc, tol):
+    system, force, pos, box = ts.water_box(nw, cutoff=rc, ewald_tol=tol, every_bond_angle=3)
+    k = HipCalcCoulForceKernel(kspace_algo=GRID).initialize(system, force)
+    o = Oracle(force, box)
+    for fl, en in ((True, True), (True, False), (False, True)):
+        _compare(_run(k, pos, box, fl, en), o.execute(pos, box, fl, en))
+
+
+@pytest.mark.parametrize("width", [12, 14, 16])
+def test_grid_c2_parity(width):
+    system, force, pos, box = ts.make("C2")
+    k = HipCalcCoulForceKernel(kspace_algo=GRID, grid_width=width).initialize(system, force)
+    assert k.ewald_params()[1] == (7, 7, 7)
+    _compare(_run(k, pos, box), Oracle(force, box).execute(pos, box))
+
+
+def test_grid_c2_golden_fixture():
+    import os
+    d = np.load(os.path.join(os.path.dirname(__file__), "golden", "c2.npz"))
+    system, force, pos, box = ts.make("C2")
+    k = HipCalcCoulForceKernel(kspace_algo=GRID).initialize(system, force)
+    e, f = k.execute_host(pos, box)
+    assert abs(e - float(d["energy"])) <= 1e-9 * abs(float(d["energy"]))
+    assert np.abs(f - d["forces"]).max() <= F_TOL
+
+
+def test_grid_nacl_madelung_atoms_on_grid_points():
+    # ions sit exactly on grid points (first taps at the support edge: phi = 0 there)
+    system, force, pos, box = ts.nacl_crystal(cells=4, a=0.5, cutoff=1.0, ewald_tol=1e-10)
+    k = HipCalcCoulForceKernel(kspace_algo=GRID).initialize(system, force)
+    e, f = k.execute_host(pos, box)
+    expect = -(len(pos) / 2) * 1.747564594633182 * 138.935456 / 0.25
+    assert e == pytest.approx(expect, rel=2e-9)
+    assert np.abs(f).max() < 1e-6
+
+
+def test_grid_moved_box_and_wrapped_positions():
+    system, force, pos, box = ts.water_box(400, cutoff=0.7, ewald_tol=1e-4)
+    p2 = pos + np.array([3.1, -7.4, 12.0])
+    box2 = box * 1.02
+    k = HipCalcCoulForceKernel(kspace_algo=GRID).initialize(system, force)
+    _compare(_run(k, p2, box2), Oracle(force, box).execute(p2, box2))
+
+
+def test_grid_noncubic_box():
+    system, force, pos, box = ts.water_box(400, cutoff=0.7, ewald_tol=1e-4)
+    box2 = box.copy()
+    box2[0, 0] *= 1.3
+    box2[2, 2] *= 0.95
+    system.setDefaultPeriodicBoxVectors(*box2)
+    k = HipCalcCoulForceKernel(kspace_algo=GRID).initialize(system, force)
+    o = Oracle(force, box2)
+    assert k.ewald_params()[1] == o.ewald()[1]
+    _compare(_run(k, pos, box2), o.execute(pos, box2))
+
+
+def test_grid_device_api_deterministic():
+    system, force, pos, box = ts.water_box(1500, cutoff=1.0, ewald_tol=1e-4)
+    stream = torch.cuda.current_stream().cuda_stream
+    k = HipCalcCoulForceKernel(stream=stream, kspace_algo=GRID).initialize(system, force)
+    e_h, f_h = k.execute_host(pos, box)
+    pt = torch.tensor(pos, dtype=torch.float64, device="cuda")
+    outs = []
+    for _ in range(2):
+        f = torch.zeros_like(pt)
+        e = torch.zeros(1, dtype=torch.float64, device="cuda")
+        k.execute_device(pt, box, True, True, f, e)
+        torch.cuda.synchronize()
+        outs.append((e.item(), f.cpu().numpy()))
+    assert outs[0][0] == outs[1][0] and np.array_equal(outs[0][1], outs[1][1])  # bitwise reproducible
+    assert outs[0][0] == e_h and np.array_equal(outs[0][1], f_h)
+
+
+def test_grid_two_rank_decomposition_on_one_gpu():
+    system, force, pos, box = ts.water_box(2400, cutoff=1.0, ewald_tol=1e-4, every_bond_angle=4)
+    stream = torch.cuda.current_stream().cuda_stream
+    pt = torch.tensor(pos, dtype=torch.float64, device="cuda")
+    single = HipCalcCoulForceKernel(stream=stream, kspace_algo=GRID).initialize(system, force)
+    e1, f1 = single.execute_host(pos, box)
+    ks = [HipCalcCoulForceKernel(stream=stream, rank=r, world_size=2, kspace_algo=GRID).initialize(system, force)
+          for r in range(2)]
+    for k in ks:
+        k.begin(pt, box, True, True)
+    bufs = [device_buffer_as_tensor(*k.kspace_buffer(), "cuda") for k in ks]
+    total = bufs[0] + bufs[1]
+    for b in bufs:
+        b.copy_(total)
+    f = torch.zeros_like(pt)
+    es = []
+    for k in ks:
+        e = torch.zeros(1, dtype=torch.float64, device="cuda")
+        k.end(f, e)
+        es.append(e)
+    torch.cuda.synchronize()
+    assert (es[0] + es[1]).item() == pytest.approx(e1, rel=1e-11)
+    assert np.abs(f.cpu().numpy() - f1).max() < 1e-8
+
+
+def test_grid_c3_matches_exact_mfma_path():
+    # full C3 (96k atoms, kmax 31): grid path against the exact fp64-MFMA k-sum
+    system, force, pos, box = ts.make("C3")
+    ka = HipCalcCoulForceKernel(kspace_algo=0).initialize(system, force)
+    kg = HipCalcCoulForceKernel(kspace_algo=GRID).initialize(system, force)
+    ea, fa = ka.execute_host(pos, box)
+    eg, fg = kg.execute_host(pos, box)
+    assert abs(eg - ea) <= 1e-9 * abs(ea) + 1e-8, (eg, ea)
+    assert np.abs(fg - fa).max() <= F_TOL, np.abs(fg - fa).max()
+    da, dg = ka.dedq(), kg.dedq()
+    assert np.abs(dg - da).max() <= 1e-9 * np.abs(da).max() + 1e-9
+    ta, tg = ka.energy_terms(), kg.energy_terms()
+    assert tg[1] == pytest.approx(ta[1], rel=1e-10)
+
+
+def test_grid_options_validation():
+    system, force, pos, box = ts.water_box(100, cutoff=0.6)
+    with pytest.raises(ChargeFluxError):
+        HipCalcCoulForceKernel(kspace_algo=GRID, grid_width=3).initialize(system, force)
+    with pytest.raises(ChargeFluxError):
+        HipCalcCoulForceKernel(kspace_algo=7).initialize(system, force)
