@@ -428,6 +428,7 @@ CF_EXPORT int cf_create(const cf_params* p, const cf_options* opt, cf_handle** o
         h.e_atom = dalloc<double>(H, (size_t)3 * n);
         h.f_part = dalloc<double>(H, (size_t)3 * n);
         h.terms_dev = dalloc<double>(H, 4);
+        h.e_part = dalloc<double>(H, 3 * ((size_t)n / 2048 + 2));
         h.energy_dev = dalloc<double>(H, 1);
         check_hip(hipMemset(h.dedq, 0, sizeof(double) * n), "memset");
         check_hip(hipMemset(h.f_part, 0, sizeof(double) * 3 * n), "memset");
@@ -437,10 +438,28 @@ CF_EXPORT int cf_create(const cf_params* p, const cf_options* opt, cf_handle** o
         if (h.pbc) {
             const cf::KGeom& g = h.kg;
             set_cells(H, std::vector<double>{p->default_box[0], p->default_box[4], p->default_box[8]}.data());
+            h.erfc_tab = dupload(H, cf::erfc_table(h.alpha * h.cutoff * (1.0 + 1e-9), &h.erfc_scale, &h.erfc_m));
             h.cell_key = dalloc<int>(H, n); h.cell_key_sorted = dalloc<int>(H, n);
             h.atom_val = dalloc<int>(H, n); h.atom_sorted = dalloc<int>(H, n);
             h.pos4s = dalloc<double4>(H, n);
             h.ljs = dalloc<double2>(H, n);
+            // LJ types: exact-equal (sigma/2, 2 sqrt eps) pairs; <= 64 types ride in the list entries
+            {
+                std::vector<int> at(n);
+                std::vector<double2> tt;
+                for (int i = 0; i < n && (int)tt.size() <= 64; i++) {
+                    int k = 0;
+                    while (k < (int)tt.size() && !(tt[k].x == lj[i].x && tt[k].y == lj[i].y)) k++;
+                    if (k == (int)tt.size()) tt.push_back(lj[i]);
+                    at[i] = k;
+                }
+                if ((int)tt.size() <= 64) {
+                    h.lj_ntypes = (int)tt.size();
+                    h.atom_type = dupload(H, at);
+                    h.lj_tab = dupload(H, tt);
+                    h.typ_s = dalloc<int>(H, n);
+                }
+            }
             h.key_tmp = dalloc<int>(H, n);
             h.atom_tmp = dalloc<int>(H, n);
             h.skin_flag = dalloc<int>(H, 1);

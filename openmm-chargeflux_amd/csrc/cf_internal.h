@@ -122,6 +122,10 @@ struct Handle {
     int* cell_start = nullptr; int* cell_end = nullptr; int* cell_cnt = nullptr;
     double4* pos4s = nullptr;   // [N] sorted wrapped (x,y,z,q)
     double2* ljs = nullptr;     // [N] sorted LJ
+    int lj_ntypes = 0;          // distinct (sigma/2, 2 sqrt eps) pairs if <= 64, else 0
+    int* atom_type = nullptr;   // [N] LJ type per atom
+    int* typ_s = nullptr;       // [N] LJ type per sorted slot (null without types)
+    double2* lj_tab = nullptr;  // [lj_ntypes]
     // persistent list with skin: pairs within rc + list_skin at the last
     // build; reused while every atom has moved <= list_skin/2 and the box is unchanged
     double skin = 0.0;          // requested skin (nm); 0 = rebuild on every evaluation
@@ -176,7 +180,10 @@ struct Handle {
     double4* kvec = nullptr;    // [khalf] (kx,ky,kz, w=2*c*eak)
     int sk_nchunk = 0;
     // energy
+    double* erfc_tab = nullptr;  // erfcx interval polynomials (cf_kernels_core.hip erfc_table)
+    double erfc_scale = 0; int erfc_m = 0;
     double* terms_dev = nullptr; // [4]
+    double* e_part = nullptr;    // [ceil(Nown/2048)][3] energy block partials
     double* energy_dev = nullptr;// [1] internal
     // state
     int pending_flags = -1;     // flags of a begun evaluation
@@ -185,6 +192,7 @@ struct Handle {
 };
 
 // ---- launchers (cf_kernels_*.hip) ------------------------------------------------
+std::vector<double> erfc_table(double xmax, double* scale, int* m);
 void launch_flux_terms(Handle& h, const double* pos);
 void launch_atoms_prep(Handle& h, const double* pos);
 void launch_cell_sort(Handle& h, const double* pos);

@@ -3,6 +3,8 @@
 // gathers in a fixed order (no atomics), so results are bitwise reproducible.
 //
 // Reference semantics: platforms/reference/src/ReferenceCoulKernels.cpp (RCK).
+#include <algorithm>
+
 #include "cf_internal.h"
 
 namespace cf {
@@ -290,6 +292,7 @@ __global__ void __launch_bounds__(256) k_cell_commit(int n, const int* __restric
                                                      const double2* __restrict__ lj, double3 L,
                                                      int* __restrict__ key_s, int* __restrict__ idx_s,
                                                      double4* __restrict__ pos4s, double2* __restrict__ ljs,
+                                                     const int* __restrict__ atype, int* __restrict__ typ_s,
                                                      double* __restrict__ pos_ref, long long* __restrict__ n_builds) {
     int s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= n) return;
@@ -301,6 +304,7 @@ __global__ void __launch_bounds__(256) k_cell_commit(int n, const int* __restric
         pos4s[s] = make_double4(x.x - floor(x.x / L.x) * L.x, x.y - floor(x.y / L.y) * L.y,
                                 x.z - floor(x.z / L.z) * L.z, q[i]);
         ljs[s] = lj[i];
+        if (typ_s) typ_s[s] = atype[i];
         if (pos_ref) { pos_ref[3 * i] = x.x; pos_ref[3 * i + 1] = x.y; pos_ref[3 * i + 2] = x.z; }
         if (s == 0) *n_builds += 1;
     } else {
@@ -339,14 +343,19 @@ __global__ void __launch_bounds__(256) k_skin_check(int n, const double* __restr
 //       exclusion correction, and finishes dE/dq_i and the non-chain forces.
 // ---------------------------------------------------------------------------------
 constexpr int kMaxRegExcl = 8;
+constexpr int kErfcDeg = 12;     // erfcx polynomial degree per interval
+constexpr int kErfcMaxM = 32;    // intervals (width 0.375): x = alpha r up to 12
+constexpr int kMaxLjTypes = 64;  // LJ types carried in the 6 high bits of a list entry
 constexpr int kSeg = 4;          // neighbour sub-lists per atom (one per scanning wave / pair lane)
 constexpr int kShiftBits = 26;
 constexpr int kBruteShift = 31;  // shift code: minimum image by floor (brute-force path)
 
 struct DirectArgs {
     int n, lo, hi, include_forces;
-    double3 L; int3 nc; int brute;
+    double3 L; double3 invL; int3 nc; int brute;
     double rc2, alpha;
+    const double* erfc_tab;     // [erfc_m][kErfcDeg+1] erfcx(x) on intervals of width 1/erfc_scale
+    double erfc_scale; int erfc_m;
     double rl2;                 // list radius^2: (rc + list skin)^2
     int nb_cap;                 // capacity of ONE of the kSeg sub-lists
     int nlr;                    // list rows = owned atoms; row c <-> sorted slot own_slot(c)
@@ -355,6 +364,8 @@ struct DirectArgs {
     const int* atom_sorted; const int* key_sorted;
     const int* cstart; const int* cend;
     const double4* pos4s; const double2* ljs;
+    const int* typ_s;           // [N] LJ type per sorted slot (null: > kMaxLjTypes distinct types)
+    const double2* lj_tab; int lj_ntypes;   // per-type (sigma/2, 2 sqrt(eps))
     const double* pos; const double* q;
     const int* ex_start; const int* ex_list;
     const double* dedq_self;
@@ -375,8 +386,11 @@ __device__ __forceinline__ bool in_excl(int j, const int* reg, int cnt, const in
 }
 
 __device__ __forceinline__ double3 shift_of(int code, double3 L) {
-    int ox = code / 9 - 1, oy = (code / 3) % 3 - 1, oz = code % 3 - 1;
-    return make_double3(ox * L.x, oy * L.y, oz * L.z);
+    // code = kx*9 + ky*3 + kz in [0, 27) -> image offsets (k - 1) * L, by multiply-shift division
+    const unsigned c = (unsigned)code;
+    const unsigned kx = (c * 57u) >> 9, r = c - 9u * kx;
+    const unsigned ky = (r * 11u) >> 5, kz = r - 3u * ky;
+    return make_double3(((int)kx - 1) * L.x, ((int)ky - 1) * L.y, ((int)kz - 1) * L.z);
 }
 
 // Visit the 27 neighbour cells of sorted atom s; fn(t, code, dx, dy, dz, r2) for every
@@ -437,7 +451,7 @@ __global__ void __launch_bounds__(256) k_nlist(DirectArgs a) {
         int cnt = 0;
         scan_cells(a, s, pi, a.rl2, [&](int t, int code, double, double, double, double) {
             if (exc && in_excl(a.atom_sorted[t], reg, exc, a.ex_list, ex0)) return;
-            if (cnt < a.nb_cap) a.nl[((size_t)seg * a.nb_cap + cnt) * a.nlr + c] = t | (code << kShiftBits);
+            if (cnt < a.nb_cap) a.nl[((size_t)seg * a.nb_cap + cnt) * a.nlr + c] = t | ((a.typ_s ? a.typ_s[t] : code) << kShiftBits);
             cnt++;
         }, seg, kSeg);
         a.nl_cnt[(size_t)seg * a.nlr + c] = cnt;
@@ -506,7 +520,7 @@ __global__ void __launch_bounds__(kWaveNL * kSeg) k_nlist_wave(DirectArgs a) {
     int cnt = 0;
     auto emit = [&](int t, int j, int code) {
         if (j >= ex_min && j <= ex_max && in_excl(j, reg, exc, a.ex_list, ex0)) return;
-        if (cnt < a.nb_cap) a.nl[(seg_off + cnt) * a.nlr + c] = t | (code << kShiftBits);
+        if (cnt < a.nb_cap) a.nl[(seg_off + cnt) * a.nlr + c] = t | ((a.typ_s ? a.typ_s[t] : code) << kShiftBits);
         cnt++;
     };
     if (!fits) {  // wave-uniform (and block-uniform: every wave sees the same 64 atoms)
@@ -645,15 +659,33 @@ struct PairAcc {
     double fx = 0, fy = 0, fz = 0, dq = 0, e = 0;
 };
 
-// real-space Ewald + LJ pair (RCK:567-592), d = pos_i - pos_j (minimum image)
-__device__ __forceinline__ void pair_term(PairAcc& acc, const DirectArgs& a, double4 pi, double2 li, double4 pj,
-                                          double2 lj2, double dx, double dy, double dz, double r2) {
+// erfc(x) = e^{-x^2} erfcx(x): erfcx from a piecewise degree-12 polynomial (interval table
+// in LDS, fitted at cf_create in long double, relative error ~4e-15 over [0, alpha*rc]),
+// and e^{-x^2} is shared with the force term -> one exp per pair instead of erfc + exp.
+__device__ __forceinline__ double erfc_exp(double x, const double* __restrict__ tab, double scale, double& e2) {
+    const double y = x * scale;
+    const int i = (int)y;
+    const double u = 2.0 * (y - (double)i) - 1.0;
+    const double* c = tab + i * (kErfcDeg + 1);
+    double p = c[kErfcDeg];
+#pragma unroll
+    for (int j = kErfcDeg - 1; j >= 0; j--) p = fma(p, u, c[j]);
+    e2 = exp(-x * x);
+    return e2 * p;
+}
+
+// real-space Ewald + LJ pair (RCK:567-592), d = pos_i - pos_j (minimum image); tab = LDS
+// copy of the erfcx table (the cutoff test r <= rc guarantees alpha r lies inside it)
+__device__ __forceinline__ void pair_term(PairAcc& acc, const DirectArgs& a, const double* __restrict__ tab,
+                                          double4 pi, double2 li, double4 pj, double2 lj2, double dx, double dy,
+                                          double dz, double r2) {
     const double ke = kOne4PiEps0;
     const double two_over_sqrtpi = 1.1283791670955126;
     double inv_r = rsqrt_fp64(r2);
     double r = r2 * inv_r;
     double ar = a.alpha * r;
-    double ec = erfc(ar);
+    double e2;
+    double ec = erfc_exp(ar, tab, a.erfc_scale, e2);
     double sig = li.x + lj2.x;
     double s2 = inv_r * sig; s2 *= s2;
     double sig6 = s2 * s2 * s2;
@@ -661,12 +693,18 @@ __device__ __forceinline__ void pair_term(PairAcc& acc, const DirectArgs& a, dou
     double qq = ke * pi.w * pj.w * inv_r;
     if (a.include_forces) {
         double inv_r2 = inv_r * inv_r;
-        double dEdR = qq * inv_r2 * (ec + ar * exp(-ar * ar) * two_over_sqrtpi);
+        double dEdR = qq * inv_r2 * (ec + ar * e2 * two_over_sqrtpi);
         dEdR += es6 * (12 * sig6 - 6) * inv_r2;
         acc.fx += dEdR * dx; acc.fy += dEdR * dy; acc.fz += dEdR * dz;
         acc.dq += ke * pj.w * inv_r * ec;
     }
     acc.e += 0.5 * (qq * ec + es6 * (sig6 - 1));
+}
+
+// stage the erfcx table in LDS (all threads of the block; call before any early return)
+__device__ __forceinline__ void load_erfc_tab(const DirectArgs& a, double* tab) {
+    for (int e = threadIdx.x; e < a.erfc_m * (kErfcDeg + 1); e += blockDim.x) tab[e] = a.erfc_tab[e];
+    __syncthreads();
 }
 
 // exclusion correction of atom i (RCK:596-622) + finish dE/dq and the non-chain forces
@@ -724,8 +762,15 @@ __global__ void __launch_bounds__(256) k_recip_add(int lo, int nown, int nparts,
 // overflowed sub-list are left to k_pairs_overflow.
 // LPA lanes per atom (4, 8 or 16; more when few atoms are owned, so the grid still fills
 // the chip): lane g walks entries g/4, g/4 + LPA/4, ... of sub-list g%4.
-template <int LPA>
+// TYPES: the partner's LJ parameters come from the per-type table (LDS) indexed by the high
+// bits of the list entry instead of a third gathered 16-B load per candidate.
+template <int LPA, bool TYPES>
 __global__ void __launch_bounds__(256) k_pairs(DirectArgs a) {
+    __shared__ double tab[kErfcMaxM * (kErfcDeg + 1)];
+    __shared__ double2 ljt[kMaxLjTypes];
+    if (TYPES)
+        for (int e = threadIdx.x; e < a.lj_ntypes; e += blockDim.x) ljt[e] = a.lj_tab[e];
+    load_erfc_tab(a, tab);
     const int gt = blockIdx.x * blockDim.x + threadIdx.x;
     const int c = gt / LPA, g = gt % LPA;
     const int seg = g % kSeg, part = g / kSeg;
@@ -743,21 +788,28 @@ __global__ void __launch_bounds__(256) k_pairs(DirectArgs a) {
         const double4 pi = a.pos4s[ss];
         const double2 li = a.ljs[ss];
         const int* nl = a.nl + (size_t)seg * a.nb_cap * a.nlr + cc;
-        for (int k = part; k < cnt; k += LPA / kSeg) {
-            int v = nl[(size_t)k * a.nlr];
-            int t = v & ((1 << kShiftBits) - 1), code = v >> kShiftBits;
-            double4 pj = a.pos4s[t];
-            double2 lj2 = a.ljs[t];
-            double dx, dy, dz;
-            if (code != kBruteShift) {
-                double3 sh = shift_of(code, a.L);
-                dx = pi.x - (pj.x + sh.x); dy = pi.y - (pj.y + sh.y); dz = pi.z - (pj.z + sh.z);
-            } else {
-                double3 d = delta_r(make_double3(pj.x, pj.y, pj.z), make_double3(pi.x, pi.y, pi.z), a.L, 1);
-                dx = d.x; dy = d.y; dz = d.z;
-            }
+        constexpr int step = LPA / kSeg;
+        constexpr int kMask = (1 << kShiftBits) - 1;
+        // software pipeline: list entry k + 2*step and the coordinates of entry k + step are
+        // in flight while entry k is evaluated (out-of-range entries read atom 0, unused).
+        // The pair vector is the minimum image d - L rint(d/L) (getDeltaRPeriodic's
+        // floor(d/L + 0.5) up to exact half-box ties, which lie beyond the cutoff), so the
+        // image code stored in the list is not needed here.
+        int v0 = part < cnt ? nl[(size_t)part * a.nlr] : 0;
+        int v1 = part + step < cnt ? nl[(size_t)(part + step) * a.nlr] : 0;
+        double4 pj = a.pos4s[v0 & kMask];
+        double2 lj2 = TYPES ? ljt[(unsigned)v0 >> kShiftBits] : a.ljs[v0 & kMask];
+        for (int k = part; k < cnt; k += step) {
+            const int v2 = k + 2 * step < cnt ? nl[(size_t)(k + 2 * step) * a.nlr] : 0;
+            const double4 pjn = a.pos4s[v1 & kMask];
+            const double2 ljn = TYPES ? ljt[(unsigned)v1 >> kShiftBits] : a.ljs[v1 & kMask];
+            double dx = pi.x - pj.x, dy = pi.y - pj.y, dz = pi.z - pj.z;
+            dx -= a.L.x * rint(dx * a.invL.x);
+            dy -= a.L.y * rint(dy * a.invL.y);
+            dz -= a.L.z * rint(dz * a.invL.z);
             double r2 = dx * dx + dy * dy + dz * dz;
-            if (r2 <= a.rc2) pair_term(acc, a, pi, li, pj, lj2, dx, dy, dz, r2);  // exact voxel-hash test
+            if (r2 <= a.rc2) pair_term(acc, a, tab, pi, li, pj, lj2, dx, dy, dz, r2);  // exact voxel-hash test
+            v1 = v2; pj = pjn; lj2 = ljn;
         }
     }
 #pragma unroll
@@ -772,6 +824,8 @@ __global__ void __launch_bounds__(256) k_pairs(DirectArgs a) {
 
 // 4c: atoms whose neighbour list overflowed (denser than planned): rescan the cells
 __global__ void __launch_bounds__(256) k_pairs_overflow(DirectArgs a) {
+    __shared__ double tab[kErfcMaxM * (kErfcDeg + 1)];
+    load_erfc_tab(a, tab);
     int c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= a.nlr) return;
     bool over = false;
@@ -788,7 +842,7 @@ __global__ void __launch_bounds__(256) k_pairs_overflow(DirectArgs a) {
     PairAcc acc;
     scan_cells(a, s, pi, a.rc2, [&](int t, int, double dx, double dy, double dz, double r2) {
         if (exc && in_excl(a.atom_sorted[t], reg, exc, a.ex_list, ex0)) return;
-        pair_term(acc, a, pi, li, a.pos4s[t], a.ljs[t], dx, dy, dz, r2);
+        pair_term(acc, a, tab, pi, li, a.pos4s[t], a.ljs[t], dx, dy, dz, r2);
     });
     finish_atom(acc, a, i, ex0, exc);
 }
@@ -884,29 +938,53 @@ __global__ void __launch_bounds__(256) k_assemble(int lo, int hi, const int* __r
     out[3 * b + 2] += fz;
 }
 
-// 7. energy: one workgroup, fixed-order tree reduction (deterministic).
-__global__ void __launch_bounds__(1024) k_energy(int lo, int hi, const double* __restrict__ e_atom,
-                                                 const double* __restrict__ e_rec_part, int nrec,
-                                                 int pbc, double* __restrict__ terms, double* __restrict__ energy_out,
-                                                 double* __restrict__ energy_int) {
-    __shared__ double red[4][1024];
-    double a0 = 0, a1 = 0, a2 = 0, a3 = 0;
-    for (int i = lo + threadIdx.x; i < hi; i += blockDim.x) {
-        a0 += e_atom[3 * i]; a2 += e_atom[3 * i + 1]; a3 += e_atom[3 * i + 2];
-    }
-    for (int k = threadIdx.x; k < nrec; k += blockDim.x) a1 += e_rec_part[k];
-    red[0][threadIdx.x] = a0; red[1][threadIdx.x] = a1; red[2][threadIdx.x] = a2; red[3][threadIdx.x] = a3;
+// 7. energy: fixed-order two-stage tree reduction (deterministic).  Stage 1: each block
+//    sums kEChunk atoms' (self, direct, exclusion) energies; stage 2: one block sums the
+//    block partials and the reciprocal-space partials.
+constexpr int kEChunk = 2048;
+
+__device__ __forceinline__ void block_sum3(double& a0, double& a1, double& a2, double (*red)[256]) {
+    red[0][threadIdx.x] = a0; red[1][threadIdx.x] = a1; red[2][threadIdx.x] = a2;
     __syncthreads();
-    for (int w = blockDim.x / 2; w > 0; w >>= 1) {
+    for (int w = 128; w > 0; w >>= 1) {
         if (threadIdx.x < w)
 #pragma unroll
-            for (int c = 0; c < 4; c++) red[c][threadIdx.x] += red[c][threadIdx.x + w];
+            for (int c = 0; c < 3; c++) red[c][threadIdx.x] += red[c][threadIdx.x + w];
         __syncthreads();
     }
+    a0 = red[0][0]; a1 = red[1][0]; a2 = red[2][0];
+}
+
+__global__ void __launch_bounds__(256) k_energy_part(int lo, int hi, const double* __restrict__ e_atom,
+                                                     double* __restrict__ part) {
+    __shared__ double red[3][256];
+    double a0 = 0, a1 = 0, a2 = 0;
+    const int i0 = lo + blockIdx.x * kEChunk;
+    const int i1 = min(hi, i0 + kEChunk);
+    for (int i = i0 + threadIdx.x; i < i1; i += 256) {
+        a0 += e_atom[3 * i]; a1 += e_atom[3 * i + 1]; a2 += e_atom[3 * i + 2];
+    }
+    block_sum3(a0, a1, a2, red);
+    if (threadIdx.x == 0) { part[3 * blockIdx.x] = a0; part[3 * blockIdx.x + 1] = a1; part[3 * blockIdx.x + 2] = a2; }
+}
+
+__global__ void __launch_bounds__(256) k_energy(int nparts, const double* __restrict__ part,
+                                                const double* __restrict__ e_rec_part, int nrec, int pbc,
+                                                double* __restrict__ terms, double* __restrict__ energy_out,
+                                                double* __restrict__ energy_int) {
+    __shared__ double red[3][256];
+    double a0 = 0, a1 = 0, a2 = 0;
+    for (int k = threadIdx.x; k < nparts; k += 256) { a0 += part[3 * k]; a1 += part[3 * k + 1]; a2 += part[3 * k + 2]; }
+    double r = 0;
+    for (int k = threadIdx.x; k < nrec; k += 256) r += e_rec_part[k];
+    block_sum3(a0, a1, a2, red);
+    __syncthreads();
+    double z0 = r, z1 = 0, z2 = 0;
+    block_sum3(z0, z1, z2, red);
     if (threadIdx.x == 0) {
-        double t0 = red[0][0], t1 = red[1][0], t2 = red[2][0], t3 = red[3][0];
+        const double t0 = a0, t1 = z0, t2 = a1, t3 = a2;
         terms[0] = t0; terms[1] = t1; terms[2] = t2; terms[3] = t3;
-        double e = pbc ? (t0 + t1 + t2 + t3) : t2;
+        const double e = pbc ? (t0 + t1 + t2 + t3) : t2;
         *energy_int = e;
         if (energy_out) *energy_out = e;
     }
@@ -916,6 +994,44 @@ __global__ void __launch_bounds__(1024) k_energy(int lo, int hi, const double* _
 // launchers
 // ---------------------------------------------------------------------------------
 static inline int nblk(int64_t n, int b) { return (int)((n + b - 1) / b); }
+
+// erfcx(x) = erfc(x) e^{x^2} on [0, xmax]: intervals of width 0.375, Chebyshev interpolation
+// of degree kErfcDeg in long double, stored as monomials in u in [-1, 1] per interval
+std::vector<double> erfc_table(double xmax, double* scale, int* m) {
+    const long double w = 0.375L;
+    int M = (int)std::ceil((long double)xmax / w) + 1;
+    if (M > kErfcMaxM) throw std::invalid_argument("alpha * cutoff too large for the erfc table");
+    const int n = kErfcDeg + 1;
+    std::vector<double> tab((size_t)M * n);
+    for (int i = 0; i < M; i++) {
+        std::vector<long double> f(n), c(n, 0.0L);
+        for (int k = 0; k < n; k++) {
+            const long double t = cosl(3.14159265358979323846264338327950288L * (k + 0.5L) / n);
+            const long double x = w * (i + 0.5L * (t + 1.0L));
+            f[k] = erfcl(x) * expl(x * x);
+        }
+        for (int j = 0; j < n; j++) {
+            long double sum = 0;
+            for (int k = 0; k < n; k++)
+                sum += f[k] * cosl(3.14159265358979323846264338327950288L * j * (k + 0.5L) / n);
+            c[j] = (j == 0 ? 1.0L : 2.0L) * sum / n;
+        }
+        // Chebyshev -> monomial: T_0 = 1, T_1 = u, T_{j+1} = 2u T_j - T_{j-1}
+        std::vector<std::vector<long double>> T(n, std::vector<long double>(n, 0.0L));
+        T[0][0] = 1.0L;
+        if (n > 1) T[1][1] = 1.0L;
+        for (int j = 1; j + 1 < n; j++)
+            for (int e = 0; e < n; e++) T[j + 1][e] = (e > 0 ? 2.0L * T[j][e - 1] : 0.0L) - T[j - 1][e];
+        for (int e = 0; e < n; e++) {
+            long double v = 0;
+            for (int j = 0; j < n; j++) v += c[j] * T[j][e];
+            tab[(size_t)i * n + e] = (double)v;
+        }
+    }
+    *scale = (double)(1.0L / w);
+    *m = M;
+    return tab;
+}
 
 void launch_flux_terms(Handle& h, const double* pos) {
     if (h.nterms == 0) return;
@@ -955,7 +1071,8 @@ void launch_cell_sort(Handle& h, const double* pos) {
                            h.atom_val, h.own_s);
     }
     hipLaunchKernelGGL(k_cell_commit, dim3(nblk(h.n, 256)), dim3(256), 0, h.stream, h.n, f, h.cell_key, h.key_tmp,
-                       pos, h.q, h.lj, L, h.cell_key_sorted, h.atom_sorted, h.pos4s, h.ljs, h.pos_ref,
+                       pos, h.q, h.lj, L, h.cell_key_sorted, h.atom_sorted, h.pos4s, h.ljs, h.atom_type, h.typ_s,
+                       h.pos_ref,
                        h.n_builds_dev);
 }
 
@@ -974,9 +1091,11 @@ static DirectArgs direct_args(Handle& h, const double* pos, int include_forces) 
     DirectArgs a;
     a.n = h.n; a.lo = h.lo; a.hi = h.hi; a.include_forces = include_forces;
     a.L = make_double3(h.box_L[0], h.box_L[1], h.box_L[2]);
+    a.invL = make_double3(1.0 / h.box_L[0], 1.0 / h.box_L[1], 1.0 / h.box_L[2]);
     a.nc = make_int3(h.nc[0], h.nc[1], h.nc[2]);
     a.brute = (h.nc[0] < 3 || h.nc[1] < 3 || h.nc[2] < 3) ? 1 : 0;
     a.rc2 = h.cutoff * h.cutoff; a.alpha = h.alpha;
+    a.erfc_tab = h.erfc_tab; a.erfc_scale = h.erfc_scale; a.erfc_m = h.erfc_m;
     a.rl2 = (h.cutoff + h.list_skin) * (h.cutoff + h.list_skin);
     a.nb_cap = h.nb_cap;
     a.nlr = h.hi - h.lo;
@@ -985,6 +1104,7 @@ static DirectArgs direct_args(Handle& h, const double* pos, int include_forces) 
     a.atom_sorted = h.atom_sorted; a.key_sorted = h.cell_key_sorted;
     a.cstart = h.cell_start; a.cend = h.cell_end;
     a.pos4s = h.pos4s; a.ljs = h.ljs;
+    a.typ_s = h.typ_s; a.lj_tab = h.lj_tab; a.lj_ntypes = h.lj_ntypes;
     a.q = h.q; a.ex_start = h.ex_start; a.ex_list = h.ex_list;
     a.dedq_self = h.dedq_self;
     a.nl = h.nl; a.nl_cnt = h.nl_cnt;
@@ -1005,12 +1125,17 @@ void launch_direct(Handle& h, const double* pos, int include_forces) {
     DirectArgs a = direct_args(h, pos, include_forces);
     // lanes per atom: enough threads for ~2 waves per SIMD on 256 CUs
     const int64_t want = 256LL * 4 * 2 * 64;
-    if ((int64_t)a.nlr * 4 >= want)
-        hipLaunchKernelGGL(k_pairs<4>, dim3(nblk((int64_t)a.nlr * 4, 256)), dim3(256), 0, h.stream, a);
-    else if ((int64_t)a.nlr * 8 >= want)
-        hipLaunchKernelGGL(k_pairs<8>, dim3(nblk((int64_t)a.nlr * 8, 256)), dim3(256), 0, h.stream, a);
-    else
-        hipLaunchKernelGGL(k_pairs<16>, dim3(nblk((int64_t)a.nlr * 16, 256)), dim3(256), 0, h.stream, a);
+    const bool ty = a.typ_s != nullptr;
+    if ((int64_t)a.nlr * 4 >= want) {
+        if (ty) hipLaunchKernelGGL((k_pairs<4, true>), dim3(nblk((int64_t)a.nlr * 4, 256)), dim3(256), 0, h.stream, a);
+        else hipLaunchKernelGGL((k_pairs<4, false>), dim3(nblk((int64_t)a.nlr * 4, 256)), dim3(256), 0, h.stream, a);
+    } else if ((int64_t)a.nlr * 8 >= want) {
+        if (ty) hipLaunchKernelGGL((k_pairs<8, true>), dim3(nblk((int64_t)a.nlr * 8, 256)), dim3(256), 0, h.stream, a);
+        else hipLaunchKernelGGL((k_pairs<8, false>), dim3(nblk((int64_t)a.nlr * 8, 256)), dim3(256), 0, h.stream, a);
+    } else {
+        if (ty) hipLaunchKernelGGL((k_pairs<16, true>), dim3(nblk((int64_t)a.nlr * 16, 256)), dim3(256), 0, h.stream, a);
+        else hipLaunchKernelGGL((k_pairs<16, false>), dim3(nblk((int64_t)a.nlr * 16, 256)), dim3(256), 0, h.stream, a);
+    }
     hipLaunchKernelGGL(k_pairs_overflow, dim3(nblk(a.nlr, 256)), dim3(256), 0, h.stream, a);
 }
 
@@ -1036,7 +1161,9 @@ void launch_assemble(Handle& h, double* forces_out) {
 
 void launch_energy(Handle& h, int include_energy, double* energy_out) {
     int nrec = (h.pbc && include_energy && h.rank == 0) ? h.e_rec_nblk : 0;
-    hipLaunchKernelGGL(k_energy, dim3(1), dim3(1024), 0, h.stream, h.lo, h.hi, h.e_atom, h.e_rec_part, nrec, h.pbc,
+    const int nparts = std::max(1, nblk(h.hi - h.lo, kEChunk));
+    hipLaunchKernelGGL(k_energy_part, dim3(nparts), dim3(256), 0, h.stream, h.lo, h.hi, h.e_atom, h.e_part);
+    hipLaunchKernelGGL(k_energy, dim3(1), dim3(256), 0, h.stream, nparts, h.e_part, h.e_rec_part, nrec, h.pbc,
                        h.terms_dev, energy_out, h.energy_dev);
 }
 

@@ -160,20 +160,26 @@ constexpr int kTapStride = 3 * kRow;
 __global__ void __launch_bounds__(256) k_g_taps(int nown, int W, double beta, int3 ng, const int* __restrict__ order,
                                                 const double4* __restrict__ srec, const int4* __restrict__ g0u,
                                                 double* __restrict__ taps, int4* __restrict__ g0s) {
-    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= (int64_t)nown * kTapStride) return;
-    const int slot = (int)(t / kTapStride), r = (int)(t % kTapStride);
-    const int d = r / kRow, p = r % kRow;
+    // one thread per (slot, axis): the W taps of the row, written as 12 double2 with zeros
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= nown * 3) return;
+    const int slot = t / 3, d = t - 3 * slot;
     const int io = order[slot];
     const double4 sr = srec[io];
     const int4 g = g0u[io];
     const double sd = d == 0 ? sr.x : (d == 1 ? sr.y : sr.z);
     const int g0 = d == 0 ? g.x : (d == 1 ? g.y : g.z);
-    const int m = p - (g0 & 7);   // g0 & 7 == wrapped g0 mod 8 (ng is a multiple of 8)
-    double v = (m >= 0 && m < W) ? es_val((double)(g0 + m) - sd, 2.0 / W, beta) : 0.0;
-    if (d == 0) v *= sr.w;
-    taps[t] = v;
-    if (r == 0)
+    const int r = g0 & 7;   // == wrapped g0 mod 8 (ng is a multiple of 8)
+    const double scale = d == 0 ? sr.w : 1.0;
+    double* out = taps + (size_t)slot * kTapStride + d * kRow;
+#pragma unroll
+    for (int m = 0; m < 16; m++) out[r + m] = m < W ? scale * es_val((double)(g0 + m) - sd, 2.0 / W, beta) : 0.0;
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+        if (q < r) out[q] = 0.0;            // leading zeros [0, r)
+        if (q < 8 - r) out[r + 16 + q] = 0.0;  // trailing zeros [r + 16, 24)
+    }
+    if (d == 0)
         g0s[slot] = make_int4(g.x < 0 ? g.x + ng.x : g.x, g.y < 0 ? g.y + ng.y : g.y, g.z < 0 ? g.z + ng.z : g.z, io);
 }
 
@@ -188,7 +194,7 @@ __global__ void __launch_bounds__(256) k_g_taps(int nown, int W, double beta, in
 //    its z column (8 muls + 64 FMAs per atom).  The 8 atom lanes of a column are summed
 //    in fixed order through LDS at the end -> deterministic.
 // ---------------------------------------------------------------------------------
-constexpr int kSpreadCap = 112;                         // atoms staged per pass (63 KB)
+constexpr int kSpreadCap = 56;                          // atoms staged per pass (31.5 KB)
 constexpr int kSpreadU = (kSpreadCap * (kTapStride / 2) + 511) / 512;   // double2 per thread
 
 struct SpreadPass {
@@ -253,17 +259,17 @@ __global__ void __launch_bounds__(512) k_g_spread(int3 ng, int3 nb, const int* _
                                                   const double* __restrict__ taps, double* __restrict__ grid) {
     extern __shared__ double st[];   // 2 x [kSpreadCap][kTapStride]
     const int lane = threadIdx.x & 63, w = wave_id();
-    const int ka = lane >> 3, k = lane & 7;   // atom-in-group, z column
+    const int ka = lane >> 4, jh = (lane >> 3) & 1, k = lane & 7;   // atom-in-group, y half, z column
     const int nbbz = (nb.z + 1) >> 1, nbby = (nb.y + 1) >> 1;
     const int BZ = blockIdx.x % nbbz, BY = (blockIdx.x / nbbz) % nbby, BX = blockIdx.x / (nbbz * nbby);
     const int wx = (w >> 2) & 1, wy = (w >> 1) & 1, wz = w & 1;
     const int tx = 2 * BX + wx, ty = 2 * BY + wy, tz = 2 * BZ + wz;
     const bool active = tx < nb.x && ty < nb.y && tz < nb.z;
-    double acc[8][8];
+    double acc[8][4];
 #pragma unroll
     for (int i = 0; i < 8; i++)
 #pragma unroll
-        for (int jj = 0; jj < 8; jj++) acc[i][jj] = 0.0;
+        for (int jj = 0; jj < 4; jj++) acc[i][jj] = 0.0;
     SpreadPass p;
     p.col = -1; p.base = 0;
     p.cn[0] = p.cn[1] = p.cn[2] = p.cn[3] = 0;
@@ -282,7 +288,7 @@ __global__ void __launch_bounds__(512) k_g_spread(int3 ng, int3 nb, const int* _
         const double* buf = st + (size_t)cur * kSpreadCap * kTapStride;
         const int dbx = wx + 2 - (p.col >> 2), dby = wy + 2 - (p.col & 3);
         if (active && dbx >= 0 && dbx <= 2 && dby >= 0 && dby <= 2) {
-            const int ox = 8 * dbx, oy = kRow + 8 * dby;
+            const int ox = 8 * dbx, oy = kRow + 8 * dby + 4 * jh;
             int off = 0;
 #pragma unroll
             for (int sz = 0; sz < 4; sz++) {
@@ -291,18 +297,18 @@ __global__ void __launch_bounds__(512) k_g_spread(int3 ng, int3 nb, const int* _
                 off += p.cn[sz];
                 if (dbz < 0 || dbz > 2 || lo >= hi) continue;
                 const int oz = 2 * kRow + 8 * dbz + k;
-                for (int u0 = lo; u0 < hi; u0 += 8) {
+                for (int u0 = lo; u0 < hi; u0 += 4) {
                     const int u = min(u0 + ka, hi - 1);
                     const double* rr = buf + (size_t)u * kTapStride;
                     const double zq = u0 + ka < hi ? rr[oz] : 0.0;
-                    double yz[8];
+                    double yz[4];
 #pragma unroll
-                    for (int jj = 0; jj < 8; jj++) yz[jj] = rr[oy + jj] * zq;
+                    for (int jj = 0; jj < 4; jj++) yz[jj] = rr[oy + jj] * zq;
 #pragma unroll
                     for (int i = 0; i < 8; i++) {
                         const double xi = rr[ox + i];
 #pragma unroll
-                        for (int jj = 0; jj < 8; jj++) acc[i][jj] += xi * yz[jj];
+                        for (int jj = 0; jj < 4; jj++) acc[i][jj] += xi * yz[jj];
                     }
                 }
             }
@@ -313,20 +319,18 @@ __global__ void __launch_bounds__(512) k_g_spread(int3 ng, int3 nb, const int* _
         p = pn;
         __syncthreads();
     }
-    // sum the 8 atom lanes of each z column in fixed order through LDS, one x row at a time
+    // sum the 4 atom lanes of each (j, k) point in fixed order through LDS, one x row at a time
     __syncthreads();
-    double* red = st + (size_t)w * 512;   // [ka][jj][k] of this wave
+    double* red = st + (size_t)w * 256;   // [ka][jh*4+jj][k] of this wave
 #pragma unroll
     for (int i = 0; i < 8; i++) {
 #pragma unroll
-        for (int jj = 0; jj < 8; jj++) red[(ka * 8 + jj) * 8 + k] = acc[i][jj];
+        for (int jj = 0; jj < 4; jj++) red[(ka * 8 + jh * 4 + jj) * 8 + k] = acc[i][jj];
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        const int jl = lane >> 3;   // lane = (jl, k) sums the 8 atom partials of point (i, jl, k)
-        double v = red[jl * 8 + k];
-#pragma unroll
-        for (int a2 = 1; a2 < 8; a2++) v += red[(a2 * 8 + jl) * 8 + k];
+        const int jl = lane >> 3;   // lane = (jl, k) sums the 4 atom partials of point (i, jl, k)
+        const double v = ((red[jl * 8 + k] + red[(8 + jl) * 8 + k]) + red[(16 + jl) * 8 + k]) + red[(24 + jl) * 8 + k];
         if (active) grid[((size_t)(8 * tx + i) * ng.y + 8 * ty + jl) * ng.z + 8 * tz + k] = v;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
@@ -437,6 +441,122 @@ __global__ void __launch_bounds__(256) k_g_dftz_inv(int rows, int ngz, int KZ, c
 #pragma unroll
     for (int r = 0; r < kRW; r++)
         if (r0 + r < nrows) grid[(size_t)(row0 + r0 + r) * ngz + z] = acc[r];
+}
+
+// Every pruned-DFT stage as one batched complex GEMM on 16x16 wave tiles:
+//   C[m][n] = sum_k A[m][k] B[k][n],  A = twiddles (complex), B complex or real, C complex or
+//   its real part.  n is split as (n1, n0) = (n / nin, n % nin) so a batch index can be folded
+//   into n.  Each wave stages 16-deep k-chunks of its A and B tiles in its own LDS (no
+//   workgroup barrier); lane (lm, ln) owns the 2x2 outputs (2lm.., 2ln..): 4 ds_read_b128
+//   feed 16 FMAs per k.
+struct ZGemm {
+    int M, N, K, nin;
+    const double2* A; long sam, sak;
+    const void* B; long sbk, sb0, sb1;
+    void* C; long scm, sc0, sc1;
+    int b_kfast;   // B is contiguous along k (load lanes walk k first)
+};
+
+template <bool BREAL, bool CREAL>
+__global__ void __launch_bounds__(256) k_g_zgemm(ZGemm g) {
+    __shared__ v2d sa[4][16][17];   // [wave][m][k] (+1 pad: conflict-free column reads)
+    __shared__ v2d sb[4][16][17];   // [wave][n][k]
+    const int lane = threadIdx.x & 63, w = wave_id();
+    const int tiles_m = (g.M + 15) >> 4;
+    const int tile = blockIdx.x * 4 + w;
+    const int tm = tile % tiles_m, tn = tile / tiles_m;
+    if (tn * 16 >= g.N) return;
+    const int m0 = tm * 16, n0 = tn * 16;
+    const int lm = lane >> 3, ln = lane & 7;
+    // load roles (fixed over k): element e = lane + 64q of the 16x16 chunk
+    const int ak = lane & 15;   // A: k fastest
+    long aoff[4];
+    bool aok[4];
+    long boff[4];
+    bool bok[4];
+    int bkk[4], bnn[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const int mm = (lane >> 4) + 4 * q;
+        aok[q] = m0 + mm < g.M;
+        aoff[q] = (long)(aok[q] ? m0 + mm : 0) * g.sam;
+        bkk[q] = g.b_kfast ? (lane & 15) : (lane >> 4) + 4 * q;
+        bnn[q] = g.b_kfast ? (lane >> 4) + 4 * q : (lane & 15);
+        const int n = n0 + bnn[q];
+        bok[q] = n < g.N;
+        const int nn = bok[q] ? n : 0;
+        boff[q] = (long)(nn / g.nin) * g.sb1 + (long)(nn % g.nin) * g.sb0;
+    }
+    v2d c[2][2];
+#pragma unroll
+    for (int p = 0; p < 2; p++)
+#pragma unroll
+        for (int q = 0; q < 2; q++) c[p][q] = v2d{0.0, 0.0};
+    v2d ra[4], rb[4];
+    auto fetch = [&](int k0) {
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const int ka = k0 + ak;
+            ra[q] = v2d{0.0, 0.0};
+            if (aok[q] && ka < g.K) {
+                const double2 t = g.A[aoff[q] + (long)ka * g.sak];
+                ra[q] = v2d{t.x, t.y};
+            }
+            const int kb = k0 + bkk[q];
+            rb[q] = v2d{0.0, 0.0};
+            if (bok[q] && kb < g.K) {
+                const long off = boff[q] + (long)kb * g.sbk;
+                if (BREAL) {
+                    rb[q] = v2d{reinterpret_cast<const double*>(g.B)[off], 0.0};
+                } else {
+                    const double2 t = reinterpret_cast<const double2*>(g.B)[off];
+                    rb[q] = v2d{t.x, t.y};
+                }
+            }
+        }
+    };
+    fetch(0);
+    for (int k0 = 0; k0 < g.K; k0 += 16) {
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            sa[w][(lane >> 4) + 4 * q][ak] = ra[q];
+            sb[w][bnn[q]][bkk[q]] = rb[q];
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (k0 + 16 < g.K) fetch(k0 + 16);   // next chunk in flight during the FMAs
+#pragma unroll 4
+        for (int k = 0; k < 16; k++) {
+            const v2d a[2] = {sa[w][2 * lm][k], sa[w][2 * lm + 1][k]};
+            const v2d b[2] = {sb[w][2 * ln][k], sb[w][2 * ln + 1][k]};
+#pragma unroll
+            for (int p = 0; p < 2; p++)
+#pragma unroll
+                for (int q = 0; q < 2; q++) {
+                    if (BREAL) {
+                        c[p][q].x += a[p].x * b[q].x;
+                        c[p][q].y += a[p].y * b[q].x;
+                    } else {
+                        c[p][q].x += a[p].x * b[q].x - a[p].y * b[q].y;
+                        if (!CREAL) c[p][q].y += a[p].x * b[q].y + a[p].y * b[q].x;
+                    }
+                }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+#pragma unroll
+    for (int p = 0; p < 2; p++)
+#pragma unroll
+        for (int q = 0; q < 2; q++) {
+            const int m = m0 + 2 * lm + p, n = n0 + 2 * ln + q;
+            if (m >= g.M || n >= g.N) continue;
+            const long off = (long)m * g.scm + (long)(n / g.nin) * g.sc1 + (long)(n % g.nin) * g.sc0;
+            if (CREAL) reinterpret_cast<double*>(g.C)[off] = c[p][q].x;
+            else reinterpret_cast<double2*>(g.C)[off] = make_double2(c[p][q].x, c[p][q].y);
+        }
 }
 
 // ---------------------------------------------------------------------------------
@@ -666,7 +786,7 @@ void launch_grid_sort(Handle& h, const double* pos) {
                        h.g_tmp);
     hipLaunchKernelGGL(k_g_order, dim3(nblk(p.nbins, 4)), dim3(256), 0, h.stream, p.nbins, h.g_start, h.g_tmp,
                        h.g_order);
-    hipLaunchKernelGGL(k_g_taps, dim3(nblk((int64_t)nown * kTapStride, 256)), dim3(256), 0, h.stream, nown, p.W, p.beta,
+    hipLaunchKernelGGL(k_g_taps, dim3(nblk((int64_t)nown * 3, 256)), dim3(256), 0, h.stream, nown, p.W, p.beta,
                        ng, h.g_order, h.g_srec, h.g_g0u, h.g_taps, h.g_g0s);
 }
 
@@ -695,17 +815,24 @@ void launch_grid_spread(Handle& h) {
                        nb, h.g_start, h.g_taps, h.g_grid);
 }
 
+template <bool BREAL, bool CREAL>
+static void zgemm(Handle& h, const ZGemm& g) {
+    const int tiles = ((g.M + 15) / 16) * ((g.N + 15) / 16);
+    hipLaunchKernelGGL((k_g_zgemm<BREAL, CREAL>), dim3(nblk(tiles, 4)), dim3(256), 0, h.stream, g);
+}
+
 void launch_grid_dft_fwd(Handle& h) {
     const GridPlan& p = h.gp;
-    const int rows = p.ng[0] * p.ng[1];
-    hipLaunchKernelGGL(k_g_dftz_fwd, dim3(nblk(rows, 256), p.KZP / kNZB), dim3(256), 0, h.stream, rows, p.ng[2], p.KZ,
-                       p.KZP, h.g_grid, h.g_twz, h.g_t1);
-    // y: [X][ngy][KZ] -> [X][NY][KZ]
-    hipLaunchKernelGGL(k_g_contract, dim3(nblk(p.ng[0] * p.KZ, 256), nblk(p.NY, kAP)), dim3(256), 0, h.stream, p.ng[0],
-                       p.ng[1], p.NY, p.KZ, h.g_t1, h.g_tw[1], p.ng[1], 1, h.g_t2);
-    // x: [ngx][NY*KZ] -> [NX][NY*KZ]
-    hipLaunchKernelGGL(k_g_contract, dim3(nblk(p.NY * p.KZ, 256), nblk(p.NX, kAP)), dim3(256), 0, h.stream, 1, p.ng[0],
-                       p.NX, p.NY * p.KZ, h.g_t2, h.g_tw[0], p.ng[0], 1, h.g_b);
+    const int ngx = p.ng[0], ngy = p.ng[1], ngz = p.ng[2], KZ = p.KZ, NY = p.NY, NX = p.NX;
+    const long NYKZ = (long)NY * KZ;
+    const double2* tzh = h.g_tw[2] + (size_t)(KZ - 1) * ngz;   // e^{i th nz z}, nz >= 0
+    // z (real rows -> half spectrum): t1[row][nz] = sum_z grid[row][z] Tz[nz][z]
+    zgemm<true, false>(h, ZGemm{KZ, ngx * ngy, ngz, ngx * ngy, tzh, ngz, 1, h.g_grid, 1, ngz, 0, h.g_t1, 1, KZ, 0, 1});
+    // y: t2[o][ny][i] = sum_y Ty[ny][y] t1[o][y][i]
+    zgemm<false, false>(h, ZGemm{NY, ngx * KZ, ngy, KZ, h.g_tw[1], ngy, 1, h.g_t1, KZ, 1, (long)ngy * KZ, h.g_t2, KZ, 1,
+                                 NYKZ, 0});
+    // x: b[nx][r] = sum_x Tx[nx][x] t2[x][r]
+    zgemm<false, false>(h, ZGemm{NX, (int)NYKZ, ngx, (int)NYKZ, h.g_tw[0], ngx, 1, h.g_t2, NYKZ, 1, 0, h.g_b, NYKZ, 1, 0, 0});
 }
 
 double* grid_reduce_buffer(Handle& h, int64_t* count) {
@@ -726,17 +853,16 @@ void launch_grid_coeffs(Handle& h, int include_energy) {
 
 void launch_grid_dft_inv(Handle& h) {
     const GridPlan& p = h.gp;
-    // x: [NX][NY*KZ] -> [ngx][NY*KZ]
-    hipLaunchKernelGGL(k_g_contract, dim3(nblk(p.NY * p.KZ, 256), nblk(p.ng[0], kAP)), dim3(256), 0, h.stream, 1, p.NX,
-                       p.ng[0], p.NY * p.KZ, h.g_b, h.g_tw[0], 1, p.ng[0], h.g_t2);
-    // y: [ngx][NY][KZ] -> [ngx][ngy][KZ]
-    hipLaunchKernelGGL(k_g_contract, dim3(nblk(p.ng[0] * p.KZ, 256), nblk(p.ng[1], kAP)), dim3(256), 0, h.stream,
-                       p.ng[0], p.NY, p.ng[1], p.KZ, h.g_t2, h.g_tw[1], 1, p.ng[1], h.g_t1);
-    // z: half spectrum -> real rows
-    const int rows = p.ng[0] * p.ng[1];
-    const int nblocks = nblk(rows, 4 * kRW) * ((p.ng[2] + 63) / 64);
-    hipLaunchKernelGGL(k_g_dftz_inv, dim3(nblocks), dim3(256), sizeof(double2) * 4 * kRW * p.KZ, h.stream, rows,
-                       p.ng[2], p.KZ, h.g_t1, h.g_tw[2] + (size_t)(p.KZ - 1) * p.ng[2], h.g_grid);
+    const int ngx = p.ng[0], ngy = p.ng[1], ngz = p.ng[2], KZ = p.KZ, NY = p.NY, NX = p.NX;
+    const long NYKZ = (long)NY * KZ;
+    const double2* tzh = h.g_tw[2] + (size_t)(KZ - 1) * ngz;
+    // x: t2[x][r] = sum_nx Tx[nx][x] f[nx][r]
+    zgemm<false, false>(h, ZGemm{ngx, (int)NYKZ, NX, (int)NYKZ, h.g_tw[0], 1, ngx, h.g_b, NYKZ, 1, 0, h.g_t2, NYKZ, 1, 0, 0});
+    // y: t1[o][y][i] = sum_ny Ty[ny][y] t2[o][ny][i]
+    zgemm<false, false>(h, ZGemm{ngy, ngx * KZ, NY, KZ, h.g_tw[1], 1, ngy, h.g_t2, KZ, 1, NYKZ, h.g_t1, KZ, 1,
+                                 (long)ngy * KZ, 0});
+    // z (half spectrum -> real rows): grid[row][z] = Re sum_nz Tz[nz][z] t1[row][nz]
+    zgemm<false, true>(h, ZGemm{ngz, ngx * ngy, KZ, ngx * ngy, tzh, 1, ngz, h.g_t1, 1, KZ, 0, h.g_grid, 1, ngz, 0, 1});
 }
 
 void launch_grid_interp(Handle& h) {
