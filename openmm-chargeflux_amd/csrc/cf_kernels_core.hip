@@ -518,15 +518,17 @@ __global__ void __launch_bounds__(kWaveNL * kSeg) k_nlist_wave(DirectArgs a) {
     // exclusion lists are sorted: a candidate outside [ex_min, ex_max] needs no lookup
     const int ex_min = exc ? a.ex_list[ex0] : 1, ex_max = exc ? a.ex_list[ex0 + exc - 1] : 0;
     int cnt = 0;
-    auto emit = [&](int t, int j, int code) {
+    // high bits of a list entry: the partner's LJ type when types are used, else the image code
+    auto emit = [&](int t, int j, int hb) {
         if (j >= ex_min && j <= ex_max && in_excl(j, reg, exc, a.ex_list, ex0)) return;
-        if (cnt < a.nb_cap) a.nl[(seg_off + cnt) * a.nlr + c] = t | ((a.typ_s ? a.typ_s[t] : code) << kShiftBits);
+        if (cnt < a.nb_cap) a.nl[(seg_off + cnt) * a.nlr + c] = t | (hb << kShiftBits);
         cnt++;
     };
     if (!fits) {  // wave-uniform (and block-uniform: every wave sees the same 64 atoms)
         if (active)
-            scan_cells(a, s, pi, a.rl2, [&](int t, int code, double, double, double, double) { emit(t, a.atom_sorted[t], code); },
-                       seg, kSeg);
+            scan_cells(a, s, pi, a.rl2, [&](int t, int code, double, double, double, double) {
+                emit(t, a.atom_sorted[t], a.typ_s ? a.typ_s[t] : code);
+            }, seg, kSeg);
         if (active) a.nl_cnt[(size_t)seg * a.nlr + c] = cnt;
         return;
     }
@@ -553,20 +555,22 @@ __global__ void __launch_bounds__(kWaveNL * kSeg) k_nlist_wave(DirectArgs a) {
         return (w[0] * a.nc.y + w[1]) * a.nc.z + w[2];
     };
     double4 rp[4];
-    int rj[4];
+    int rj[4], rt[4];
     auto fetch = [&](int t0, int t1) {
 #pragma unroll
         for (int v = 0; v < 4; v++) {
             int t = t0 + v * kWaveNL + lane;
-            if (t < t1) { rp[v] = a.pos4s[t]; rj[v] = a.atom_sorted[t]; }
+            if (t < t1) { rp[v] = a.pos4s[t]; rj[v] = a.atom_sorted[t]; rt[v] = a.typ_s ? a.typ_s[t] : 0; }
         }
     };
+    // staged candidate: fp32 block-frame position, LJ type bits in .w
     auto stage = [&](int t0, int t1, double3 off) {
 #pragma unroll
         for (int v = 0; v < 4; v++) {
             int u = v * kWaveNL + lane;
             if (t0 + u < t1) {
-                cand[u] = make_float4((float)(rp[v].x + off.x), (float)(rp[v].y + off.y), (float)(rp[v].z + off.z), 0.f);
+                cand[u] = make_float4((float)(rp[v].x + off.x), (float)(rp[v].y + off.y), (float)(rp[v].z + off.z),
+                                      __int_as_float(rt[v]));
                 cand_j[u] = rj[v];
             }
         }
@@ -586,7 +590,7 @@ __global__ void __launch_bounds__(kWaveNL * kSeg) k_nlist_wave(DirectArgs a) {
             while (bits) {
                 int v = __builtin_ctz(bits);
                 bits &= bits - 1;
-                emit(t0 + u0 + v, cand_j[u0 + v], code);
+                emit(t0 + u0 + v, cand_j[u0 + v], a.typ_s ? __float_as_int(cand[u0 + v].w) : code);
             }
         }
     };
@@ -632,7 +636,8 @@ __global__ void __launch_bounds__(kWaveNL * kSeg) k_nlist_wave(DirectArgs a) {
                 if (t < te) {
                     double4 pj = a.pos4s[t];
                     cand[v * kWaveNL + lane] = make_float4((float)(pj.x + off.x), (float)(pj.y + off.y),
-                                                           (float)(pj.z + off.z), 0.f);
+                                                           (float)(pj.z + off.z),
+                                                           __int_as_float(a.typ_s ? a.typ_s[t] : 0));
                     cand_j[v * kWaveNL + lane] = a.atom_sorted[t];
                 }
             }

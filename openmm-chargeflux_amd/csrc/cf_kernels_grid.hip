@@ -603,11 +603,14 @@ __global__ void __launch_bounds__(256) k_g_coeffs(int KX, int KY, int KZ, double
 //    (j = 4jj + jg, k) columns (2 FMAs per LDS read, x taps as wave-uniform scalars), then
 //    pot = sum t0 Y Z, grad = (t1 Y Z, t0 dY Z, t0 Y dZ) in a fixed-order wave reduction.
 // ---------------------------------------------------------------------------------
+constexpr int kInterpThreads = 512;
+
 template <int W>
-__global__ void __launch_bounds__(256) k_g_interp(int3 ng, int3 nb, const int* __restrict__ start,
-                                                  const int4* __restrict__ g0s, const double4* __restrict__ srec,
-                                                  double beta, double3 gscale, const double* __restrict__ G,
-                                                  double* __restrict__ t_part) {
+__global__ void __launch_bounds__(kInterpThreads) k_g_interp(int3 ng, int3 nb, const int* __restrict__ start,
+                                                             const int4* __restrict__ g0s,
+                                                             const double4* __restrict__ srec, double beta,
+                                                             double3 gscale, const double* __restrict__ G,
+                                                             double* __restrict__ t_part) {
     constexpr int R = 7 + W;
     constexpr int NJ = (W + 3) / 4;
     extern __shared__ double sg[];   // [R][R][R]
@@ -615,20 +618,28 @@ __global__ void __launch_bounds__(256) k_g_interp(int3 ng, int3 nb, const int* _
     const int s0 = start[tile], s1 = start[tile + 1];
     if (s0 == s1) return;
     const int tz = tile % nb.z, ty = (tile / nb.z) % nb.y, tx = tile / (nb.z * nb.y);
-    // rows of R consecutive z: thread t loads element c = t % R... of rows r = t / R, ...
+    // rows of R consecutive z: thread t covers column c = t % R of rows t / R, t / R + RPP, ...
+    {
+        constexpr int RPP = kInterpThreads / R;   // rows per pass
+        const int c = threadIdx.x % R, r0 = threadIdx.x / R;
+        int z = 8 * tz + c;
+        z -= z >= ng.z ? ng.z : 0;
+        if (r0 < RPP) {
 #pragma unroll 4
-    for (int e = threadIdx.x; e < R * R * R; e += 256) {
-        const int row = e / R, c = e - row * R;
-        const int b = row % R, a = row / R;
-        int x = 8 * tx + a, y = 8 * ty + b, z = 8 * tz + c;
-        x -= x >= ng.x ? ng.x : 0; y -= y >= ng.y ? ng.y : 0; z -= z >= ng.z ? ng.z : 0;
-        sg[e] = G[((size_t)x * ng.y + y) * ng.z + z];
+            for (int row = r0; row < R * R; row += RPP) {
+                const int a = row / R, b = row - a * R;
+                int x = 8 * tx + a, y = 8 * ty + b;
+                x -= x >= ng.x ? ng.x : 0;
+                y -= y >= ng.y ? ng.y : 0;
+                sg[row * R + c] = G[((size_t)x * ng.y + y) * ng.z + z];
+            }
+        }
     }
     __syncthreads();
     const int lane = threadIdx.x & 63, w = wave_id();
     const int d = lane >> 4, m = lane & 15;
     const int k = lane & 15, jg = lane >> 4;
-    for (int s = s0 + w; s < s1; s += 4) {
+    for (int s = s0 + w; s < s1; s += kInterpThreads / 64) {
         const int4 g = g0s[s];
         const double4 sr = srec[g.w];
         // taps: lane (d, m)
@@ -872,7 +883,8 @@ void launch_grid_interp(Handle& h) {
     const size_t R = 7 + p.W;
     const size_t lds = R * R * R * sizeof(double);
 #define CF_INTERP(W_)                                                                                               \
-    hipLaunchKernelGGL(k_g_interp<W_>, dim3(p.nbins), dim3(256), lds, h.stream, ng, nb, h.g_start, h.g_g0s, h.g_srec, \
+    hipLaunchKernelGGL(k_g_interp<W_>, dim3(p.nbins), dim3(kInterpThreads), lds, h.stream, ng, nb, h.g_start,       \
+                       h.g_g0s, h.g_srec,                                                                        \
                        p.beta, gs, h.g_grid, h.t_part)
     CF_GRID_W_DISPATCH(p.W, CF_INTERP)
 #undef CF_INTERP
