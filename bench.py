@@ -90,8 +90,28 @@ def cpu_baseline(force, pos, box, k_sample):
     }
 
 
-# rocprofv3 kernel names of the library's timing phases (k-space MFMA kernels at C3)
-PMC_KERNEL = {"kspace_force": "cf::k_force<2>", "kspace_sfac": "cf::k_sfac<4, 32>"}
+# rocprofv3 kernel names of the library's timing phases at C3
+PMC_KERNEL = {"kspace_force": "cf::k_force<2>", "kspace_sfac": "cf::k_sfac<4, 32>",
+              "direct_pairs": "cf::k_pairs<4, true>", "grid_spread": "cf::k_g_spread",
+              "grid_interp": "cf::k_g_interp<14>"}
+
+
+def pair_count(force, pos, box):
+    """P_c: non-excluded pairs with r <= rc under minimum image (the reference's neighbour
+    list, ReferenceCoulKernels.cpp:559), at the initial positions."""
+    from scipy.spatial import cKDTree
+    L = np.array([box[0][0], box[1][1], box[2][2]])
+    rc = force.getCutoffDistance()
+    w = np.mod(pos, L)
+    w[w >= L] = 0.0
+    n_all = (cKDTree(w, boxsize=L).count_neighbors(cKDTree(w, boxsize=L), rc) - len(pos)) // 2
+    ex = {tuple(sorted(force.getExceptionParameters(k)[:2])) for k in range(force.getNumExceptions())}
+    n_ex = 0
+    for a, b in ex:
+        d = pos[a] - pos[b]
+        d -= L * np.round(d / L)
+        n_ex += int(np.dot(d, d) <= rc * rc)
+    return int(n_all - n_ex)
 
 
 def pmc_traffic(config, world, phase):
@@ -117,7 +137,11 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="C3", choices=["C2", "C3", "C5"])
-    ap.add_argument("--kspace-algo", type=int, default=0)
+    ap.add_argument("--kspace-algo", type=int, default=2,
+                    help="0 exact k-sum (fp64 MFMA), 1 exact (direct VALU), 2 grid (ES spread / pruned DFT)")
+    ap.add_argument("--grid-width", type=int, default=0, help="ES kernel width for --kspace-algo 2 (0 = 14)")
+    ap.add_argument("--no-exact-compare", action="store_true",
+                    help="skip timing the exact k-sum path beside the grid path")
     ap.add_argument("--cpu-k-sample", type=int, default=1500)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dt", type=float, default=0.001, help="ps")
@@ -137,7 +161,8 @@ def main():
     system, force, pos_np, box = ts.make(args.config)
     n = len(pos_np)
     n_waters = force.getNumFluxWaters() + force.getNumFluxAngles()
-    kern = ShardedCoulKernel(system, force, local, kspace_algo=args.kspace_algo, neighbor_skin=args.neighbor_skin)
+    kern = ShardedCoulKernel(system, force, local, kspace_algo=args.kspace_algo, neighbor_skin=args.neighbor_skin,
+                             grid_width=args.grid_width)
     lo, hi = kern.lo, kern.hi
     alpha, kmax = kern.kernel.ewald_params()
     k_half = (kmax[2] - 1) + (kmax[1] - 1) * (2 * kmax[2] - 1) + (kmax[0] - 1) * (2 * kmax[1] - 1) * (2 * kmax[2] - 1)
@@ -201,24 +226,64 @@ def main():
 
     per_launch = {k: (v[0] / v[1] if v[1] else 0.0) for k, v in timing.items()}
     per_step = {k: v[0] / args.steps for k, v in timing.items()}   # amortized (list phases are not every step)
-    kernels = per_launch
     n_own = hi - lo
+    # algorithmic work per launch of each hot phase:
+    #  direct_pairs  HBM bytes 4 P_c + 80 N (half list + per-atom in/out), fp64 flops 80 P_c
+    #  grid_spread   2 N W^3 flops (one FMA per atom x grid point of its support)
+    #  grid_interp   4 N W^3 flops (two FMAs per grid value: potential and x-gradient sums)
+    #  kspace_sfac / kspace_force (exact path)  4 / 8 flops per atom x half-space k-vector
+    p_c = pair_count(force, pos_np, box) * n_own / n
+    w_grid = args.grid_width or 14
     units = float(n_own) * k_half
-    # algorithmic fp64 flops per (atom, half-space k-vector) of the separable GEMM form
-    # (DESIGN.md §4.3): S-pass 4 (w x (cos, sin), re and im), force pass 8 (4 outputs x
-    # (cos, sin)).  SURVEY §8(d) prices the direct VALU form at 10 / 20 per unit.
-    alg = {"kspace_sfac": 4.0 * units, "kspace_force": 8.0 * units}
-    survey = {"kspace_sfac": 10.0 * units, "kspace_force": 20.0 * units}
-    dom = max(alg, key=lambda k: kernels.get(k, 0.0))
-    t_dom = kernels.get(dom, 0.0) * 1e-3
-    achieved = alg[dom] / t_dom / 1e12 if t_dom > 0 else 0.0
+    alg = {"direct_pairs": ("hbm", 4.0 * p_c + 80.0 * n_own, 80.0 * p_c),
+           "grid_spread": ("mfma", None, 2.0 * n_own * w_grid ** 3),
+           "grid_interp": ("mfma", None, 4.0 * n_own * w_grid ** 3),
+           "kspace_sfac": ("mfma", None, 4.0 * units), "kspace_force": ("mfma", None, 8.0 * units)}
+    present = [k for k in alg if per_step.get(k, 0.0) > 0]
+    dom = max(present, key=lambda k: per_step[k])
+    t_dom = per_launch[dom] * 1e-3
+    bound, abytes, aflops = alg[dom]
     traffic, traffic_src = pmc_traffic(args.config, world, dom)
-    roofline = {"kernel": dom, "bound": "mfma", "achieved": round(achieved, 3), "peak": FP64_MFMA_PEAK_TFLOPS,
-                "unit": "TFLOP/s", "frac": round(achieved / FP64_MFMA_PEAK_TFLOPS, 4), "traffic": traffic,
-                "traffic_source": traffic_src,
-                "alg_flops_per_launch": alg[dom], "avg_launch_ms": kernels.get(dom, 0.0),
-                "per_unit": "4 (S-pass) / 8 (force pass) fp64 flops per atom x half-space k-vector (GEMM form)",
-                "survey_equiv_tflops": round(survey[dom] / t_dom / 1e12, 3) if t_dom > 0 else 0.0}
+    fp64_tflops = aflops / t_dom / 1e12
+    if bound == "hbm":
+        achieved, peak, unit = abytes / t_dom / 1e9, HBM_PEAK_GBS, "GB/s"
+    else:
+        achieved, peak, unit = fp64_tflops, FP64_MFMA_PEAK_TFLOPS, "TFLOP/s"
+    roofline = {"kernel": dom, "bound": bound, "achieved": round(achieved, 3), "peak": peak, "unit": unit,
+                "frac": round(achieved / peak, 4), "traffic": traffic, "traffic_source": traffic_src,
+                "alg_bytes_per_launch": abytes, "alg_flops_per_launch": aflops,
+                "fp64_tflops": round(fp64_tflops, 3), "avg_launch_ms": per_launch[dom],
+                "pairs_within_cutoff": int(p_c)}
+    others = {}
+    for k in present:
+        if k == dom:
+            continue
+        tk = per_launch[k] * 1e-3
+        others[k] = {"avg_launch_ms": round(per_launch[k], 4), "fp64_tflops": round(alg[k][2] / tk / 1e12, 3),
+                     "frac_fp64_peak": round(alg[k][2] / tk / 1e12 / FP64_MFMA_PEAK_TFLOPS, 4)}
+    exact = None
+    if world == 1 and args.kspace_algo == 2 and not args.no_exact_compare:
+        # the exact fp64 k-sum path (kspace_algo 0) timed beside the grid path on the same
+        # positions: force evaluations only, HIP events around each
+        ke = ShardedCoulKernel(system, force, local, kspace_algo=0, neighbor_skin=args.neighbor_skin)
+        fe = torch.zeros_like(pos)
+        for _ in range(3):
+            ke.execute(pos, box, fe, include_energy=True)
+        evs = []
+        for _ in range(10):
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            fe.zero_()
+            ee = ke.execute(pos, box, fe, include_energy=True)
+            b.record()
+            evs.append((a, b))
+        fg = torch.zeros_like(pos)
+        eg = kern.execute(pos, box, fg, include_energy=True)
+        torch.cuda.synchronize()
+        exact = {"ms_per_force_eval": round(float(np.mean([a.elapsed_time(b) for a, b in evs])), 4),
+                 "max_abs_dforce_grid_vs_exact": float((fg - fe).abs().max().item()),
+                 "denergy_grid_vs_exact": float(eg.item() - ee.item())}
+        del ke
 
     if rank == 0:
         cpu = None
@@ -235,12 +300,16 @@ def main():
                                    f"{dt * 1000:g} fs, fp64",
                        "atoms": n, "kmax": list(kmax), "k_half": k_half,
                        "neighbor_skin_nm": args.neighbor_skin,
+                       "kspace": {0: "exact k-sum, fp64 MFMA", 1: "exact k-sum, VALU",
+                                  2: f"grid (ES kernel W={w_grid}, pruned DFT), same k-set"}[args.kspace_algo],
                        "nlist_builds_in_timed_steps": f"{builds1 - builds0}/{evals1 - evals0}",
                        "parallelism": f"atom-decomposition x{world}" + (" (RCCL all-reduce of S(k))" if world > 1 else "")},
             "ms_per_force_eval": round(ms_eval, 4),
             "energy_kj_mol": e_final,
             "kernels_ms_per_step": {k: round(v, 4) for k, v in per_step.items()},
             "roofline": roofline,
+            "kernels_roofline": others,
+            "exact_kspace": exact,
             "cpu_baseline": cpu,
         }
         if cpu:
