@@ -167,6 +167,10 @@ CF_EXPORT int cf_synchronize(cf_handle* h);
  * cf_get_timing synchronises and returns, per phase, the summed milliseconds and the
  * number of recorded launches since cf_set_timing; names are 16-byte NUL-padded. */
 CF_EXPORT int cf_set_timing(cf_handle* h, int enable);
+/* As cf_set_timing, but only the phases whose bit is set in phase_mask (bit p = the p-th
+ * phase name cf_get_timing reports) are bracketed by events; 0 disables timing.  Each timed
+ * launch costs two event records on the stream, so a benchmark times only what it reports. */
+CF_EXPORT int cf_set_timing_mask(cf_handle* h, uint32_t phase_mask);
 CF_EXPORT int cf_get_timing(cf_handle* h, int32_t max_phases, char* names, double* total_ms, int32_t* calls,
                             int32_t* nphases);
 

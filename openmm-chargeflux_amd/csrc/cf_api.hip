@@ -33,6 +33,7 @@ constexpr int kMaxTimed = 8192;
 struct cf_handle {
     cf::Handle h;
     bool timing = false;
+    uint32_t timing_mask = 0xffffffffu;    // phases timed while timing is on
     std::vector<hipEvent_t> ev[PH_COUNT];  // pairs (start, stop)
     int nrec[PH_COUNT] = {};
     std::vector<void*> allocs;
@@ -212,7 +213,8 @@ void partition(const cf_params* p, int world, int rank, int* lo, int* hi) {
 
 struct Timed {
     cf_handle* H; int ph; bool on;
-    Timed(cf_handle* H_, int ph_) : H(H_), ph(ph_), on(H_->timing && H_->nrec[ph_] < kMaxTimed) {
+    Timed(cf_handle* H_, int ph_)
+        : H(H_), ph(ph_), on(H_->timing && ((H_->timing_mask >> ph_) & 1u) && H_->nrec[ph_] < kMaxTimed) {
         if (!on) return;
         auto& v = H->ev[ph];
         size_t need = 2 * (size_t)(H->nrec[ph] + 1);
@@ -797,6 +799,17 @@ CF_EXPORT int cf_set_timing(cf_handle* H, int enable) {
         if (!H) fail(CF_ERR_INVALID, "null handle");
         check_hip(hipStreamSynchronize(H->h.stream), "sync");
         H->timing = enable != 0;
+        H->timing_mask = 0xffffffffu;
+        for (int p = 0; p < PH_COUNT; p++) H->nrec[p] = 0;
+    });
+}
+
+CF_EXPORT int cf_set_timing_mask(cf_handle* H, uint32_t phase_mask) {
+    return guarded([&] {
+        if (!H) fail(CF_ERR_INVALID, "null handle");
+        check_hip(hipStreamSynchronize(H->h.stream), "sync");
+        H->timing = phase_mask != 0;
+        H->timing_mask = phase_mask;
         for (int p = 0; p < PH_COUNT; p++) H->nrec[p] = 0;
     });
 }

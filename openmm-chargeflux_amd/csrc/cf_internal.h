@@ -231,4 +231,15 @@ void launch_grid_interp(Handle& h);
 
 void check_hip(hipError_t e, const char* what);
 
+// Workgroups are dispatched round-robin over the 8 XCDs (block b -> XCD b % 8), each XCD with
+// its own L2.  This maps the blocks one XCD receives onto a contiguous 1/8 of the logical
+// block range, so cell-sorted atoms (spatially coherent) share that XCD's L2 with their
+// neighbours.  A bijection on [0, gridDim.x) for any grid size.
+constexpr int kNumXcd = 8;
+__device__ __forceinline__ int xcd_block() {
+    const int b = blockIdx.x, nb = gridDim.x;
+    const int x = b % kNumXcd, per = nb / kNumXcd, rem = nb % kNumXcd;
+    return x * per + min(x, rem) + b / kNumXcd;
+}
+
 }  // namespace cf

@@ -481,7 +481,7 @@ __global__ void __launch_bounds__(kWaveNL * kSeg) k_nlist_wave(DirectArgs a) {
     float4* cand = cand_all[seg];
     int* cand_j = cand_j_all[seg];
     if (!*a.flag) return;  // list still valid (skin): nothing to build
-    const int base = blockIdx.x * kWaveNL;
+    const int base = xcd_block() * kWaveNL;
     const int c = base + lane;  // list row (owned atom, cell-sorted order)
     const bool active = c < a.nlr;
     const int s = own_slot(a, active ? c : a.nlr - 1);
@@ -664,6 +664,30 @@ struct PairAcc {
     double fx = 0, fy = 0, fz = 0, dq = 0, e = 0;
 };
 
+// e^y for y in [-700, 0] (no overflow / NaN handling needed there): y = k ln2 + r with
+// |r| <= ln2/2 (Cody-Waite split of ln2), e^r by its degree-12 Taylor polynomial (truncation
+// < 2e-16 relative), times 2^k.  17 VALU instructions against ~35 for the libm exp, whose
+// range checks and coefficient register copies this path does not need.
+__device__ __forceinline__ double exp_nonpos(double y) {
+    const double k = rint(y * 1.4426950408889634);
+    double r = fma(-k, 6.93147180369123816490e-01, y);
+    r = fma(-k, 1.90821492927058770002e-10, r);
+    double p = 2.0876756987868098979e-09;
+    p = fma(p, r, 2.5052108385441718775e-08);
+    p = fma(p, r, 2.7557319223985890653e-07);
+    p = fma(p, r, 2.7557319223985888276e-06);
+    p = fma(p, r, 2.4801587301587301566e-05);
+    p = fma(p, r, 1.9841269841269841253e-04);
+    p = fma(p, r, 1.3888888888888888889e-03);
+    p = fma(p, r, 8.3333333333333332177e-03);
+    p = fma(p, r, 4.1666666666666664354e-02);
+    p = fma(p, r, 1.6666666666666665741e-01);
+    p = fma(p, r, 0.5);
+    p = fma(p, r, 1.0);
+    p = fma(p, r, 1.0);
+    return ldexp(p, (int)k);
+}
+
 // erfc(x) = e^{-x^2} erfcx(x): erfcx from a piecewise degree-12 polynomial (interval table
 // in LDS, fitted at cf_create in long double, relative error ~4e-15 over [0, alpha*rc]),
 // and e^{-x^2} is shared with the force term -> one exp per pair instead of erfc + exp.
@@ -675,7 +699,7 @@ __device__ __forceinline__ double erfc_exp(double x, const double* __restrict__ 
     double p = c[kErfcDeg];
 #pragma unroll
     for (int j = kErfcDeg - 1; j >= 0; j--) p = fma(p, u, c[j]);
-    e2 = exp(-x * x);
+    e2 = exp_nonpos(-x * x);
     return e2 * p;
 }
 
@@ -776,7 +800,7 @@ __global__ void __launch_bounds__(256) k_pairs(DirectArgs a) {
     if (TYPES)
         for (int e = threadIdx.x; e < a.lj_ntypes; e += blockDim.x) ljt[e] = a.lj_tab[e];
     load_erfc_tab(a, tab);
-    const int gt = blockIdx.x * blockDim.x + threadIdx.x;
+    const int gt = xcd_block() * blockDim.x + threadIdx.x;
     const int c = gt / LPA, g = gt % LPA;
     const int seg = g % kSeg, part = g / kSeg;
     bool active = c < a.nlr;
@@ -795,26 +819,41 @@ __global__ void __launch_bounds__(256) k_pairs(DirectArgs a) {
         const int* nl = a.nl + (size_t)seg * a.nb_cap * a.nlr + cc;
         constexpr int step = LPA / kSeg;
         constexpr int kMask = (1 << kShiftBits) - 1;
-        // software pipeline: list entry k + 2*step and the coordinates of entry k + step are
-        // in flight while entry k is evaluated (out-of-range entries read atom 0, unused).
-        // The pair vector is the minimum image d - L rint(d/L) (getDeltaRPeriodic's
-        // floor(d/L + 0.5) up to exact half-box ties, which lie beyond the cutoff), so the
-        // image code stored in the list is not needed here.
-        int v0 = part < cnt ? nl[(size_t)part * a.nlr] : 0;
-        int v1 = part + step < cnt ? nl[(size_t)(part + step) * a.nlr] : 0;
-        double4 pj = a.pos4s[v0 & kMask];
-        double2 lj2 = TYPES ? ljt[(unsigned)v0 >> kShiftBits] : a.ljs[v0 & kMask];
-        for (int k = part; k < cnt; k += step) {
-            const int v2 = k + 2 * step < cnt ? nl[(size_t)(k + 2 * step) * a.nlr] : 0;
-            const double4 pjn = a.pos4s[v1 & kMask];
-            const double2 ljn = TYPES ? ljt[(unsigned)v1 >> kShiftBits] : a.ljs[v1 & kMask];
+        // software pipeline: list entries k + step .. k + 4*step (streamed from HBM) and the
+        // coordinates of entry k + step (L2) are in flight while entry k is evaluated
+        // (out-of-range entries read atom 0, unused).  The pair vector is the minimum image
+        // d - L rint(d/L) (getDeltaRPeriodic's floor(d/L + 0.5) up to exact half-box ties,
+        // which lie beyond the cutoff), so the image code stored in the list is not needed.
+        // Unrolled by two with ping-pong registers (A, B) so that no freshly loaded value is
+        // ever copied (a register move of a pending load makes the compiler drain vmcnt); list
+        // loads are branch-free (row clamped into the list, value replaced after the load).
+        const int klast = cnt > 0 ? cnt - 1 : 0;
+        auto entry = [&](int kk) {  // streamed once: non-temporal, keeps L2 for the coordinates
+            const int v = __builtin_nontemporal_load(nl + (size_t)min(kk, klast) * a.nlr);
+            return kk < cnt ? v : 0;
+        };
+        auto eval = [&](const double4& pj, const double2& lj2) {
             double dx = pi.x - pj.x, dy = pi.y - pj.y, dz = pi.z - pj.z;
             dx -= a.L.x * rint(dx * a.invL.x);
             dy -= a.L.y * rint(dy * a.invL.y);
             dz -= a.L.z * rint(dz * a.invL.z);
-            double r2 = dx * dx + dy * dy + dz * dz;
+            const double r2 = dx * dx + dy * dy + dz * dz;
             if (r2 <= a.rc2) pair_term(acc, a, tab, pi, li, pj, lj2, dx, dy, dz, r2);  // exact voxel-hash test
-            v1 = v2; pj = pjn; lj2 = ljn;
+        };
+        const int i0 = entry(part);
+        int iB = entry(part + step), iA = entry(part + 2 * step);
+        double4 pA = a.pos4s[i0 & kMask];
+        double2 lA = TYPES ? ljt[(unsigned)i0 >> kShiftBits] : a.ljs[i0 & kMask];
+        for (int k = part; k < cnt; k += 2 * step) {
+            // state: pA/lA = entry k, iB = index of k+step, iA = index of k+2step
+            const double4 pB = a.pos4s[iB & kMask];
+            const double2 lB = TYPES ? ljt[(unsigned)iB >> kShiftBits] : a.ljs[iB & kMask];
+            iB = entry(k + 3 * step);
+            eval(pA, lA);
+            pA = a.pos4s[iA & kMask];
+            lA = TYPES ? ljt[(unsigned)iA >> kShiftBits] : a.ljs[iA & kMask];
+            iA = entry(k + 4 * step);
+            if (k + step < cnt) eval(pB, lB);
         }
     }
 #pragma unroll

@@ -160,10 +160,13 @@ constexpr int kTapStride = 3 * kRow;
 __global__ void __launch_bounds__(256) k_g_taps(int nown, int W, double beta, int3 ng, const int* __restrict__ order,
                                                 const double4* __restrict__ srec, const int4* __restrict__ g0u,
                                                 double* __restrict__ taps, int4* __restrict__ g0s) {
-    // one thread per (slot, axis): the W taps of the row, written as 12 double2 with zeros
+    // one thread per (slot, 16-byte pair p of the slot's 72 values): consecutive lanes write
+    // consecutive 16 B, so every store instruction of a wave is one contiguous 1 KB run
+    constexpr int kPairs = kTapStride / 2;   // 36
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= nown * 3) return;
-    const int slot = t / 3, d = t - 3 * slot;
+    if (t >= nown * kPairs) return;
+    const int slot = t / kPairs, pp = t - kPairs * slot;
+    const int d = pp / (kRow / 2), p0 = 2 * (pp - d * (kRow / 2));   // axis, first point of the pair
     const int io = order[slot];
     const double4 sr = srec[io];
     const int4 g = g0u[io];
@@ -171,15 +174,14 @@ __global__ void __launch_bounds__(256) k_g_taps(int nown, int W, double beta, in
     const int g0 = d == 0 ? g.x : (d == 1 ? g.y : g.z);
     const int r = g0 & 7;   // == wrapped g0 mod 8 (ng is a multiple of 8)
     const double scale = d == 0 ? sr.w : 1.0;
-    double* out = taps + (size_t)slot * kTapStride + d * kRow;
+    double v[2];
 #pragma unroll
-    for (int m = 0; m < 16; m++) out[r + m] = m < W ? scale * es_val((double)(g0 + m) - sd, 2.0 / W, beta) : 0.0;
-#pragma unroll
-    for (int q = 0; q < 8; q++) {
-        if (q < r) out[q] = 0.0;            // leading zeros [0, r)
-        if (q < 8 - r) out[r + 16 + q] = 0.0;  // trailing zeros [r + 16, 24)
+    for (int e = 0; e < 2; e++) {
+        const int m = p0 + e - r;   // tap index of bin-aligned point p0 + e
+        v[e] = (m >= 0 && m < W) ? scale * es_val((double)(g0 + m) - sd, 2.0 / W, beta) : 0.0;
     }
-    if (d == 0)
+    reinterpret_cast<v2d*>(taps)[(size_t)slot * kPairs + pp] = v2d{v[0], v[1]};
+    if (pp == 0)
         g0s[slot] = make_int4(g.x < 0 ? g.x + ng.x : g.x, g.y < 0 ? g.y + ng.y : g.y, g.z < 0 ? g.z + ng.z : g.z, io);
 }
 
@@ -261,7 +263,8 @@ __global__ void __launch_bounds__(512) k_g_spread(int3 ng, int3 nb, const int* _
     const int lane = threadIdx.x & 63, w = wave_id();
     const int ka = lane >> 4, jh = (lane >> 3) & 1, k = lane & 7;   // atom-in-group, y half, z column
     const int nbbz = (nb.z + 1) >> 1, nbby = (nb.y + 1) >> 1;
-    const int BZ = blockIdx.x % nbbz, BY = (blockIdx.x / nbbz) % nbby, BX = blockIdx.x / (nbbz * nbby);
+    const int blk = xcd_block();   // neighbouring blocks (shared source bins) on one XCD's L2
+    const int BZ = blk % nbbz, BY = (blk / nbbz) % nbby, BX = blk / (nbbz * nbby);
     const int wx = (w >> 2) & 1, wy = (w >> 1) & 1, wz = w & 1;
     const int tx = 2 * BX + wx, ty = 2 * BY + wy, tz = 2 * BZ + wz;
     const bool active = tx < nb.x && ty < nb.y && tz < nb.z;
@@ -614,7 +617,7 @@ __global__ void __launch_bounds__(kInterpThreads) k_g_interp(int3 ng, int3 nb, c
     constexpr int R = 7 + W;
     constexpr int NJ = (W + 3) / 4;
     extern __shared__ double sg[];   // [R][R][R]
-    const int tile = blockIdx.x;
+    const int tile = xcd_block();   // neighbouring tiles (shared halo) on one XCD's L2
     const int s0 = start[tile], s1 = start[tile + 1];
     if (s0 == s1) return;
     const int tz = tile % nb.z, ty = (tile / nb.z) % nb.y, tx = tile / (nb.z * nb.y);
@@ -797,7 +800,7 @@ void launch_grid_sort(Handle& h, const double* pos) {
                        h.g_tmp);
     hipLaunchKernelGGL(k_g_order, dim3(nblk(p.nbins, 4)), dim3(256), 0, h.stream, p.nbins, h.g_start, h.g_tmp,
                        h.g_order);
-    hipLaunchKernelGGL(k_g_taps, dim3(nblk((int64_t)nown * 3, 256)), dim3(256), 0, h.stream, nown, p.W, p.beta,
+    hipLaunchKernelGGL(k_g_taps, dim3(nblk((int64_t)nown * (kTapStride / 2), 256)), dim3(256), 0, h.stream, nown, p.W, p.beta,
                        ng, h.g_order, h.g_srec, h.g_g0u, h.g_taps, h.g_g0s);
 }
 

@@ -81,6 +81,7 @@ SIGNATURES = [
     ("cf_get_energy_terms", C.c_int, [C.c_void_p, DP]),
     ("cf_synchronize", C.c_int, [C.c_void_p]),
     ("cf_set_timing", C.c_int, [C.c_void_p, C.c_int]),
+    ("cf_set_timing_mask", C.c_int, [C.c_void_p, C.c_uint32]),
     ("cf_get_timing", C.c_int, [C.c_void_p, C.c_int32, C.c_char_p, DP, C.POINTER(C.c_int32),
                                 C.POINTER(C.c_int32)]),
     ("cf_partition", C.c_int, [C.POINTER(cf_params), C.c_int32, C.c_int32, C.POINTER(C.c_int32),

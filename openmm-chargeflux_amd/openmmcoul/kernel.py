@@ -219,8 +219,20 @@ class HipCalcCoulForceKernel:
         _cabi.check(self._lib.cf_get_energy_terms(self._h, _dp(out)), self._lib)
         return out
 
-    def set_timing(self, enable=True):
-        _cabi.check(self._lib.cf_set_timing(self._h, 1 if enable else 0), self._lib)
+    # phase names in cf_get_timing order (bit p of cf_set_timing_mask)
+    PHASES = ("flux_terms", "atoms_prep", "cell_sort", "neighbor_list", "kspace_tables", "kspace_sfac",
+              "kspace_coeffs", "kspace_force", "direct_pairs", "assemble", "energy", "grid_sort", "grid_spread",
+              "grid_dft_fwd", "grid_dft_inv", "grid_interp")
+
+    def set_timing(self, enable=True, phases=None):
+        """Per-kernel HIP-event timing of every phase, or only of the named phases."""
+        if phases is None:
+            _cabi.check(self._lib.cf_set_timing(self._h, 1 if enable else 0), self._lib)
+        else:
+            mask = 0
+            for p in phases:
+                mask |= 1 << self.PHASES.index(p)
+            _cabi.check(self._lib.cf_set_timing_mask(self._h, mask if enable else 0), self._lib)
 
     def timing(self):
         """{phase: (total_ms, launches)} recorded since set_timing(True)."""
