@@ -118,6 +118,13 @@ CF_EXPORT int cf_partition(const cf_params* params, int32_t world_size, int32_t 
  * continuous between calls (a re-wrapped atom just triggers a rebuild).  The skin is capped
  * at half the smallest box length minus the cutoff. */
 CF_EXPORT int cf_set_neighbor_skin(cf_handle* h, double skin);
+/* updateParametersInContext (the reference's CoulForce has none): replace
+ * the charges, LJ parameters and flux-term parameters of a created handle.  The topology
+ * must be unchanged -- the same particle count, flux terms on the same particles in the same
+ * order, the same set of excluded pairs -- and so must periodicity, cutoff and Ewald
+ * tolerance (alpha and kmax stay those of cf_create); otherwise CF_ERR_INVALID.  The next
+ * evaluation rebuilds the neighbour list.  Not allowed between cf_compute_begin and _end. */
+CF_EXPORT int cf_update_parameters(cf_handle* h, const cf_params* params);
 /* Number of neighbour-list builds and evaluations since cf_create. */
 CF_EXPORT int cf_get_neighbor_stats(const cf_handle* h, int64_t* builds, int64_t* evaluations);
 

@@ -42,6 +42,10 @@ struct cf_handle {
     double* ene_host_dev = nullptr;
     double default_box[9] = {};
     const double* pos_pending = nullptr;
+    // host copy of the topology cf_create was given (cf_update_parameters may change only
+    // parameters, not which atoms the flux terms and exclusions connect)
+    std::vector<int4> topo_terms;
+    std::vector<int> topo_ex_start, topo_ex_list;
 };
 
 namespace {
@@ -211,6 +215,105 @@ void partition(const cf_params* p, int world, int rank, int* lo, int* hi) {
     if (*hi < *lo) *hi = *lo;
 }
 
+// particles: q0 and the LJ transform (sigma/2, 2 sqrt(eps))   RCK:234-240
+void parse_particles(const cf_params* p, std::vector<double>& q0, std::vector<double2>& lj) {
+    const int n = p->num_particles;
+    if (!p->charges || !p->sigmas || !p->epsilons) fail(CF_ERR_INVALID, "particle arrays are null");
+    q0.resize(n);
+    lj.resize(n);
+    for (int i = 0; i < n; i++) {
+        if (!(p->epsilons[i] >= 0)) fail(CF_ERR_INVALID, "epsilon must be >= 0");
+        q0[i] = p->charges[i];
+        lj[i] = make_double2(0.5 * p->sigmas[i], 2.0 * std::sqrt(p->epsilons[i]));
+    }
+}
+
+// flux terms in reference order (bonds, angles, waters; RCK:242-284): (type, a0, a1, a2) and
+// 5 parameters per term
+void parse_terms(const cf_params* p, std::vector<int4>& tidx, std::vector<double>& tpar,
+                 std::vector<std::vector<int>>* term_atoms) {
+    const int n = p->num_particles;
+    const int B = p->num_flux_bonds, A = p->num_flux_angles, W = p->num_flux_waters;
+    if (B < 0 || A < 0 || W < 0) fail(CF_ERR_INVALID, "negative flux term count");
+    if ((B && (!p->flux_bond_idx || !p->flux_bond_params)) || (A && (!p->flux_angle_idx || !p->flux_angle_params)) ||
+        (W && (!p->flux_water_idx || !p->flux_water_params)))
+        fail(CF_ERR_INVALID, "flux term arrays are null");
+    auto chk = [&](int a, const char* what) {
+        if (a < 0 || a >= n) fail(CF_ERR_INVALID, std::string(what) + " particle index out of range");
+    };
+    const int T = B + A + W;
+    tidx.assign(T, make_int4(0, 0, 0, 0));
+    tpar.assign((size_t)T * 5, 0.0);
+    if (term_atoms) term_atoms->assign(T, {});
+    for (int t = 0; t < B; t++) {
+        int a0 = p->flux_bond_idx[2 * t], a1 = p->flux_bond_idx[2 * t + 1];
+        chk(a0, "flux bond"); chk(a1, "flux bond");
+        tidx[t] = make_int4(0, a0, a1, -1);
+        tpar[5 * t] = p->flux_bond_params[2 * t]; tpar[5 * t + 1] = p->flux_bond_params[2 * t + 1];
+        if (term_atoms) (*term_atoms)[t] = {a0, a1};
+    }
+    for (int u = 0; u < A; u++) {
+        int t = B + u;
+        int a0 = p->flux_angle_idx[3 * u], a1 = p->flux_angle_idx[3 * u + 1], a2 = p->flux_angle_idx[3 * u + 2];
+        chk(a0, "flux angle"); chk(a1, "flux angle"); chk(a2, "flux angle");
+        tidx[t] = make_int4(1, a0, a1, a2);
+        tpar[5 * t] = p->flux_angle_params[2 * u]; tpar[5 * t + 1] = p->flux_angle_params[2 * u + 1];
+        if (term_atoms) (*term_atoms)[t] = {a0, a1, a2};
+    }
+    for (int u = 0; u < W; u++) {
+        int t = B + A + u;
+        int a0 = p->flux_water_idx[3 * u], a1 = p->flux_water_idx[3 * u + 1], a2 = p->flux_water_idx[3 * u + 2];
+        chk(a0, "flux water"); chk(a1, "flux water"); chk(a2, "flux water");
+        tidx[t] = make_int4(2, a0, a1, a2);
+        for (int k = 0; k < 5; k++) tpar[5 * t + k] = p->flux_water_params[5 * u + k];
+        if (term_atoms) (*term_atoms)[t] = {a0, a1, a2};
+    }
+}
+
+// exclusions: unique, ordered, no self pairs (std::set semantics RCK:385-391), as CSR
+void parse_exclusions(const cf_params* p, std::vector<int>& exs, std::vector<int>& exl, int* max_excl) {
+    const int n = p->num_particles, E = p->num_exceptions;
+    if (E < 0 || (E && !p->exceptions)) fail(CF_ERR_INVALID, "bad exception list");
+    std::vector<std::vector<int>> ex(n);
+    for (int k = 0; k < E; k++) {
+        int a0 = p->exceptions[2 * k], a1 = p->exceptions[2 * k + 1];
+        if (a0 < 0 || a0 >= n || a1 < 0 || a1 >= n) fail(CF_ERR_INVALID, "exception particle index out of range");
+        if (a0 == a1) continue;
+        ex[a0].push_back(a1);
+        ex[a1].push_back(a0);
+    }
+    exs.assign(n + 1, 0);
+    exl.clear();
+    int mx = 0;
+    for (int i = 0; i < n; i++) {
+        std::sort(ex[i].begin(), ex[i].end());
+        ex[i].erase(std::unique(ex[i].begin(), ex[i].end()), ex[i].end());
+        exs[i + 1] = exs[i] + (int)ex[i].size();
+        mx = std::max(mx, (int)ex[i].size());
+        exl.insert(exl.end(), ex[i].begin(), ex[i].end());
+    }
+    if (max_excl) *max_excl = mx;
+}
+
+// LJ types: exact-equal (sigma/2, 2 sqrt eps) pairs; <= kMaxLjTypes types ride in the
+// neighbour-list entries.  Returns false when there are more.
+constexpr int kMaxLjTypesHost = 64;
+bool lj_types(const std::vector<double2>& lj, std::vector<int>& at, std::vector<double2>& tt) {
+    const int n = (int)lj.size();
+    at.assign(n, 0);
+    tt.clear();
+    for (int i = 0; i < n; i++) {
+        int k = 0;
+        while (k < (int)tt.size() && !(tt[k].x == lj[i].x && tt[k].y == lj[i].y)) k++;
+        if (k == (int)tt.size()) {
+            if ((int)tt.size() == kMaxLjTypesHost) return false;
+            tt.push_back(lj[i]);
+        }
+        at[i] = k;
+    }
+    return true;
+}
+
 struct Timed {
     cf_handle* H; int ph; bool on;
     Timed(cf_handle* H_, int ph_)
@@ -285,50 +388,18 @@ CF_EXPORT int cf_create(const cf_params* p, const cf_options* opt, cf_handle** o
         h.stream = (hipStream_t)o.stream;  // NULL = the null stream (orders with torch's default stream)
 
         // ---- particles: q0, LJ (sigma/2, 2 sqrt(eps))   RCK:234-240
-        std::vector<double> q0(n);
-        std::vector<double2> lj(n);
-        for (int i = 0; i < n; i++) {
-            if (!(p->epsilons[i] >= 0)) fail(CF_ERR_INVALID, "epsilon must be >= 0");
-            q0[i] = p->charges[i];
-            lj[i] = make_double2(0.5 * p->sigmas[i], 2.0 * std::sqrt(p->epsilons[i]));
-        }
+        std::vector<double> q0;
+        std::vector<double2> lj;
+        parse_particles(p, q0, lj);
 
         // ---- flux terms  RCK:242-284
         const int B = p->num_flux_bonds, A = p->num_flux_angles, W = p->num_flux_waters;
-        if (B < 0 || A < 0 || W < 0) fail(CF_ERR_INVALID, "negative flux term count");
-        if ((B && (!p->flux_bond_idx || !p->flux_bond_params)) || (A && (!p->flux_angle_idx || !p->flux_angle_params)) ||
-            (W && (!p->flux_water_idx || !p->flux_water_params)))
-            fail(CF_ERR_INVALID, "flux term arrays are null");
-        auto chk = [&](int a, const char* what) {
-            if (a < 0 || a >= n) fail(CF_ERR_INVALID, std::string(what) + " particle index out of range");
-        };
         const int T = B + A + W;
-        std::vector<int4> tidx(T);
-        std::vector<double> tpar((size_t)T * 5, 0.0);
-        std::vector<std::vector<int>> term_atoms(T);
-        for (int t = 0; t < B; t++) {
-            int a0 = p->flux_bond_idx[2 * t], a1 = p->flux_bond_idx[2 * t + 1];
-            chk(a0, "flux bond"); chk(a1, "flux bond");
-            tidx[t] = make_int4(0, a0, a1, -1);
-            tpar[5 * t] = p->flux_bond_params[2 * t]; tpar[5 * t + 1] = p->flux_bond_params[2 * t + 1];
-            term_atoms[t] = {a0, a1};
-        }
-        for (int u = 0; u < A; u++) {
-            int t = B + u;
-            int a0 = p->flux_angle_idx[3 * u], a1 = p->flux_angle_idx[3 * u + 1], a2 = p->flux_angle_idx[3 * u + 2];
-            chk(a0, "flux angle"); chk(a1, "flux angle"); chk(a2, "flux angle");
-            tidx[t] = make_int4(1, a0, a1, a2);
-            tpar[5 * t] = p->flux_angle_params[2 * u]; tpar[5 * t + 1] = p->flux_angle_params[2 * u + 1];
-            term_atoms[t] = {a0, a1, a2};
-        }
-        for (int u = 0; u < W; u++) {
-            int t = B + A + u;
-            int a0 = p->flux_water_idx[3 * u], a1 = p->flux_water_idx[3 * u + 1], a2 = p->flux_water_idx[3 * u + 2];
-            chk(a0, "flux water"); chk(a1, "flux water"); chk(a2, "flux water");
-            tidx[t] = make_int4(2, a0, a1, a2);
-            for (int k = 0; k < 5; k++) tpar[5 * t + k] = p->flux_water_params[5 * u + k];
-            term_atoms[t] = {a0, a1, a2};
-        }
+        std::vector<int4> tidx;
+        std::vector<double> tpar;
+        std::vector<std::vector<int>> term_atoms;
+        parse_terms(p, tidx, tpar, &term_atoms);
+        H->topo_terms = tidx;
         h.nb = B; h.na = A; h.nw = W; h.nterms = T;
         h.nslots_dq = 2 * B + 3 * A + 3 * W;
         h.nd = 4 * B + 9 * A + 9 * W;
@@ -364,24 +435,10 @@ CF_EXPORT int cf_create(const cf_params* p, const cf_options* opt, cf_handle** o
         }
 
         // ---- exclusions: unique, ordered, no self pairs (std::set semantics RCK:385-391)
-        const int E = p->num_exceptions;
-        if (E < 0 || (E && !p->exceptions)) fail(CF_ERR_INVALID, "bad exception list");
-        std::vector<std::vector<int>> ex(n);
-        for (int k = 0; k < E; k++) {
-            int a0 = p->exceptions[2 * k], a1 = p->exceptions[2 * k + 1];
-            chk(a0, "exception"); chk(a1, "exception");
-            if (a0 == a1) continue;
-            ex[a0].push_back(a1);
-            ex[a1].push_back(a0);
-        }
-        std::vector<int> exs(n + 1, 0), exl;
-        for (int i = 0; i < n; i++) {
-            std::sort(ex[i].begin(), ex[i].end());
-            ex[i].erase(std::unique(ex[i].begin(), ex[i].end()), ex[i].end());
-            exs[i + 1] = exs[i] + (int)ex[i].size();
-            h.max_excl = std::max(h.max_excl, (int)ex[i].size());
-            exl.insert(exl.end(), ex[i].begin(), ex[i].end());
-        }
+        std::vector<int> exs, exl;
+        parse_exclusions(p, exs, exl, &h.max_excl);
+        H->topo_ex_start = exs;
+        H->topo_ex_list = exl;
 
         // ---- ownership for atom decomposition (see partition())
         partition(p, world, o.rank, &h.lo, &h.hi);
@@ -447,18 +504,14 @@ CF_EXPORT int cf_create(const cf_params* p, const cf_options* opt, cf_handle** o
             h.ljs = dalloc<double2>(H, n);
             // LJ types: exact-equal (sigma/2, 2 sqrt eps) pairs; <= 64 types ride in the list entries
             {
-                std::vector<int> at(n);
+                std::vector<int> at;
                 std::vector<double2> tt;
-                for (int i = 0; i < n && (int)tt.size() <= 64; i++) {
-                    int k = 0;
-                    while (k < (int)tt.size() && !(tt[k].x == lj[i].x && tt[k].y == lj[i].y)) k++;
-                    if (k == (int)tt.size()) tt.push_back(lj[i]);
-                    at[i] = k;
-                }
-                if ((int)tt.size() <= 64) {
+                if (lj_types(lj, at, tt)) {
                     h.lj_ntypes = (int)tt.size();
                     h.atom_type = dupload(H, at);
-                    h.lj_tab = dupload(H, tt);
+                    h.lj_tab = dalloc<double2>(H, kMaxLjTypesHost);   // capacity for cf_update_parameters
+                    check_hip(hipMemcpy(h.lj_tab, tt.data(), sizeof(double2) * tt.size(), hipMemcpyHostToDevice),
+                              "upload LJ types");
                     h.typ_s = dalloc<int>(H, n);
                 }
             }
@@ -570,6 +623,57 @@ CF_EXPORT int cf_set_neighbor_skin(cf_handle* H, double skin) {
         if (!h.pbc) return;
         alloc_nlist(H, skin);
         if (skin > 0 && !h.pos_ref) h.pos_ref = dalloc<double>(H, (size_t)3 * h.n);
+    });
+}
+
+// updateParametersInContext for CoulForce (the reference has none): new
+// charges, LJ parameters and flux-term parameters on the same topology.
+CF_EXPORT int cf_update_parameters(cf_handle* H, const cf_params* p) {
+    return guarded([&] {
+        if (!H || !p) fail(CF_ERR_INVALID, "null argument");
+        cf::Handle& h = H->h;
+        if (h.pending_flags >= 0) fail(CF_ERR_STATE, "cf_update_parameters during a begun evaluation");
+        if (p->num_particles != h.n) fail(CF_ERR_INVALID, "the number of particles has changed");
+        if ((p->use_pbc ? 1 : 0) != h.pbc) fail(CF_ERR_INVALID, "periodicity cannot be changed by an update");
+        if (h.pbc && (p->cutoff != h.cutoff || p->ewald_tol != h.tol))
+            fail(CF_ERR_INVALID, "the cutoff and Ewald tolerance cannot be changed by an update");
+        std::vector<double> q0;
+        std::vector<double2> lj;
+        parse_particles(p, q0, lj);
+        std::vector<int4> tidx;
+        std::vector<double> tpar;
+        parse_terms(p, tidx, tpar, nullptr);
+        bool same = tidx.size() == H->topo_terms.size();
+        for (size_t t = 0; same && t < tidx.size(); t++) {
+            const int4 a = tidx[t], b = H->topo_terms[t];
+            same = a.x == b.x && a.y == b.y && a.z == b.z && a.w == b.w;
+        }
+        if (!same) fail(CF_ERR_INVALID, "the flux terms' particles have changed (only parameters can be updated)");
+        std::vector<int> exs, exl;
+        parse_exclusions(p, exs, exl, nullptr);
+        if (exs != H->topo_ex_start || exl != H->topo_ex_list)
+            fail(CF_ERR_INVALID, "the set of excluded pairs has changed (only parameters can be updated)");
+        check_hip(hipSetDevice(h.device), "hipSetDevice");
+        check_hip(hipStreamSynchronize(h.stream), "stream sync");
+        check_hip(hipMemcpy(h.q0, q0.data(), sizeof(double) * h.n, hipMemcpyHostToDevice), "upload charges");
+        check_hip(hipMemcpy(h.lj, lj.data(), sizeof(double2) * h.n, hipMemcpyHostToDevice), "upload LJ");
+        if (!tpar.empty())
+            check_hip(hipMemcpy(h.term_par, tpar.data(), sizeof(double) * tpar.size(), hipMemcpyHostToDevice),
+                      "upload flux parameters");
+        if (h.typ_s) {
+            std::vector<int> at;
+            std::vector<double2> tt;
+            if (lj_types(lj, at, tt)) {
+                h.lj_ntypes = (int)tt.size();
+                check_hip(hipMemcpy(h.atom_type, at.data(), sizeof(int) * h.n, hipMemcpyHostToDevice), "upload types");
+                check_hip(hipMemcpy(h.lj_tab, tt.data(), sizeof(double2) * tt.size(), hipMemcpyHostToDevice),
+                          "upload LJ types");
+            } else {
+                h.typ_s = nullptr;   // more than 64 LJ parameter sets now: per-atom LJ gathers
+                h.lj_ntypes = 0;
+            }
+        }
+        h.list_valid = false;   // sorted LJ / types are refreshed by the next list build
     });
 }
 

@@ -87,6 +87,7 @@ SIGNATURES = [
     ("cf_partition", C.c_int, [C.POINTER(cf_params), C.c_int32, C.c_int32, C.POINTER(C.c_int32),
                                C.POINTER(C.c_int32)]),
     ("cf_set_neighbor_skin", C.c_int, [C.c_void_p, C.c_double]),
+    ("cf_update_parameters", C.c_int, [C.c_void_p, C.POINTER(cf_params)]),
     ("cf_get_neighbor_stats", C.c_int, [C.c_void_p, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
 ]
 

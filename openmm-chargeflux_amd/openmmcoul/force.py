@@ -130,6 +130,13 @@ class CoulForce:
             raise ValueError("force group must be in [0, 31]")
         self._group = int(group)
 
+    def updateParametersInContext(self, context):
+        """Copy this force's current charges, LJ and flux-term parameters into a Context
+        (OpenMM's updateParametersInContext convention; the reference lacks it, SURVEY §8(f)
+        #4).  The topology -- which particles the flux terms and exceptions connect -- as well
+        as periodicity, cutoff and Ewald tolerance must be unchanged."""
+        context._update_force_parameters(self)
+
     # SWIG %extend helpers (python/openmmcoul.i:67-75)
     @staticmethod
     def cast(force):

@@ -107,6 +107,15 @@ class HipCalcCoulForceKernel:
         self._pbc = force.usesPeriodicBoundaryConditions()
         return self
 
+    def copyParametersToContext(self, force: CoulForce):
+        """New charges / LJ / flux parameters on the same topology (cf_update_parameters; the
+        reference has no updateParametersInContext, SURVEY §8(f) #4)."""
+        if force.getNumParticles() != self._n:
+            raise _cabi.ChargeFluxError(_cabi.CF_ERR_INVALID, "the number of particles has changed")
+        params, keep = force.to_cparams()
+        _cabi.check(self._lib.cf_update_parameters(self._h, C.byref(params)), self._lib)
+        del keep
+
     def destroy(self):
         if self._h:
             self._lib.cf_destroy(self._h)
@@ -289,6 +298,15 @@ class Context:
 
     def kernels(self):
         return [k for _, k in self._impls]
+
+    def _update_force_parameters(self, force):
+        hit = False
+        for f, k in self._impls:
+            if f is force:
+                k.copyParametersToContext(force)
+                hit = True
+        if not hit:
+            raise ValueError("this CoulForce is not part of the Context's System")
 
     def _execute_kernel(self, kernel, include_forces, include_energy):
         forces = np.zeros((self._n, 3))
