@@ -139,7 +139,10 @@ def main():
     ap.add_argument("--config", default="C3", choices=["C2", "C3", "C5"])
     ap.add_argument("--kspace-algo", type=int, default=2,
                     help="0 exact k-sum (fp64 MFMA), 1 exact (direct VALU), 2 grid (ES spread / pruned DFT)")
-    ap.add_argument("--grid-width", type=int, default=0, help="ES kernel width for --kspace-algo 2 (0 = 14)")
+    ap.add_argument("--grid-width", type=int, default=0,
+                    help="ES kernel width for --kspace-algo 2 (0 = 14, or 8 with --precision mixed)")
+    ap.add_argument("--precision", default="double", choices=["double", "mixed"],
+                    help="mixed: fp32 direct-space pair kernel (fp32 force / fp64 energy accumulation), W=8 grid")
     ap.add_argument("--no-exact-compare", action="store_true",
                     help="skip timing the exact k-sum path beside the grid path")
     ap.add_argument("--cpu-k-sample", type=int, default=1500)
@@ -164,7 +167,7 @@ def main():
     n = len(pos_np)
     n_waters = force.getNumFluxWaters() + force.getNumFluxAngles()
     kern = ShardedCoulKernel(system, force, local, kspace_algo=args.kspace_algo, neighbor_skin=args.neighbor_skin,
-                             grid_width=args.grid_width)
+                             grid_width=args.grid_width, precision=args.precision)
     lo, hi = kern.lo, kern.hi
     alpha, kmax = kern.kernel.ewald_params()
     k_half = (kmax[2] - 1) + (kmax[1] - 1) * (2 * kmax[2] - 1) + (kmax[0] - 1) * (2 * kmax[1] - 1) * (2 * kmax[2] - 1)
@@ -250,7 +253,7 @@ def main():
     #  grid_spread   2 N W^3 flops (one FMA per atom x grid point of its support)
     #  grid_interp   4 N W^3 flops (two FMAs per grid value: potential and x-gradient sums)
     #  kspace_sfac / kspace_force (exact path)  4 / 8 flops per atom x half-space k-vector
-    w_grid = args.grid_width or 14
+    w_grid = args.grid_width or (8 if args.precision == "mixed" else 14)
     roofline, others = None, {}
     if dom is not None:
         p_c = pair_count(force, pos_np, box) * n_own / n
@@ -299,8 +302,10 @@ def main():
         fg = torch.zeros_like(pos)
         eg = kern.execute(pos, box, fg, include_energy=True)
         torch.cuda.synchronize()
+        d2 = ((fg - fe) ** 2).sum(1).mean().item()
         exact = {"ms_per_force_eval": round(float(np.mean([a.elapsed_time(b) for a, b in evs])), 4),
                  "max_abs_dforce_grid_vs_exact": float((fg - fe).abs().max().item()),
+                 "rms_rel_dforce_vs_exact": float(math.sqrt(d2 / (fe ** 2).sum(1).mean().item())),
                  "denergy_grid_vs_exact": float(eg.item() - ee.item())}
         del ke
 
@@ -312,11 +317,13 @@ def main():
         out = {
             "metric": METRIC, "value": round(ns_day, 4), "unit": "ns/day", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_step, 4), "higher_is_better": True,
-            "scaling": "strong", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+            "scaling": "strong", "vs_baseline": None,
+            "dtype": "f64" if args.precision == "double" else "f32 pairs / f64 rest (mixed)", "data": "synthetic",
             "config": {"workload": f"{args.config}: periodic flexible charge-flux water box, {n} atoms, Ewald "
                                    f"rc={force.getCutoffDistance()} nm tol={force.getEwaldErrorTolerance()} "
                                    f"(alpha {alpha:.5f}, kmax {kmax[0]}, K_half {k_half}), velocity Verlet dt="
-                                   f"{dt * 1000:g} fs, fp64",
+                                   f"{dt * 1000:g} fs, " + ("fp64" if args.precision == "double" else
+                                                            "mixed precision (fp32 pair kernel)"),
                        "atoms": n, "kmax": list(kmax), "k_half": k_half,
                        "neighbor_skin_nm": args.neighbor_skin,
                        "kspace": {0: "exact k-sum, fp64 MFMA", 1: "exact k-sum, VALU",

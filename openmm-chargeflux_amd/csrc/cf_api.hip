@@ -384,6 +384,9 @@ CF_EXPORT int cf_create(const cf_params* p, const cf_options* opt, cf_handle** o
         if (o.kspace_algo < 0 || o.kspace_algo > 2) fail(CF_ERR_INVALID, "kspace_algo must be 0, 1 or 2");
         if (o.grid_width != 0 && (o.grid_width < 4 || o.grid_width > 16))
             fail(CF_ERR_INVALID, "grid_width must be 0 (default) or in [4, 16]");
+        if (o.precision != CF_PRECISION_DOUBLE && o.precision != CF_PRECISION_MIXED)
+            fail(CF_ERR_INVALID, "precision must be CF_PRECISION_DOUBLE or CF_PRECISION_MIXED");
+        h.mixed = o.precision == CF_PRECISION_MIXED;
         h.kspace_algo = o.kspace_algo;
         h.stream = (hipStream_t)o.stream;  // NULL = the null stream (orders with torch's default stream)
 
@@ -465,7 +468,7 @@ CF_EXPORT int cf_create(const cf_params* p, const cf_options* opt, cf_handle** o
             h.kg.KX = h.kmax[0];
             cf::kspace_plan(h);
             h.khalf = h.kg.k_half();
-            if (h.kspace_algo == 2) cf::grid_plan(h, o.grid_width, 2.0);
+            if (h.kspace_algo == 2) cf::grid_plan(h, o.grid_width ? o.grid_width : (h.mixed ? 8 : 14), 2.0);
         }
 
         // ---- device allocation + upload
@@ -498,9 +501,14 @@ CF_EXPORT int cf_create(const cf_params* p, const cf_options* opt, cf_handle** o
             const cf::KGeom& g = h.kg;
             set_cells(H, std::vector<double>{p->default_box[0], p->default_box[4], p->default_box[8]}.data());
             h.erfc_tab = dupload(H, cf::erfc_table(h.alpha * h.cutoff * (1.0 + 1e-9), &h.erfc_scale, &h.erfc_m));
+            if (h.mixed) {
+                double sc; int m;
+                h.erfc_tab_f = dupload(H, cf::erfc_table_f(h.alpha * h.cutoff * (1.0 + 1e-6), &sc, &m));
+            }
             h.cell_key = dalloc<int>(H, n); h.cell_key_sorted = dalloc<int>(H, n);
             h.atom_val = dalloc<int>(H, n); h.atom_sorted = dalloc<int>(H, n);
             h.pos4s = dalloc<double4>(H, n);
+            if (h.mixed) h.pos4f = dalloc<float4>(H, n);
             h.ljs = dalloc<double2>(H, n);
             // LJ types: exact-equal (sigma/2, 2 sqrt eps) pairs; <= 64 types ride in the list entries
             {

@@ -87,6 +87,7 @@ struct Handle {
     int rank = 0, world = 1;
     int lo = 0, hi = 0;  // owned atoms [lo,hi)
     int kspace_algo = 0;
+    bool mixed = false;         // CF_PRECISION_MIXED: fp32 direct-space pair kernel
     KGeom kg;
     SPassPlan sp;
     FPassPlan fp;
@@ -121,6 +122,7 @@ struct Handle {
     int* atom_val = nullptr; int* atom_sorted = nullptr;
     int* cell_start = nullptr; int* cell_end = nullptr; int* cell_cnt = nullptr;
     double4* pos4s = nullptr;   // [N] sorted wrapped (x,y,z,q)
+    float4* pos4f = nullptr;    // [N] the same in fp32 (mixed precision only)
     double2* ljs = nullptr;     // [N] sorted LJ
     int lj_ntypes = 0;          // distinct (sigma/2, 2 sqrt eps) pairs if <= 64, else 0
     int* atom_type = nullptr;   // [N] LJ type per atom
@@ -182,6 +184,7 @@ struct Handle {
     // energy
     double* erfc_tab = nullptr;  // erfcx interval polynomials (cf_kernels_core.hip erfc_table)
     double erfc_scale = 0; int erfc_m = 0;
+    float* erfc_tab_f = nullptr; // fp32 erfcx table (mixed precision)
     double* terms_dev = nullptr; // [4]
     double* e_part = nullptr;    // [ceil(Nown/2048)][3] energy block partials
     double* energy_dev = nullptr;// [1] internal
@@ -192,7 +195,9 @@ struct Handle {
 };
 
 // ---- launchers (cf_kernels_*.hip) ------------------------------------------------
-std::vector<double> erfc_table(double xmax, double* scale, int* m);
+std::vector<double> erfc_table(double xmax, double* scale, int* m);     // degree 12, fp64 pair kernel
+std::vector<float> erfc_table_f(double xmax, double* scale, int* m);    // degree 6, mixed-precision kernel
+std::vector<double> erfc_table_deg(double xmax, int deg, double* scale, int* m);
 void launch_flux_terms(Handle& h, const double* pos);
 void launch_atoms_prep(Handle& h, const double* pos);
 void launch_cell_sort(Handle& h, const double* pos);

@@ -293,16 +293,18 @@ __global__ void __launch_bounds__(256) k_cell_commit(int n, const int* __restric
                                                      int* __restrict__ key_s, int* __restrict__ idx_s,
                                                      double4* __restrict__ pos4s, double2* __restrict__ ljs,
                                                      const int* __restrict__ atype, int* __restrict__ typ_s,
-                                                     double* __restrict__ pos_ref, long long* __restrict__ n_builds) {
+                                                     double* __restrict__ pos_ref, long long* __restrict__ n_builds,
+                                                     float4* __restrict__ pos4f) {
     int s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= n) return;
+    double4 p4;
     if (*flag) {
         int i = idx_new[s];
         key_s[s] = key[i];
         idx_s[s] = i;
         double3 x = ld3(pos, i);
-        pos4s[s] = make_double4(x.x - floor(x.x / L.x) * L.x, x.y - floor(x.y / L.y) * L.y,
-                                x.z - floor(x.z / L.z) * L.z, q[i]);
+        p4 = make_double4(x.x - floor(x.x / L.x) * L.x, x.y - floor(x.y / L.y) * L.y, x.z - floor(x.z / L.z) * L.z,
+                          q[i]);
         ljs[s] = lj[i];
         if (typ_s) typ_s[s] = atype[i];
         if (pos_ref) { pos_ref[3 * i] = x.x; pos_ref[3 * i + 1] = x.y; pos_ref[3 * i + 2] = x.z; }
@@ -310,9 +312,11 @@ __global__ void __launch_bounds__(256) k_cell_commit(int n, const int* __restric
     } else {
         int i = idx_s[s];
         double3 x = ld3(pos, i), r = ld3(pos_ref, i);
-        pos4s[s] = make_double4(x.x - floor(r.x / L.x) * L.x, x.y - floor(r.y / L.y) * L.y,
-                                x.z - floor(r.z / L.z) * L.z, q[i]);
+        p4 = make_double4(x.x - floor(r.x / L.x) * L.x, x.y - floor(r.y / L.y) * L.y, x.z - floor(r.z / L.z) * L.z,
+                          q[i]);
     }
+    pos4s[s] = p4;
+    if (pos4f) pos4f[s] = make_float4((float)p4.x, (float)p4.y, (float)p4.z, (float)p4.w);
 }
 
 // list validity: flag = 1 if any atom moved more than half the skin since the last build
@@ -339,11 +343,12 @@ __global__ void __launch_bounds__(256) k_skin_check(int n, const double* __restr
 //       list, RCK:559) to a transposed list nl[k*N + s] = t | shift<<26.  Only ~12% of the
 //       candidates pass the cutoff, so the expensive erfc/exp math is kept out of this
 //       divergent loop.
-//    4b k_pairs: one lane per owned atom walks its list with every lane busy, then the
-//       exclusion correction, and finishes dE/dq_i and the non-chain forces.
+//    4b k_pairs: lanes per owned atom walk its list with every lane busy and store the raw
+//       pair sums; k_excl applies the exclusion correction and the self term of dE/dq_i.
 // ---------------------------------------------------------------------------------
 constexpr int kMaxRegExcl = 8;
 constexpr int kErfcDeg = 12;     // erfcx polynomial degree per interval
+constexpr int kErfcDegF = 6;     // the same in fp32 (mixed precision): relative error ~1e-7
 constexpr int kErfcMaxM = 32;    // intervals (width 0.375): x = alpha r up to 12
 constexpr int kMaxLjTypes = 64;  // LJ types carried in the 6 high bits of a list entry
 constexpr int kSeg = 4;          // neighbour sub-lists per atom (one per scanning wave / pair lane)
@@ -355,6 +360,7 @@ struct DirectArgs {
     double3 L; double3 invL; int3 nc; int brute;
     double rc2, alpha;
     const double* erfc_tab;     // [erfc_m][kErfcDeg+1] erfcx(x) on intervals of width 1/erfc_scale
+    const float* erfc_tab_f;    // [erfc_m][kErfcDegF+1] fp32 (mixed precision)
     double erfc_scale; int erfc_m;
     double rl2;                 // list radius^2: (rc + list skin)^2
     int nb_cap;                 // capacity of ONE of the kSeg sub-lists
@@ -364,6 +370,7 @@ struct DirectArgs {
     const int* atom_sorted; const int* key_sorted;
     const int* cstart; const int* cend;
     const double4* pos4s; const double2* ljs;
+    const float4* pos4f;        // fp32 copy of pos4s (mixed precision)
     const int* typ_s;           // [N] LJ type per sorted slot (null: > kMaxLjTypes distinct types)
     const double2* lj_tab; int lj_ntypes;   // per-type (sigma/2, 2 sqrt(eps))
     const double* pos; const double* q;
@@ -736,11 +743,32 @@ __device__ __forceinline__ void load_erfc_tab(const DirectArgs& a, double* tab) 
     __syncthreads();
 }
 
-// exclusion correction of atom i (RCK:596-622) + finish dE/dq and the non-chain forces
-__device__ __forceinline__ void finish_atom(PairAcc acc, const DirectArgs& a, int i, int ex0, int exc) {
+// pair-loop results of atom i: raw direct-space sums (dE/dq_i without the self term, forces,
+// energy); k_excl then applies the exclusion correction and the self term in place
+__device__ __forceinline__ void store_pairs(const PairAcc& acc, const DirectArgs& a, int i) {
+    a.e_atom[3 * i + 1] = acc.e;
+    if (a.include_forces) {  // reciprocal partials are added by k_recip_add after the k-space pass
+        a.dedq[i] = acc.dq;
+        a.f_part[3 * i] = acc.fx;
+        a.f_part[3 * i + 1] = acc.fy;
+        a.f_part[3 * i + 2] = acc.fz;
+    }
+}
+
+// exclusion correction of every owned atom (RCK:596-622: every excluded pair, minimum image,
+// no cutoff, no LJ) on top of the stored pair sums, then dE/dq += the self term.  A kernel of
+// its own so that the pair loop is not sized for the erf code (VGPRs -> occupancy).  The
+// operation order per atom is that of one fused loop: pair sums, then exclusions in list
+// order, then dE/dq_self + sum.
+__global__ void __launch_bounds__(256) k_excl(DirectArgs a) {
+    const int io = blockIdx.x * blockDim.x + threadIdx.x;
+    if (io >= a.hi - a.lo) return;
+    const int i = a.lo + io;
     const double ke = kOne4PiEps0;
     const double two_over_sqrtpi = 1.1283791670955126;
-    double ex_e = 0;
+    const int ex0 = a.ex_start[i], exc = a.ex_start[i + 1] - ex0;
+    double fx = 0, fy = 0, fz = 0, dq = 0, ex_e = 0;
+    if (a.include_forces) { fx = a.f_part[3 * i]; fy = a.f_part[3 * i + 1]; fz = a.f_part[3 * i + 2]; dq = a.dedq[i]; }
     if (exc) {
         double3 xi = ld3(a.pos, i);
         double qi = a.q[i];
@@ -753,19 +781,18 @@ __device__ __forceinline__ void finish_atom(PairAcc acc, const DirectArgs& a, in
             double qj = a.q[j];
             if (a.include_forces) {
                 double g = ke * qi * qj * inv_r * inv_r * inv_r * (ef - ar * exp(-ar * ar) * two_over_sqrtpi);
-                acc.fx -= g * d.x; acc.fy -= g * d.y; acc.fz -= g * d.z;
-                acc.dq -= ke * qj * inv_r * ef;
+                fx -= g * d.x; fy -= g * d.y; fz -= g * d.z;
+                dq -= ke * qj * inv_r * ef;
             }
             ex_e -= 0.5 * ke * qi * qj * inv_r * ef;
         }
     }
-    a.e_atom[3 * i + 1] = acc.e;
     a.e_atom[3 * i + 2] = ex_e;
-    if (a.include_forces) {  // reciprocal partials are added by k_recip_add after the k-space pass
-        a.dedq[i] = a.dedq_self[i] + acc.dq;
-        a.f_part[3 * i] = acc.fx;
-        a.f_part[3 * i + 1] = acc.fy;
-        a.f_part[3 * i + 2] = acc.fz;
+    if (a.include_forces) {
+        a.dedq[i] = a.dedq_self[i] + dq;
+        a.f_part[3 * i] = fx;
+        a.f_part[3 * i + 1] = fy;
+        a.f_part[3 * i + 2] = fz;
     }
 }
 
@@ -794,7 +821,7 @@ __global__ void __launch_bounds__(256) k_recip_add(int lo, int nown, int nparts,
 // TYPES: the partner's LJ parameters come from the per-type table (LDS) indexed by the high
 // bits of the list entry instead of a third gathered 16-B load per candidate.
 template <int LPA, bool TYPES>
-__global__ void __launch_bounds__(256) k_pairs(DirectArgs a) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 8))) k_pairs(DirectArgs a) {
     __shared__ double tab[kErfcMaxM * (kErfcDeg + 1)];
     __shared__ double2 ljt[kMaxLjTypes];
     if (TYPES)
@@ -862,8 +889,133 @@ __global__ void __launch_bounds__(256) k_pairs(DirectArgs a) {
         acc.dq += __shfl_xor(acc.dq, m); acc.e += __shfl_xor(acc.e, m);
     }
     if (!active || g != 0) return;
-    const int ex0 = a.ex_start[i], exc = a.ex_start[i + 1] - ex0;
-    finish_atom(acc, a, i, ex0, exc);
+    store_pairs(acc, a, i);
+}
+
+// ---------------------------------------------------------------------------------
+// 4b' mixed precision (CF_PRECISION_MIXED): the same list walk with the pair term in fp32.
+//     Positions come from the fp32 sorted copy (16-B gathers instead of 32 B); minimum image,
+//     r^2 and the cutoff test in fp32; erfc(alpha r) = e^{-x^2} erfcx(x) with erfcx from a
+//     piecewise degree-6 fp32 polynomial (relative error ~1e-7 on [0, alpha rc], so the
+//     energy tail of the many distant pairs keeps fp32 relative accuracy, unlike the
+//     1.5e-7-absolute Abramowitz-Stegun form) and one v_exp_f32; forces and dE/dq accumulate
+//     in fp32 per lane, the energy in fp64; lanes are combined and the exclusion correction
+//     is applied in fp64 (k_excl).
+// ---------------------------------------------------------------------------------
+struct PairAccF {
+    float fx = 0, fy = 0, fz = 0, dq = 0;
+    double e = 0;
+};
+
+__device__ __forceinline__ void pair_term_f(PairAccF& acc, float alpha, int include_forces, const float* tab,
+                                            float scale, float4 pi, float2 li, float4 pj, float2 lj2, float dx,
+                                            float dy, float dz, float r2) {
+    const float ke = (float)kOne4PiEps0;
+    const float inv_r = rsqrtf(r2);
+    const float r = r2 * inv_r;
+    const float ar = alpha * r;
+    const float y = ar * scale;
+    const int it = (int)y;
+    const float u = 2.0f * (y - (float)it) - 1.0f;
+    const float* c = tab + it * (kErfcDegF + 1);
+    float pc = c[kErfcDegF];
+#pragma unroll
+    for (int j = kErfcDegF - 1; j >= 0; j--) pc = fmaf(pc, u, c[j]);
+    const float e2 = __expf(-ar * ar);
+    const float ec = e2 * pc;
+    const float sig = li.x + lj2.x;
+    float s2 = inv_r * sig;
+    s2 *= s2;
+    const float sig6 = s2 * s2 * s2;
+    const float es6 = sig6 * li.y * lj2.y;
+    const float qq = ke * pi.w * pj.w * inv_r;
+    if (include_forces) {
+        const float inv_r2 = inv_r * inv_r;
+        const float dEdR = qq * inv_r2 * fmaf(ar * e2, 1.1283791670955126f, ec) + es6 * (12.0f * sig6 - 6.0f) * inv_r2;
+        acc.fx = fmaf(dEdR, dx, acc.fx);
+        acc.fy = fmaf(dEdR, dy, acc.fy);
+        acc.fz = fmaf(dEdR, dz, acc.fz);
+        acc.dq = fmaf(ke * pj.w * inv_r, ec, acc.dq);
+    }
+    acc.e += 0.5 * (double)fmaf(qq, ec, es6 * (sig6 - 1.0f));
+}
+
+template <int LPA, bool TYPES>
+__global__ void __launch_bounds__(256) k_pairs_mixed(DirectArgs a) {
+    __shared__ float2 ljt[kMaxLjTypes];
+    __shared__ float tabf[kErfcMaxM * (kErfcDegF + 1)];
+    if (TYPES)
+        for (int e = threadIdx.x; e < a.lj_ntypes; e += blockDim.x)
+            ljt[e] = make_float2((float)a.lj_tab[e].x, (float)a.lj_tab[e].y);
+    for (int e = threadIdx.x; e < a.erfc_m * (kErfcDegF + 1); e += blockDim.x) tabf[e] = a.erfc_tab_f[e];
+    __syncthreads();
+    const float escale = (float)a.erfc_scale;
+    const int gt = xcd_block() * blockDim.x + threadIdx.x;
+    const int c = gt / LPA, g = gt % LPA;
+    const int seg = g % kSeg, part = g / kSeg;
+    bool active = c < a.nlr;
+    const int cc = active ? c : a.nlr - 1;
+    const int ss = own_slot(a, cc);
+    const int i = a.atom_sorted[ss];
+    int cnt = active ? a.nl_cnt[(size_t)seg * a.nlr + cc] : 0;
+    bool over = cnt > a.nb_cap;
+#pragma unroll
+    for (int m = 1; m < LPA; m <<= 1) over = __shfl_xor(over, m) || over;
+    if (over) active = false;
+    PairAccF acc;
+    if (active) {
+        const float4 pi = a.pos4f[ss];
+        const double2 lid = a.ljs[ss];
+        const float2 li = make_float2((float)lid.x, (float)lid.y);
+        const float3 L = make_float3((float)a.L.x, (float)a.L.y, (float)a.L.z);
+        const float3 iL = make_float3((float)a.invL.x, (float)a.invL.y, (float)a.invL.z);
+        const float rc2 = (float)a.rc2, alpha = (float)a.alpha;
+        const int* nl = a.nl + (size_t)seg * a.nb_cap * a.nlr + cc;
+        constexpr int step = LPA / kSeg;
+        constexpr int kMask = (1 << kShiftBits) - 1;
+        const int klast = cnt > 0 ? cnt - 1 : 0;
+        auto entry = [&](int kk) {
+            const int v = __builtin_nontemporal_load(nl + (size_t)min(kk, klast) * a.nlr);
+            return kk < cnt ? v : 0;
+        };
+        auto ljof = [&](int v) {
+            if (TYPES) return ljt[(unsigned)v >> kShiftBits];
+            const double2 d = a.ljs[v & kMask];
+            return make_float2((float)d.x, (float)d.y);
+        };
+        auto eval = [&](const float4& pj, const float2& lj2) {
+            float dx = pi.x - pj.x, dy = pi.y - pj.y, dz = pi.z - pj.z;
+            dx = fmaf(-L.x, rintf(dx * iL.x), dx);
+            dy = fmaf(-L.y, rintf(dy * iL.y), dy);
+            dz = fmaf(-L.z, rintf(dz * iL.z), dz);
+            const float r2 = fmaf(dx, dx, fmaf(dy, dy, dz * dz));
+            if (r2 <= rc2) pair_term_f(acc, alpha, a.include_forces, tabf, escale, pi, li, pj, lj2, dx, dy, dz, r2);
+        };
+        // same two-way software pipeline as k_pairs (ping-pong registers, branch-free loads)
+        const int i0 = entry(part);
+        int iB = entry(part + step), iA = entry(part + 2 * step);
+        float4 pA = a.pos4f[i0 & kMask];
+        float2 lA = ljof(i0);
+        for (int k = part; k < cnt; k += 2 * step) {
+            const float4 pB = a.pos4f[iB & kMask];
+            const float2 lB = ljof(iB);
+            iB = entry(k + 3 * step);
+            eval(pA, lA);
+            pA = a.pos4f[iA & kMask];
+            lA = ljof(iA);
+            iA = entry(k + 4 * step);
+            if (k + step < cnt) eval(pB, lB);
+        }
+    }
+#pragma unroll
+    for (int m = 1; m < LPA; m <<= 1) {
+        acc.fx += __shfl_xor(acc.fx, m); acc.fy += __shfl_xor(acc.fy, m); acc.fz += __shfl_xor(acc.fz, m);
+        acc.dq += __shfl_xor(acc.dq, m); acc.e += __shfl_xor(acc.e, m);
+    }
+    if (!active || g != 0) return;
+    PairAcc ad;
+    ad.fx = acc.fx; ad.fy = acc.fy; ad.fz = acc.fz; ad.dq = acc.dq; ad.e = acc.e;
+    store_pairs(ad, a, i);
 }
 
 // 4c: atoms whose neighbour list overflowed (denser than planned): rescan the cells
@@ -888,7 +1040,7 @@ __global__ void __launch_bounds__(256) k_pairs_overflow(DirectArgs a) {
         if (exc && in_excl(a.atom_sorted[t], reg, exc, a.ex_list, ex0)) return;
         pair_term(acc, a, tab, pi, li, a.pos4s[t], a.ljs[t], dx, dy, dz, r2);
     });
-    finish_atom(acc, a, i, ex0, exc);
+    store_pairs(acc, a, i);
 }
 
 // ---------------------------------------------------------------------------------
@@ -1041,11 +1193,18 @@ static inline int nblk(int64_t n, int b) { return (int)((n + b - 1) / b); }
 
 // erfcx(x) = erfc(x) e^{x^2} on [0, xmax]: intervals of width 0.375, Chebyshev interpolation
 // of degree kErfcDeg in long double, stored as monomials in u in [-1, 1] per interval
-std::vector<double> erfc_table(double xmax, double* scale, int* m) {
+std::vector<double> erfc_table(double xmax, double* scale, int* m) { return erfc_table_deg(xmax, kErfcDeg, scale, m); }
+
+std::vector<float> erfc_table_f(double xmax, double* scale, int* m) {
+    std::vector<double> t = erfc_table_deg(xmax, kErfcDegF, scale, m);
+    return std::vector<float>(t.begin(), t.end());
+}
+
+std::vector<double> erfc_table_deg(double xmax, int deg, double* scale, int* m) {
     const long double w = 0.375L;
     int M = (int)std::ceil((long double)xmax / w) + 1;
     if (M > kErfcMaxM) throw std::invalid_argument("alpha * cutoff too large for the erfc table");
-    const int n = kErfcDeg + 1;
+    const int n = deg + 1;
     std::vector<double> tab((size_t)M * n);
     for (int i = 0; i < M; i++) {
         std::vector<long double> f(n), c(n, 0.0L);
@@ -1116,8 +1275,7 @@ void launch_cell_sort(Handle& h, const double* pos) {
     }
     hipLaunchKernelGGL(k_cell_commit, dim3(nblk(h.n, 256)), dim3(256), 0, h.stream, h.n, f, h.cell_key, h.key_tmp,
                        pos, h.q, h.lj, L, h.cell_key_sorted, h.atom_sorted, h.pos4s, h.ljs, h.atom_type, h.typ_s,
-                       h.pos_ref,
-                       h.n_builds_dev);
+                       h.pos_ref, h.n_builds_dev, h.pos4f);
 }
 
 void launch_skin_check(Handle& h, const double* pos) {
@@ -1140,6 +1298,7 @@ static DirectArgs direct_args(Handle& h, const double* pos, int include_forces) 
     a.brute = (h.nc[0] < 3 || h.nc[1] < 3 || h.nc[2] < 3) ? 1 : 0;
     a.rc2 = h.cutoff * h.cutoff; a.alpha = h.alpha;
     a.erfc_tab = h.erfc_tab; a.erfc_scale = h.erfc_scale; a.erfc_m = h.erfc_m;
+    a.erfc_tab_f = h.erfc_tab_f;
     a.rl2 = (h.cutoff + h.list_skin) * (h.cutoff + h.list_skin);
     a.nb_cap = h.nb_cap;
     a.nlr = h.hi - h.lo;
@@ -1147,7 +1306,7 @@ static DirectArgs direct_args(Handle& h, const double* pos, int include_forces) 
     a.flag = h.skin_flag;
     a.atom_sorted = h.atom_sorted; a.key_sorted = h.cell_key_sorted;
     a.cstart = h.cell_start; a.cend = h.cell_end;
-    a.pos4s = h.pos4s; a.ljs = h.ljs;
+    a.pos4s = h.pos4s; a.ljs = h.ljs; a.pos4f = h.pos4f;
     a.typ_s = h.typ_s; a.lj_tab = h.lj_tab; a.lj_ntypes = h.lj_ntypes;
     a.q = h.q; a.ex_start = h.ex_start; a.ex_list = h.ex_list;
     a.dedq_self = h.dedq_self;
@@ -1170,7 +1329,17 @@ void launch_direct(Handle& h, const double* pos, int include_forces) {
     // lanes per atom: enough threads for ~2 waves per SIMD on 256 CUs
     const int64_t want = 256LL * 4 * 2 * 64;
     const bool ty = a.typ_s != nullptr;
-    if ((int64_t)a.nlr * 4 >= want) {
+    if (h.mixed) {
+#define CF_PAIRS_MIXED(LPA_)                                                                                        \
+    if (ty) hipLaunchKernelGGL((k_pairs_mixed<LPA_, true>), dim3(nblk((int64_t)a.nlr * LPA_, 256)), dim3(256), 0,   \
+                               h.stream, a);                                                                        \
+    else hipLaunchKernelGGL((k_pairs_mixed<LPA_, false>), dim3(nblk((int64_t)a.nlr * LPA_, 256)), dim3(256), 0,     \
+                            h.stream, a)
+        if ((int64_t)a.nlr * 4 >= want) { CF_PAIRS_MIXED(4); }
+        else if ((int64_t)a.nlr * 8 >= want) { CF_PAIRS_MIXED(8); }
+        else { CF_PAIRS_MIXED(16); }
+#undef CF_PAIRS_MIXED
+    } else if ((int64_t)a.nlr * 4 >= want) {
         if (ty) hipLaunchKernelGGL((k_pairs<4, true>), dim3(nblk((int64_t)a.nlr * 4, 256)), dim3(256), 0, h.stream, a);
         else hipLaunchKernelGGL((k_pairs<4, false>), dim3(nblk((int64_t)a.nlr * 4, 256)), dim3(256), 0, h.stream, a);
     } else if ((int64_t)a.nlr * 8 >= want) {
@@ -1181,6 +1350,7 @@ void launch_direct(Handle& h, const double* pos, int include_forces) {
         else hipLaunchKernelGGL((k_pairs<16, false>), dim3(nblk((int64_t)a.nlr * 16, 256)), dim3(256), 0, h.stream, a);
     }
     hipLaunchKernelGGL(k_pairs_overflow, dim3(nblk(a.nlr, 256)), dim3(256), 0, h.stream, a);
+    hipLaunchKernelGGL(k_excl, dim3(nblk(a.nlr, 256)), dim3(256), 0, h.stream, a);
 }
 
 void launch_recip_add(Handle& h) {

@@ -207,27 +207,34 @@ struct SpreadPass {
 
 __device__ __forceinline__ int wrapb(int b, int n) { return b < 0 ? b + n : (b >= n ? b - n : b); }
 
+// NS = source bins per axis that reach a tile (3 for W <= 17, 2 for W <= 9); the 2x2x2-tile
+// block reads a window of NW = NS + 1 bins per axis, starting NS - 1 bins before the block
+template <int NS>
 __device__ __forceinline__ void spread_column(SpreadPass& p, int3 nb, int BX, int BY, int BZ,
                                               const int* __restrict__ start) {
-    const int bx = wrapb(2 * BX - 2 + (p.col >> 2), nb.x), by = wrapb(2 * BY - 2 + (p.col & 3), nb.y);
+    constexpr int NW = NS + 1;
+    const int bx = wrapb(2 * BX - (NS - 1) + p.col / NW, nb.x), by = wrapb(2 * BY - (NS - 1) + p.col % NW, nb.y);
 #pragma unroll
     for (int sz = 0; sz < 4; sz++) {
-        const int b = (bx * nb.y + by) * nb.z + wrapb(2 * BZ - 2 + sz, nb.z);
+        if (sz >= NW) { p.cs[sz] = 0; p.cn[sz] = 0; continue; }
+        const int b = (bx * nb.y + by) * nb.z + wrapb(2 * BZ - (NS - 1) + sz, nb.z);
         p.cs[sz] = start[b];
         p.cn[sz] = start[b + 1] - p.cs[sz];
     }
 }
 
 // advance to the next non-empty pass; false when the columns are exhausted
+template <int NS>
 __device__ __forceinline__ bool spread_next(SpreadPass& p, int3 nb, int BX, int BY, int BZ,
                                             const int* __restrict__ start) {
+    constexpr int NCOL = (NS + 1) * (NS + 1);
     int tot = p.cn[0] + p.cn[1] + p.cn[2] + p.cn[3];
-    if (p.col < 16 && p.base + kSpreadCap < tot) {
+    if (p.col < NCOL && p.base + kSpreadCap < tot) {
         p.base += kSpreadCap;
     } else {
         do {
-            if (++p.col >= 16) return false;
-            spread_column(p, nb, BX, BY, BZ, start);
+            if (++p.col >= NCOL) return false;
+            spread_column<NS>(p, nb, BX, BY, BZ, start);
             tot = p.cn[0] + p.cn[1] + p.cn[2] + p.cn[3];
         } while (tot == 0);
         p.base = 0;
@@ -257,8 +264,10 @@ __device__ __forceinline__ void spread_store(const SpreadPass& p, double* __rest
     }
 }
 
+template <int NS>
 __global__ void __launch_bounds__(512) k_g_spread(int3 ng, int3 nb, const int* __restrict__ start,
                                                   const double* __restrict__ taps, double* __restrict__ grid) {
+    constexpr int NW = NS + 1;
     extern __shared__ double st[];   // 2 x [kSpreadCap][kTapStride]
     const int lane = threadIdx.x & 63, w = wave_id();
     const int ka = lane >> 4, jh = (lane >> 3) & 1, k = lane & 7;   // atom-in-group, y half, z column
@@ -276,7 +285,7 @@ __global__ void __launch_bounds__(512) k_g_spread(int3 ng, int3 nb, const int* _
     SpreadPass p;
     p.col = -1; p.base = 0;
     p.cn[0] = p.cn[1] = p.cn[2] = p.cn[3] = 0;
-    bool have = spread_next(p, nb, BX, BY, BZ, start);
+    bool have = spread_next<NS>(p, nb, BX, BY, BZ, start);
     v2d r[kSpreadU];
     int cur = 0;
     if (have) {
@@ -286,19 +295,20 @@ __global__ void __launch_bounds__(512) k_g_spread(int3 ng, int3 nb, const int* _
     __syncthreads();
     while (have) {
         SpreadPass pn = p;
-        const bool more = spread_next(pn, nb, BX, BY, BZ, start);
+        const bool more = spread_next<NS>(pn, nb, BX, BY, BZ, start);
         if (more) spread_fetch(pn, taps, r);   // in flight during the compute below
         const double* buf = st + (size_t)cur * kSpreadCap * kTapStride;
-        const int dbx = wx + 2 - (p.col >> 2), dby = wy + 2 - (p.col & 3);
-        if (active && dbx >= 0 && dbx <= 2 && dby >= 0 && dby <= 2) {
+        const int dbx = wx + (NS - 1) - p.col / NW, dby = wy + (NS - 1) - p.col % NW;
+        if (active && dbx >= 0 && dbx < NS && dby >= 0 && dby < NS) {
             const int ox = 8 * dbx, oy = kRow + 8 * dby + 4 * jh;
             int off = 0;
 #pragma unroll
             for (int sz = 0; sz < 4; sz++) {
-                const int dbz = wz + 2 - sz;
+                if (sz >= NW) break;
+                const int dbz = wz + (NS - 1) - sz;
                 const int lo = max(off, p.base) - p.base, hi = min(off + p.cn[sz], p.base + p.nst) - p.base;
                 off += p.cn[sz];
-                if (dbz < 0 || dbz > 2 || lo >= hi) continue;
+                if (dbz < 0 || dbz >= NS || lo >= hi) continue;
                 const int oz = 2 * kRow + 8 * dbz + k;
                 for (int u0 = lo; u0 < hi; u0 += 4) {
                     const int u = min(u0 + ka, hi - 1);
@@ -825,8 +835,14 @@ void launch_grid_spread(Handle& h) {
     const GridPlan& p = h.gp;
     const int3 ng = make_int3(p.ng[0], p.ng[1], p.ng[2]), nb = make_int3(p.nb[0], p.nb[1], p.nb[2]);
     const int nblocks = ((p.nb[0] + 1) / 2) * ((p.nb[1] + 1) / 2) * ((p.nb[2] + 1) / 2);
-    hipLaunchKernelGGL(k_g_spread, dim3(nblocks), dim3(512), sizeof(double) * 2 * kSpreadCap * kTapStride, h.stream, ng,
-                       nb, h.g_start, h.g_taps, h.g_grid);
+    // a first tap in bin B reaches tiles B .. B + NS - 1: NS = 2 when W <= 9 (8 source bins per
+    // tile instead of 27)
+    if (p.W <= 9)
+        hipLaunchKernelGGL(k_g_spread<2>, dim3(nblocks), dim3(512), sizeof(double) * 2 * kSpreadCap * kTapStride,
+                           h.stream, ng, nb, h.g_start, h.g_taps, h.g_grid);
+    else
+        hipLaunchKernelGGL(k_g_spread<3>, dim3(nblocks), dim3(512), sizeof(double) * 2 * kSpreadCap * kTapStride,
+                           h.stream, ng, nb, h.g_start, h.g_taps, h.g_grid);
 }
 
 template <bool BREAL, bool CREAL>

@@ -19,6 +19,8 @@ CF_ERR_INVALID = -1
 CF_ERR_HIP = -2
 CF_ERR_STATE = -3
 CF_ERR_NOMEM = -4
+CF_PRECISION_DOUBLE = 0
+CF_PRECISION_MIXED = 1
 CF_INCLUDE_FORCES = 1
 CF_INCLUDE_ENERGY = 2
 ONE_4PI_EPS0 = 138.935456
@@ -56,7 +58,8 @@ class cf_options(C.Structure):
         ("world_size", C.c_int32),
         ("kspace_algo", C.c_int32),
         ("grid_width", C.c_int32),
-        ("reserved", C.c_int32 * 6),
+        ("precision", C.c_int32),
+        ("reserved", C.c_int32 * 5),
     ]
 
 

@@ -76,9 +76,12 @@ class HipCalcCoulForceKernel:
     KSPACE_GRID = 2         # same k-sum via ES-kernel grid (spread, pruned DFT, interpolate)
 
     def __init__(self, device: int = 0, stream=None, rank: int = 0, world_size: int = 1, kspace_algo: int = 0,
-                 grid_width: int = 0):
+                 grid_width: int = 0, precision: str = "double"):
         self._lib = _cabi.load_library()
         self._grid_width = grid_width
+        if precision not in ("double", "mixed"):
+            raise ValueError("precision must be 'double' or 'mixed'")
+        self._precision = _cabi.CF_PRECISION_MIXED if precision == "mixed" else _cabi.CF_PRECISION_DOUBLE
         self._h = C.c_void_p()
         self._device = device
         self._stream = stream
@@ -100,6 +103,7 @@ class HipCalcCoulForceKernel:
         opt.stream = C.c_void_p(self._stream) if self._stream else None
         opt.rank, opt.world_size, opt.kspace_algo = self._rank, self._world, self._algo
         opt.grid_width = self._grid_width
+        opt.precision = self._precision
         self.destroy()
         _cabi.check(self._lib.cf_create(C.byref(params), C.byref(opt), C.byref(self._h)), self._lib)
         del keep
@@ -277,7 +281,8 @@ class Context:
     System (CoulForceImpl::initialize, CoulForceImpl.cpp:16-21) and evaluates them with the
     force-group test of CoulForceImpl::calcForcesAndEnergy (CoulForceImpl.cpp:23-27)."""
 
-    def __init__(self, system: System, device: int = 0, kspace_algo: int = 0, grid_width: int = 0):
+    def __init__(self, system: System, device: int = 0, kspace_algo: int = 0, grid_width: int = 0,
+                 precision: str = "double"):
         self._system = system
         self._n = system.getNumParticles()
         self._pos = np.zeros((self._n, 3))
@@ -287,7 +292,7 @@ class Context:
         for f in system.getForces():
             if isinstance(f, CoulForce):
                 k = HipCalcCoulForceKernel(device=device, kspace_algo=kspace_algo,
-                                           grid_width=grid_width).initialize(system, f)
+                                           grid_width=grid_width, precision=precision).initialize(system, f)
                 self._impls.append((f, k))
 
     def setPositions(self, positions):
