@@ -92,7 +92,7 @@ def cpu_baseline(force, pos, box, k_sample):
 
 # rocprofv3 kernel names of the library's timing phases at C3
 PMC_KERNEL = {"kspace_force": "cf::k_force<2>", "kspace_sfac": "cf::k_sfac<4, 32>",
-              "direct_pairs": "cf::k_pairs<4, true>", "grid_spread": "cf::k_g_spread",
+              "direct_pairs": "cf::k_pairs<4, true>", "grid_spread": "cf::k_g_spread<3>",
               "grid_interp": "cf::k_g_interp<14>"}
 
 

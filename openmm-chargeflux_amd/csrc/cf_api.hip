@@ -153,6 +153,7 @@ void set_cells(cf_handle* H, const double L[3]) {
         cf::check_hip(hipMalloc(&h.cell_start, sizeof(int) * ncell), "cells");
         cf::check_hip(hipMalloc(&h.cell_end, sizeof(int) * ncell), "cells");
         cf::check_hip(hipMalloc(&h.cell_cnt, sizeof(int) * ncell), "cells");
+        cf::check_hip(hipMemset(h.cell_cnt, 0, sizeof(int) * ncell), "cells");   // re-zeroed by each build
         h.ncell_alloc = (int)ncell;
     }
     h.nc[0] = nc[0]; h.nc[1] = nc[1]; h.nc[2] = nc[2];
@@ -492,6 +493,8 @@ CF_EXPORT int cf_create(const cf_params* p, const cf_options* opt, cf_handle** o
         h.terms_dev = dalloc<double>(H, 4);
         h.e_part = dalloc<double>(H, 3 * ((size_t)n / 2048 + 2));
         h.energy_dev = dalloc<double>(H, 1);
+        h.e_ticket = dalloc<int>(H, 1);
+        check_hip(hipMemset(h.e_ticket, 0, sizeof(int)), "memset");
         check_hip(hipMemset(h.dedq, 0, sizeof(double) * n), "memset");
         check_hip(hipMemset(h.f_part, 0, sizeof(double) * 3 * n), "memset");
         check_hip(hipMemset(h.e_atom, 0, sizeof(double) * 3 * n), "memset");
@@ -526,6 +529,7 @@ CF_EXPORT int cf_create(const cf_params* p, const cf_options* opt, cf_handle** o
             h.key_tmp = dalloc<int>(H, n);
             h.atom_tmp = dalloc<int>(H, n);
             h.skin_flag = dalloc<int>(H, 1);
+            check_hip(hipMemset(h.skin_flag, 0, sizeof(int)), "memset");
             h.n_builds_dev = dalloc<long long>(H, 1);
             check_hip(hipMemset(h.n_builds_dev, 0, sizeof(long long)), "memset");
             if (h.world > 1) h.own_s = dalloc<int>(H, std::max(nown, 1));  // owned atoms, cell-sorted
@@ -559,6 +563,7 @@ CF_EXPORT int cf_create(const cf_params* p, const cf_options* opt, cf_handle** o
                 h.g_t2 = dalloc<double2>(H, (size_t)gp.ng[0] * gp.NY * gp.KZ);
                 h.g_b = dalloc<double2>(H, (size_t)gp.NX * gp.NY * gp.KZ);
                 h.g_cnt = dalloc<int>(H, gp.nbins);
+                check_hip(hipMemset(h.g_cnt, 0, sizeof(int) * gp.nbins), "memset");   // re-zeroed by k_g_scatter
                 h.g_start = dalloc<int>(H, gp.nbins + 1);
                 const size_t no = std::max(nown, 1);
                 h.g_srec = dalloc<double4>(H, no);
@@ -568,6 +573,11 @@ CF_EXPORT int cf_create(const cf_params* p, const cf_options* opt, cf_handle** o
                 h.g_order = dalloc<int>(H, no);
                 h.g_g0s = dalloc<int4>(H, no);
                 h.g_taps = dalloc<double>(H, no * 72);
+                if (h.world > 1) {
+                    h.g_xrange = dalloc<int>(H, 3);
+                    const int init[3] = {INT_MAX, INT_MIN, 0};
+                    check_hip(hipMemcpy(h.g_xrange, init, sizeof(init), hipMemcpyHostToDevice), "x-slab init");
+                }
                 h.t_part = dalloc<double>(H, no * 4);
                 h.e_rec_part = dalloc<double>(H, (size_t)(gp.NX * gp.NY * gp.KZ + 255) / 256 + 1);
             } else {
@@ -829,7 +839,7 @@ CF_EXPORT int cf_compute_end(cf_handle* H, double* forces_dev, double* energy_de
                 }
                 if (forces && h.kspace_algo == 2) {
                     { Timed t(H, PH_GDFTI); cf::launch_grid_dft_inv(h); }
-                    { Timed t(H, PH_GINTERP); cf::launch_grid_interp(h); cf::launch_recip_add(h); }
+                    { Timed t(H, PH_GINTERP); cf::launch_grid_interp(h); }   // adds into dE/dq and forces
                 } else if (forces) {
                     Timed t(H, PH_FORCE);
                     if (h.kspace_algo == 0) cf::launch_kspace_force(h, pos);

@@ -174,7 +174,8 @@ struct Handle {
     int* g_tmp = nullptr;       // [Nown]
     int* g_order = nullptr;     // [Nown] sorted slot -> owned index
     int4* g_g0s = nullptr;      // [Nown] wrapped first taps per sorted slot
-    double* g_taps = nullptr;   // [Nown][48]
+    double* g_taps = nullptr;   // [Nown][72]
+    int* g_xrange = nullptr;    // [3] multi-rank x-slab of the owned atoms' taps (null on one rank)
     // k-space (direct VALU check path)
     int64_t khalf = 0;
     double* sk_slab = nullptr;  // [nchunk][2][khalf]
@@ -188,6 +189,7 @@ struct Handle {
     double* terms_dev = nullptr; // [4]
     double* e_part = nullptr;    // [ceil(Nown/2048)][3] energy block partials
     double* energy_dev = nullptr;// [1] internal
+    int* e_ticket = nullptr;     // [1] k_energy block ticket (0 between launches)
     // state
     int pending_flags = -1;     // flags of a begun evaluation
     bool direct_done = false;   // cf_compute_direct already ran for the begun evaluation

@@ -138,11 +138,6 @@ __global__ void __launch_bounds__(256) k_atoms_prep(int n, const double* __restr
 //      clear counts -> keys + histogram -> scan (bounds) -> scatter -> order within cells
 //      -> [owned compaction] -> commit (or refresh of the kept list's coordinates)
 // ---------------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) k_cell_zero(int ncell, const int* __restrict__ flag, int* __restrict__ cnt) {
-    int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= ncell || !*flag) return;
-    cnt[c] = 0;
-}
 
 __global__ void __launch_bounds__(256) k_cell_hist(int n, const int* __restrict__ flag, const double* __restrict__ pos,
                                                    double3 L, int3 nc, int* __restrict__ key, int* __restrict__ rank,
@@ -199,11 +194,15 @@ __global__ void __launch_bounds__(kScanThreads) k_cell_scan(int ncell, const int
     }
 }
 
+// also re-zeroes the per-cell counts (consumed by k_cell_scan) for the next build, so no
+// separate zeroing launch precedes k_cell_hist
 __global__ void __launch_bounds__(256) k_cell_scatter(int n, const int* __restrict__ flag, const int* __restrict__ key,
                                                       const int* __restrict__ rank, const int* __restrict__ cstart,
-                                                      int* __restrict__ tmp) {
+                                                      int* __restrict__ tmp, int ncell, int* __restrict__ cnt) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n || !*flag) return;
+    if (!*flag) return;
+    for (int c = i; c < ncell; c += gridDim.x * blockDim.x) cnt[c] = 0;
+    if (i >= n) return;
     tmp[cstart[key[i]] + rank[i]] = i;
 }
 
@@ -344,7 +343,7 @@ __global__ void __launch_bounds__(256) k_skin_check(int n, const double* __restr
 //       candidates pass the cutoff, so the expensive erfc/exp math is kept out of this
 //       divergent loop.
 //    4b k_pairs: lanes per owned atom walk its list with every lane busy and store the raw
-//       pair sums; k_excl applies the exclusion correction and the self term of dE/dq_i.
+//       pair sums; k_excl applies the exclusion correction and the self term.
 // ---------------------------------------------------------------------------------
 constexpr int kMaxRegExcl = 8;
 constexpr int kErfcDeg = 12;     // erfcx polynomial degree per interval
@@ -755,15 +754,13 @@ __device__ __forceinline__ void store_pairs(const PairAcc& acc, const DirectArgs
     }
 }
 
-// exclusion correction of every owned atom (RCK:596-622: every excluded pair, minimum image,
-// no cutoff, no LJ) on top of the stored pair sums, then dE/dq += the self term.  A kernel of
-// its own so that the pair loop is not sized for the erf code (VGPRs -> occupancy).  The
+// exclusion correction of owned atom i (RCK:596-622: every excluded pair, minimum image,
+// no cutoff, no LJ) on top of the stored pair sums, then dE/dq += the self term.  Run by
+// k_excl after the pair kernels, so that the pair loop is not sized for the erf code
+// (VGPRs -> occupancy).  The
 // operation order per atom is that of one fused loop: pair sums, then exclusions in list
 // order, then dE/dq_self + sum.
-__global__ void __launch_bounds__(256) k_excl(DirectArgs a) {
-    const int io = blockIdx.x * blockDim.x + threadIdx.x;
-    if (io >= a.hi - a.lo) return;
-    const int i = a.lo + io;
+__device__ __forceinline__ void excl_atom(const DirectArgs& a, int i) {
     const double ke = kOne4PiEps0;
     const double two_over_sqrtpi = 1.1283791670955126;
     const int ex0 = a.ex_start[i], exc = a.ex_start[i + 1] - ex0;
@@ -900,7 +897,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 8))
 //     energy tail of the many distant pairs keeps fp32 relative accuracy, unlike the
 //     1.5e-7-absolute Abramowitz-Stegun form) and one v_exp_f32; forces and dE/dq accumulate
 //     in fp32 per lane, the energy in fp64; lanes are combined and the exclusion correction
-//     is applied in fp64 (k_excl).
+//     is applied in fp64 (excl_atom).
 // ---------------------------------------------------------------------------------
 struct PairAccF {
     float fx = 0, fy = 0, fz = 0, dq = 0;
@@ -1018,17 +1015,7 @@ __global__ void __launch_bounds__(256) k_pairs_mixed(DirectArgs a) {
     store_pairs(ad, a, i);
 }
 
-// 4c: atoms whose neighbour list overflowed (denser than planned): rescan the cells
-__global__ void __launch_bounds__(256) k_pairs_overflow(DirectArgs a) {
-    __shared__ double tab[kErfcMaxM * (kErfcDeg + 1)];
-    load_erfc_tab(a, tab);
-    int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= a.nlr) return;
-    bool over = false;
-    for (int g = 0; g < kSeg; g++) over = over || a.nl_cnt[(size_t)g * a.nlr + c] > a.nb_cap;
-    if (!over) return;
-    int s = own_slot(a, c);
-    int i = a.atom_sorted[s];
+__device__ __forceinline__ void pair_rescan(const DirectArgs& a, const double* tab, int s, int i) {
     const double4 pi = a.pos4s[s];
     const double2 li = a.ljs[s];
     const int ex0 = a.ex_start[i], exc = a.ex_start[i + 1] - ex0;
@@ -1041,6 +1028,25 @@ __global__ void __launch_bounds__(256) k_pairs_overflow(DirectArgs a) {
         pair_term(acc, a, tab, pi, li, a.pos4s[t], a.ljs[t], dx, dy, dz, r2);
     });
     store_pairs(acc, a, i);
+}
+
+// 4c: atoms whose neighbour list overflowed (denser than planned): rescan the cells
+__global__ void __launch_bounds__(256) k_pairs_overflow(DirectArgs a) {
+    __shared__ double tab[kErfcMaxM * (kErfcDeg + 1)];
+    load_erfc_tab(a, tab);
+    int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= a.nlr) return;
+    bool over = false;
+    for (int g = 0; g < kSeg; g++) over = over || a.nl_cnt[(size_t)g * a.nlr + c] > a.nb_cap;
+    if (!over) return;
+    int s = own_slot(a, c);
+    pair_rescan(a, tab, s, a.atom_sorted[s]);
+}
+
+// 4d: exclusion correction + self term of every owned atom (in atom order: coalesced)
+__global__ void __launch_bounds__(256) k_excl(DirectArgs a) {
+    const int io = blockIdx.x * blockDim.x + threadIdx.x;
+    if (io < a.hi - a.lo) excl_atom(a, a.lo + io);
 }
 
 // ---------------------------------------------------------------------------------
@@ -1151,25 +1157,38 @@ __device__ __forceinline__ void block_sum3(double& a0, double& a1, double& a2, d
     a0 = red[0][0]; a1 = red[1][0]; a2 = red[2][0];
 }
 
-__global__ void __launch_bounds__(256) k_energy_part(int lo, int hi, const double* __restrict__ e_atom,
-                                                     double* __restrict__ part) {
+// Per-block partial sums of the per-atom energies; the block that finishes last (atomic
+// ticket) sums the partials and the reciprocal partials in fixed order, so the result does
+// not depend on block scheduling.  It also clears the neighbour-list rebuild flag for the
+// next evaluation and re-arms the ticket.
+__global__ void __launch_bounds__(256) k_energy(int lo, int hi, const double* __restrict__ e_atom,
+                                                double* __restrict__ part, const double* __restrict__ e_rec_part,
+                                                int nrec, int pbc, double* __restrict__ terms,
+                                                double* __restrict__ energy_out, double* __restrict__ energy_int,
+                                                int* __restrict__ ticket, int* __restrict__ flag,
+                                                int* __restrict__ xrange) {
     __shared__ double red[3][256];
+    __shared__ bool last;
     double a0 = 0, a1 = 0, a2 = 0;
-    const int i0 = lo + blockIdx.x * kEChunk;
-    const int i1 = min(hi, i0 + kEChunk);
-    for (int i = i0 + threadIdx.x; i < i1; i += 256) {
-        a0 += e_atom[3 * i]; a1 += e_atom[3 * i + 1]; a2 += e_atom[3 * i + 2];
+    {
+        const int i0 = lo + blockIdx.x * kEChunk;
+        const int i1 = min(hi, i0 + kEChunk);
+        for (int i = i0 + threadIdx.x; i < i1; i += 256) {
+            a0 += e_atom[3 * i]; a1 += e_atom[3 * i + 1]; a2 += e_atom[3 * i + 2];
+        }
+        block_sum3(a0, a1, a2, red);
+        if (threadIdx.x == 0) {
+            part[3 * blockIdx.x] = a0; part[3 * blockIdx.x + 1] = a1; part[3 * blockIdx.x + 2] = a2;
+            __threadfence();
+            last = atomicAdd(ticket, 1) == (int)gridDim.x - 1;
+        }
+        __syncthreads();
+        if (!last) return;
+        __threadfence();
     }
-    block_sum3(a0, a1, a2, red);
-    if (threadIdx.x == 0) { part[3 * blockIdx.x] = a0; part[3 * blockIdx.x + 1] = a1; part[3 * blockIdx.x + 2] = a2; }
-}
-
-__global__ void __launch_bounds__(256) k_energy(int nparts, const double* __restrict__ part,
-                                                const double* __restrict__ e_rec_part, int nrec, int pbc,
-                                                double* __restrict__ terms, double* __restrict__ energy_out,
-                                                double* __restrict__ energy_int) {
-    __shared__ double red[3][256];
-    double a0 = 0, a1 = 0, a2 = 0;
+    const int nparts = gridDim.x;
+    a0 = 0; a1 = 0; a2 = 0;
+    __syncthreads();
     for (int k = threadIdx.x; k < nparts; k += 256) { a0 += part[3 * k]; a1 += part[3 * k + 1]; a2 += part[3 * k + 2]; }
     double r = 0;
     for (int k = threadIdx.x; k < nrec; k += 256) r += e_rec_part[k];
@@ -1183,6 +1202,9 @@ __global__ void __launch_bounds__(256) k_energy(int nparts, const double* __rest
         const double e = pbc ? (t0 + t1 + t2 + t3) : t2;
         *energy_int = e;
         if (energy_out) *energy_out = e;
+        *ticket = 0;
+        if (flag) *flag = 0;
+        if (xrange) { xrange[0] = INT_MAX; xrange[1] = INT_MIN; }   // re-arm the grid x-slab
     }
 }
 
@@ -1256,13 +1278,12 @@ void launch_cell_sort(Handle& h, const double* pos) {
     const int* f = h.skin_flag;
     // scratch: cell_key = per-atom key, atom_val = provisional rank, key_tmp = per-cell
     // counts, atom_tmp = scattered order, cell_key_sorted's partner atom_new = final order
-    hipLaunchKernelGGL(k_cell_zero, dim3(nblk(ncell, 256)), dim3(256), 0, h.stream, ncell, f, h.cell_cnt);
     hipLaunchKernelGGL(k_cell_hist, dim3(nblk(h.n, 256)), dim3(256), 0, h.stream, h.n, f, pos, L, nc, h.cell_key,
                        h.atom_val, h.cell_cnt);
     hipLaunchKernelGGL(k_cell_scan, dim3(1), dim3(kScanThreads), 0, h.stream, ncell, f, h.cell_cnt, h.cell_start,
                        h.cell_end);
     hipLaunchKernelGGL(k_cell_scatter, dim3(nblk(h.n, 256)), dim3(256), 0, h.stream, h.n, f, h.cell_key, h.atom_val,
-                       h.cell_start, h.atom_tmp);
+                       h.cell_start, h.atom_tmp, ncell, h.cell_cnt);
     hipLaunchKernelGGL(k_cell_order, dim3(nblk(ncell, 4)), dim3(256), 0, h.stream, ncell, f, h.cell_start,
                        h.cell_end, h.atom_tmp, h.key_tmp);
     if (h.own_s) {
@@ -1279,7 +1300,7 @@ void launch_cell_sort(Handle& h, const double* pos) {
 }
 
 void launch_skin_check(Handle& h, const double* pos) {
-    check_hip(hipMemsetAsync(h.skin_flag, 0, sizeof(int), h.stream), "memset skin flag");
+    // the flag is 0 here: cleared at cf_create and by k_energy at the end of every evaluation
     const double lim = 0.5 * h.list_skin;
     hipLaunchKernelGGL(k_skin_check, dim3(nblk(h.n, 256)), dim3(256), 0, h.stream, h.n, pos, h.pos_ref, lim * lim,
                        h.skin_flag);
@@ -1376,9 +1397,8 @@ void launch_assemble(Handle& h, double* forces_out) {
 void launch_energy(Handle& h, int include_energy, double* energy_out) {
     int nrec = (h.pbc && include_energy && h.rank == 0) ? h.e_rec_nblk : 0;
     const int nparts = std::max(1, nblk(h.hi - h.lo, kEChunk));
-    hipLaunchKernelGGL(k_energy_part, dim3(nparts), dim3(256), 0, h.stream, h.lo, h.hi, h.e_atom, h.e_part);
-    hipLaunchKernelGGL(k_energy, dim3(1), dim3(256), 0, h.stream, nparts, h.e_part, h.e_rec_part, nrec, h.pbc,
-                       h.terms_dev, energy_out, h.energy_dev);
+    hipLaunchKernelGGL(k_energy, dim3(nparts), dim3(256), 0, h.stream, h.lo, h.hi, h.e_atom, h.e_part, h.e_rec_part,
+                       nrec, h.pbc, h.terms_dev, energy_out, h.energy_dev, h.e_ticket, h.skin_flag, h.g_xrange);
 }
 
 }  // namespace cf

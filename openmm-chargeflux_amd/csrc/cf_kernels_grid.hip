@@ -63,14 +63,72 @@ __device__ __forceinline__ double es_val(double t, double hw_inv, double beta) {
 }
 
 // ---------------------------------------------------------------------------------
+// Multi-rank x-slab: on a rank that owns a spatially compact set of atoms, only the grid
+// x-planes its atoms' taps reach carry data.  xr[0..1] = min / max over owned atoms of the
+// first x tap relative to xr[2] (the first owned atom's first tap, folded into
+// [-ng/2, ng/2)), accumulated by k_g_bin with atomics (order-independent) and reset by
+// k_energy.  Planes outside [xr[2] + xr[0], xr[2] + xr[1] + W) (mod ng) are skipped by the
+// spread, both DFT passes and are never read by the interpolation.  xr == null: all planes.
+// ---------------------------------------------------------------------------------
+// slab as (first plane in [0, ngx), number of planes); len >= ngx means every plane
+__device__ __forceinline__ void slab_of(const int* __restrict__ xr, int W, int ngx, int& s0, int& len) {
+    len = xr[1] - xr[0] + W;
+    s0 = (xr[2] + xr[0]) % ngx;
+    s0 += s0 < 0 ? ngx : 0;
+}
+
+__device__ __forceinline__ bool x_in_slab(int x, const int* __restrict__ xr, int W, int ngx) {
+    if (!xr) return true;
+    const int len = xr[1] - xr[0] + W;
+    if (len >= ngx) return true;
+    int d = (x - (xr[2] + xr[0])) % ngx;
+    d += d < 0 ? ngx : 0;
+    return d < len;
+}
+
+__device__ __forceinline__ bool x_range_in_slab(int x0, int x1, const int* __restrict__ xr, int W, int ngx) {
+    if (!xr) return true;
+    for (int x = x0; x <= x1; x++)
+        if (x_in_slab(x, xr, W, ngx)) return true;
+    return false;
+}
+
+// ---------------------------------------------------------------------------------
 // 1. bin owned atoms by the 8^3 grid tile holding their first tap; deterministic counting
 //    sort (atomic provisional rank, then the order of a stable sort by atom index)
 // ---------------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) k_g_bin(int lo, int nown, const double* __restrict__ pos,
                                                const double* __restrict__ q, double3 L, int3 ng, int W, int3 nb,
                                                double4* __restrict__ srec, int4* __restrict__ g0u,
-                                               int* __restrict__ rank, int* __restrict__ cnt) {
+                                               int* __restrict__ rank, int* __restrict__ cnt, int* __restrict__ xr) {
     const int io = blockIdx.x * blockDim.x + threadIdx.x;
+    if (xr) {   // x-slab of the owned atoms' first taps, relative to the first owned atom's
+        double u0 = pos[3 * lo] / L.x;
+        u0 -= floor(u0);
+        double s0 = u0 * ng.x;
+        if (s0 >= ng.x) s0 -= ng.x;
+        const int gref = (int)ceil(s0 - 0.5 * W);
+        int rmin = INT_MAX, rmax = INT_MIN;
+        if (io < nown) {
+            double u = pos[3 * (lo + io)] / L.x;
+            u -= floor(u);
+            double sd = u * ng.x;
+            if (sd >= ng.x) sd -= ng.x;
+            int rel = ((int)ceil(sd - 0.5 * W) - gref) % ng.x;
+            rel += rel < 0 ? ng.x : 0;
+            rel -= rel >= ng.x / 2 ? ng.x : 0;
+            rmin = rmax = rel;
+        }
+        for (int off = 32; off > 0; off >>= 1) {
+            rmin = min(rmin, __shfl_xor(rmin, off));
+            rmax = max(rmax, __shfl_xor(rmax, off));
+        }
+        if ((threadIdx.x & 63) == 0 && rmin <= rmax) {
+            atomicMin(&xr[0], rmin);
+            atomicMax(&xr[1], rmax);
+        }
+        if (io == 0) xr[2] = gref;
+    }
     if (io >= nown) return;
     const int i = lo + io;
     const double x[3] = {pos[3 * i], pos[3 * i + 1], pos[3 * i + 2]};
@@ -119,9 +177,12 @@ __global__ void __launch_bounds__(kGScan) k_g_scan(int nbins, const int* __restr
     if (t == kGScan - 1) start[nbins] = sh[t];
 }
 
+// also re-zeroes the bin counts (consumed by k_g_scan) for the next evaluation
 __global__ void __launch_bounds__(256) k_g_scatter(int nown, const int4* __restrict__ g0u, const int* __restrict__ rank,
-                                                   const int* __restrict__ start, int* __restrict__ tmp) {
+                                                   const int* __restrict__ start, int* __restrict__ tmp, int nbins,
+                                                   int* __restrict__ cnt) {
     const int io = blockIdx.x * blockDim.x + threadIdx.x;
+    for (int b = io; b < nbins; b += gridDim.x * blockDim.x) cnt[b] = 0;
     if (io >= nown) return;
     tmp[start[g0u[io].w] + rank[io]] = io;
 }
@@ -266,14 +327,18 @@ __device__ __forceinline__ void spread_store(const SpreadPass& p, double* __rest
 
 template <int NS>
 __global__ void __launch_bounds__(512) k_g_spread(int3 ng, int3 nb, const int* __restrict__ start,
-                                                  const double* __restrict__ taps, double* __restrict__ grid) {
+                                                  const double* __restrict__ taps, double* __restrict__ grid,
+                                                  const int* __restrict__ xr, int W) {
     constexpr int NW = NS + 1;
     extern __shared__ double st[];   // 2 x [kSpreadCap][kTapStride]
     const int lane = threadIdx.x & 63, w = wave_id();
     const int ka = lane >> 4, jh = (lane >> 3) & 1, k = lane & 7;   // atom-in-group, y half, z column
     const int nbbz = (nb.z + 1) >> 1, nbby = (nb.y + 1) >> 1;
-    const int blk = xcd_block();   // neighbouring blocks (shared source bins) on one XCD's L2
+    // default round-robin block order: on a multi-rank run the work sits in one x-slab, which an
+    // XCD-contiguous mapping would put on a single XCD
+    const int blk = blockIdx.x;
     const int BZ = blk % nbbz, BY = (blk / nbbz) % nbby, BX = blk / (nbbz * nbby);
+    if (!x_range_in_slab(16 * BX, min(16 * BX + 15, ng.x - 1), xr, W, ng.x)) return;
     const int wx = (w >> 2) & 1, wy = (w >> 1) & 1, wz = w & 1;
     const int tx = 2 * BX + wx, ty = 2 * BY + wy, tz = 2 * BZ + wz;
     const bool active = tx < nb.x && ty < nb.y && tz < nb.z;
@@ -468,6 +533,11 @@ struct ZGemm {
     const void* B; long sbk, sb0, sb1;
     void* C; long scm, sc0, sc1;
     int b_kfast;   // B is contiguous along k (load lanes walk k first)
+    // x-slab (multi-rank): which index is the grid x-plane -- 0 none, 1 m, 2 n / xdiv, 3 k.
+    // Tiles whose x-planes lie outside the slab are skipped; along k they contribute zero.
+    int xdim = 0, xdiv = 1;
+    const int* xr = nullptr;
+    int W = 0, ngx = 0;
 };
 
 template <bool BREAL, bool CREAL>
@@ -480,6 +550,15 @@ __global__ void __launch_bounds__(256) k_g_zgemm(ZGemm g) {
     const int tm = tile % tiles_m, tn = tile / tiles_m;
     if (tn * 16 >= g.N) return;
     const int m0 = tm * 16, n0 = tn * 16;
+    if (g.xdim == 1 && !x_range_in_slab(m0, min(m0 + 15, g.M - 1), g.xr, g.W, g.ngx)) return;
+    if (g.xdim == 2 && !x_range_in_slab(n0 / g.xdiv, min(n0 + 15, g.N - 1) / g.xdiv, g.xr, g.W, g.ngx)) return;
+    // along k (the x-plane): walk only the slab's planes, k = kbase + t (mod K), t < kcount
+    int kbase = 0, kcount = g.K;
+    if (g.xdim == 3 && g.xr) {
+        int s0, len;
+        slab_of(g.xr, g.W, g.ngx, s0, len);
+        if (len < g.K) { kbase = s0; kcount = len; }
+    }
     const int lm = lane >> 3, ln = lane & 7;
     // load roles (fixed over k): element e = lane + 64q of the 16x16 chunk
     const int ak = lane & 15;   // A: k fastest
@@ -509,15 +588,21 @@ __global__ void __launch_bounds__(256) k_g_zgemm(ZGemm g) {
     auto fetch = [&](int k0) {
 #pragma unroll
         for (int q = 0; q < 4; q++) {
-            const int ka = k0 + ak;
+            int ka = k0 + ak;
             ra[q] = v2d{0.0, 0.0};
-            if (aok[q] && ka < g.K) {
+            if (aok[q] && ka < kcount) {
+                ka += kbase;
+                ka -= ka >= g.K ? g.K : 0;
                 const double2 t = g.A[aoff[q] + (long)ka * g.sak];
                 ra[q] = v2d{t.x, t.y};
             }
-            const int kb = k0 + bkk[q];
+            int kb = k0 + bkk[q];
             rb[q] = v2d{0.0, 0.0};
-            if (bok[q] && kb < g.K) {
+            // out-of-slab planes of B were never written this evaluation (stale, possibly NaN):
+            // never read
+            if (bok[q] && kb < kcount) {
+                kb += kbase;
+                kb -= kb >= g.K ? g.K : 0;
                 const long off = boff[q] + (long)kb * g.sbk;
                 if (BREAL) {
                     rb[q] = v2d{reinterpret_cast<const double*>(g.B)[off], 0.0};
@@ -529,7 +614,7 @@ __global__ void __launch_bounds__(256) k_g_zgemm(ZGemm g) {
         }
     };
     fetch(0);
-    for (int k0 = 0; k0 < g.K; k0 += 16) {
+    for (int k0 = 0; k0 < kcount; k0 += 16) {
 #pragma unroll
         for (int q = 0; q < 4; q++) {
             sa[w][(lane >> 4) + 4 * q][ak] = ra[q];
@@ -538,7 +623,7 @@ __global__ void __launch_bounds__(256) k_g_zgemm(ZGemm g) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        if (k0 + 16 < g.K) fetch(k0 + 16);   // next chunk in flight during the FMAs
+        if (k0 + 16 < kcount) fetch(k0 + 16);   // next chunk in flight during the FMAs
 #pragma unroll 4
         for (int k = 0; k < 16; k++) {
             const v2d a[2] = {sa[w][2 * lm][k], sa[w][2 * lm + 1][k]};
@@ -622,12 +707,12 @@ template <int W>
 __global__ void __launch_bounds__(kInterpThreads) k_g_interp(int3 ng, int3 nb, const int* __restrict__ start,
                                                              const int4* __restrict__ g0s,
                                                              const double4* __restrict__ srec, double beta,
-                                                             double3 gscale, const double* __restrict__ G,
-                                                             double* __restrict__ t_part) {
+                                                             double3 gscale, const double* __restrict__ G, int lo,
+                                                             double* __restrict__ dedq, double* __restrict__ f_part) {
     constexpr int R = 7 + W;
     constexpr int NJ = (W + 3) / 4;
     extern __shared__ double sg[];   // [R][R][R]
-    const int tile = xcd_block();   // neighbouring tiles (shared halo) on one XCD's L2
+    const int tile = blockIdx.x;
     const int s0 = start[tile], s1 = start[tile + 1];
     if (s0 == s1) return;
     const int tz = tile % nb.z, ty = (tile / nb.z) % nb.y, tx = tile / (nb.z * nb.y);
@@ -696,12 +781,12 @@ __global__ void __launch_bounds__(kInterpThreads) k_g_interp(int3 ng, int3 nb, c
             pv += __shfl_xor(pv, off); px += __shfl_xor(px, off);
             py += __shfl_xor(py, off); pz += __shfl_xor(pz, off);
         }
-        if (lane == 0) {
-            double* o = t_part + (size_t)g.w * 4;
-            o[0] = pv;
-            o[1] = -sr.w * gscale.x * px;
-            o[2] = -sr.w * gscale.y * py;
-            o[3] = -sr.w * gscale.z * pz;
+        if (lane == 0) {   // each owned atom is in exactly one bin: no other writer
+            const int i = lo + g.w;
+            dedq[i] += pv;
+            f_part[3 * i] += -sr.w * gscale.x * px;
+            f_part[3 * i + 1] += -sr.w * gscale.y * py;
+            f_part[3 * i + 2] += -sr.w * gscale.z * pz;
         }
     }
 }
@@ -802,12 +887,12 @@ void launch_grid_sort(Handle& h, const double* pos) {
     const int nown = h.hi - h.lo;
     const int3 ng = make_int3(p.ng[0], p.ng[1], p.ng[2]), nb = make_int3(p.nb[0], p.nb[1], p.nb[2]);
     const double3 L = make_double3(h.box_L[0], h.box_L[1], h.box_L[2]);
-    check_hip(hipMemsetAsync(h.g_cnt, 0, sizeof(int) * p.nbins, h.stream), "memset bins");
+    // g_cnt is zero here: cleared at cf_create and by k_g_scatter of the previous evaluation
     hipLaunchKernelGGL(k_g_bin, dim3(nblk(nown, 256)), dim3(256), 0, h.stream, h.lo, nown, pos, h.q, L, ng, p.W,
-                       nb, h.g_srec, h.g_g0u, h.g_rank, h.g_cnt);
+                       nb, h.g_srec, h.g_g0u, h.g_rank, h.g_cnt, h.g_xrange);
     hipLaunchKernelGGL(k_g_scan, dim3(1), dim3(kGScan), 0, h.stream, p.nbins, h.g_cnt, h.g_start);
     hipLaunchKernelGGL(k_g_scatter, dim3(nblk(nown, 256)), dim3(256), 0, h.stream, nown, h.g_g0u, h.g_rank, h.g_start,
-                       h.g_tmp);
+                       h.g_tmp, p.nbins, h.g_cnt);
     hipLaunchKernelGGL(k_g_order, dim3(nblk(p.nbins, 4)), dim3(256), 0, h.stream, p.nbins, h.g_start, h.g_tmp,
                        h.g_order);
     hipLaunchKernelGGL(k_g_taps, dim3(nblk((int64_t)nown * (kTapStride / 2), 256)), dim3(256), 0, h.stream, nown, p.W, p.beta,
@@ -839,14 +924,17 @@ void launch_grid_spread(Handle& h) {
     // tile instead of 27)
     if (p.W <= 9)
         hipLaunchKernelGGL(k_g_spread<2>, dim3(nblocks), dim3(512), sizeof(double) * 2 * kSpreadCap * kTapStride,
-                           h.stream, ng, nb, h.g_start, h.g_taps, h.g_grid);
+                           h.stream, ng, nb, h.g_start, h.g_taps, h.g_grid, h.g_xrange, p.W);
     else
         hipLaunchKernelGGL(k_g_spread<3>, dim3(nblocks), dim3(512), sizeof(double) * 2 * kSpreadCap * kTapStride,
-                           h.stream, ng, nb, h.g_start, h.g_taps, h.g_grid);
+                           h.stream, ng, nb, h.g_start, h.g_taps, h.g_grid, h.g_xrange, p.W);
 }
 
 template <bool BREAL, bool CREAL>
-static void zgemm(Handle& h, const ZGemm& g) {
+static void zgemm(Handle& h, ZGemm g, int xdim = 0, int xdiv = 1) {
+    if (h.g_xrange && xdim) {
+        g.xdim = xdim; g.xdiv = xdiv; g.xr = h.g_xrange; g.W = h.gp.W; g.ngx = h.gp.ng[0];
+    }
     const int tiles = ((g.M + 15) / 16) * ((g.N + 15) / 16);
     hipLaunchKernelGGL((k_g_zgemm<BREAL, CREAL>), dim3(nblk(tiles, 4)), dim3(256), 0, h.stream, g);
 }
@@ -857,12 +945,14 @@ void launch_grid_dft_fwd(Handle& h) {
     const long NYKZ = (long)NY * KZ;
     const double2* tzh = h.g_tw[2] + (size_t)(KZ - 1) * ngz;   // e^{i th nz z}, nz >= 0
     // z (real rows -> half spectrum): t1[row][nz] = sum_z grid[row][z] Tz[nz][z]
-    zgemm<true, false>(h, ZGemm{KZ, ngx * ngy, ngz, ngx * ngy, tzh, ngz, 1, h.g_grid, 1, ngz, 0, h.g_t1, 1, KZ, 0, 1});
+    zgemm<true, false>(h, ZGemm{KZ, ngx * ngy, ngz, ngx * ngy, tzh, ngz, 1, h.g_grid, 1, ngz, 0, h.g_t1, 1, KZ, 0, 1}, 2,
+                       ngy);
     // y: t2[o][ny][i] = sum_y Ty[ny][y] t1[o][y][i]
     zgemm<false, false>(h, ZGemm{NY, ngx * KZ, ngy, KZ, h.g_tw[1], ngy, 1, h.g_t1, KZ, 1, (long)ngy * KZ, h.g_t2, KZ, 1,
-                                 NYKZ, 0});
+                                 NYKZ, 0}, 2, KZ);
     // x: b[nx][r] = sum_x Tx[nx][x] t2[x][r]
-    zgemm<false, false>(h, ZGemm{NX, (int)NYKZ, ngx, (int)NYKZ, h.g_tw[0], ngx, 1, h.g_t2, NYKZ, 1, 0, h.g_b, NYKZ, 1, 0, 0});
+    zgemm<false, false>(h, ZGemm{NX, (int)NYKZ, ngx, (int)NYKZ, h.g_tw[0], ngx, 1, h.g_t2, NYKZ, 1, 0, h.g_b, NYKZ, 1, 0, 0},
+                        3);
 }
 
 double* grid_reduce_buffer(Handle& h, int64_t* count) {
@@ -887,12 +977,14 @@ void launch_grid_dft_inv(Handle& h) {
     const long NYKZ = (long)NY * KZ;
     const double2* tzh = h.g_tw[2] + (size_t)(KZ - 1) * ngz;
     // x: t2[x][r] = sum_nx Tx[nx][x] f[nx][r]
-    zgemm<false, false>(h, ZGemm{ngx, (int)NYKZ, NX, (int)NYKZ, h.g_tw[0], 1, ngx, h.g_b, NYKZ, 1, 0, h.g_t2, NYKZ, 1, 0, 0});
+    zgemm<false, false>(h, ZGemm{ngx, (int)NYKZ, NX, (int)NYKZ, h.g_tw[0], 1, ngx, h.g_b, NYKZ, 1, 0, h.g_t2, NYKZ, 1, 0, 0},
+                        1);
     // y: t1[o][y][i] = sum_ny Ty[ny][y] t2[o][ny][i]
     zgemm<false, false>(h, ZGemm{ngy, ngx * KZ, NY, KZ, h.g_tw[1], 1, ngy, h.g_t2, KZ, 1, NYKZ, h.g_t1, KZ, 1,
-                                 (long)ngy * KZ, 0});
+                                 (long)ngy * KZ, 0}, 2, KZ);
     // z (half spectrum -> real rows): grid[row][z] = Re sum_nz Tz[nz][z] t1[row][nz]
-    zgemm<false, true>(h, ZGemm{ngz, ngx * ngy, KZ, ngx * ngy, tzh, 1, ngz, h.g_t1, 1, KZ, 0, h.g_grid, 1, ngz, 0, 1});
+    zgemm<false, true>(h, ZGemm{ngz, ngx * ngy, KZ, ngx * ngy, tzh, 1, ngz, h.g_t1, 1, KZ, 0, h.g_grid, 1, ngz, 0, 1}, 2,
+                       ngy);
 }
 
 void launch_grid_interp(Handle& h) {
@@ -903,8 +995,7 @@ void launch_grid_interp(Handle& h) {
     const size_t lds = R * R * R * sizeof(double);
 #define CF_INTERP(W_)                                                                                               \
     hipLaunchKernelGGL(k_g_interp<W_>, dim3(p.nbins), dim3(kInterpThreads), lds, h.stream, ng, nb, h.g_start,       \
-                       h.g_g0s, h.g_srec,                                                                        \
-                       p.beta, gs, h.g_grid, h.t_part)
+                       h.g_g0s, h.g_srec, p.beta, gs, h.g_grid, h.lo, h.dedq, h.f_part)
     CF_GRID_W_DISPATCH(p.W, CF_INTERP)
 #undef CF_INTERP
 }

@@ -123,29 +123,43 @@ def test_grid_device_api_deterministic():
     assert outs[0][0] == e_h and np.array_equal(outs[0][1], f_h)
 
 
-def test_grid_two_rank_decomposition_on_one_gpu():
+@pytest.mark.parametrize("world,shuffled", [(2, False), (4, False), (8, False), (4, True)])
+def test_grid_multi_rank_decomposition_on_one_gpu(world, shuffled):
+    # W ranks of an atom decomposition driven on one GPU (the all-reduce done by hand): each
+    # rank spreads / transforms only the grid x-planes its atoms reach.  Contiguous ranks of
+    # the lattice-ordered box are x-slabs (rank 0's straddles the periodic boundary: its H
+    # atoms wrap to x ~ L); shuffled molecules make every rank span the box (full range).
     system, force, pos, box = ts.water_box(2400, cutoff=1.0, ewald_tol=1e-4, every_bond_angle=4)
+    if shuffled:   # permute molecule positions within each topology class
+        rng = np.random.default_rng(11)
+        w = pos.reshape(-1, 3, 3).copy()
+        kinds = np.arange(len(w)) % 4 == 3
+        for cls in (kinds, ~kinds):
+            ids = np.flatnonzero(cls)
+            w[ids] = w[rng.permutation(ids)]
+        pos = w.reshape(-1, 3)
     stream = torch.cuda.current_stream().cuda_stream
     pt = torch.tensor(pos, dtype=torch.float64, device="cuda")
     single = HipCalcCoulForceKernel(stream=stream, kspace_algo=GRID).initialize(system, force)
     e1, f1 = single.execute_host(pos, box)
-    ks = [HipCalcCoulForceKernel(stream=stream, rank=r, world_size=2, kspace_algo=GRID).initialize(system, force)
-          for r in range(2)]
-    for k in ks:
-        k.begin(pt, box, True, True)
-    bufs = [device_buffer_as_tensor(*k.kspace_buffer(), "cuda") for k in ks]
-    total = bufs[0] + bufs[1]
-    for b in bufs:
-        b.copy_(total)
-    f = torch.zeros_like(pt)
-    es = []
-    for k in ks:
-        e = torch.zeros(1, dtype=torch.float64, device="cuda")
-        k.end(f, e)
-        es.append(e)
-    torch.cuda.synchronize()
-    assert (es[0] + es[1]).item() == pytest.approx(e1, rel=1e-11)
-    assert np.abs(f.cpu().numpy() - f1).max() < 1e-8
+    ks = [HipCalcCoulForceKernel(stream=stream, rank=r, world_size=world, kspace_algo=GRID).initialize(system, force)
+          for r in range(world)]
+    for step in range(2):   # the second evaluation checks that the x-slab state re-arms
+        for k in ks:
+            k.begin(pt, box, True, True)
+        bufs = [device_buffer_as_tensor(*k.kspace_buffer(), "cuda") for k in ks]
+        total = sum(bufs[1:], bufs[0].clone())
+        for b in bufs:
+            b.copy_(total)
+        f = torch.zeros_like(pt)
+        es = []
+        for k in ks:
+            e = torch.zeros(1, dtype=torch.float64, device="cuda")
+            k.end(f, e)
+            es.append(e)
+        torch.cuda.synchronize()
+        assert sum(x.item() for x in es) == pytest.approx(e1, rel=1e-11)
+        assert np.abs(f.cpu().numpy() - f1).max() < 1e-8
 
 
 def test_grid_c3_matches_exact_mfma_path():

@@ -24,10 +24,10 @@ from openmmcoul import testsystems as ts  # noqa: E402
 from openmmcoul.distributed import ShardedCoulKernel  # noqa: E402
 
 
-def probe(system, force, pos_np, box, world, steps, skin):
+def probe(system, force, pos_np, box, world, steps, skin, algo=2):
     dev = torch.device("cuda", 0)
     stream = torch.cuda.current_stream(dev).cuda_stream
-    k = HipCalcCoulForceKernel(device=0, stream=stream, rank=0, world_size=world).initialize(system, force)
+    k = HipCalcCoulForceKernel(device=0, stream=stream, rank=0, world_size=world, kspace_algo=algo).initialize(system, force)
     if skin > 0:
         k.set_neighbor_skin(skin)
     kern = ShardedCoulKernel(system, force, dev, kernel=k)
@@ -79,10 +79,11 @@ def main():
     ap.add_argument("--steps", type=int, default=40)
     ap.add_argument("--config", default="C3")
     ap.add_argument("--neighbor-skin", type=float, default=0.1)
+    ap.add_argument("--kspace-algo", type=int, default=2)
     args = ap.parse_args()
     system, force, pos_np, box = ts.make(args.config)
     for w in args.worlds:
-        print(json.dumps(probe(system, force, pos_np, box, w, args.steps, args.neighbor_skin)), flush=True)
+        print(json.dumps(probe(system, force, pos_np, box, w, args.steps, args.neighbor_skin, args.kspace_algo)), flush=True)
 
 
 if __name__ == "__main__":
