@@ -240,6 +240,7 @@ def main():
     timing = kern.kernel.timing()
     builds1, evals1 = kern.kernel.neighbor_stats()
     kern.kernel.set_timing(False)
+    kern.synchronize()   # energy all-reduce still in flight (multi-rank)
     e_final = energy.item()
     ms_step = elapsed / args.steps * 1e3
     ns_day = 86.4 / ms_step * (dt / 0.001)

@@ -49,7 +49,13 @@ class ShardedCoulKernel:
             self.device = torch.device(device) if not isinstance(device, torch.device) else device
         self.kernel = kernel
         self.lo, self.hi = self.kernel.owned_range()
-        self.energy = torch.zeros(1, dtype=torch.float64, device=self.device)
+        # two energy buffers: the scalar all-reduce of one evaluation is left in flight (the
+        # compute stream does not wait for it) and completed before its buffer is reused, or
+        # when the caller asks for the value (energy_value / synchronize)
+        self._ebufs = [torch.zeros(1, dtype=torch.float64, device=self.device) for _ in range(2)]
+        self._ework = [None, None]
+        self._ecur = 0
+        self.energy = self._ebufs[0]
         self._sbuf = self.kernel.kspace_tensor(self.device)
         self._gidx = None
         if self.world > 1:
@@ -75,10 +81,26 @@ class ShardedCoulKernel:
             if hasattr(k, "direct"):
                 k.direct()
             work.wait()
+        i = self._ecur = 1 - self._ecur
+        if self._ework[i] is not None:
+            self._ework[i].wait()
+            self._ework[i] = None
+        self.energy = self._ebufs[i]
         k.end(forces, self.energy)
         if self.world > 1 and include_energy:
-            dist.all_reduce(self.energy, op=dist.ReduceOp.SUM, group=self.group)
+            self._ework[i] = dist.all_reduce(self.energy, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
         return self.energy
+
+    def synchronize(self):
+        """Complete the energy reductions still in flight (before reading an energy)."""
+        for i, w in enumerate(self._ework):
+            if w is not None:
+                w.wait()
+                self._ework[i] = None
+
+    def energy_value(self) -> float:
+        self.synchronize()
+        return self.energy.item()
 
     def replicate_positions(self, positions: torch.Tensor):
         """After each rank updated positions[lo:hi], make every rank's copy identical

@@ -100,6 +100,11 @@ def _worker(rank, world, port, pos, q, box, ranges, out):
     p = torch.tensor(pos)
     f = torch.zeros_like(p)
     e = kern.execute(p, box, f, include_energy=True)
+    e = kern.energy_value()   # the energy all-reduce is left in flight by execute
+    # a second evaluation uses the other energy buffer; the first value must be untouched
+    f2 = torch.zeros_like(p)
+    kern.execute(p, box, f2, include_energy=True)
+    assert kern.energy_value() == e and torch.equal(f2, f)
     # owned forces -> gather all ranks' owned slices through the position re-replication path
     full = kern.replicate_positions(f.clone())
     # a rank moves only its owned atoms; replication must make every copy identical
