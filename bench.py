@@ -250,7 +250,7 @@ def main():
         per_launch[dom] = timing[dom][0] / timing[dom][1]   # measured inside the timed region
     n_own = hi - lo
     # algorithmic work per launch of each hot phase:
-    #  direct_pairs  HBM bytes 4 P_c + 80 N (half list + per-atom in/out), fp64 flops 80 P_c
+    #  direct_pairs  (k_pairs alone) HBM bytes 4 P_c + 80 N (half list + per-atom in/out), fp64 flops 80 P_c
     #  grid_spread   2 N W^3 flops (one FMA per atom x grid point of its support)
     #  grid_interp   4 N W^3 flops (two FMAs per grid value: potential and x-gradient sums)
     #  kspace_sfac / kspace_force (exact path)  4 / 8 flops per atom x half-space k-vector

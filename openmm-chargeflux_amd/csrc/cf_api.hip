@@ -23,11 +23,11 @@
 // recorded on the handle's stream around every launch, so bench.py can report kernel
 // durations measured on the stream the kernels actually run on.
 enum Phase { PH_FLUX, PH_PREP, PH_CELLS, PH_NLIST, PH_TABLES, PH_SFAC, PH_COEFFS, PH_FORCE, PH_DIRECT,
-             PH_ASSEMBLE, PH_ENERGY, PH_GSORT, PH_GSPREAD, PH_GDFTF, PH_GDFTI, PH_GINTERP, PH_COUNT };
+             PH_ASSEMBLE, PH_ENERGY, PH_GSORT, PH_GSPREAD, PH_GDFTF, PH_GDFTI, PH_GINTERP, PH_EXCL, PH_COUNT };
 static const char* kPhaseNames[PH_COUNT] = {"flux_terms", "atoms_prep", "cell_sort", "neighbor_list",
                                             "kspace_tables", "kspace_sfac", "kspace_coeffs", "kspace_force",
                                             "direct_pairs", "assemble", "energy", "grid_sort", "grid_spread",
-                                            "grid_dft_fwd", "grid_dft_inv", "grid_interp"};
+                                            "grid_dft_fwd", "grid_dft_inv", "grid_interp", "direct_excl"};
 constexpr int kMaxTimed = 8192;
 
 struct cf_handle {
@@ -803,9 +803,13 @@ static void run_direct(cf_handle* H) {
     if (h.hi <= h.lo) return;
     const int flags = h.pending_flags;
     const int forces = flags & CF_INCLUDE_FORCES, energy = flags & CF_INCLUDE_ENERGY;
-    Timed t(H, PH_DIRECT);
-    if (h.pbc) cf::launch_direct(h, H->pos_pending, forces);
-    else cf::launch_nopbc(h, H->pos_pending, forces, energy);
+    if (h.pbc) {
+        { Timed t(H, PH_DIRECT); cf::launch_direct(h, H->pos_pending, forces); }
+        { Timed t(H, PH_EXCL); cf::launch_direct_finish(h, H->pos_pending, forces); }
+    } else {
+        Timed t(H, PH_DIRECT);
+        cf::launch_nopbc(h, H->pos_pending, forces, energy);
+    }
 }
 
 CF_EXPORT int cf_compute_direct(cf_handle* H) {

@@ -206,7 +206,8 @@ void launch_cell_sort(Handle& h, const double* pos);
 void launch_skin_check(Handle& h, const double* pos);   // skin_flag = some atom moved > list_skin/2
 void launch_force_rebuild(Handle& h);                   // skin_flag = 1
 void launch_nlist(Handle& h, const double* pos);
-void launch_direct(Handle& h, const double* pos, int include_forces);
+void launch_direct(Handle& h, const double* pos, int include_forces);          // the pair kernel
+void launch_direct_finish(Handle& h, const double* pos, int include_forces);   // overflow rescan + exclusions
 void launch_recip_add(Handle& h);   // dedq, f_part += reciprocal partials
 void launch_nopbc(Handle& h, const double* pos, int include_forces, int include_energy);
 void launch_assemble(Handle& h, double* forces_out);

@@ -1370,6 +1370,11 @@ void launch_direct(Handle& h, const double* pos, int include_forces) {
         if (ty) hipLaunchKernelGGL((k_pairs<16, true>), dim3(nblk((int64_t)a.nlr * 16, 256)), dim3(256), 0, h.stream, a);
         else hipLaunchKernelGGL((k_pairs<16, false>), dim3(nblk((int64_t)a.nlr * 16, 256)), dim3(256), 0, h.stream, a);
     }
+}
+
+// overflowed atoms' rescan + the exclusion correction (after launch_direct)
+void launch_direct_finish(Handle& h, const double* pos, int include_forces) {
+    DirectArgs a = direct_args(h, pos, include_forces);
     hipLaunchKernelGGL(k_pairs_overflow, dim3(nblk(a.nlr, 256)), dim3(256), 0, h.stream, a);
     hipLaunchKernelGGL(k_excl, dim3(nblk(a.nlr, 256)), dim3(256), 0, h.stream, a);
 }

@@ -235,7 +235,7 @@ class HipCalcCoulForceKernel:
     # phase names in cf_get_timing order (bit p of cf_set_timing_mask)
     PHASES = ("flux_terms", "atoms_prep", "cell_sort", "neighbor_list", "kspace_tables", "kspace_sfac",
               "kspace_coeffs", "kspace_force", "direct_pairs", "assemble", "energy", "grid_sort", "grid_spread",
-              "grid_dft_fwd", "grid_dft_inv", "grid_interp")
+              "grid_dft_fwd", "grid_dft_inv", "grid_interp", "direct_excl")
 
     def set_timing(self, enable=True, phases=None):
         """Per-kernel HIP-event timing of every phase, or only of the named phases."""
