@@ -521,32 +521,39 @@ __global__ void __launch_bounds__(256) k_g_dftz_inv(int rows, int ngz, int KZ, c
         if (r0 + r < nrows) grid[(size_t)(row0 + r0 + r) * ngz + z] = acc[r];
 }
 
-// Every pruned-DFT stage as one batched complex GEMM on 16x16 wave tiles:
+// Every pruned-DFT stage as one batched complex GEMM on the fp64 matrix cores:
 //   C[m][n] = sum_k A[m][k] B[k][n],  A = twiddles (complex), B complex or real, C complex or
 //   its real part.  n is split as (n1, n0) = (n / nin, n % nin) so a batch index can be folded
-//   into n.  Each wave stages 16-deep k-chunks of its A and B tiles in its own LDS (no
-//   workgroup barrier); lane (lm, ln) owns the 2x2 outputs (2lm.., 2ln..): 4 ds_read_b128
-//   feed 16 FMAs per k.
+//   into n.  One 16x16 output tile per wave, v_mfma_f64_16x16x4_f64 on four k per step:
+//   lane l supplies A[m0 + (l & 15)][k0 + (l >> 4)] and B[k0 + (l >> 4)][n0 + (l & 15)]
+//   straight from global memory (no LDS; the twiddles and B rows are L2-resident), the next
+//   step's operands in flight during the current step's MFMAs.  Complex products as real
+//   MFMAs: re += Ar Br + (-Ai) Bi, im += Ar Bi + Ai Br (2 MFMAs when B or C is real).
+//   Accumulator layout (CDNA4 f64 MFMA): register r of lane l is C[(l >> 4) + 4r][l & 15].
 struct ZGemm {
     int M, N, K, nin;
     const double2* A; long sam, sak;
     const void* B; long sbk, sb0, sb1;
     void* C; long scm, sc0, sc1;
-    int b_kfast;   // B is contiguous along k (load lanes walk k first)
+    int b_kfast;   // (unused by the MFMA kernel; kept for the call sites' layout notes)
     // x-slab (multi-rank): which index is the grid x-plane -- 0 none, 1 m, 2 n / xdiv, 3 k.
-    // Tiles whose x-planes lie outside the slab are skipped; along k they contribute zero.
+    // Tiles whose x-planes lie outside the slab are skipped; along k only the slab is walked.
     int xdim = 0, xdiv = 1;
     const int* xr = nullptr;
     int W = 0, ngx = 0;
 };
 
+typedef double d4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ d4 mfma64(double a, double b, d4 c) {
+    return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+}
+
 template <bool BREAL, bool CREAL>
 __global__ void __launch_bounds__(256) k_g_zgemm(ZGemm g) {
-    __shared__ v2d sa[4][16][17];   // [wave][m][k] (+1 pad: conflict-free column reads)
-    __shared__ v2d sb[4][16][17];   // [wave][n][k]
-    const int lane = threadIdx.x & 63, w = wave_id();
+    const int lane = threadIdx.x & 63;
     const int tiles_m = (g.M + 15) >> 4;
-    const int tile = blockIdx.x * 4 + w;
+    const int tile = blockIdx.x * 4 + wave_id();
     const int tm = tile % tiles_m, tn = tile / tiles_m;
     if (tn * 16 >= g.N) return;
     const int m0 = tm * 16, n0 = tn * 16;
@@ -559,102 +566,77 @@ __global__ void __launch_bounds__(256) k_g_zgemm(ZGemm g) {
         slab_of(g.xr, g.W, g.ngx, s0, len);
         if (len < g.K) { kbase = s0; kcount = len; }
     }
-    const int lm = lane >> 3, ln = lane & 7;
-    // load roles (fixed over k): element e = lane + 64q of the 16x16 chunk
-    const int ak = lane & 15;   // A: k fastest
-    long aoff[4];
-    bool aok[4];
-    long boff[4];
-    bool bok[4];
-    int bkk[4], bnn[4];
-#pragma unroll
-    for (int q = 0; q < 4; q++) {
-        const int mm = (lane >> 4) + 4 * q;
-        aok[q] = m0 + mm < g.M;
-        aoff[q] = (long)(aok[q] ? m0 + mm : 0) * g.sam;
-        bkk[q] = g.b_kfast ? (lane & 15) : (lane >> 4) + 4 * q;
-        bnn[q] = g.b_kfast ? (lane >> 4) + 4 * q : (lane & 15);
-        const int n = n0 + bnn[q];
-        bok[q] = n < g.N;
-        const int nn = bok[q] ? n : 0;
-        boff[q] = (long)(nn / g.nin) * g.sb1 + (long)(nn % g.nin) * g.sb0;
-    }
-    v2d c[2][2];
-#pragma unroll
-    for (int p = 0; p < 2; p++)
-#pragma unroll
-        for (int q = 0; q < 2; q++) c[p][q] = v2d{0.0, 0.0};
-    v2d ra[4], rb[4];
-    auto fetch = [&](int k0) {
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-            int ka = k0 + ak;
-            ra[q] = v2d{0.0, 0.0};
-            if (aok[q] && ka < kcount) {
-                ka += kbase;
-                ka -= ka >= g.K ? g.K : 0;
-                const double2 t = g.A[aoff[q] + (long)ka * g.sak];
-                ra[q] = v2d{t.x, t.y};
+    const int r = lane & 15, kq = lane >> 4;
+    const int m = m0 + r, n = n0 + r;
+    const bool aok = m < g.M, bok = n < g.N;
+    const double2* Ap = g.A + (long)(aok ? m : 0) * g.sam;
+    const int nn = bok ? n : 0;
+    const long boff = (long)(nn / g.nin) * g.sb1 + (long)(nn % g.nin) * g.sb0;
+    // operands of step t: k = kbase + t + kq (mod K); zero beyond kcount / outside the tile
+    auto load = [&](int t, double& ar, double& ai, double& br, double& bi) {
+        int k = t + kq;
+        ar = ai = br = bi = 0.0;
+        if (k < kcount) {
+            k += kbase;
+            k -= k >= g.K ? g.K : 0;
+            if (aok) {
+                const double2 v = Ap[(long)k * g.sak];
+                ar = v.x; ai = v.y;
             }
-            int kb = k0 + bkk[q];
-            rb[q] = v2d{0.0, 0.0};
-            // out-of-slab planes of B were never written this evaluation (stale, possibly NaN):
-            // never read
-            if (bok[q] && kb < kcount) {
-                kb += kbase;
-                kb -= kb >= g.K ? g.K : 0;
-                const long off = boff[q] + (long)kb * g.sbk;
+            if (bok) {
                 if (BREAL) {
-                    rb[q] = v2d{reinterpret_cast<const double*>(g.B)[off], 0.0};
+                    br = reinterpret_cast<const double*>(g.B)[boff + (long)k * g.sbk];
                 } else {
-                    const double2 t = reinterpret_cast<const double2*>(g.B)[off];
-                    rb[q] = v2d{t.x, t.y};
+                    const double2 v = reinterpret_cast<const double2*>(g.B)[boff + (long)k * g.sbk];
+                    br = v.x; bi = v.y;
                 }
             }
         }
     };
-    fetch(0);
-    for (int k0 = 0; k0 < kcount; k0 += 16) {
+    // groups of kG steps (4 k each): a group's operands are loaded together while the previous
+    // group's MFMAs issue.  Measured at C3: kG = 1 and the former VALU/LDS kernel take the same
+    // time per stage (11-23 us), kG = 4 is 15% slower (94 VGPRs): the stages are bound by the
+    // strided operand fetch (16 cache lines per load instruction), not by MFMA issue
+    constexpr int kG = 1;
+    d4 cre = {0.0, 0.0, 0.0, 0.0}, cim = {0.0, 0.0, 0.0, 0.0};
+    double ar[kG], ai[kG], br[kG], bi[kG];
 #pragma unroll
-        for (int q = 0; q < 4; q++) {
-            sa[w][(lane >> 4) + 4 * q][ak] = ra[q];
-            sb[w][bnn[q]][bkk[q]] = rb[q];
+    for (int j = 0; j < kG; j++) load(4 * j, ar[j], ai[j], br[j], bi[j]);
+    for (int t = 0; t < kcount; t += 4 * kG) {
+        double nar[kG], nai[kG], nbr[kG], nbi[kG];
+        const bool more = t + 4 * kG < kcount;
+#pragma unroll
+        for (int j = 0; j < kG; j++) {
+            nar[j] = nai[j] = nbr[j] = nbi[j] = 0.0;
+            if (more) load(t + 4 * kG + 4 * j, nar[j], nai[j], nbr[j], nbi[j]);
         }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        if (k0 + 16 < kcount) fetch(k0 + 16);   // next chunk in flight during the FMAs
-#pragma unroll 4
-        for (int k = 0; k < 16; k++) {
-            const v2d a[2] = {sa[w][2 * lm][k], sa[w][2 * lm + 1][k]};
-            const v2d b[2] = {sb[w][2 * ln][k], sb[w][2 * ln + 1][k]};
 #pragma unroll
-            for (int p = 0; p < 2; p++)
-#pragma unroll
-                for (int q = 0; q < 2; q++) {
-                    if (BREAL) {
-                        c[p][q].x += a[p].x * b[q].x;
-                        c[p][q].y += a[p].y * b[q].x;
-                    } else {
-                        c[p][q].x += a[p].x * b[q].x - a[p].y * b[q].y;
-                        if (!CREAL) c[p][q].y += a[p].x * b[q].y + a[p].y * b[q].x;
-                    }
+        for (int j = 0; j < kG; j++) {
+            if (BREAL) {
+                cre = mfma64(ar[j], br[j], cre);
+                cim = mfma64(ai[j], br[j], cim);
+            } else {
+                cre = mfma64(ar[j], br[j], cre);
+                cre = mfma64(-ai[j], bi[j], cre);
+                if (!CREAL) {
+                    cim = mfma64(ar[j], bi[j], cim);
+                    cim = mfma64(ai[j], br[j], cim);
                 }
+            }
         }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+        for (int j = 0; j < kG; j++) { ar[j] = nar[j]; ai[j] = nai[j]; br[j] = nbr[j]; bi[j] = nbi[j]; }
     }
+    if (!bok) return;
+    const long coff = (long)(n / g.nin) * g.sc1 + (long)(n % g.nin) * g.sc0;
 #pragma unroll
-    for (int p = 0; p < 2; p++)
-#pragma unroll
-        for (int q = 0; q < 2; q++) {
-            const int m = m0 + 2 * lm + p, n = n0 + 2 * ln + q;
-            if (m >= g.M || n >= g.N) continue;
-            const long off = (long)m * g.scm + (long)(n / g.nin) * g.sc1 + (long)(n % g.nin) * g.sc0;
-            if (CREAL) reinterpret_cast<double*>(g.C)[off] = c[p][q].x;
-            else reinterpret_cast<double2*>(g.C)[off] = make_double2(c[p][q].x, c[p][q].y);
-        }
+    for (int q = 0; q < 4; q++) {
+        const int mm = m0 + kq + 4 * q;
+        if (mm >= g.M) continue;
+        const long off = (long)mm * g.scm + coff;
+        if (CREAL) reinterpret_cast<double*>(g.C)[off] = cre[q];
+        else reinterpret_cast<double2*>(g.C)[off] = make_double2(cre[q], cim[q]);
+    }
 }
 
 // ---------------------------------------------------------------------------------
