@@ -270,24 +270,24 @@ __device__ __forceinline__ int wrapb(int b, int n) { return b < 0 ? b + n : (b >
 
 // NS = source bins per axis that reach a tile (3 for W <= 17, 2 for W <= 9); the 2x2x2-tile
 // block reads a window of NW = NS + 1 bins per axis, starting NS - 1 bins before the block
+// ws / wn: lane l of every wave holds (first slot, count) of bin l of the block's NW^3 window
+// ([col * NW + sz]), loaded once per block; a pass reads them with readlane (no memory access
+// on the pass-to-pass critical path)
 template <int NS>
-__device__ __forceinline__ void spread_column(SpreadPass& p, int3 nb, int BX, int BY, int BZ,
-                                              const int* __restrict__ start) {
+__device__ __forceinline__ void spread_column(SpreadPass& p, int ws, int wn) {
     constexpr int NW = NS + 1;
-    const int bx = wrapb(2 * BX - (NS - 1) + p.col / NW, nb.x), by = wrapb(2 * BY - (NS - 1) + p.col % NW, nb.y);
 #pragma unroll
     for (int sz = 0; sz < 4; sz++) {
         if (sz >= NW) { p.cs[sz] = 0; p.cn[sz] = 0; continue; }
-        const int b = (bx * nb.y + by) * nb.z + wrapb(2 * BZ - (NS - 1) + sz, nb.z);
-        p.cs[sz] = start[b];
-        p.cn[sz] = start[b + 1] - p.cs[sz];
+        const int l = __builtin_amdgcn_readfirstlane(p.col * NW + sz);
+        p.cs[sz] = __builtin_amdgcn_readlane(ws, l);
+        p.cn[sz] = __builtin_amdgcn_readlane(wn, l);
     }
 }
 
 // advance to the next non-empty pass; false when the columns are exhausted
 template <int NS>
-__device__ __forceinline__ bool spread_next(SpreadPass& p, int3 nb, int BX, int BY, int BZ,
-                                            const int* __restrict__ start) {
+__device__ __forceinline__ bool spread_next(SpreadPass& p, int ws, int wn) {
     constexpr int NCOL = (NS + 1) * (NS + 1);
     int tot = p.cn[0] + p.cn[1] + p.cn[2] + p.cn[3];
     if (p.col < NCOL && p.base + kSpreadCap < tot) {
@@ -295,7 +295,7 @@ __device__ __forceinline__ bool spread_next(SpreadPass& p, int3 nb, int BX, int 
     } else {
         do {
             if (++p.col >= NCOL) return false;
-            spread_column<NS>(p, nb, BX, BY, BZ, start);
+            spread_column<NS>(p, ws, wn);
             tot = p.cn[0] + p.cn[1] + p.cn[2] + p.cn[3];
         } while (tot == 0);
         p.base = 0;
@@ -347,10 +347,18 @@ __global__ void __launch_bounds__(512) k_g_spread(int3 ng, int3 nb, const int* _
     for (int i = 0; i < 8; i++)
 #pragma unroll
         for (int jj = 0; jj < 4; jj++) acc[i][jj] = 0.0;
+    int ws = 0, wn = 0;
+    if (lane < NW * NW * NW) {
+        const int col = lane / NW, sz = lane - NW * col;
+        const int bx = wrapb(2 * BX - (NS - 1) + col / NW, nb.x), by = wrapb(2 * BY - (NS - 1) + col % NW, nb.y);
+        const int b = (bx * nb.y + by) * nb.z + wrapb(2 * BZ - (NS - 1) + sz, nb.z);
+        ws = start[b];
+        wn = start[b + 1] - ws;
+    }
     SpreadPass p;
     p.col = -1; p.base = 0;
     p.cn[0] = p.cn[1] = p.cn[2] = p.cn[3] = 0;
-    bool have = spread_next<NS>(p, nb, BX, BY, BZ, start);
+    bool have = spread_next<NS>(p, ws, wn);
     v2d r[kSpreadU];
     int cur = 0;
     if (have) {
@@ -360,7 +368,7 @@ __global__ void __launch_bounds__(512) k_g_spread(int3 ng, int3 nb, const int* _
     __syncthreads();
     while (have) {
         SpreadPass pn = p;
-        const bool more = spread_next<NS>(pn, nb, BX, BY, BZ, start);
+        const bool more = spread_next<NS>(pn, ws, wn);
         if (more) spread_fetch(pn, taps, r);   // in flight during the compute below
         const double* buf = st + (size_t)cur * kSpreadCap * kTapStride;
         const int dbx = wx + (NS - 1) - p.col / NW, dby = wy + (NS - 1) - p.col % NW;
