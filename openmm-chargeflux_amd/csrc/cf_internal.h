@@ -239,6 +239,48 @@ void launch_grid_interp(Handle& h);
 
 void check_hip(hipError_t e, const char* what);
 
+// ---- fp64 math helpers shared by the pair and grid kernels -------------------------
+// 1/sqrt(r2): hardware v_rsq_f64 estimate (relative error 5.3e-8 on MI355X, tools/rsq_probe.hip)
+// + one Newton step -> 4.3e-15 relative (a second step would give 2.4e-16; the pair terms'
+// other roundings and the 1e-5 kJ/mol/nm force bar make it unnecessary)
+__device__ __forceinline__ double rsqrt_fp64(double r2) {
+    double y = __builtin_amdgcn_rsq(r2);
+    return y * fma(-0.5 * r2 * y, y, 1.5);
+}
+
+// d = a*b + c as one VOP3 v_fma_f64.  For a Horner step with a constant addend the compiler
+// otherwise emits v_mov_b64 (constant -> accumulator) + v_fmac_f64: one extra VALU op per step.
+__device__ __forceinline__ double fma3(double a, double b, double c) {
+    double d;
+    asm("v_fma_f64 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+    return d;
+}
+
+// e^y for y in [-700, 0] (no overflow / NaN handling needed there): y = k ln2 + r with
+// |r| <= ln2/2 (Cody-Waite split of ln2), e^r by its degree-12 Taylor polynomial (truncation
+// < 2e-16 relative), times 2^k.  17 VALU instructions against ~35 for the libm exp, whose
+// range checks and coefficient register copies this path does not need (fma3 keeps the
+// Horner steps with VGPR-held constants as single VOP3 FMAs).
+__device__ __forceinline__ double exp_nonpos(double y) {
+    const double k = rint(y * 1.4426950408889634);
+    double r = fma(-k, 6.93147180369123816490e-01, y);
+    r = fma(-k, 1.90821492927058770002e-10, r);
+    double p = 2.0876756987868098979e-09;
+    p = fma3(p, r, 2.5052108385441718775e-08);
+    p = fma3(p, r, 2.7557319223985890653e-07);
+    p = fma3(p, r, 2.7557319223985888276e-06);
+    p = fma3(p, r, 2.4801587301587301566e-05);
+    p = fma3(p, r, 1.9841269841269841253e-04);
+    p = fma3(p, r, 1.3888888888888888889e-03);
+    p = fma3(p, r, 8.3333333333333332177e-03);
+    p = fma3(p, r, 4.1666666666666664354e-02);
+    p = fma3(p, r, 1.6666666666666665741e-01);
+    p = fma(p, r, 0.5);
+    p = fma(p, r, 1.0);
+    p = fma(p, r, 1.0);
+    return ldexp(p, (int)k);
+}
+
 // Workgroups are dispatched round-robin over the 8 XCDs (block b -> XCD b % 8), each XCD with
 // its own L2.  This maps the blocks one XCD receives onto a contiguous 1/8 of the logical
 // block range, so cell-sorted atoms (spatially coherent) share that XCD's L2 with their

@@ -657,42 +657,9 @@ __global__ void __launch_bounds__(kWaveNL * kSeg) k_nlist_wave(DirectArgs a) {
     if (active) a.nl_cnt[(size_t)seg * a.nlr + c] = cnt;
 }
 
-// 1/sqrt(r2) to full fp64 accuracy: hardware v_rsq_f64 estimate + two Newton steps
-__device__ __forceinline__ double rsqrt_fp64(double r2) {
-    double y = __builtin_amdgcn_rsq(r2);
-    double h = 0.5 * r2;
-    y = y * fma(-h * y, y, 1.5);
-    y = y * fma(-h * y, y, 1.5);
-    return y;
-}
-
 struct PairAcc {
     double fx = 0, fy = 0, fz = 0, dq = 0, e = 0;
 };
-
-// e^y for y in [-700, 0] (no overflow / NaN handling needed there): y = k ln2 + r with
-// |r| <= ln2/2 (Cody-Waite split of ln2), e^r by its degree-12 Taylor polynomial (truncation
-// < 2e-16 relative), times 2^k.  17 VALU instructions against ~35 for the libm exp, whose
-// range checks and coefficient register copies this path does not need.
-__device__ __forceinline__ double exp_nonpos(double y) {
-    const double k = rint(y * 1.4426950408889634);
-    double r = fma(-k, 6.93147180369123816490e-01, y);
-    r = fma(-k, 1.90821492927058770002e-10, r);
-    double p = 2.0876756987868098979e-09;
-    p = fma(p, r, 2.5052108385441718775e-08);
-    p = fma(p, r, 2.7557319223985890653e-07);
-    p = fma(p, r, 2.7557319223985888276e-06);
-    p = fma(p, r, 2.4801587301587301566e-05);
-    p = fma(p, r, 1.9841269841269841253e-04);
-    p = fma(p, r, 1.3888888888888888889e-03);
-    p = fma(p, r, 8.3333333333333332177e-03);
-    p = fma(p, r, 4.1666666666666664354e-02);
-    p = fma(p, r, 1.6666666666666665741e-01);
-    p = fma(p, r, 0.5);
-    p = fma(p, r, 1.0);
-    p = fma(p, r, 1.0);
-    return ldexp(p, (int)k);
-}
 
 // erfc(x) = e^{-x^2} erfcx(x): erfcx from a piecewise degree-12 polynomial (interval table
 // in LDS, fitted at cf_create in long double, relative error ~4e-15 over [0, alpha*rc]),

@@ -35,21 +35,17 @@ typedef double v2d __attribute__((ext_vector_type(2)));
 // derived from it is scalar (the compiler treats threadIdx.x >> 6 as divergent)
 __device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
 
-__device__ __forceinline__ double readlane_d(double v, int lane) {
-    int2 p = *reinterpret_cast<int2*>(&v);
-    p.x = __builtin_amdgcn_readlane(p.x, lane);
-    p.y = __builtin_amdgcn_readlane(p.y, lane);
-    return *reinterpret_cast<double*>(&p);
-}
-
-// phi(t) and d/ds phi(g - s) (= -phi'(t)) at t = g - s; zero outside the open support
+// phi(t) and d/ds phi(g - s) (= -phi'(t)) at t = g - s; zero outside the open support.
+// sqrt(u) = u * rsqrt(u) and z / sqrt(u) = z * rsqrt(u) from one v_rsq_f64 + Newton step
+// (relative 4e-15), exp of the non-positive exponent by exp_nonpos: no sqrt, divide or libm
+// exp on the per-atom path.
 __device__ __forceinline__ void es_tap(double t, double hw_inv, double beta, double& v, double& dv) {
     const double z = t * hw_inv;
     const double u = 1.0 - z * z;
     if (u > 0.0) {
-        const double r = sqrt(u);
-        v = exp(beta * (r - 1.0));
-        dv = v * beta * z / r * hw_inv;
+        const double rs = rsqrt_fp64(u);
+        v = exp_nonpos(beta * (u * rs - 1.0));
+        dv = v * beta * z * rs * hw_inv;
     } else {
         v = 0.0;
         dv = 0.0;
@@ -59,7 +55,7 @@ __device__ __forceinline__ void es_tap(double t, double hw_inv, double beta, dou
 __device__ __forceinline__ double es_val(double t, double hw_inv, double beta) {
     const double z = t * hw_inv;
     const double u = 1.0 - z * z;
-    return u > 0.0 ? exp(beta * (sqrt(u) - 1.0)) : 0.0;
+    return u > 0.0 ? exp_nonpos(beta * (u * rsqrt_fp64(u) - 1.0)) : 0.0;
 }
 
 // ---------------------------------------------------------------------------------
@@ -702,6 +698,7 @@ __global__ void __launch_bounds__(kInterpThreads) k_g_interp(int3 ng, int3 nb, c
     constexpr int R = 7 + W;
     constexpr int NJ = (W + 3) / 4;
     extern __shared__ double sg[];   // [R][R][R]
+    __shared__ double2 xt[kInterpThreads / 64][16];   // per wave: the current atom's x taps (v, dv)
     const int tile = blockIdx.x;
     const int s0 = start[tile], s1 = start[tile + 1];
     if (s0 == s1) return;
@@ -712,14 +709,24 @@ __global__ void __launch_bounds__(kInterpThreads) k_g_interp(int3 ng, int3 nb, c
         const int c = threadIdx.x % R, r0 = threadIdx.x / R;
         int z = 8 * tz + c;
         z -= z >= ng.z ? ng.z : 0;
+        // every load of the staging issued before the first LDS store (one memory latency per
+        // block instead of one per group of 4 rows): the block's halo comes from L2 / MALL
+        constexpr int kRows = (R * R + RPP - 1) / RPP;
         if (r0 < RPP) {
-#pragma unroll 4
-            for (int row = r0; row < R * R; row += RPP) {
+            double gv[kRows];
+#pragma unroll
+            for (int q = 0; q < kRows; q++) {
+                const int row = min(r0 + q * RPP, R * R - 1);
                 const int a = row / R, b = row - a * R;
                 int x = 8 * tx + a, y = 8 * ty + b;
                 x -= x >= ng.x ? ng.x : 0;
                 y -= y >= ng.y ? ng.y : 0;
-                sg[row * R + c] = G[((size_t)x * ng.y + y) * ng.z + z];
+                gv[q] = G[((size_t)x * ng.y + y) * ng.z + z];
+            }
+#pragma unroll
+            for (int q = 0; q < kRows; q++) {
+                const int row = r0 + q * RPP;
+                if (row < R * R) sg[row * R + c] = gv[q];
             }
         }
     }
@@ -735,6 +742,12 @@ __global__ void __launch_bounds__(kInterpThreads) k_g_interp(int3 ng, int3 nb, c
         const double sd = d == 0 ? sr.x : (d == 1 ? sr.y : sr.z);
         double v = 0, dv = 0;
         if (d < 3 && m < W) es_tap(ceil(sd - 0.5 * W) + m - sd, 2.0 / W, beta, v, dv);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");   // previous atom's reads of xt done
+        __builtin_amdgcn_wave_barrier();
+        if (d == 0) xt[w][m] = make_double2(v, dv);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         const int rx = g.x & 7, ry = g.y & 7, rz = g.z & 7;
         const double zt = __shfl(v, 32 + k), dzt = __shfl(dv, 32 + k);
         double t0[NJ], t1[NJ];
@@ -744,7 +757,8 @@ __global__ void __launch_bounds__(kInterpThreads) k_g_interp(int3 ng, int3 nb, c
         const double* base = sg + (rx * R + ry) * R + rz + kk;
 #pragma unroll
         for (int i = 0; i < W; i++) {
-            const double xi = readlane_d(v, i), dxi = readlane_d(dv, i);
+            const double2 xv = xt[w][i];   // broadcast LDS read (was 4 v_readlane per i)
+            const double xi = xv.x, dxi = xv.y;
 #pragma unroll
             for (int jj = 0; jj < NJ; jj++) {
                 const int j = 4 * jj + jg;
