@@ -157,10 +157,15 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal of the multi-rank path on a one-GPU box (not a benchmark configuration):
+    # CF_BENCH_ONE_GPU=1 puts every rank on device 0, CF_BENCH_BACKEND=gloo replaces RCCL
+    if os.environ.get("CF_BENCH_ONE_GPU") == "1":
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        backend = os.environ.get("CF_BENCH_BACKEND", "nccl")
+        dist.init_process_group(backend, **({"device_id": dev} if backend == "nccl" else {}))
 
     t_setup = time.time()
     system, force, pos_np, box = ts.make(args.config)

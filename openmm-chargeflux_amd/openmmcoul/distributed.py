@@ -109,6 +109,9 @@ class ShardedCoulKernel:
             return positions
         p = positions.view(-1, 3)
         self._send[: self.hi - self.lo].copy_(p[self.lo:self.hi])
-        dist.all_gather_into_tensor(self._recv, self._send, group=self.group)
+        if dist.get_backend(self.group) == "gloo":   # gloo has no all_gather_into_tensor
+            dist.all_gather(list(self._recv.view(self.world, self._maxown, 3).unbind(0)), self._send, group=self.group)
+        else:
+            dist.all_gather_into_tensor(self._recv, self._send, group=self.group)
         torch.index_select(self._recv, 0, self._gidx, out=p)
         return positions
