@@ -61,7 +61,7 @@ class MDHarness:
         self.inv_m = inv_mass
         self.stream = C.c_void_p(stream)
 
-    def kick_drift(self, pos, vel, frc):
+    def kick_drift(self, pos, vel, frc):   # also zeroes frc[lo:hi] (its last reader in the step)
         rc = self.L.md_kick_drift(self.lo, self.hi, self.dt, pos.data_ptr(), vel.data_ptr(), frc.data_ptr(),
                                   self.inv_m.data_ptr(), self.stream)
         assert rc == 0
@@ -194,13 +194,12 @@ def main():
     ev = []
 
     def step(record):
-        md.kick_drift(pos, vel, frc)            # v += dt/2 f/m ; x += dt v  (owned atoms)
+        md.kick_drift(pos, vel, frc)            # v += dt/2 f/m ; x += dt v ; f = 0  (owned atoms)
         kern.replicate_positions(pos)
         if record:
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             a.record()
-        frc.zero_()
-        e = kern.execute(pos, box, frc, include_energy=True)
+        e = kern.execute(pos, box, frc, include_energy=True)   # forces ADDED into the zeroed frc
         if record:
             b.record()
             ev.append((a, b))

@@ -16,8 +16,10 @@
 
 namespace {
 
+// v += dt/2 f/m ; x += dt v for the owned atoms, and f = 0 (its last reader this step: the
+// next force evaluation adds into it, so the step needs no separate zeroing launch)
 __global__ void __launch_bounds__(256) k_kick_drift(int lo, int hi, double dt, double* __restrict__ x,
-                                                    double* __restrict__ v, const double* __restrict__ f,
+                                                    double* __restrict__ v, double* __restrict__ f,
                                                     const double* __restrict__ inv_m) {
     int i = lo + blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= hi) return;
@@ -27,6 +29,7 @@ __global__ void __launch_bounds__(256) k_kick_drift(int lo, int hi, double dt, d
         double vv = v[3 * i + d] + h * f[3 * i + d];
         v[3 * i + d] = vv;
         x[3 * i + d] += dt * vv;
+        f[3 * i + d] = 0.0;
     }
 }
 
@@ -68,7 +71,7 @@ inline int nblk(int n) { return (n + 255) / 256; }
 
 }  // namespace
 
-MD_EXPORT int md_kick_drift(int lo, int hi, double dt, double* x, double* v, const double* f, const double* inv_m,
+MD_EXPORT int md_kick_drift(int lo, int hi, double dt, double* x, double* v, double* f, const double* inv_m,
                             void* stream) {
     if (hi <= lo) return 0;
     hipLaunchKernelGGL(k_kick_drift, dim3(nblk(hi - lo)), dim3(256), 0, (hipStream_t)stream, lo, hi, dt, x, v, f,

@@ -123,8 +123,9 @@ def test_grid_device_api_deterministic():
     assert outs[0][0] == e_h and np.array_equal(outs[0][1], f_h)
 
 
-@pytest.mark.parametrize("world,shuffled", [(2, False), (4, False), (8, False), (4, True)])
-def test_grid_multi_rank_decomposition_on_one_gpu(world, shuffled):
+@pytest.mark.parametrize("world,shuffled,precision", [(2, False, "double"), (4, False, "double"), (8, False, "double"),
+                                                     (4, True, "double"), (4, False, "mixed")])
+def test_grid_multi_rank_decomposition_on_one_gpu(world, shuffled, precision):
     # W ranks of an atom decomposition driven on one GPU (the all-reduce done by hand): each
     # rank spreads / transforms only the grid x-planes its atoms reach.  Contiguous ranks of
     # the lattice-ordered box are x-slabs (rank 0's straddles the periodic boundary: its H
@@ -140,9 +141,10 @@ def test_grid_multi_rank_decomposition_on_one_gpu(world, shuffled):
         pos = w.reshape(-1, 3)
     stream = torch.cuda.current_stream().cuda_stream
     pt = torch.tensor(pos, dtype=torch.float64, device="cuda")
-    single = HipCalcCoulForceKernel(stream=stream, kspace_algo=GRID).initialize(system, force)
+    single = HipCalcCoulForceKernel(stream=stream, kspace_algo=GRID, precision=precision).initialize(system, force)
     e1, f1 = single.execute_host(pos, box)
-    ks = [HipCalcCoulForceKernel(stream=stream, rank=r, world_size=world, kspace_algo=GRID).initialize(system, force)
+    ks = [HipCalcCoulForceKernel(stream=stream, rank=r, world_size=world, kspace_algo=GRID,
+                                 precision=precision).initialize(system, force)
           for r in range(world)]
     for step in range(2):   # the second evaluation checks that the x-slab state re-arms
         for k in ks:
@@ -159,7 +161,10 @@ def test_grid_multi_rank_decomposition_on_one_gpu(world, shuffled):
             es.append(e)
         torch.cuda.synchronize()
         assert sum(x.item() for x in es) == pytest.approx(e1, rel=1e-11)
-        assert np.abs(f.cpu().numpy() - f1).max() < 1e-8
+        if precision == "double":
+            assert np.abs(f.cpu().numpy() - f1).max() < 1e-8
+        else:   # fp32 per-lane force sums: the rank's lanes-per-atom choice changes their rounding
+            assert np.abs(f.cpu().numpy() - f1).max() < 1e-6 * np.abs(f1).max()
 
 
 def test_grid_c3_matches_exact_mfma_path():

@@ -50,9 +50,13 @@ def test_md_harness_matches_torch(lo, hi):
     # kick + drift
     xr, vr = x.clone(), v + 0.5 * dt * f * inv_m * own
     xr = xr + dt * vr * own
+    f_before = f.clone()
     md.kick_drift(x, v, f)
     torch.cuda.synchronize()
     assert torch.allclose(v, vr, rtol=1e-12, atol=0) and torch.allclose(x, xr, rtol=1e-12, atol=0)
+    # the owned forces are zeroed for the next evaluation to add into; the rest untouched
+    assert torch.count_nonzero(f[lo:hi]) == 0
+    assert torch.equal(f[:lo], f_before[:lo]) and torch.equal(f[hi:], f_before[hi:])
     # restraints + kick
     fr = f + _restraints_ref(x, nw) * own
     vr = v + 0.5 * dt * fr * inv_m * own
