@@ -104,7 +104,7 @@ void dfree(cf_handle* H, void* p) {
 }
 
 // neighbour-list capacity: the mean count within rc + skin at the default-box density,
-// split over kSeg = 4 sub-lists, x2 + margin (k_pairs_overflow rescans the cells for any
+// split over kSeg = 4 sub-lists, x2 + margin (k_excl rescans the cells for any
 // atom that overflows, so this is a speed knob, not a correctness limit)
 void alloc_nlist(cf_handle* H, double skin) {
     cf::Handle& h = H->h;
@@ -493,10 +493,10 @@ CF_EXPORT int cf_create(const cf_params* p, const cf_options* opt, cf_handle** o
         h.e_atom = dalloc<double>(H, (size_t)3 * n);
         h.f_part = dalloc<double>(H, (size_t)3 * n);
         h.terms_dev = dalloc<double>(H, 4);
-        h.e_part = dalloc<double>(H, 3 * ((size_t)n / 2048 + 2));
+        h.e_part = dalloc<double>(H, 3 * ((size_t)n / 256 + 2));
         h.energy_dev = dalloc<double>(H, 1);
-        h.e_ticket = dalloc<int>(H, 1);
-        check_hip(hipMemset(h.e_ticket, 0, sizeof(int)), "memset");
+        h.e_ticket = dalloc<int>(H, cf::kNumTickets);
+        check_hip(hipMemset(h.e_ticket, 0, sizeof(int) * cf::kNumTickets), "memset");
         check_hip(hipMemset(h.dedq, 0, sizeof(double) * n), "memset");
         check_hip(hipMemset(h.f_part, 0, sizeof(double) * 3 * n), "memset");
         check_hip(hipMemset(h.e_atom, 0, sizeof(double) * 3 * n), "memset");
@@ -736,23 +736,21 @@ CF_EXPORT int cf_compute_begin(cf_handle* H, const double* pos_dev, const double
         check_hip(hipSetDevice(h.device), "hipSetDevice");
         set_box(H, box9);
         const int forces = flags & CF_INCLUDE_FORCES, energy = flags & CF_INCLUDE_ENERGY;
+        // neighbour list: rebuilt on every call (skin 0, the reference's behaviour, RCK:559),
+        // or kept while no atom has moved more than half the skin.  The host forces a rebuild
+        // (first call, new box, skin change); otherwise k_atoms_prep checks the displacements
+        // on the device and the cell commit / list kernels follow its flag, so nothing waits
+        // on the host and the sequence is graph-capturable.
+        const double Lmin = std::min(h.box_L[0], std::min(h.box_L[1], h.box_L[2]));
+        const double s_call = h.skin > 0 ? std::max(0.0, std::min(h.skin, 0.5 * Lmin - h.cutoff)) : 0.0;
+        const bool reusable = h.pbc && h.skin > 0 && h.list_valid && s_call == h.list_skin &&
+                              h.list_L[0] == h.box_L[0] && h.list_L[1] == h.box_L[1] && h.list_L[2] == h.box_L[2];
         { Timed t(H, PH_FLUX); cf::launch_flux_terms(h, pos_dev); }
-        { Timed t(H, PH_PREP); cf::launch_atoms_prep(h, pos_dev); }
+        { Timed t(H, PH_PREP); cf::launch_atoms_prep(h, pos_dev, reusable); }
         if (h.pbc) {
-            // neighbour list: rebuilt on every call (skin 0, the reference's behaviour,
-            // RCK:559), or kept while no atom has moved more than half the skin.  The host
-            // forces a rebuild (first call, new box, skin change); otherwise k_skin_check
-            // decides on the device and the cell commit / list kernels follow its flag, so
-            // nothing waits on the host and the sequence is graph-capturable.
-            const double Lmin = std::min(h.box_L[0], std::min(h.box_L[1], h.box_L[2]));
-            const double s_call = h.skin > 0 ? std::max(0.0, std::min(h.skin, 0.5 * Lmin - h.cutoff)) : 0.0;
-            const bool reusable = h.skin > 0 && h.list_valid && s_call == h.list_skin &&
-                                  h.list_L[0] == h.box_L[0] && h.list_L[1] == h.box_L[1] && h.list_L[2] == h.box_L[2];
             {
                 Timed t(H, PH_CELLS);
-                if (reusable) {
-                    cf::launch_skin_check(h, pos_dev);
-                } else {
+                if (!reusable) {
                     h.list_skin = s_call;
                     set_cells(H, h.box_L);
                     cf::launch_force_rebuild(h);
@@ -853,9 +851,12 @@ CF_EXPORT int cf_compute_end(cf_handle* H, double* forces_dev, double* energy_de
                     cf::launch_recip_add(h);
                 }
             }
-            if (forces && forces_dev) { Timed t(H, PH_ASSEMBLE); cf::launch_assemble(h, forces_dev); }
         }
-        { Timed t(H, PH_ENERGY); cf::launch_energy(h, energy, energy_dev); }
+        {   // chain rule (when forces are requested) and the energy reduction in one launch
+            Timed t(H, PH_ENERGY);
+            cf::launch_assemble_energy(h, (forces && forces_dev && h.hi > h.lo) ? forces_dev : nullptr, energy,
+                                       energy_dev);
+        }
         launch_check("compute_end");
     });
 }

@@ -187,9 +187,9 @@ struct Handle {
     double erfc_scale = 0; int erfc_m = 0;
     float* erfc_tab_f = nullptr; // fp32 erfcx table (mixed precision)
     double* terms_dev = nullptr; // [4]
-    double* e_part = nullptr;    // [ceil(Nown/2048)][3] energy block partials
+    double* e_part = nullptr;    // [ceil(Nown/256)][3] energy block partials
     double* energy_dev = nullptr;// [1] internal
-    int* e_ticket = nullptr;     // [1] k_energy block ticket (0 between launches)
+    int* e_ticket = nullptr;     // [kNumTickets] last-block tickets (0 between launches)
     // state
     int pending_flags = -1;     // flags of a begun evaluation
     bool direct_done = false;   // cf_compute_direct already ran for the begun evaluation
@@ -201,17 +201,15 @@ std::vector<double> erfc_table(double xmax, double* scale, int* m);     // degre
 std::vector<float> erfc_table_f(double xmax, double* scale, int* m);    // degree 6, mixed-precision kernel
 std::vector<double> erfc_table_deg(double xmax, int deg, double* scale, int* m);
 void launch_flux_terms(Handle& h, const double* pos);
-void launch_atoms_prep(Handle& h, const double* pos);
+void launch_atoms_prep(Handle& h, const double* pos, bool skin_check);   // q, self term [, skin_flag |= moved > list_skin/2]
 void launch_cell_sort(Handle& h, const double* pos);
-void launch_skin_check(Handle& h, const double* pos);   // skin_flag = some atom moved > list_skin/2
 void launch_force_rebuild(Handle& h);                   // skin_flag = 1
 void launch_nlist(Handle& h, const double* pos);
 void launch_direct(Handle& h, const double* pos, int include_forces);          // the pair kernel
 void launch_direct_finish(Handle& h, const double* pos, int include_forces);   // overflow rescan + exclusions
 void launch_recip_add(Handle& h);   // dedq, f_part += reciprocal partials
 void launch_nopbc(Handle& h, const double* pos, int include_forces, int include_energy);
-void launch_assemble(Handle& h, double* forces_out);
-void launch_energy(Handle& h, int include_energy, double* energy_out);
+void launch_assemble_energy(Handle& h, double* forces_out, int include_energy, double* energy_out);   // chain rule (forces_out != null) + energy
 
 void kspace_plan(Handle& h);
 size_t kspace_alloc_bytes(const Handle& h);
@@ -290,6 +288,115 @@ __device__ __forceinline__ int xcd_block() {
     const int b = blockIdx.x, nb = gridDim.x;
     const int x = b % kNumXcd, per = nb / kNumXcd, rem = nb % kNumXcd;
     return x * per + min(x, rem) + b / kNumXcd;
+}
+
+// last-block tickets (Handle::e_ticket[]): the energy reduction, the cell-count bounds, the
+// grid-bin bounds
+constexpr int kTicketEnergy = 0, kTicketCells = 1, kTicketGrid = 2, kNumTickets = 4;
+
+// ---- counting-sort helpers shared by the cell and grid-bin sorts ----------------------
+// atomicAdd(&cnt[key], 1) aggregated over runs of equal keys in consecutive lanes (spatially
+// ordered atoms put long runs of a wave in one cell or bin, whose counter would otherwise
+// serialize up to 64 atomics): the first lane of each run adds the run length, all runs'
+// atomics in flight at once (one round trip), and the run's lanes take consecutive ranks.
+// The valid lanes must be a prefix of the wave (i < n).  Returns a provisional rank within
+// the key; the sorts fix the final order in a separate, deterministic pass.
+__device__ __forceinline__ int wave_agg_inc(int* cnt, int key, bool valid) {
+    const int lane = threadIdx.x & 63;
+    const int prev = __shfl_up(key, 1);
+    const bool head = valid && (lane == 0 || prev != key);
+    const unsigned long long cut = __ballot(head || !valid);        // run starts + invalid lanes
+    const unsigned long long upto = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);   // bits 0..lane
+    const int leader = 63 - __clzll((long long)(cut & upto));        // start of this lane's run
+    const unsigned long long after = cut & ~upto;
+    const int next = after ? __ffsll((long long)after) - 1 : 64;     // first lane past this run
+    int base = 0;
+    if (head) base = atomicAdd(&cnt[key], next - lane);
+    base = __shfl(base, leader);
+    return base + (lane - leader);
+}
+
+// Last-block-done: true (in every thread) for the block that finishes last; it re-arms the
+// ticket.  Every thread of the block must call it.  The data the last block reads from the
+// other blocks must be device-scope atomics (RMWs whose results the threads waited for, or
+// agent-scope atomic stores followed by a wait), read back with agent-scope atomic loads
+// (ld_agent): then no release/acquire fence is needed, whose L2 writeback in every block
+// cost more than the kernels themselves (measured: 375-block grid sort 10 -> 39 us).
+__device__ __forceinline__ bool last_block_done(int* ticket) {
+    __shared__ bool last;
+    __builtin_amdgcn_s_waitcnt(0);   // this wave's atomic stores are performed
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        last = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (int)gridDim.x - 1;
+        if (last) __hip_atomic_store(ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    return last;
+}
+
+template <class T>
+__device__ __forceinline__ T ld_agent(const T* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <class T>
+__device__ __forceinline__ void st_agent(T* p, T v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// exclusive scan of one int per thread over a block of NT threads (sh: NT ints of LDS)
+template <int NT>
+__device__ __forceinline__ int block_exclusive_scan_t(int v, int* sh) {
+    const int t = threadIdx.x;
+    sh[t] = v;
+    __syncthreads();
+    for (int off = 1; off < NT; off <<= 1) {
+        int u = t >= off ? sh[t - off] : 0;
+        __syncthreads();
+        sh[t] += u;
+        __syncthreads();
+    }
+    int incl = sh[t];
+    __syncthreads();
+    return incl - v;
+}
+
+// counts cnt[0..m) (device-scope atomics of other blocks: read with ld_agent) -> start[c]
+// (and end[c] = start[c + 1] when end != null; start[m] = total when total_at_end), by the NT
+// threads of one block, in tiles of 8 NT counts: each thread issues its 8 coalesced loads of
+// a tile at once (one memory latency per tile, not one per count)
+template <int NT>
+__device__ __forceinline__ void block_counts_to_bounds(int m, int* cnt, int* start, int* end, bool total_at_end,
+                                                       int* sh) {
+    __shared__ int tile[8 * NT];
+    const int t = threadIdx.x;
+    int carry = 0;
+    for (int base = 0; base < m; base += 8 * NT) {
+        int v[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            const int c = base + k * NT + t;
+            v[k] = c < m ? ld_agent(cnt + c) : 0;
+        }
+#pragma unroll
+        for (int k = 0; k < 8; k++) tile[k * NT + t] = v[k];
+        __syncthreads();
+        int sum = 0;
+#pragma unroll
+        for (int k = 0; k < 8; k++) { v[k] = tile[8 * t + k]; sum += v[k]; }
+        int run = carry + block_exclusive_scan_t<NT>(sum, sh);
+        carry += sh[NT - 1];   // inclusive total of the tile
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            const int c = base + 8 * t + k;
+            if (c < m) {
+                start[c] = run;
+                run += v[k];
+                if (end) end[c] = run;
+            }
+        }
+        __syncthreads();
+    }
+    if (total_at_end && t == 0) start[m] = carry;
 }
 
 }  // namespace cf

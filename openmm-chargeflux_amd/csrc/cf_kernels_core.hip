@@ -109,13 +109,26 @@ __global__ void __launch_bounds__(256) k_flux_terms(int nterms, int nb, int na, 
 }
 
 // 2. per-atom charges q_i = q0_i + sum of its slots (term order), self term
-//    (RCK:38-40, 507-510).
+//    (RCK:38-40, 507-510).  With skin_flag set, the same launch also does the neighbour-
+//    list validity check: flag = 1 if any atom moved more than half the skin since the
+//    last build (one launch fewer per step than a separate check kernel).
 __global__ void __launch_bounds__(256) k_atoms_prep(int n, const double* __restrict__ q0,
                                                     const int* __restrict__ qs, const int* __restrict__ qslot,
                                                     const double* __restrict__ dq_slot, int pbc, double alpha,
                                                     double* __restrict__ q, double* __restrict__ dedq_self,
-                                                    double* __restrict__ e_atom) {
+                                                    double* __restrict__ e_atom, const double* __restrict__ pos,
+                                                    const double* __restrict__ pos_ref, double lim2,
+                                                    int* __restrict__ skin_flag) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (skin_flag) {
+        bool moved = false;
+        if (i < n) {
+            double3 x = ld3(pos, i), r = ld3(pos_ref, i);
+            double dx = x.x - r.x, dy = x.y - r.y, dz = x.z - r.z;
+            moved = !(dx * dx + dy * dy + dz * dz <= lim2);  // NaN counts as moved
+        }
+        if (__ballot(moved) && (threadIdx.x & 63) == 0) atomicOr(skin_flag, 1);
+    }
     if (i >= n) return;
     double qi = q0[i];
     for (int s = qs[i]; s < qs[i + 1]; s++) qi += dq_slot[qslot[s]];
@@ -139,62 +152,41 @@ __global__ void __launch_bounds__(256) k_atoms_prep(int n, const double* __restr
 //      -> [owned compaction] -> commit (or refresh of the kept list's coordinates)
 // ---------------------------------------------------------------------------------
 
+// keys + histogram (wave-aggregated atomics: provisional ranks), then the block that
+// finishes last turns the counts into cell bounds (no separate scan launch)
 __global__ void __launch_bounds__(256) k_cell_hist(int n, const int* __restrict__ flag, const double* __restrict__ pos,
                                                    double3 L, int3 nc, int* __restrict__ key, int* __restrict__ rank,
-                                                   int* __restrict__ cnt) {
-    int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n || !*flag) return;
-    double3 x = ld3(pos, i);
-    double w[3] = {x.x - floor(x.x / L.x) * L.x, x.y - floor(x.y / L.y) * L.y, x.z - floor(x.z / L.z) * L.z};
-    double Ls[3] = {L.x, L.y, L.z};
-    int ncs[3] = {nc.x, nc.y, nc.z};
-    int c[3];
+                                                   int* __restrict__ cnt, int* __restrict__ ticket,
+                                                   int* __restrict__ cstart, int* __restrict__ cend) {
+    __shared__ int sh[256];
+    if (!*flag) return;   // uniform over the grid
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool valid = i < n;
+    int k = 0;
+    if (valid) {
+        double3 x = ld3(pos, i);
+        double w[3] = {x.x - floor(x.x / L.x) * L.x, x.y - floor(x.y / L.y) * L.y, x.z - floor(x.z / L.z) * L.z};
+        double Ls[3] = {L.x, L.y, L.z};
+        int ncs[3] = {nc.x, nc.y, nc.z};
+        int c[3];
 #pragma unroll
-    for (int d = 0; d < 3; d++) {
-        int ci = (int)(w[d] / Ls[d] * ncs[d]);
-        c[d] = ci < 0 ? 0 : (ci >= ncs[d] ? ncs[d] - 1 : ci);
+        for (int d = 0; d < 3; d++) {
+            int ci = (int)(w[d] / Ls[d] * ncs[d]);
+            c[d] = ci < 0 ? 0 : (ci >= ncs[d] ? ncs[d] - 1 : ci);
+        }
+        k = (c[0] * nc.y + c[1]) * nc.z + c[2];
+        key[i] = k;
     }
-    int k = (c[0] * nc.y + c[1]) * nc.z + c[2];
-    key[i] = k;
-    rank[i] = atomicAdd(&cnt[k], 1);  // provisional slot; k_cell_order fixes the order
+    const int r = wave_agg_inc(cnt, k, valid);   // provisional slot; k_cell_order fixes the order
+    if (valid) rank[i] = r;
+    if (!last_block_done(ticket)) return;
+    block_counts_to_bounds<256>(nc.x * nc.y * nc.z, cnt, cstart, cend, false, sh);
 }
 
 // one workgroup: exclusive scan of m counts (chunked per thread); bounds -> start/end
 constexpr int kScanThreads = 1024;
 
-__device__ __forceinline__ int block_exclusive_scan(int v, int* sh) {
-    const int t = threadIdx.x;
-    sh[t] = v;
-    __syncthreads();
-    for (int off = 1; off < kScanThreads; off <<= 1) {
-        int u = t >= off ? sh[t - off] : 0;
-        __syncthreads();
-        sh[t] += u;
-        __syncthreads();
-    }
-    int incl = sh[t];
-    __syncthreads();
-    return incl - v;
-}
-
-__global__ void __launch_bounds__(kScanThreads) k_cell_scan(int ncell, const int* __restrict__ flag,
-                                                            const int* __restrict__ cnt, int* __restrict__ cstart,
-                                                            int* __restrict__ cend) {
-    __shared__ int sh[kScanThreads];
-    if (!*flag) return;
-    const int per = (ncell + kScanThreads - 1) / kScanThreads;
-    const int c0 = min(ncell, threadIdx.x * per), c1 = min(ncell, c0 + per);
-    int sum = 0;
-    for (int c = c0; c < c1; c++) sum += cnt[c];
-    int run = block_exclusive_scan(sum, sh);
-    for (int c = c0; c < c1; c++) {
-        cstart[c] = run;
-        run += cnt[c];
-        cend[c] = run;
-    }
-}
-
-// also re-zeroes the per-cell counts (consumed by k_cell_scan) for the next build, so no
+// also re-zeroes the per-cell counts (consumed by k_cell_hist's bounds) for the next build, so no
 // separate zeroing launch precedes k_cell_hist
 __global__ void __launch_bounds__(256) k_cell_scatter(int n, const int* __restrict__ flag, const int* __restrict__ key,
                                                       const int* __restrict__ rank, const int* __restrict__ cstart,
@@ -255,7 +247,7 @@ __global__ void __launch_bounds__(kScanThreads) k_own_scan(int nb, const int* __
     const int b0 = min(nb, threadIdx.x * per), b1 = min(nb, b0 + per);
     int sum = 0;
     for (int b = b0; b < b1; b++) sum += bsum[b];
-    int run = block_exclusive_scan(sum, sh);
+    int run = block_exclusive_scan_t<kScanThreads>(sum, sh);
     for (int b = b0; b < b1; b++) {
         int v = bsum[b];
         bsum[b] = run;  // in place: counts -> offsets
@@ -316,20 +308,6 @@ __global__ void __launch_bounds__(256) k_cell_commit(int n, const int* __restric
     }
     pos4s[s] = p4;
     if (pos4f) pos4f[s] = make_float4((float)p4.x, (float)p4.y, (float)p4.z, (float)p4.w);
-}
-
-// list validity: flag = 1 if any atom moved more than half the skin since the last build
-__global__ void __launch_bounds__(256) k_skin_check(int n, const double* __restrict__ pos,
-                                                    const double* __restrict__ pos_ref, double lim2,
-                                                    int* __restrict__ flag) {
-    int i = blockIdx.x * blockDim.x + threadIdx.x;
-    bool moved = false;
-    if (i < n) {
-        double3 x = ld3(pos, i), r = ld3(pos_ref, i);
-        double dx = x.x - r.x, dy = x.y - r.y, dz = x.z - r.z;
-        moved = !(dx * dx + dy * dy + dz * dz <= lim2);  // NaN counts as moved
-    }
-    if (__ballot(moved) && (threadIdx.x & 63) == 0) atomicOr(flag, 1);
 }
 
 // ---------------------------------------------------------------------------------
@@ -477,14 +455,20 @@ __global__ void __launch_bounds__(256) k_nlist(DirectArgs a) {
 // The fp32 test uses a margin; k_pairs applies the exact fp64 r <= rc test.  Falls back to
 // the per-lane scan when the box would wrap onto itself.
 constexpr int kWaveNL = 64;
-constexpr int kStage = 4 * kWaveNL;
+constexpr int kStageU = 2;                 // candidates per lane staged per cell pass
+constexpr int kStage = kStageU * kWaveNL;
 
 __global__ void __launch_bounds__(kWaveNL * kSeg) k_nlist_wave(DirectArgs a) {
-    __shared__ float4 cand_all[kSeg][kStage + 8];
-    __shared__ int cand_j_all[kSeg][kStage + 8];
+    // staged candidates, SoA so that one ds_read_b128 gives 4 candidates' x (two packed-fp32
+    // operands): x, y, z in the block frame, LJ type bits, atom index
+    __shared__ __attribute__((aligned(16))) float cand_all[kSeg][4][kStage + 16];
+    __shared__ int cand_j_all[kSeg][kStage + 16];
     const int lane = threadIdx.x & 63;
     const int seg = threadIdx.x >> 6;   // this wave's share of the cell box and its sub-list
-    float4* cand = cand_all[seg];
+    float* cx = cand_all[seg][0];
+    float* cy = cand_all[seg][1];
+    float* cz = cand_all[seg][2];
+    int* ctp = reinterpret_cast<int*>(cand_all[seg][3]);
     int* cand_j = cand_j_all[seg];
     if (!*a.flag) return;  // list still valid (skin): nothing to build
     const int base = xcd_block() * kWaveNL;
@@ -560,11 +544,11 @@ __global__ void __launch_bounds__(kWaveNL * kSeg) k_nlist_wave(DirectArgs a) {
         off = make_double3((k[0] - 1) * Ls[0] - org.x, (k[1] - 1) * Ls[1] - org.y, (k[2] - 1) * Ls[2] - org.z);
         return (w[0] * a.nc.y + w[1]) * a.nc.z + w[2];
     };
-    double4 rp[4];
-    int rj[4], rt[4];
+    double4 rp[kStageU];
+    int rj[kStageU], rt[kStageU];
     auto fetch = [&](int t0, int t1) {
 #pragma unroll
-        for (int v = 0; v < 4; v++) {
+        for (int v = 0; v < kStageU; v++) {
             int t = t0 + v * kWaveNL + lane;
             if (t < t1) { rp[v] = a.pos4s[t]; rj[v] = a.atom_sorted[t]; rt[v] = a.typ_s ? a.typ_s[t] : 0; }
         }
@@ -572,31 +556,47 @@ __global__ void __launch_bounds__(kWaveNL * kSeg) k_nlist_wave(DirectArgs a) {
     // staged candidate: fp32 block-frame position, LJ type bits in .w
     auto stage = [&](int t0, int t1, double3 off) {
 #pragma unroll
-        for (int v = 0; v < 4; v++) {
+        for (int v = 0; v < kStageU; v++) {
             int u = v * kWaveNL + lane;
             if (t0 + u < t1) {
-                cand[u] = make_float4((float)(rp[v].x + off.x), (float)(rp[v].y + off.y), (float)(rp[v].z + off.z),
-                                      __int_as_float(rt[v]));
+                cx[u] = (float)(rp[v].x + off.x);
+                cy[u] = (float)(rp[v].y + off.y);
+                cz[u] = (float)(rp[v].z + off.z);
+                ctp[u] = rt[v];
                 cand_j[u] = rj[v];
             }
         }
     };
+    // 16 candidates per chunk, tested two at a time in packed fp32 (v_pk_add/mul/fma_f32: half
+    // the VALU instructions of scalar fp32), then the lane's hits of the chunk are emitted
+    // (a longer chunk amortizes the divergent emit loop: its trip count is the maximum hit
+    // count over the wave's lanes)
+    typedef float v2f __attribute__((ext_vector_type(2)));
+    typedef float v4f __attribute__((ext_vector_type(4)));
     auto test = [&](int t0, int m, int code) {
         if (!active) return;
-        for (int u0 = 0; u0 < m; u0 += 8) {
+        const v2f px = {pf.x, pf.x}, py = {pf.y, pf.y}, pz = {pf.z, pf.z};
+        for (int u0 = 0; u0 < m; u0 += 16) {
             unsigned bits = 0;
 #pragma unroll
-            for (int v = 0; v < 8; v++) {
-                const float4 cv = cand[u0 + v];
-                float dx = pf.x - cv.x, dy = pf.y - cv.y, dz = pf.z - cv.z;
-                float r2 = fmaf(dx, dx, fmaf(dy, dy, dz * dz));
-                bits |= (r2 <= rc2f && u0 + v < m) ? (1u << v) : 0u;
+            for (int v = 0; v < 16; v += 4) {
+                const v4f X = *reinterpret_cast<const v4f*>(cx + u0 + v);
+                const v4f Y = *reinterpret_cast<const v4f*>(cy + u0 + v);
+                const v4f Z = *reinterpret_cast<const v4f*>(cz + u0 + v);
+#pragma unroll
+                for (int h = 0; h < 2; h++) {
+                    const v2f dx = px - (h ? X.zw : X.xy), dy = py - (h ? Y.zw : Y.xy), dz = pz - (h ? Z.zw : Z.xy);
+                    const v2f r2 = dx * dx + dy * dy + dz * dz;
+                    bits |= (r2.x <= rc2f ? 1u : 0u) << (v + 2 * h);
+                    bits |= (r2.y <= rc2f ? 1u : 0u) << (v + 2 * h + 1);
+                }
             }
-            if (s >= t0 + u0 && s < t0 + u0 + 8) bits &= ~(1u << (s - t0 - u0));
+            if (m - u0 < 16) bits &= (1u << (m - u0)) - 1u;
+            if (s >= t0 + u0 && s < t0 + u0 + 16) bits &= ~(1u << (s - t0 - u0));
             while (bits) {
                 int v = __builtin_ctz(bits);
                 bits &= bits - 1;
-                emit(t0 + u0 + v, cand_j[u0 + v], a.typ_s ? __float_as_int(cand[u0 + v].w) : code);
+                emit(t0 + u0 + v, cand_j[u0 + v], a.typ_s ? ctp[u0 + v] : code);
             }
         }
     };
@@ -637,14 +637,16 @@ __global__ void __launch_bounds__(kWaveNL * kSeg) k_nlist_wave(DirectArgs a) {
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
 #pragma unroll
-            for (int v = 0; v < 4; v++) {
+            for (int v = 0; v < kStageU; v++) {
                 int t = tb + v * kWaveNL + lane;
                 if (t < te) {
                     double4 pj = a.pos4s[t];
-                    cand[v * kWaveNL + lane] = make_float4((float)(pj.x + off.x), (float)(pj.y + off.y),
-                                                           (float)(pj.z + off.z),
-                                                           __int_as_float(a.typ_s ? a.typ_s[t] : 0));
-                    cand_j[v * kWaveNL + lane] = a.atom_sorted[t];
+                    const int u = v * kWaveNL + lane;
+                    cx[u] = (float)(pj.x + off.x);
+                    cy[u] = (float)(pj.y + off.y);
+                    cz[u] = (float)(pj.z + off.z);
+                    ctp[u] = a.typ_s ? a.typ_s[t] : 0;
+                    cand_j[u] = a.atom_sorted[t];
                 }
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -779,7 +781,7 @@ __global__ void __launch_bounds__(256) k_recip_add(int lo, int nown, int nparts,
 
 // 4b: walk the list — kSeg adjacent lanes per atom, lane g walks sub-list g; partial sums
 // are combined with two xor-shuffles (fixed order: deterministic).  Atoms with an
-// overflowed sub-list are left to k_pairs_overflow.
+// overflowed sub-list are left to k_excl (cell rescan).
 // LPA lanes per atom (4, 8 or 16; more when few atoms are owned, so the grid still fills
 // the chip): lane g walks entries g/4, g/4 + LPA/4, ... of sub-list g%4.
 // TYPES: the partner's LJ parameters come from the per-type table (LDS) indexed by the high
@@ -997,23 +999,19 @@ __device__ __forceinline__ void pair_rescan(const DirectArgs& a, const double* t
     store_pairs(acc, a, i);
 }
 
-// 4c: atoms whose neighbour list overflowed (denser than planned): rescan the cells
-__global__ void __launch_bounds__(256) k_pairs_overflow(DirectArgs a) {
-    __shared__ double tab[kErfcMaxM * (kErfcDeg + 1)];
-    load_erfc_tab(a, tab);
-    int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= a.nlr) return;
-    bool over = false;
-    for (int g = 0; g < kSeg; g++) over = over || a.nl_cnt[(size_t)g * a.nlr + c] > a.nb_cap;
-    if (!over) return;
-    int s = own_slot(a, c);
-    pair_rescan(a, tab, s, a.atom_sorted[s]);
-}
-
-// 4d: exclusion correction + self term of every owned atom (in atom order: coalesced)
+// 4c: per list row (owned atom): an atom whose neighbour list overflowed (denser than
+//     planned; k_pairs skipped it) first rescans its cells, then the exclusion correction +
+//     self term (one launch for both: the overflow check costs 4 coalesced count loads)
 __global__ void __launch_bounds__(256) k_excl(DirectArgs a) {
-    const int io = blockIdx.x * blockDim.x + threadIdx.x;
-    if (io < a.hi - a.lo) excl_atom(a, a.lo + io);
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= a.nlr) return;
+    const int s = own_slot(a, c);
+    const int i = a.atom_sorted[s];
+    bool over = false;
+#pragma unroll
+    for (int g = 0; g < kSeg; g++) over = over || a.nl_cnt[(size_t)g * a.nlr + c] > a.nb_cap;
+    if (over) pair_rescan(a, a.erfc_tab, s, i);   // rare: erfcx table read from global memory
+    excl_atom(a, i);
 }
 
 // ---------------------------------------------------------------------------------
@@ -1086,31 +1084,16 @@ __global__ void __launch_bounds__(kNopbcTile) k_nopbc(int n, int lo, int hi, int
 }
 
 // ---------------------------------------------------------------------------------
-// 6. assemble: F_b += F_part_b - sum_e dE/dq[a_e] * dq_{a_e}/dx_b   (chain rule as a
-//    per-x-atom gather; reference scatter RCK:493-499, 626-632)
+// 6. assemble + energy, one launch.  Assemble: F_b += F_part_b - sum_e dE/dq[a_e] *
+//    dq_{a_e}/dx_b (chain rule as a per-x-atom gather; reference scatter RCK:493-499,
+//    626-632), skipped when out is null.  Energy: fixed-order two-stage tree reduction
+//    (deterministic): each block sums its kEChunk atoms' (self, direct, exclusion) energies;
+//    the block that finishes last (atomic ticket) sums the block partials and the
+//    reciprocal-space partials in fixed order, so the result does not depend on block
+//    scheduling.  It also clears the neighbour-list rebuild flag for the next evaluation,
+//    re-arms the multi-rank x-slab and (last_block_done) the ticket.
 // ---------------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) k_assemble(int lo, int hi, const int* __restrict__ cs, const int2* __restrict__ ce,
-                                                  const double* __restrict__ dedq, const double* __restrict__ dqdx,
-                                                  const double* __restrict__ f_part, double* __restrict__ out) {
-    int b = lo + blockIdx.x * blockDim.x + threadIdx.x;
-    if (b >= hi) return;
-    double fx = f_part[3 * b], fy = f_part[3 * b + 1], fz = f_part[3 * b + 2];
-    for (int k = cs[b]; k < cs[b + 1]; k++) {
-        int2 en = ce[k];
-        double g = dedq[en.y];
-        fx -= g * dqdx[3 * en.x];
-        fy -= g * dqdx[3 * en.x + 1];
-        fz -= g * dqdx[3 * en.x + 2];
-    }
-    out[3 * b] += fx;
-    out[3 * b + 1] += fy;
-    out[3 * b + 2] += fz;
-}
-
-// 7. energy: fixed-order two-stage tree reduction (deterministic).  Stage 1: each block
-//    sums kEChunk atoms' (self, direct, exclusion) energies; stage 2: one block sums the
-//    block partials and the reciprocal-space partials.
-constexpr int kEChunk = 2048;
+constexpr int kEChunk = 256;
 
 __device__ __forceinline__ void block_sum3(double& a0, double& a1, double& a2, double (*red)[256]) {
     red[0][threadIdx.x] = a0; red[1][threadIdx.x] = a1; red[2][threadIdx.x] = a2;
@@ -1124,41 +1107,47 @@ __device__ __forceinline__ void block_sum3(double& a0, double& a1, double& a2, d
     a0 = red[0][0]; a1 = red[1][0]; a2 = red[2][0];
 }
 
-// Per-block partial sums of the per-atom energies; the block that finishes last (atomic
-// ticket) sums the partials and the reciprocal partials in fixed order, so the result does
-// not depend on block scheduling.  It also clears the neighbour-list rebuild flag for the
-// next evaluation and re-arms the ticket.
-__global__ void __launch_bounds__(256) k_energy(int lo, int hi, const double* __restrict__ e_atom,
-                                                double* __restrict__ part, const double* __restrict__ e_rec_part,
-                                                int nrec, int pbc, double* __restrict__ terms,
-                                                double* __restrict__ energy_out, double* __restrict__ energy_int,
-                                                int* __restrict__ ticket, int* __restrict__ flag,
-                                                int* __restrict__ xrange) {
+__global__ void __launch_bounds__(kEChunk) k_assemble_energy(int lo, int hi, const int* __restrict__ cs,
+                                                             const int2* __restrict__ ce, const double* __restrict__ dedq,
+                                                             const double* __restrict__ dqdx,
+                                                             const double* __restrict__ f_part, double* __restrict__ out,
+                                                             const double* __restrict__ e_atom, double* __restrict__ part,
+                                                             const double* __restrict__ e_rec_part, int nrec, int pbc,
+                                                             double* __restrict__ terms, double* __restrict__ energy_out,
+                                                             double* __restrict__ energy_int, int* __restrict__ ticket,
+                                                             int* __restrict__ flag, int* __restrict__ xrange) {
     __shared__ double red[3][256];
-    __shared__ bool last;
+    const int b = lo + blockIdx.x * kEChunk + threadIdx.x;
     double a0 = 0, a1 = 0, a2 = 0;
-    {
-        const int i0 = lo + blockIdx.x * kEChunk;
-        const int i1 = min(hi, i0 + kEChunk);
-        for (int i = i0 + threadIdx.x; i < i1; i += 256) {
-            a0 += e_atom[3 * i]; a1 += e_atom[3 * i + 1]; a2 += e_atom[3 * i + 2];
+    if (b < hi) {
+        if (out) {
+            double fx = f_part[3 * b], fy = f_part[3 * b + 1], fz = f_part[3 * b + 2];
+            for (int k = cs[b]; k < cs[b + 1]; k++) {
+                int2 en = ce[k];
+                double g = dedq[en.y];
+                fx -= g * dqdx[3 * en.x];
+                fy -= g * dqdx[3 * en.x + 1];
+                fz -= g * dqdx[3 * en.x + 2];
+            }
+            out[3 * b] += fx;
+            out[3 * b + 1] += fy;
+            out[3 * b + 2] += fz;
         }
-        block_sum3(a0, a1, a2, red);
-        if (threadIdx.x == 0) {
-            part[3 * blockIdx.x] = a0; part[3 * blockIdx.x + 1] = a1; part[3 * blockIdx.x + 2] = a2;
-            __threadfence();
-            last = atomicAdd(ticket, 1) == (int)gridDim.x - 1;
-        }
-        __syncthreads();
-        if (!last) return;
-        __threadfence();
+        a0 = e_atom[3 * b]; a1 = e_atom[3 * b + 1]; a2 = e_atom[3 * b + 2];
     }
+    block_sum3(a0, a1, a2, red);
+    if (threadIdx.x == 0) {   // agent-scope stores, read back by the last block (last_block_done)
+        st_agent(part + 3 * blockIdx.x, a0); st_agent(part + 3 * blockIdx.x + 1, a1); st_agent(part + 3 * blockIdx.x + 2, a2);
+    }
+    if (!last_block_done(ticket)) return;
     const int nparts = gridDim.x;
     a0 = 0; a1 = 0; a2 = 0;
-    __syncthreads();
-    for (int k = threadIdx.x; k < nparts; k += 256) { a0 += part[3 * k]; a1 += part[3 * k + 1]; a2 += part[3 * k + 2]; }
+    for (int k = threadIdx.x; k < nparts; k += 256) {
+        a0 += ld_agent(part + 3 * k); a1 += ld_agent(part + 3 * k + 1); a2 += ld_agent(part + 3 * k + 2);
+    }
     double r = 0;
     for (int k = threadIdx.x; k < nrec; k += 256) r += e_rec_part[k];
+    __syncthreads();
     block_sum3(a0, a1, a2, red);
     __syncthreads();
     double z0 = r, z1 = 0, z2 = 0;
@@ -1169,7 +1158,6 @@ __global__ void __launch_bounds__(256) k_energy(int lo, int hi, const double* __
         const double e = pbc ? (t0 + t1 + t2 + t3) : t2;
         *energy_int = e;
         if (energy_out) *energy_out = e;
-        *ticket = 0;
         if (flag) *flag = 0;
         if (xrange) { xrange[0] = INT_MAX; xrange[1] = INT_MIN; }   // re-arm the grid x-slab
     }
@@ -1232,10 +1220,12 @@ void launch_flux_terms(Handle& h, const double* pos) {
                        h.term_idx, h.term_par, pos, L, h.pbc, h.dq_slot, h.dqdx);
 }
 
-void launch_atoms_prep(Handle& h, const double* pos) {
-    (void)pos;
+void launch_atoms_prep(Handle& h, const double* pos, bool skin_check) {
+    // the flag is 0 here: cleared at cf_create and by k_energy at the end of every evaluation
+    const double lim = 0.5 * h.list_skin;
     hipLaunchKernelGGL(k_atoms_prep, dim3(nblk(h.n, 256)), dim3(256), 0, h.stream, h.n, h.q0, h.qcsr_start,
-                       h.qcsr_slot, h.dq_slot, h.pbc, h.alpha, h.q, h.dedq_self, h.e_atom);
+                       h.qcsr_slot, h.dq_slot, h.pbc, h.alpha, h.q, h.dedq_self, h.e_atom, pos, h.pos_ref, lim * lim,
+                       skin_check ? h.skin_flag : nullptr);
 }
 
 void launch_cell_sort(Handle& h, const double* pos) {
@@ -1246,9 +1236,7 @@ void launch_cell_sort(Handle& h, const double* pos) {
     // scratch: cell_key = per-atom key, atom_val = provisional rank, key_tmp = per-cell
     // counts, atom_tmp = scattered order, cell_key_sorted's partner atom_new = final order
     hipLaunchKernelGGL(k_cell_hist, dim3(nblk(h.n, 256)), dim3(256), 0, h.stream, h.n, f, pos, L, nc, h.cell_key,
-                       h.atom_val, h.cell_cnt);
-    hipLaunchKernelGGL(k_cell_scan, dim3(1), dim3(kScanThreads), 0, h.stream, ncell, f, h.cell_cnt, h.cell_start,
-                       h.cell_end);
+                       h.atom_val, h.cell_cnt, h.e_ticket + kTicketCells, h.cell_start, h.cell_end);
     hipLaunchKernelGGL(k_cell_scatter, dim3(nblk(h.n, 256)), dim3(256), 0, h.stream, h.n, f, h.cell_key, h.atom_val,
                        h.cell_start, h.atom_tmp, ncell, h.cell_cnt);
     hipLaunchKernelGGL(k_cell_order, dim3(nblk(ncell, 4)), dim3(256), 0, h.stream, ncell, f, h.cell_start,
@@ -1264,13 +1252,6 @@ void launch_cell_sort(Handle& h, const double* pos) {
     hipLaunchKernelGGL(k_cell_commit, dim3(nblk(h.n, 256)), dim3(256), 0, h.stream, h.n, f, h.cell_key, h.key_tmp,
                        pos, h.q, h.lj, L, h.cell_key_sorted, h.atom_sorted, h.pos4s, h.ljs, h.atom_type, h.typ_s,
                        h.pos_ref, h.n_builds_dev, h.pos4f);
-}
-
-void launch_skin_check(Handle& h, const double* pos) {
-    // the flag is 0 here: cleared at cf_create and by k_energy at the end of every evaluation
-    const double lim = 0.5 * h.list_skin;
-    hipLaunchKernelGGL(k_skin_check, dim3(nblk(h.n, 256)), dim3(256), 0, h.stream, h.n, pos, h.pos_ref, lim * lim,
-                       h.skin_flag);
 }
 
 void launch_force_rebuild(Handle& h) {
@@ -1342,7 +1323,6 @@ void launch_direct(Handle& h, const double* pos, int include_forces) {
 // overflowed atoms' rescan + the exclusion correction (after launch_direct)
 void launch_direct_finish(Handle& h, const double* pos, int include_forces) {
     DirectArgs a = direct_args(h, pos, include_forces);
-    hipLaunchKernelGGL(k_pairs_overflow, dim3(nblk(a.nlr, 256)), dim3(256), 0, h.stream, a);
     hipLaunchKernelGGL(k_excl, dim3(nblk(a.nlr, 256)), dim3(256), 0, h.stream, a);
 }
 
@@ -1360,17 +1340,13 @@ void launch_nopbc(Handle& h, const double* pos, int include_forces, int include_
                        h.e_atom);
 }
 
-void launch_assemble(Handle& h, double* forces_out) {
-    int nown = h.hi - h.lo;
-    hipLaunchKernelGGL(k_assemble, dim3(nblk(nown, 256)), dim3(256), 0, h.stream, h.lo, h.hi, h.ccsr_start,
-                       h.ccsr_ent, h.dedq, h.dqdx, h.f_part, forces_out);
-}
-
-void launch_energy(Handle& h, int include_energy, double* energy_out) {
+void launch_assemble_energy(Handle& h, double* forces_out, int include_energy, double* energy_out) {
+    const int nown = std::max(0, h.hi - h.lo);
     int nrec = (h.pbc && include_energy && h.rank == 0) ? h.e_rec_nblk : 0;
-    const int nparts = std::max(1, nblk(h.hi - h.lo, kEChunk));
-    hipLaunchKernelGGL(k_energy, dim3(nparts), dim3(256), 0, h.stream, h.lo, h.hi, h.e_atom, h.e_part, h.e_rec_part,
-                       nrec, h.pbc, h.terms_dev, energy_out, h.energy_dev, h.e_ticket, h.skin_flag, h.g_xrange);
+    const int nparts = std::max(1, nblk(nown, kEChunk));
+    hipLaunchKernelGGL(k_assemble_energy, dim3(nparts), dim3(kEChunk), 0, h.stream, h.lo, h.hi, h.ccsr_start,
+                       h.ccsr_ent, h.dedq, h.dqdx, h.f_part, forces_out, h.e_atom, h.e_part, h.e_rec_part, nrec, h.pbc,
+                       h.terms_dev, energy_out, h.energy_dev, h.e_ticket + kTicketEnergy, h.skin_flag, h.g_xrange);
 }
 
 }  // namespace cf

@@ -91,13 +91,18 @@ __device__ __forceinline__ bool x_range_in_slab(int x0, int x1, const int* __res
 
 // ---------------------------------------------------------------------------------
 // 1. bin owned atoms by the 8^3 grid tile holding their first tap; deterministic counting
-//    sort (atomic provisional rank, then the order of a stable sort by atom index)
+//    sort: k_g_bin (wave-aggregated atomic provisional rank; the block that finishes last
+//    turns the counts into bin bounds), k_g_scatter, then k_g_order_taps fixes the order of
+//    a stable sort by atom index and writes each sorted atom's tap rows
 // ---------------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) k_g_bin(int lo, int nown, const double* __restrict__ pos,
                                                const double* __restrict__ q, double3 L, int3 ng, int W, int3 nb,
                                                double4* __restrict__ srec, int4* __restrict__ g0u,
-                                               int* __restrict__ rank, int* __restrict__ cnt, int* __restrict__ xr) {
+                                               int* __restrict__ rank, int* __restrict__ cnt, int* __restrict__ xr,
+                                               int* __restrict__ ticket, int* __restrict__ start) {
+    __shared__ int sh[256];
     const int io = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool valid = io < nown;
     if (xr) {   // x-slab of the owned atoms' first taps, relative to the first owned atom's
         double u0 = pos[3 * lo] / L.x;
         u0 -= floor(u0);
@@ -105,7 +110,7 @@ __global__ void __launch_bounds__(256) k_g_bin(int lo, int nown, const double* _
         if (s0 >= ng.x) s0 -= ng.x;
         const int gref = (int)ceil(s0 - 0.5 * W);
         int rmin = INT_MAX, rmax = INT_MIN;
-        if (io < nown) {
+        if (valid) {
             double u = pos[3 * (lo + io)] / L.x;
             u -= floor(u);
             double sd = u * ng.x;
@@ -125,55 +130,35 @@ __global__ void __launch_bounds__(256) k_g_bin(int lo, int nown, const double* _
         }
         if (io == 0) xr[2] = gref;
     }
-    if (io >= nown) return;
-    const int i = lo + io;
-    const double x[3] = {pos[3 * i], pos[3 * i + 1], pos[3 * i + 2]};
-    const double Ls[3] = {L.x, L.y, L.z};
-    const int n[3] = {ng.x, ng.y, ng.z};
-    double s[3];
-    int g[3], gw[3];
+    int bin = 0;
+    if (valid) {
+        const int i = lo + io;
+        const double x[3] = {pos[3 * i], pos[3 * i + 1], pos[3 * i + 2]};
+        const double Ls[3] = {L.x, L.y, L.z};
+        const int n[3] = {ng.x, ng.y, ng.z};
+        double s[3];
+        int g[3], gw[3];
 #pragma unroll
-    for (int d = 0; d < 3; d++) {
-        double u = x[d] / Ls[d];
-        u -= floor(u);
-        double sd = u * n[d];
-        if (sd >= n[d]) sd -= n[d];
-        s[d] = sd;
-        g[d] = (int)ceil(sd - 0.5 * W);
-        gw[d] = g[d] < 0 ? g[d] + n[d] : g[d];
+        for (int d = 0; d < 3; d++) {
+            double u = x[d] / Ls[d];
+            u -= floor(u);
+            double sd = u * n[d];
+            if (sd >= n[d]) sd -= n[d];
+            s[d] = sd;
+            g[d] = (int)ceil(sd - 0.5 * W);
+            gw[d] = g[d] < 0 ? g[d] + n[d] : g[d];
+        }
+        bin = ((gw[0] >> 3) * nb.y + (gw[1] >> 3)) * nb.z + (gw[2] >> 3);
+        srec[io] = make_double4(s[0], s[1], s[2], q[i]);
+        g0u[io] = make_int4(g[0], g[1], g[2], bin);
     }
-    const int bin = ((gw[0] >> 3) * nb.y + (gw[1] >> 3)) * nb.z + (gw[2] >> 3);
-    srec[io] = make_double4(s[0], s[1], s[2], q[i]);
-    g0u[io] = make_int4(g[0], g[1], g[2], bin);
-    rank[io] = atomicAdd(&cnt[bin], 1);
+    const int r = wave_agg_inc(cnt, bin, valid);
+    if (valid) rank[io] = r;
+    if (!last_block_done(ticket)) return;
+    block_counts_to_bounds<256>(nb.x * nb.y * nb.z, cnt, start, nullptr, true, sh);
 }
 
-constexpr int kGScan = 1024;
-
-__global__ void __launch_bounds__(kGScan) k_g_scan(int nbins, const int* __restrict__ cnt, int* __restrict__ start) {
-    __shared__ int sh[kGScan];
-    const int t = threadIdx.x;
-    const int per = (nbins + kGScan - 1) / kGScan;
-    const int b0 = min(nbins, t * per), b1 = min(nbins, b0 + per);
-    int sum = 0;
-    for (int b = b0; b < b1; b++) sum += cnt[b];
-    sh[t] = sum;
-    __syncthreads();
-    for (int off = 1; off < kGScan; off <<= 1) {
-        int u = t >= off ? sh[t - off] : 0;
-        __syncthreads();
-        sh[t] += u;
-        __syncthreads();
-    }
-    int run = sh[t] - sum;
-    for (int b = b0; b < b1; b++) {
-        start[b] = run;
-        run += cnt[b];
-    }
-    if (t == kGScan - 1) start[nbins] = sh[t];
-}
-
-// also re-zeroes the bin counts (consumed by k_g_scan) for the next evaluation
+// also re-zeroes the bin counts (consumed by k_g_bin's bounds) for the next evaluation
 __global__ void __launch_bounds__(256) k_g_scatter(int nown, const int4* __restrict__ g0u, const int* __restrict__ rank,
                                                    const int* __restrict__ start, int* __restrict__ tmp, int nbins,
                                                    int* __restrict__ cnt) {
@@ -183,63 +168,68 @@ __global__ void __launch_bounds__(256) k_g_scatter(int nown, const int4* __restr
     tmp[start[g0u[io].w] + rank[io]] = io;
 }
 
-// one wave per bin: slot of each member = bin start + number of members with a smaller index
-__global__ void __launch_bounds__(256) k_g_order(int nbins, const int* __restrict__ start,
-                                                 const int* __restrict__ tmp, int* __restrict__ order) {
-    __shared__ int mem[4][256];
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int b = blockIdx.x * 4 + w;
-    if (b >= nbins) return;
-    const int b0 = start[b], m = start[b + 1] - b0;
-    const int* src = tmp + b0;
-    if (m <= 256) {
-        for (int e = lane; e < m; e += 64) mem[w][e] = src[e];
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        src = mem[w];
-    }
-    for (int e = lane; e < m; e += 64) {
-        const int v = src[e];
-        int r = 0;
-        for (int j = 0; j < m; j++) r += src[j] < v;
-        order[b0 + r] = v;
-    }
-}
-
 // taps of every sorted atom in bin-aligned rows: taps[slot][d][p], p in [0, 24), is the
 // kernel weight of grid point 8*bin_d + p (tap m = p - (g0_d mod 8); zero outside 0 <= m < W),
 // q folded into the x row.  A tile db tiles ahead of the atom's bin then reads the fixed
 // window p = 8*db + i, so no per-atom offset is needed to address the taps.
 constexpr int kRow = 24;
 constexpr int kTapStride = 3 * kRow;
+constexpr int kOrderLdsG = 512;   // bin members staged in LDS (denser bins read global memory)
 
-__global__ void __launch_bounds__(256) k_g_taps(int nown, int W, double beta, int3 ng, const int* __restrict__ order,
-                                                const double4* __restrict__ srec, const int4* __restrict__ g0u,
-                                                double* __restrict__ taps, int4* __restrict__ g0s) {
-    // one thread per (slot, 16-byte pair p of the slot's 72 values): consecutive lanes write
-    // consecutive 16 B, so every store instruction of a wave is one contiguous 1 KB run
+// one 256-thread block per bin: slot of each member = bin start + number of members with a
+// smaller atom index (the order of a stable sort), then the block writes the members' tap
+// rows, one thread per 16-byte pair of a row, so consecutive threads store consecutive 16 B
+// of the bin's contiguous slot range (one launch for the order and the taps)
+__global__ void __launch_bounds__(256) k_g_order_taps(int nbins, const int* __restrict__ start,
+                                                      const int* __restrict__ tmp, int* __restrict__ order, int W,
+                                                      double beta, int3 ng, const double4* __restrict__ srec,
+                                                      const int4* __restrict__ g0u, double* __restrict__ taps,
+                                                      int4* __restrict__ g0s) {
+    __shared__ int mem[kOrderLdsG];
+    __shared__ int srt[kOrderLdsG];
     constexpr int kPairs = kTapStride / 2;   // 36
-    const int t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= nown * kPairs) return;
-    const int slot = t / kPairs, pp = t - kPairs * slot;
-    const int d = pp / (kRow / 2), p0 = 2 * (pp - d * (kRow / 2));   // axis, first point of the pair
-    const int io = order[slot];
-    const double4 sr = srec[io];
-    const int4 g = g0u[io];
-    const double sd = d == 0 ? sr.x : (d == 1 ? sr.y : sr.z);
-    const int g0 = d == 0 ? g.x : (d == 1 ? g.y : g.z);
-    const int r = g0 & 7;   // == wrapped g0 mod 8 (ng is a multiple of 8)
-    const double scale = d == 0 ? sr.w : 1.0;
-    double v[2];
-#pragma unroll
-    for (int e = 0; e < 2; e++) {
-        const int m = p0 + e - r;   // tap index of bin-aligned point p0 + e
-        v[e] = (m >= 0 && m < W) ? scale * es_val((double)(g0 + m) - sd, 2.0 / W, beta) : 0.0;
+    const int b = blockIdx.x;
+    const int b0 = start[b], m = start[b + 1] - b0;
+    if (m == 0) return;   // block-uniform
+    const int* src = tmp + b0;
+    const bool in_lds = m <= kOrderLdsG;
+    if (in_lds) {
+        for (int e = threadIdx.x; e < m; e += 256) mem[e] = src[e];
+        __syncthreads();
+        src = mem;
     }
-    reinterpret_cast<v2d*>(taps)[(size_t)slot * kPairs + pp] = v2d{v[0], v[1]};
-    if (pp == 0)
-        g0s[slot] = make_int4(g.x < 0 ? g.x + ng.x : g.x, g.y < 0 ? g.y + ng.y : g.y, g.z < 0 ? g.z + ng.z : g.z, io);
+    for (int e = threadIdx.x; e < m; e += 256) {
+        const int v = src[e];
+        int r = 0;
+        for (int j = 0; j < m; j++) r += src[j] < v;
+        order[b0 + r] = v;
+        if (in_lds) srt[r] = v;
+    }
+    if (in_lds) __syncthreads();
+    else __threadfence_block();   // order[] stores of this block, read back below
+    if (!in_lds) __syncthreads();
+    const int* so = in_lds ? srt : order + b0;
+    for (int e = threadIdx.x; e < m * kPairs; e += 256) {
+        const int u = e / kPairs, pp = e - kPairs * u;
+        const int d = pp / (kRow / 2), p0 = 2 * (pp - d * (kRow / 2));   // axis, first point of the pair
+        const int io = so[u];
+        const double4 sr = srec[io];
+        const int4 g = g0u[io];
+        const double sd = d == 0 ? sr.x : (d == 1 ? sr.y : sr.z);
+        const int g0 = d == 0 ? g.x : (d == 1 ? g.y : g.z);
+        const int r = g0 & 7;   // == wrapped g0 mod 8 (ng is a multiple of 8)
+        const double scale = d == 0 ? sr.w : 1.0;
+        double v[2];
+#pragma unroll
+        for (int k = 0; k < 2; k++) {
+            const int mm = p0 + k - r;   // tap index of bin-aligned point p0 + k
+            v[k] = (mm >= 0 && mm < W) ? scale * es_val((double)(g0 + mm) - sd, 2.0 / W, beta) : 0.0;
+        }
+        const size_t slot = (size_t)b0 + u;
+        reinterpret_cast<v2d*>(taps)[slot * kPairs + pp] = v2d{v[0], v[1]};
+        if (pp == 0)
+            g0s[slot] = make_int4(g.x < 0 ? g.x + ng.x : g.x, g.y < 0 ? g.y + ng.y : g.y, g.z < 0 ? g.z + ng.z : g.z, io);
+    }
 }
 
 // ---------------------------------------------------------------------------------
@@ -893,14 +883,11 @@ void launch_grid_sort(Handle& h, const double* pos) {
     const double3 L = make_double3(h.box_L[0], h.box_L[1], h.box_L[2]);
     // g_cnt is zero here: cleared at cf_create and by k_g_scatter of the previous evaluation
     hipLaunchKernelGGL(k_g_bin, dim3(nblk(nown, 256)), dim3(256), 0, h.stream, h.lo, nown, pos, h.q, L, ng, p.W,
-                       nb, h.g_srec, h.g_g0u, h.g_rank, h.g_cnt, h.g_xrange);
-    hipLaunchKernelGGL(k_g_scan, dim3(1), dim3(kGScan), 0, h.stream, p.nbins, h.g_cnt, h.g_start);
+                       nb, h.g_srec, h.g_g0u, h.g_rank, h.g_cnt, h.g_xrange, h.e_ticket + kTicketGrid, h.g_start);
     hipLaunchKernelGGL(k_g_scatter, dim3(nblk(nown, 256)), dim3(256), 0, h.stream, nown, h.g_g0u, h.g_rank, h.g_start,
                        h.g_tmp, p.nbins, h.g_cnt);
-    hipLaunchKernelGGL(k_g_order, dim3(nblk(p.nbins, 4)), dim3(256), 0, h.stream, p.nbins, h.g_start, h.g_tmp,
-                       h.g_order);
-    hipLaunchKernelGGL(k_g_taps, dim3(nblk((int64_t)nown * (kTapStride / 2), 256)), dim3(256), 0, h.stream, nown, p.W, p.beta,
-                       ng, h.g_order, h.g_srec, h.g_g0u, h.g_taps, h.g_g0s);
+    hipLaunchKernelGGL(k_g_order_taps, dim3(p.nbins), dim3(256), 0, h.stream, p.nbins, h.g_start, h.g_tmp,
+                       h.g_order, p.W, p.beta, ng, h.g_srec, h.g_g0u, h.g_taps, h.g_g0s);
 }
 
 #define CF_GRID_W_DISPATCH(W_, CALL) \
