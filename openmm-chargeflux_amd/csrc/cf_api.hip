@@ -113,6 +113,7 @@ void alloc_nlist(cf_handle* H, double skin) {
     double r = h.cutoff + skin;
     double mean = 4.0 / 3.0 * M_PI * r * r * r * h.n / V;
     int cap = (int)std::min<double>(h.n, 0.5 * mean + 64);
+    cap = (cap + 3) / 4 * 4;   // whole 4-entry chunks (list layout, cf_kernels_core.hip nl_index)
     if (h.nl && cap <= h.nb_cap) return;
     const size_t rows = std::max(h.hi - h.lo, 1);  // one row per owned atom
     dfree(H, h.nl);

@@ -359,6 +359,20 @@ struct DirectArgs {
 
 __device__ __forceinline__ int own_slot(const DirectArgs& a, int c) { return a.own_s ? a.own_s[c] : c; }
 
+// List layout: sub-list seg of row c holds its entries in chunks of kChunk = 4 consecutive
+// entries (16 B), chunk q of every row contiguous in row order:
+//   nl[((seg * nb_cap/4 + q) * nlr + c) * 4 + (k & 3)],  q = k / 4.
+// The builder's lane c then fills whole 16-B granules (and, with its 7 neighbours, whole
+// 128-B lines) instead of scattering single 4-B entries over lines shared with 63 other rows
+// at different fill levels (which evicted partly written lines: ~4x write amplification);
+// the pair walk loads a chunk of 4 entries per lane with one 16-B load, 16 rows of a wave
+// reading 256 contiguous bytes per sub-list.
+constexpr int kChunk = 4;
+typedef int v4i __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ size_t nl_index(const DirectArgs& a, int seg, int k, int c) {
+    return ((size_t)(seg * (a.nb_cap / kChunk) + (k >> 2)) * a.nlr + c) * kChunk + (k & 3);
+}
+
 __device__ __forceinline__ bool in_excl(int j, const int* reg, int cnt, const int* ex_list, int ex0) {
     int m = cnt < kMaxRegExcl ? cnt : kMaxRegExcl;
 #pragma unroll
@@ -435,7 +449,7 @@ __global__ void __launch_bounds__(256) k_nlist(DirectArgs a) {
         int cnt = 0;
         scan_cells(a, s, pi, a.rl2, [&](int t, int code, double, double, double, double) {
             if (exc && in_excl(a.atom_sorted[t], reg, exc, a.ex_list, ex0)) return;
-            if (cnt < a.nb_cap) a.nl[((size_t)seg * a.nb_cap + cnt) * a.nlr + c] = t | ((a.typ_s ? a.typ_s[t] : code) << kShiftBits);
+            if (cnt < a.nb_cap) a.nl[nl_index(a, seg, cnt, c)] = t | ((a.typ_s ? a.typ_s[t] : code) << kShiftBits);
             cnt++;
         }, seg, kSeg);
         a.nl_cnt[(size_t)seg * a.nlr + c] = cnt;
@@ -478,7 +492,6 @@ __global__ void __launch_bounds__(kWaveNL * kSeg) k_nlist_wave(DirectArgs a) {
     const int i = a.atom_sorted[s];
     const double4 pi = a.pos4s[s];
     const int key = a.key_sorted[s];
-    const size_t seg_off = (size_t)seg * a.nb_cap;
     const int cl[3] = {key / (a.nc.y * a.nc.z), (key / a.nc.z) % a.nc.y, key % a.nc.z};
     const int key0 = a.key_sorted[__shfl(s, 0)];
     const int c0[3] = {key0 / (a.nc.y * a.nc.z), (key0 / a.nc.z) % a.nc.y, key0 % a.nc.z};
@@ -511,7 +524,7 @@ __global__ void __launch_bounds__(kWaveNL * kSeg) k_nlist_wave(DirectArgs a) {
     // high bits of a list entry: the partner's LJ type when types are used, else the image code
     auto emit = [&](int t, int j, int hb) {
         if (j >= ex_min && j <= ex_max && in_excl(j, reg, exc, a.ex_list, ex0)) return;
-        if (cnt < a.nb_cap) a.nl[(seg_off + cnt) * a.nlr + c] = t | (hb << kShiftBits);
+        if (cnt < a.nb_cap) a.nl[nl_index(a, seg, cnt, c)] = t | (hb << kShiftBits);
         cnt++;
     };
     if (!fits) {  // wave-uniform (and block-uniform: every wave sees the same 64 atoms)
@@ -779,15 +792,55 @@ __global__ void __launch_bounds__(256) k_recip_add(int lo, int nown, int nparts,
     f_part[3 * i + 2] += rz;
 }
 
+// Walk the entries of one sub-list that belong to this lane (chunks q = part, part + step,
+// ...) as a software pipeline: the gather of the next entry is in flight while the current
+// one is evaluated, list chunks are loaded two chunks ahead (non-temporal: streamed once,
+// L2 is kept for the coordinates), unrolled over two chunk registers (A, B) so that no
+// freshly loaded value is ever copied (a register move of a pending load makes the compiler
+// drain vmcnt).  Entries at or past cnt are gathered from slot 0 (always valid memory: the
+// chunk may hold stale values there) and not evaluated.
+template <class G, class E>
+__device__ __forceinline__ void walk_list(const v4i* __restrict__ nl4, size_t stride, int cnt, int part, int step,
+                                          G&& gather, E&& eval) {
+    if (kChunk * part >= cnt) return;
+    const int qlast = (cnt - 1) / kChunk;
+    auto chunk = [&](int q) { return __builtin_nontemporal_load(nl4 + (size_t)min(q, qlast) * stride); };
+    v4i A = chunk(part), B = chunk(part + step);
+    auto c0 = gather(A.x, true);
+    for (int q = part; kChunk * q < cnt; q += 2 * step) {
+        const int k = kChunk * q;
+        auto c1 = gather(A.y, k + 1 < cnt);
+        eval(c0);
+        c0 = gather(A.z, k + 2 < cnt);
+        if (k + 1 < cnt) eval(c1);
+        c1 = gather(A.w, k + 3 < cnt);
+        A = chunk(q + 2 * step);
+        if (k + 2 < cnt) eval(c0);
+        const int kb = kChunk * (q + step);
+        c0 = gather(B.x, kb < cnt);
+        if (k + 3 < cnt) eval(c1);
+        if (kb >= cnt) break;
+        c1 = gather(B.y, kb + 1 < cnt);
+        eval(c0);
+        c0 = gather(B.z, kb + 2 < cnt);
+        if (kb + 1 < cnt) eval(c1);
+        c1 = gather(B.w, kb + 3 < cnt);
+        B = chunk(q + 3 * step);
+        if (kb + 2 < cnt) eval(c0);
+        c0 = gather(A.x, kb + kChunk * step < cnt);
+        if (kb + 3 < cnt) eval(c1);
+    }
+}
+
 // 4b: walk the list — kSeg adjacent lanes per atom, lane g walks sub-list g; partial sums
 // are combined with two xor-shuffles (fixed order: deterministic).  Atoms with an
 // overflowed sub-list are left to k_excl (cell rescan).
 // LPA lanes per atom (4, 8 or 16; more when few atoms are owned, so the grid still fills
-// the chip): lane g walks entries g/4, g/4 + LPA/4, ... of sub-list g%4.
+// the chip): lane g walks chunks g/4, g/4 + LPA/4, ... of sub-list g%4.
 // TYPES: the partner's LJ parameters come from the per-type table (LDS) indexed by the high
 // bits of the list entry instead of a third gathered 16-B load per candidate.
 template <int LPA, bool TYPES>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 8))) k_pairs(DirectArgs a) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) k_pairs(DirectArgs a) {
     __shared__ double tab[kErfcMaxM * (kErfcDeg + 1)];
     __shared__ double2 ljt[kMaxLjTypes];
     if (TYPES)
@@ -809,45 +862,28 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 8))
     if (active) {
         const double4 pi = a.pos4s[ss];
         const double2 li = a.ljs[ss];
-        const int* nl = a.nl + (size_t)seg * a.nb_cap * a.nlr + cc;
-        constexpr int step = LPA / kSeg;
+        const v4i* nl4 = reinterpret_cast<const v4i*>(a.nl) + (size_t)seg * (a.nb_cap / kChunk) * a.nlr + cc;
         constexpr int kMask = (1 << kShiftBits) - 1;
-        // software pipeline: list entries k + step .. k + 4*step (streamed from HBM) and the
-        // coordinates of entry k + step (L2) are in flight while entry k is evaluated
-        // (out-of-range entries read atom 0, unused).  The pair vector is the minimum image
-        // d - L rint(d/L) (getDeltaRPeriodic's floor(d/L + 0.5) up to exact half-box ties,
-        // which lie beyond the cutoff), so the image code stored in the list is not needed.
-        // Unrolled by two with ping-pong registers (A, B) so that no freshly loaded value is
-        // ever copied (a register move of a pending load makes the compiler drain vmcnt); list
-        // loads are branch-free (row clamped into the list, value replaced after the load).
-        const int klast = cnt > 0 ? cnt - 1 : 0;
-        auto entry = [&](int kk) {  // streamed once: non-temporal, keeps L2 for the coordinates
-            const int v = __builtin_nontemporal_load(nl + (size_t)min(kk, klast) * a.nlr);
-            return kk < cnt ? v : 0;
+        struct Cand { double4 p; double2 lj; };
+        auto gather = [&](int e, bool ok) {
+            const int t = ok ? (e & kMask) : 0;
+            Cand cd;
+            cd.p = a.pos4s[t];
+            cd.lj = TYPES ? ljt[(unsigned)e >> kShiftBits] : a.ljs[t];
+            return cd;
         };
-        auto eval = [&](const double4& pj, const double2& lj2) {
-            double dx = pi.x - pj.x, dy = pi.y - pj.y, dz = pi.z - pj.z;
+        // The pair vector is the minimum image d - L rint(d/L) (getDeltaRPeriodic's
+        // floor(d/L + 0.5) up to exact half-box ties, which lie beyond the cutoff), so the
+        // image code stored in the list is not needed.
+        auto eval = [&](const Cand& cd) {
+            double dx = pi.x - cd.p.x, dy = pi.y - cd.p.y, dz = pi.z - cd.p.z;
             dx -= a.L.x * rint(dx * a.invL.x);
             dy -= a.L.y * rint(dy * a.invL.y);
             dz -= a.L.z * rint(dz * a.invL.z);
             const double r2 = dx * dx + dy * dy + dz * dz;
-            if (r2 <= a.rc2) pair_term(acc, a, tab, pi, li, pj, lj2, dx, dy, dz, r2);  // exact voxel-hash test
+            if (r2 <= a.rc2) pair_term(acc, a, tab, pi, li, cd.p, cd.lj, dx, dy, dz, r2);  // exact voxel-hash test
         };
-        const int i0 = entry(part);
-        int iB = entry(part + step), iA = entry(part + 2 * step);
-        double4 pA = a.pos4s[i0 & kMask];
-        double2 lA = TYPES ? ljt[(unsigned)i0 >> kShiftBits] : a.ljs[i0 & kMask];
-        for (int k = part; k < cnt; k += 2 * step) {
-            // state: pA/lA = entry k, iB = index of k+step, iA = index of k+2step
-            const double4 pB = a.pos4s[iB & kMask];
-            const double2 lB = TYPES ? ljt[(unsigned)iB >> kShiftBits] : a.ljs[iB & kMask];
-            iB = entry(k + 3 * step);
-            eval(pA, lA);
-            pA = a.pos4s[iA & kMask];
-            lA = TYPES ? ljt[(unsigned)iA >> kShiftBits] : a.ljs[iA & kMask];
-            iA = entry(k + 4 * step);
-            if (k + step < cnt) eval(pB, lB);
-        }
+        walk_list(nl4, a.nlr, cnt, part, LPA / kSeg, gather, eval);
     }
 #pragma unroll
     for (int m = 1; m < LPA; m <<= 1) {
@@ -936,42 +972,30 @@ __global__ void __launch_bounds__(256) k_pairs_mixed(DirectArgs a) {
         const float3 L = make_float3((float)a.L.x, (float)a.L.y, (float)a.L.z);
         const float3 iL = make_float3((float)a.invL.x, (float)a.invL.y, (float)a.invL.z);
         const float rc2 = (float)a.rc2, alpha = (float)a.alpha;
-        const int* nl = a.nl + (size_t)seg * a.nb_cap * a.nlr + cc;
-        constexpr int step = LPA / kSeg;
+        const v4i* nl4 = reinterpret_cast<const v4i*>(a.nl) + (size_t)seg * (a.nb_cap / kChunk) * a.nlr + cc;
         constexpr int kMask = (1 << kShiftBits) - 1;
-        const int klast = cnt > 0 ? cnt - 1 : 0;
-        auto entry = [&](int kk) {
-            const int v = __builtin_nontemporal_load(nl + (size_t)min(kk, klast) * a.nlr);
-            return kk < cnt ? v : 0;
+        struct Cand { float4 p; float2 lj; };
+        auto gather = [&](int e, bool ok) {
+            const int t = ok ? (e & kMask) : 0;
+            Cand cd;
+            cd.p = a.pos4f[t];
+            if (TYPES) {
+                cd.lj = ljt[(unsigned)e >> kShiftBits];
+            } else {
+                const double2 d = a.ljs[t];
+                cd.lj = make_float2((float)d.x, (float)d.y);
+            }
+            return cd;
         };
-        auto ljof = [&](int v) {
-            if (TYPES) return ljt[(unsigned)v >> kShiftBits];
-            const double2 d = a.ljs[v & kMask];
-            return make_float2((float)d.x, (float)d.y);
-        };
-        auto eval = [&](const float4& pj, const float2& lj2) {
-            float dx = pi.x - pj.x, dy = pi.y - pj.y, dz = pi.z - pj.z;
+        auto eval = [&](const Cand& cd) {
+            float dx = pi.x - cd.p.x, dy = pi.y - cd.p.y, dz = pi.z - cd.p.z;
             dx = fmaf(-L.x, rintf(dx * iL.x), dx);
             dy = fmaf(-L.y, rintf(dy * iL.y), dy);
             dz = fmaf(-L.z, rintf(dz * iL.z), dz);
             const float r2 = fmaf(dx, dx, fmaf(dy, dy, dz * dz));
-            if (r2 <= rc2) pair_term_f(acc, alpha, a.include_forces, tabf, escale, pi, li, pj, lj2, dx, dy, dz, r2);
+            if (r2 <= rc2) pair_term_f(acc, alpha, a.include_forces, tabf, escale, pi, li, cd.p, cd.lj, dx, dy, dz, r2);
         };
-        // same two-way software pipeline as k_pairs (ping-pong registers, branch-free loads)
-        const int i0 = entry(part);
-        int iB = entry(part + step), iA = entry(part + 2 * step);
-        float4 pA = a.pos4f[i0 & kMask];
-        float2 lA = ljof(i0);
-        for (int k = part; k < cnt; k += 2 * step) {
-            const float4 pB = a.pos4f[iB & kMask];
-            const float2 lB = ljof(iB);
-            iB = entry(k + 3 * step);
-            eval(pA, lA);
-            pA = a.pos4f[iA & kMask];
-            lA = ljof(iA);
-            iA = entry(k + 4 * step);
-            if (k + step < cnt) eval(pB, lB);
-        }
+        walk_list(nl4, a.nlr, cnt, part, LPA / kSeg, gather, eval);
     }
 #pragma unroll
     for (int m = 1; m < LPA; m <<= 1) {
