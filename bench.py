@@ -114,12 +114,13 @@ def pair_count(force, pos, box):
     return int(n_all - n_ex)
 
 
-def pmc_traffic(config, world, phase):
+def pmc_traffic(config, world, phase, precision):
     """HBM bytes per launch of the dominant kernel from the newest committed PMC summary
     (profiles/r*_c3_pmc_summary_*.json, written by tools/profile_round.sh from separate
     rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this same bench command, with the
-    gfx950 FETCH_SIZE x2 correction).  None when no profile matches this workload."""
-    if config != "C3" or world != 1:
+    gfx950 FETCH_SIZE x2 correction).  None when no profile matches this workload (the
+    profiles are of the default fp64 C3 command; mixed precision runs other kernels)."""
+    if config != "C3" or world != 1 or precision != "double":
         return None, None
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_c3_pmc_summary_*.json")))
@@ -270,7 +271,7 @@ def main():
         present = [k for k in alg if per_step.get(k, 0.0) > 0]
         t_dom = per_launch[dom] * 1e-3
         bound, abytes, aflops = alg[dom]
-        traffic, traffic_src = pmc_traffic(args.config, world, dom)
+        traffic, traffic_src = pmc_traffic(args.config, world, dom, args.precision)
         fp64_tflops = aflops / t_dom / 1e12
         if bound == "hbm":
             achieved, peak, unit = abytes / t_dom / 1e9, HBM_PEAK_GBS, "GB/s"
