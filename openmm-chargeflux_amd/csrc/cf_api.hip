@@ -508,8 +508,7 @@ CF_EXPORT int cf_create(const cf_params* p, const cf_options* opt, cf_handle** o
             set_cells(H, std::vector<double>{p->default_box[0], p->default_box[4], p->default_box[8]}.data());
             h.erfc_tab = dupload(H, cf::erfc_table(h.alpha * h.cutoff * (1.0 + 1e-9), &h.erfc_scale, &h.erfc_m));
             if (h.mixed) {
-                double sc; int m;
-                h.erfc_tab_f = dupload(H, cf::erfc_table_f(h.alpha * h.cutoff * (1.0 + 1e-6), &sc, &m));
+                h.erfc_tab_f = dupload(H, cf::erfc_table_f(h.alpha * h.cutoff * (1.0 + 1e-6), &h.erfc_scale_f, &h.erfc_m_f));
             }
             h.cell_key = dalloc<int>(H, n); h.cell_key_sorted = dalloc<int>(H, n);
             h.atom_val = dalloc<int>(H, n); h.atom_sorted = dalloc<int>(H, n);

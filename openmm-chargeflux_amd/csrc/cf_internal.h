@@ -185,6 +185,7 @@ struct Handle {
     // energy
     double* erfc_tab = nullptr;  // erfcx interval polynomials (cf_kernels_core.hip erfc_table)
     double erfc_scale = 0; int erfc_m = 0;
+    double erfc_scale_f = 0; int erfc_m_f = 0;   // fp32 table (mixed precision): its own interval width
     float* erfc_tab_f = nullptr; // fp32 erfcx table (mixed precision)
     double* terms_dev = nullptr; // [4]
     double* e_part = nullptr;    // [ceil(Nown/256)][3] energy block partials
@@ -197,9 +198,9 @@ struct Handle {
 };
 
 // ---- launchers (cf_kernels_*.hip) ------------------------------------------------
-std::vector<double> erfc_table(double xmax, double* scale, int* m);     // degree 12, fp64 pair kernel
+std::vector<double> erfc_table(double xmax, double* scale, int* m);     // width 1/16, degree 7, fp64 pair kernel
 std::vector<float> erfc_table_f(double xmax, double* scale, int* m);    // degree 6, mixed-precision kernel
-std::vector<double> erfc_table_deg(double xmax, int deg, double* scale, int* m);
+std::vector<double> erfc_table_deg(double xmax, int deg, double width, int max_m, double* scale, int* m);
 void launch_flux_terms(Handle& h, const double* pos);
 void launch_atoms_prep(Handle& h, const double* pos, bool skin_check);   // q, self term [, skin_flag |= moved > list_skin/2]
 void launch_cell_sort(Handle& h, const double* pos);
