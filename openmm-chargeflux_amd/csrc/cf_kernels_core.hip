@@ -709,15 +709,14 @@ __device__ __forceinline__ void pair_term(PairAcc& acc, const DirectArgs& a, con
     double s2 = inv_r * sig; s2 *= s2;
     double sig6 = s2 * s2 * s2;
     double es6 = sig6 * li.y * lj2.y;
-    double qq = ke * pi.w * pj.w * inv_r;
+    const double qj = ke * pj.w * inv_r;   // potential of j at i per unit erfc; qq = q_i qj
+    const double qq = pi.w * qj;
     if (a.include_forces) {
-        double inv_r2 = inv_r * inv_r;
-        double dEdR = qq * inv_r2 * (ec + ar * e2 * two_over_sqrtpi);
-        dEdR += es6 * (12 * sig6 - 6) * inv_r2;
+        const double dEdR = fma(qq, ec + ar * e2 * two_over_sqrtpi, es6 * (12 * sig6 - 6)) * (inv_r * inv_r);
         acc.fx += dEdR * dx; acc.fy += dEdR * dy; acc.fz += dEdR * dz;
-        acc.dq += ke * pj.w * inv_r * ec;
+        acc.dq += qj * ec;
     }
-    acc.e += 0.5 * (qq * ec + es6 * (sig6 - 1));
+    acc.e += qq * ec + es6 * (sig6 - 1);   // the pair's full energy; halved once in store_pairs
 }
 
 // stage the erfcx table in LDS (all threads of the block; call before any early return)
@@ -727,9 +726,11 @@ __device__ __forceinline__ void load_erfc_tab(const DirectArgs& a, double* tab) 
 }
 
 // pair-loop results of atom i: raw direct-space sums (dE/dq_i without the self term, forces,
-// energy); k_excl then applies the exclusion correction and the self term in place
+// energy); k_excl then applies the exclusion correction and the self term in place.  Each
+// pair's energy is shared half-and-half by its two atoms (full list): the 1/2 is applied here
+// once per atom instead of once per pair (a power of two: the same bits either way).
 __device__ __forceinline__ void store_pairs(const PairAcc& acc, const DirectArgs& a, int i) {
-    a.e_atom[3 * i + 1] = acc.e;
+    a.e_atom[3 * i + 1] = 0.5 * acc.e;
     if (a.include_forces) {  // reciprocal partials are added by k_recip_add after the k-space pass
         a.dedq[i] = acc.dq;
         a.f_part[3 * i] = acc.fx;
@@ -941,7 +942,7 @@ __device__ __forceinline__ void pair_term_f(PairAccF& acc, float alpha, int incl
         acc.fz = fmaf(dEdR, dz, acc.fz);
         acc.dq = fmaf(ke * pj.w * inv_r, ec, acc.dq);
     }
-    acc.e += 0.5 * (double)fmaf(qq, ec, es6 * (sig6 - 1.0f));
+    acc.e += (double)fmaf(qq, ec, es6 * (sig6 - 1.0f));   // halved once in store_pairs
 }
 
 template <int LPA, bool TYPES>
