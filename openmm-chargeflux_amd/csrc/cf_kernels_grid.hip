@@ -320,10 +320,21 @@ __global__ void __launch_bounds__(512) k_g_spread(int3 ng, int3 nb, const int* _
     const int lane = threadIdx.x & 63, w = wave_id();
     const int ka = lane >> 4, jh = (lane >> 3) & 1, k = lane & 7;   // atom-in-group, y half, z column
     const int nbbz = (nb.z + 1) >> 1, nbby = (nb.y + 1) >> 1;
-    // default round-robin block order: on a multi-rank run the work sits in one x-slab, which an
-    // XCD-contiguous mapping would put on a single XCD
-    const int blk = blockIdx.x;
-    const int BZ = blk % nbbz, BY = (blk / nbbz) % nbby, BX = blk / (nbbz * nbby);
+    // XCD-aware block order: the hardware deals workgroups to the 8 XCDs round-robin, so XCD
+    // blockIdx % 8 is given a contiguous 1/8 of the (y, z) block plane over every x -- the blocks
+    // that share source bins then share that XCD's L2, and an x-slab (multi-rank run) still
+    // spreads over all 8 XCDs.  Plain order when the (y, z) plane does not split by 8.
+    const int nyz = nbby * nbbz;
+    int BX, yz;
+    if (nyz % 8 == 0) {
+        const int per = nyz / 8, i = blockIdx.x / 8;
+        yz = (blockIdx.x % 8) * per + i % per;
+        BX = i / per;
+    } else {
+        yz = blockIdx.x % nyz;
+        BX = blockIdx.x / nyz;
+    }
+    const int BY = yz / nbbz, BZ = yz % nbbz;
     if (!x_range_in_slab(16 * BX, min(16 * BX + 15, ng.x - 1), xr, W, ng.x)) return;
     const int wx = (w >> 2) & 1, wy = (w >> 1) & 1, wz = w & 1;
     const int tx = 2 * BX + wx, ty = 2 * BY + wy, tz = 2 * BZ + wz;
@@ -689,7 +700,14 @@ __global__ void __launch_bounds__(kInterpThreads) k_g_interp(int3 ng, int3 nb, c
     constexpr int NJ = (W + 3) / 4;
     extern __shared__ double sg[];   // [R][R][R]
     __shared__ double2 xt[kInterpThreads / 64][16];   // per wave: the current atom's x taps (v, dv)
-    const int tile = blockIdx.x;
+    // XCD-aware tile order (as in k_g_spread): XCD blockIdx % 8 takes a contiguous 1/8 of the
+    // (y, z) tile plane over every x, so neighbouring tiles' potential halos share its L2
+    const int nyz = nb.y * nb.z;
+    int tile = blockIdx.x;
+    if (nyz % 8 == 0) {
+        const int per = nyz / 8, i = blockIdx.x / 8;
+        tile = (i / per) * nyz + (blockIdx.x % 8) * per + i % per;
+    }
     const int s0 = start[tile], s1 = start[tile + 1];
     if (s0 == s1) return;
     const int tz = tile % nb.z, ty = (tile / nb.z) % nb.y, tx = tile / (nb.z * nb.y);
