@@ -32,7 +32,8 @@ from openmmcoul import testsystems as ts  # noqa: E402
 from openmmcoul.distributed import ShardedCoulKernel  # noqa: E402
 
 METRIC = "ns/day + ms/force-eval, periodic charge-flux box, 1/2/4/8 MI355X"
-FP64_MFMA_PEAK_TFLOPS = 78.6   # MI355X dense FP64 matrix (= FP64 vector) peak, vendor spec
+FP64_PEAK_TFLOPS = 78.6   # MI355X FP64 vector (= dense FP64 matrix) peak, vendor spec
+FP32_PEAK_TFLOPS = 157.3  # MI355X FP32 vector peak (the mixed-precision pair kernel)
 HBM_PEAK_GBS = 8000.0
 K_OH, R_OH0 = 345000.0, 0.09572      # harness restraints (kJ/mol/nm^2, nm)
 K_HH, R_HH0 = 230000.0, 0.15139
@@ -72,21 +73,45 @@ class MDHarness:
         assert rc == 0
 
 
+# Calibration of the oracle's serial timing against the compiled reference kernel
+# (measured in the survey session on this image's build host): oracle time /
+# reference time, measured by tools/calibrate_cpu.py in the same container.
+CPU_CALIBRATION = os.path.join(ROOT, "profiles", "cpu_calibration.json")
+
+
+def host_cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(force, pos, box, k_sample):
     from oracle import Oracle
     o = Oracle(force, box)
     tn, tr, kt = o.time_sample(pos, box, k_sample)
     t_eval = tn + tr * kt / k_sample
+    cal = ""
+    if os.path.exists(CPU_CALIBRATION):
+        c = json.load(open(CPU_CALIBRATION))
+        cal = (f"; oracle/compiled-reference time ratio {c['ratio_summary']} measured on the build host "
+               f"({c['host']}), tools/calibrate_cpu.py")
     return {
         "value": 0.0864 / t_eval,   # ns/day at dt = 1 fs (t_eval in s), force evaluation only
         "unit": "ns/day",
         "cores": 1,
         "kind": "port",
         "ms_per_force_eval": t_eval * 1e3,
+        "host_cpu": host_cpu_model(),
+        "k_sample_fraction": round(k_sample / kt, 4),
         "sample": (f"C3 on the oracle (serial fp64 restatement of ReferenceCoulKernels.cpp, same "
-                   f"two-pass cos/sin k-loop, O(N) cell list), 1 host core: full flux/self/real-space/"
-                   f"exclusion/chain-rule part ({tn:.2f} s) + first {k_sample} of {kt} reciprocal "
-                   f"k-vectors ({tr:.2f} s), extrapolated linearly in K to {t_eval:.1f} s/eval"),
+                   f"two-pass cos/sin k-loop, O(N) cell list), 1 core of {host_cpu_model()}: full flux/self/"
+                   f"real-space/exclusion/chain-rule part ({tn:.2f} s) + first {k_sample} of {kt} reciprocal "
+                   f"k-vectors ({100.0 * k_sample / kt:.1f} % of K, {tr:.2f} s), extrapolated linearly in K to "
+                   f"{t_eval:.1f} s/eval" + cal),
     }
 
 
@@ -146,7 +171,8 @@ def main():
                     help="mixed: fp32 direct-space pair kernel (fp32 force / fp64 energy accumulation), W=8 grid")
     ap.add_argument("--no-exact-compare", action="store_true",
                     help="skip timing the exact k-sum path beside the grid path")
-    ap.add_argument("--cpu-k-sample", type=int, default=1500)
+    ap.add_argument("--cpu-k-sample", type=int, default=0,
+                    help="k-vectors of the CPU-baseline sample (0 = 10%% of K_half)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true",
                     help="no per-kernel HIP events in the timed steps (measures their overhead; no roofline)")
@@ -254,41 +280,57 @@ def main():
     if dom is not None and timing.get(dom, (0, 0))[1]:
         per_launch[dom] = timing[dom][0] / timing[dom][1]   # measured inside the timed region
     n_own = hi - lo
-    # algorithmic work per launch of each hot phase:
-    #  direct_pairs  (k_pairs alone) HBM bytes 4 P_c + 80 N (half list + per-atom in/out), fp64 flops 80 P_c
-    #  grid_spread   2 N W^3 flops (one FMA per atom x grid point of its support)
-    #  grid_interp   4 N W^3 flops (two FMAs per grid value: potential and x-gradient sums)
-    #  kspace_sfac / kspace_force (exact path)  4 / 8 flops per atom x half-space k-vector
+    # algorithmic work per launch of each hot phase: (HBM bytes,
+    # flops, compute pipe, its peak)
+    #  direct_pairs  (k_pairs alone) bytes 4 P_c + 80 N (int32 half list + per-atom in/out), flops 80 P_c
+    #                on the fp64 VALU (fp32 VALU for the mixed-precision kernel)
+    #  grid_spread   2 N W^3 fp64 VALU flops (one FMA per atom x grid point of its support), bytes 24 N W
+    #                (the atom's three tap rows) + 8 ng^3 (grid out)
+    #  grid_interp   4 N W^3 fp64 VALU flops (two FMAs per grid value), bytes 8 ng^3 + 24 N W + 32 N
+    #  kspace_sfac / kspace_force (exact path)  4 / 8 fp64 MFMA flops per atom x half-space k-vector
+    # fraction of the roof = max(B / BW, F / P) / t; "bound" names the larger term
     w_grid = args.grid_width or (8 if args.precision == "mixed" else 14)
     roofline, others = None, {}
     if dom is not None:
         p_c = pair_count(force, pos_np, box) * n_own / n
         units = float(n_own) * k_half
-        alg = {"direct_pairs": ("hbm", 4.0 * p_c + 80.0 * n_own, 80.0 * p_c),
-               "grid_spread": ("mfma", None, 2.0 * n_own * w_grid ** 3),
-               "grid_interp": ("mfma", None, 4.0 * n_own * w_grid ** 3),
-               "kspace_sfac": ("mfma", None, 4.0 * units), "kspace_force": ("mfma", None, 8.0 * units)}
+        ng3 = float(np.prod(kern.kernel.grid_shape())) if args.kspace_algo == 2 else 0.0
+        pair_pipe = ("valu", FP64_PEAK_TFLOPS) if args.precision == "double" else ("valu_fp32", FP32_PEAK_TFLOPS)
+        alg = {"direct_pairs": (4.0 * p_c + 80.0 * n_own, 80.0 * p_c) + pair_pipe,
+               "grid_spread": (24.0 * n_own * w_grid + 8.0 * ng3, 2.0 * n_own * w_grid ** 3, "valu", FP64_PEAK_TFLOPS),
+               "grid_interp": (8.0 * ng3 + 24.0 * n_own * w_grid + 32.0 * n_own, 4.0 * n_own * w_grid ** 3, "valu",
+                               FP64_PEAK_TFLOPS),
+               "kspace_sfac": (64.0 * n_own, 4.0 * units, "mfma", FP64_PEAK_TFLOPS),
+               "kspace_force": (64.0 * n_own, 8.0 * units, "mfma", FP64_PEAK_TFLOPS)}
+
+        def roof(k, t_ms):
+            b, f, pipe, peak_tf = alg[k]
+            t = t_ms * 1e-3
+            tb, tf = b / (HBM_PEAK_GBS * 1e9), f / (peak_tf * 1e12)
+            return {"bound": "hbm" if tb >= tf else pipe, "frac": max(tb, tf) / t, "gbs": b / t / 1e9,
+                    "tflops": f / t / 1e12, "peak_tflops": peak_tf, "alg_bytes": b, "alg_flops": f}
+
         present = [k for k in alg if per_step.get(k, 0.0) > 0]
-        t_dom = per_launch[dom] * 1e-3
-        bound, abytes, aflops = alg[dom]
+        r = roof(dom, per_launch[dom])
         traffic, traffic_src = pmc_traffic(args.config, world, dom, args.precision)
-        fp64_tflops = aflops / t_dom / 1e12
-        if bound == "hbm":
-            achieved, peak, unit = abytes / t_dom / 1e9, HBM_PEAK_GBS, "GB/s"
+        if r["bound"] == "hbm":
+            achieved, peak, unit = r["gbs"], HBM_PEAK_GBS, "GB/s"
         else:
-            achieved, peak, unit = fp64_tflops, FP64_MFMA_PEAK_TFLOPS, "TFLOP/s"
-        roofline = {"kernel": dom, "bound": bound, "achieved": round(achieved, 3), "peak": peak, "unit": unit,
-                    "frac": round(achieved / peak, 4), "traffic": traffic, "traffic_source": traffic_src,
-                    "alg_bytes_per_launch": abytes, "alg_flops_per_launch": aflops,
-                    "fp64_tflops": round(fp64_tflops, 3), "avg_launch_ms": per_launch[dom],
-                    "pairs_within_cutoff": int(p_c)}
+            achieved, peak, unit = r["tflops"], r["peak_tflops"], "TFLOP/s"
+        roofline = {"kernel": dom, "bound": r["bound"], "achieved": round(achieved, 3), "peak": peak, "unit": unit,
+                    "frac": round(r["frac"], 4), "traffic": traffic, "traffic_source": traffic_src,
+                    "traffic_ratio": round(traffic / r["alg_bytes"], 3) if traffic else None,
+                    "alg_bytes_per_launch": r["alg_bytes"], "alg_flops_per_launch": r["alg_flops"],
+                    "hbm_gbs": round(r["gbs"], 1), "tflops": round(r["tflops"], 3),
+                    "avg_launch_ms": per_launch[dom], "pairs_within_cutoff": int(p_c),
+                    "frac_definition": "max(alg_bytes/8 TB/s, alg_flops/peak)/t (SURVEY 8(d))"}
         others = {}
         for k in present:
             if k == dom:
                 continue
-            tk = per_launch[k] * 1e-3
-            others[k] = {"avg_launch_ms": round(per_launch[k], 4), "fp64_tflops": round(alg[k][2] / tk / 1e12, 3),
-                         "frac_fp64_peak": round(alg[k][2] / tk / 1e12 / FP64_MFMA_PEAK_TFLOPS, 4)}
+            rk = roof(k, per_launch[k])
+            others[k] = {"avg_launch_ms": round(per_launch[k], 4), "bound": rk["bound"], "frac": round(rk["frac"], 4),
+                         "tflops": round(rk["tflops"], 3), "hbm_gbs": round(rk["gbs"], 1)}
     exact = None
     if world == 1 and args.kspace_algo == 2 and not args.no_exact_compare:
         # the exact fp64 k-sum path (kspace_algo 0) timed beside the grid path on the same
@@ -319,7 +361,7 @@ def main():
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             log("[rank 0] timing CPU baseline sample ...")
-            cpu = cpu_baseline(force, pos_np, box, args.cpu_k_sample)
+            cpu = cpu_baseline(force, pos_np, box, args.cpu_k_sample or max(1, (k_half + 9) // 10))
         out = {
             "metric": METRIC, "value": round(ns_day, 4), "unit": "ns/day", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_step, 4), "higher_is_better": True,

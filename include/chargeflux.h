@@ -111,6 +111,9 @@ CF_EXPORT int cf_destroy(cf_handle* h);
 /* Ewald parameters chosen at initialize: alpha (nm^-1) and odd kmax per axis
  * (ReferenceCoulKernels.cpp:32-35, 401-420). */
 CF_EXPORT int cf_get_ewald_params(const cf_handle* h, double* alpha, int32_t kmax[3]);
+/* Grid of the kspace_algo 2 reciprocal path: points per axis and the ES kernel width
+ * (zeros for the exact k-sum paths and without PBC). */
+CF_EXPORT int cf_get_grid_shape(const cf_handle* h, int32_t ng[3], int32_t* width);
 /* Owned atom range [lo, hi) of this rank (all atoms when world_size <= 1). */
 CF_EXPORT int cf_get_owned_range(const cf_handle* h, int32_t* lo, int32_t* hi);
 /* Host-only (no device needed): the atom decomposition cf_create would use.  Ranges are

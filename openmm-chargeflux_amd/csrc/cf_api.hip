@@ -513,7 +513,6 @@ CF_EXPORT int cf_create(const cf_params* p, const cf_options* opt, cf_handle** o
             h.cell_key = dalloc<int>(H, n); h.cell_key_sorted = dalloc<int>(H, n);
             h.atom_val = dalloc<int>(H, n); h.atom_sorted = dalloc<int>(H, n);
             h.pos4s = dalloc<double4>(H, n);
-            if (h.mixed) h.pos4f = dalloc<float4>(H, n);
             h.ljs = dalloc<double2>(H, n);
             // LJ types: exact-equal (sigma/2, 2 sqrt eps) pairs; <= 64 types ride in the list entries
             {
@@ -721,6 +720,15 @@ CF_EXPORT int cf_get_ewald_params(const cf_handle* H, double* alpha, int32_t kma
     return CF_OK;
 }
 
+CF_EXPORT int cf_get_grid_shape(const cf_handle* H, int32_t ng[3], int32_t* width) {
+    if (!H) { g_err = "null handle"; return CF_ERR_INVALID; }
+    const bool grid = H->h.pbc && H->h.kspace_algo == 2;
+    if (ng)
+        for (int d = 0; d < 3; d++) ng[d] = grid ? H->h.gp.ng[d] : 0;
+    if (width) *width = grid ? H->h.gp.W : 0;
+    return CF_OK;
+}
+
 CF_EXPORT int cf_get_owned_range(const cf_handle* H, int32_t* lo, int32_t* hi) {
     if (!H) { g_err = "null handle"; return CF_ERR_INVALID; }
     if (lo) *lo = H->h.lo;
@@ -772,10 +780,11 @@ CF_EXPORT int cf_compute_begin(cf_handle* H, const double* pos_dev, const double
                     Timed t(H, PH_SFAC);
                     cf::launch_kspace_direct_sfac(h, pos_dev);
                 }
-            } else if (forces || energy) {
+            } else if (forces || energy) {   // no owned atoms: a zero partial S(k) (all-reduced by the caller)
                 int64_t cnt = 0;
                 double* buf = cf::kspace_reduce_buffer(h, &cnt);
                 check_hip(hipMemsetAsync(buf, 0, sizeof(double) * cnt, h.stream), "memset S");
+                if (h.kspace_algo == 1) cf::launch_kspace_kvec(h);   // read by the coefficient pass
             }
         }
         h.n_evals++;
@@ -833,14 +842,17 @@ CF_EXPORT int cf_compute_end(cf_handle* H, double* forces_dev, double* energy_de
         h.pending_flags = -1;
         const int forces = flags & CF_INCLUDE_FORCES, energy = flags & CF_INCLUDE_ENERGY;
         const double* pos = H->pos_pending;
+        // the reciprocal energy is added by rank 0 (launch_assemble_energy) from the all-reduced
+        // buffer, so rank 0 runs the coefficient pass even when it owns no atoms (its begin
+        // zeroed its partial buffer, which the caller's all-reduce then filled)
+        if (h.pbc && (forces || energy) && (h.hi > h.lo || h.rank == 0)) {
+            Timed t(H, PH_COEFFS);
+            if (h.kspace_algo == 0) cf::launch_kspace_coeffs(h, energy);
+            else if (h.kspace_algo == 2) cf::launch_grid_coeffs(h, energy);
+            else cf::launch_kspace_direct_coeffs(h, energy);
+        }
         if (h.hi > h.lo) {
             if (h.pbc) {
-                if (forces || energy) {
-                    Timed t(H, PH_COEFFS);
-                    if (h.kspace_algo == 0) cf::launch_kspace_coeffs(h, energy);
-                    else if (h.kspace_algo == 2) cf::launch_grid_coeffs(h, energy);
-                    else cf::launch_kspace_direct_coeffs(h, energy);
-                }
                 if (forces && h.kspace_algo == 2) {
                     { Timed t(H, PH_GDFTI); cf::launch_grid_dft_inv(h); }
                     { Timed t(H, PH_GINTERP); cf::launch_grid_interp(h); }   // adds into dE/dq and forces

@@ -122,7 +122,6 @@ struct Handle {
     int* atom_val = nullptr; int* atom_sorted = nullptr;
     int* cell_start = nullptr; int* cell_end = nullptr; int* cell_cnt = nullptr;
     double4* pos4s = nullptr;   // [N] sorted wrapped (x,y,z,q)
-    float4* pos4f = nullptr;    // [N] the same in fp32 (mixed precision only)
     double2* ljs = nullptr;     // [N] sorted LJ
     int lj_ntypes = 0;          // distinct (sigma/2, 2 sqrt eps) pairs if <= 64, else 0
     int* atom_type = nullptr;   // [N] LJ type per atom
@@ -221,6 +220,7 @@ void launch_kspace_coeffs(Handle& h, int include_energy);
 void launch_kspace_force(Handle& h, const double* pos);
 
 // direct VALU reference path of the reciprocal sum (kspace_algo = 1)
+void launch_kspace_kvec(Handle& h);   // k-vectors and weights of the current box (direct path)
 void launch_kspace_direct_sfac(Handle& h, const double* pos);
 void launch_kspace_direct_coeffs(Handle& h, int include_energy);
 void launch_kspace_direct_force(Handle& h, const double* pos);

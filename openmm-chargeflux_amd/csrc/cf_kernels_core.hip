@@ -284,8 +284,7 @@ __global__ void __launch_bounds__(256) k_cell_commit(int n, const int* __restric
                                                      int* __restrict__ key_s, int* __restrict__ idx_s,
                                                      double4* __restrict__ pos4s, double2* __restrict__ ljs,
                                                      const int* __restrict__ atype, int* __restrict__ typ_s,
-                                                     double* __restrict__ pos_ref, long long* __restrict__ n_builds,
-                                                     float4* __restrict__ pos4f) {
+                                                     double* __restrict__ pos_ref, long long* __restrict__ n_builds) {
     int s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= n) return;
     double4 p4;
@@ -307,7 +306,6 @@ __global__ void __launch_bounds__(256) k_cell_commit(int n, const int* __restric
                           q[i]);
     }
     pos4s[s] = p4;
-    if (pos4f) pos4f[s] = make_float4((float)p4.x, (float)p4.y, (float)p4.z, (float)p4.w);
 }
 
 // ---------------------------------------------------------------------------------
@@ -337,7 +335,7 @@ struct DirectArgs {
     int n, lo, hi, include_forces;
     double3 L; double3 invL; int3 nc; int brute;
     double rc2, alpha;
-    const double* erfc_tab;     // [erfc_m][kErfcDeg+1] erfcx(x) on intervals of width 1/erfc_scale
+    const double* erfc_tab;     // [kErfcDeg+1][kErfcMaxM] erfcx(x) on intervals of width 1/erfc_scale
     const float* erfc_tab_f;    // [erfc_m_f][kErfcDegF+1] fp32 (mixed precision), width 1/erfc_scale_f
     double erfc_scale; int erfc_m;
     double erfc_scale_f; int erfc_m_f;
@@ -349,7 +347,6 @@ struct DirectArgs {
     const int* atom_sorted; const int* key_sorted;
     const int* cstart; const int* cend;
     const double4* pos4s; const double2* ljs;
-    const float4* pos4f;        // fp32 copy of pos4s (mixed precision)
     const int* typ_s;           // [N] LJ type per sorted slot (null: > kMaxLjTypes distinct types)
     const double2* lj_tab; int lj_ntypes;   // per-type (sigma/2, 2 sqrt(eps))
     const double* pos; const double* q;
@@ -681,14 +678,18 @@ struct PairAcc {
 // erfc(x) = e^{-x^2} erfcx(x): erfcx from a piecewise degree-7 polynomial (interval table
 // in LDS, fitted at cf_create in long double, relative error ~4e-16 over [0, alpha*rc]),
 // and e^{-x^2} is shared with the force term -> one exp per pair instead of erfc + exp.
+// The table is coefficient-major, tab[j * kErfcMaxM + interval]: the 64 lanes of a read
+// fetch coefficient j of their (random) intervals from one contiguous run of doubles, so they
+// spread over the LDS banks.  (Interval-major rows of 8 doubles put every lane's read on one
+// of 4 bank groups: 6.8 conflict cycles per LDS instruction in the round-1 PMC pass.)
 __device__ __forceinline__ double erfc_exp(double x, const double* __restrict__ tab, double scale, double& e2) {
     const double y = x * scale;
     const int i = (int)y;
     const double u = 2.0 * (y - (double)i) - 1.0;
-    const double* c = tab + i * (kErfcDeg + 1);
-    double p = c[kErfcDeg];
+    const double* c = tab + i;
+    double p = c[kErfcDeg * kErfcMaxM];
 #pragma unroll
-    for (int j = kErfcDeg - 1; j >= 0; j--) p = fma(p, u, c[j]);
+    for (int j = kErfcDeg - 1; j >= 0; j--) p = fma(p, u, c[j * kErfcMaxM]);
     e2 = exp_nonpos(-x * x);
     return e2 * p;
 }
@@ -721,7 +722,7 @@ __device__ __forceinline__ void pair_term(PairAcc& acc, const DirectArgs& a, con
 
 // stage the erfcx table in LDS (all threads of the block; call before any early return)
 __device__ __forceinline__ void load_erfc_tab(const DirectArgs& a, double* tab) {
-    for (int e = threadIdx.x; e < a.erfc_m * (kErfcDeg + 1); e += blockDim.x) tab[e] = a.erfc_tab[e];
+    for (int e = threadIdx.x; e < kErfcMaxM * (kErfcDeg + 1); e += blockDim.x) tab[e] = a.erfc_tab[e];
     __syncthreads();
 }
 
@@ -899,8 +900,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))
 
 // ---------------------------------------------------------------------------------
 // 4b' mixed precision (CF_PRECISION_MIXED): the same list walk with the pair term in fp32.
-//     Positions come from the fp32 sorted copy (16-B gathers instead of 32 B); minimum image,
-//     r^2 and the cutoff test in fp32; erfc(alpha r) = e^{-x^2} erfcx(x) with erfcx from a
+//     Pair vectors are formed and minimum-imaged in fp64 from the sorted coordinates and then
+//     rounded to fp32; r^2 and the cutoff test in fp32; erfc(alpha r) = e^{-x^2} erfcx(x) with erfcx from a
 //     piecewise degree-6 fp32 polynomial (relative error ~1e-7 on [0, alpha rc], so the
 //     energy tail of the many distant pairs keeps fp32 relative accuracy, unlike the
 //     1.5e-7-absolute Abramowitz-Stegun form) and one v_exp_f32; forces and dE/dq accumulate
@@ -969,19 +970,18 @@ __global__ void __launch_bounds__(256) k_pairs_mixed(DirectArgs a) {
     if (over) active = false;
     PairAccF acc;
     if (active) {
-        const float4 pi = a.pos4f[ss];
+        const double4 pid = a.pos4s[ss];
+        const float4 pi = make_float4(0.f, 0.f, 0.f, (float)pid.w);
         const double2 lid = a.ljs[ss];
         const float2 li = make_float2((float)lid.x, (float)lid.y);
-        const float3 L = make_float3((float)a.L.x, (float)a.L.y, (float)a.L.z);
-        const float3 iL = make_float3((float)a.invL.x, (float)a.invL.y, (float)a.invL.z);
         const float rc2 = (float)a.rc2, alpha = (float)a.alpha;
         const v4i* nl4 = reinterpret_cast<const v4i*>(a.nl) + (size_t)seg * (a.nb_cap / kChunk) * a.nlr + cc;
         constexpr int kMask = (1 << kShiftBits) - 1;
-        struct Cand { float4 p; float2 lj; };
+        struct Cand { double4 p; float2 lj; };
         auto gather = [&](int e, bool ok) {
             const int t = ok ? (e & kMask) : 0;
             Cand cd;
-            cd.p = a.pos4f[t];
+            cd.p = a.pos4s[t];
             if (TYPES) {
                 cd.lj = ljt[(unsigned)e >> kShiftBits];
             } else {
@@ -990,13 +990,18 @@ __global__ void __launch_bounds__(256) k_pairs_mixed(DirectArgs a) {
             }
             return cd;
         };
+        // the pair vector is formed and minimum-imaged in fp64 and only then rounded to fp32, so
+        // its error is ~ulp(r) rather than ~ulp(L): independent of the box size (an fp32 copy of
+        // the absolute coordinates loses 2e-6 nm at C5's L = 19.7 nm)
         auto eval = [&](const Cand& cd) {
-            float dx = pi.x - cd.p.x, dy = pi.y - cd.p.y, dz = pi.z - cd.p.z;
-            dx = fmaf(-L.x, rintf(dx * iL.x), dx);
-            dy = fmaf(-L.y, rintf(dy * iL.y), dy);
-            dz = fmaf(-L.z, rintf(dz * iL.z), dz);
+            double dxd = pid.x - cd.p.x, dyd = pid.y - cd.p.y, dzd = pid.z - cd.p.z;
+            dxd -= a.L.x * rint(dxd * a.invL.x);
+            dyd -= a.L.y * rint(dyd * a.invL.y);
+            dzd -= a.L.z * rint(dzd * a.invL.z);
+            const float dx = (float)dxd, dy = (float)dyd, dz = (float)dzd;
             const float r2 = fmaf(dx, dx, fmaf(dy, dy, dz * dz));
-            if (r2 <= rc2) pair_term_f(acc, alpha, a.include_forces, tabf, escale, pi, li, cd.p, cd.lj, dx, dy, dz, r2);
+            const float4 pj = make_float4(0.f, 0.f, 0.f, (float)cd.p.w);
+            if (r2 <= rc2) pair_term_f(acc, alpha, a.include_forces, tabf, escale, pi, li, pj, cd.lj, dx, dy, dz, r2);
         };
         walk_list(nl4, a.nlr, cnt, part, LPA / kSeg, gather, eval);
     }
@@ -1200,7 +1205,12 @@ static inline int nblk(int64_t n, int b) { return (int)((n + b - 1) / b); }
 // degree 7 (max relative error 3.6e-16 on [0, 3.2], host sweep against erfcl*expl: the same
 // accuracy as width 0.375 / degree 12, for 5 FMAs and 5 LDS coefficient reads fewer per pair).
 std::vector<double> erfc_table(double xmax, double* scale, int* m) {
-    return erfc_table_deg(xmax, kErfcDeg, 0.0625, kErfcMaxM, scale, m);
+    // stored coefficient-major with a fixed stride of kErfcMaxM intervals (erfc_exp)
+    std::vector<double> t = erfc_table_deg(xmax, kErfcDeg, 0.0625, kErfcMaxM, scale, m);
+    std::vector<double> cm((size_t)(kErfcDeg + 1) * kErfcMaxM, 0.0);
+    for (int i = 0; i < *m; i++)
+        for (int j = 0; j <= kErfcDeg; j++) cm[(size_t)j * kErfcMaxM + i] = t[(size_t)i * (kErfcDeg + 1) + j];
+    return cm;
 }
 
 std::vector<float> erfc_table_f(double xmax, double* scale, int* m) {
@@ -1282,7 +1292,7 @@ void launch_cell_sort(Handle& h, const double* pos) {
     }
     hipLaunchKernelGGL(k_cell_commit, dim3(nblk(h.n, 256)), dim3(256), 0, h.stream, h.n, f, h.cell_key, h.key_tmp,
                        pos, h.q, h.lj, L, h.cell_key_sorted, h.atom_sorted, h.pos4s, h.ljs, h.atom_type, h.typ_s,
-                       h.pos_ref, h.n_builds_dev, h.pos4f);
+                       h.pos_ref, h.n_builds_dev);
 }
 
 void launch_force_rebuild(Handle& h) {
@@ -1306,7 +1316,7 @@ static DirectArgs direct_args(Handle& h, const double* pos, int include_forces) 
     a.flag = h.skin_flag;
     a.atom_sorted = h.atom_sorted; a.key_sorted = h.cell_key_sorted;
     a.cstart = h.cell_start; a.cend = h.cell_end;
-    a.pos4s = h.pos4s; a.ljs = h.ljs; a.pos4f = h.pos4f;
+    a.pos4s = h.pos4s; a.ljs = h.ljs;
     a.typ_s = h.typ_s; a.lj_tab = h.lj_tab; a.lj_ntypes = h.lj_ntypes;
     a.q = h.q; a.ex_start = h.ex_start; a.ex_list = h.ex_list;
     a.dedq_self = h.dedq_self;

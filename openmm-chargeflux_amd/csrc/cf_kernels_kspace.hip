@@ -798,12 +798,15 @@ __global__ void __launch_bounds__(256) k_dforce(int64_t K, int lo, int nown, con
     }
 }
 
-void launch_kspace_direct_sfac(Handle& h, const double* pos) {
-    const KGeom& g = h.kg;
+void launch_kspace_kvec(Handle& h) {
     double V = h.box_L[0] * h.box_L[1] * h.box_L[2];
     double cst = 4.0 / V * kPi * kOne4PiEps0;
-    hipLaunchKernelGGL(k_kvec, dim3(nblk(h.khalf, 256)), dim3(256), 0, h.stream, h.khalf, g, recip_vec(h), cst,
+    hipLaunchKernelGGL(k_kvec, dim3(nblk(h.khalf, 256)), dim3(256), 0, h.stream, h.khalf, h.kg, recip_vec(h), cst,
                        1.0 / (h.alpha * h.alpha), h.kvec);
+}
+
+void launch_kspace_direct_sfac(Handle& h, const double* pos) {
+    launch_kspace_kvec(h);
     int nown = h.hi - h.lo;
     int chunk = (nown + h.sk_nchunk - 1) / h.sk_nchunk;
     hipLaunchKernelGGL(k_dsfac, dim3(nblk(h.khalf, 256), h.sk_nchunk), dim3(256), 0, h.stream, h.khalf, h.lo, nown,

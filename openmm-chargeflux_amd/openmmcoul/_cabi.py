@@ -73,6 +73,7 @@ SIGNATURES = [
     ("cf_destroy", C.c_int, [C.c_void_p]),
     ("cf_get_ewald_params", C.c_int, [C.c_void_p, DP, C.POINTER(C.c_int32)]),
     ("cf_get_owned_range", C.c_int, [C.c_void_p, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
+    ("cf_get_grid_shape", C.c_int, [C.c_void_p, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
     ("cf_compute", C.c_int, [C.c_void_p, C.c_void_p, DP, C.c_int, C.c_void_p, C.c_void_p]),
     ("cf_compute_begin", C.c_int, [C.c_void_p, C.c_void_p, DP, C.c_int]),
     ("cf_kspace_buffer", C.c_int, [C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_int64)]),

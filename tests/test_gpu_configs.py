@@ -1,0 +1,208 @@
+"""GPU tests of BASELINE.json's configurations at their own sizes:
+
+  C3  96 000 atoms, kmax 31, 1 GPU, fp64: both k-space paths against the oracle's full-size
+      evaluation (tests/golden/c3.npz: energy terms, charge/force sums, and forces, dE/dq and
+      charges of a seeded 2 000-atom subset; made by tests/golden/make_golden.py --c3)
+  C4  the C3 box atom-decomposed over 8 ranks (here: 8 handles on one GPU, the S(k)
+      all-reduce done by hand, exactly what openmmcoul.distributed does over RCCL)
+  C5  768 000 atoms, mixed precision, against the fp64 path on the same positions; and a
+      4-rank split of it
+plus the empty-rank case of the decomposition (a molecule larger than 1/world of the
+system leaves rank 0 without atoms; rank 0 still adds the reciprocal energy).
+
+Tolerances (written here; the north star asks for forces within 1e-5 kJ/mol/nm):
+  exact k-sum vs oracle   forces <= 1e-8 kJ/mol/nm, dE/dq <= 1e-10 relative (grid: 1e-9), energy and each
+                          term <= 1e-12 / 1e-10 of sum |terms| (E ~ -1e3 is a near-cancellation
+                          of +-7.6e6 kJ/mol terms at C3)
+  grid k-sum vs oracle    forces <= 1e-6 kJ/mol/nm (W = 14: ~2e-8 observed), energy as above
+  W ranks vs 1 rank       forces <= 1e-8 kJ/mol/nm, energy <= 1e-13 of sum |terms|
+  mixed vs fp64 (C5)      RMS relative force error <= 1e-4, max |dF| <= 0.05 kJ/mol/nm
+"""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+from openmmcoul import HipCalcCoulForceKernel  # noqa: E402
+from openmmcoul import testsystems as ts  # noqa: E402
+from openmmcoul.distributed import device_buffer_as_tensor  # noqa: E402
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+EXACT, GRID = HipCalcCoulForceKernel.KSPACE_EXACT_MFMA, HipCalcCoulForceKernel.KSPACE_GRID
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+
+
+@pytest.fixture(scope="module")
+def c3():
+    system, force, pos, box = ts.make("C3")
+    return system, force, pos, box
+
+
+@pytest.fixture(scope="module")
+def c3_golden(c3):
+    import hashlib
+    d = np.load(os.path.join(GOLDEN, "c3.npz"))
+    _, _, pos, box = c3
+    assert hashlib.sha256(pos.tobytes()).hexdigest() == str(d["pos_sha256"]), "C3 positions differ from the fixture's"
+    assert np.array_equal(box, d["box"])
+    return d
+
+
+def _decomposed(system, force, pos, box, world, algo, precision="double", width=0):
+    """One evaluation split over `world` handles on this GPU: begin on every rank, sum the
+    k-space buffers (the all-reduce), end on every rank.  Returns (energy, forces, dedq)."""
+    stream = torch.cuda.current_stream().cuda_stream
+    pt = torch.tensor(pos, dtype=torch.float64, device="cuda")
+    ks = [HipCalcCoulForceKernel(stream=stream, rank=r, world_size=world, kspace_algo=algo, precision=precision,
+                                 grid_width=width).initialize(system, force) for r in range(world)]
+    for k in ks:
+        k.begin(pt, box, True, True)
+    bufs = [device_buffer_as_tensor(*k.kspace_buffer(), "cuda") for k in ks]
+    total = sum(bufs[1:], bufs[0].clone())
+    for b in bufs:
+        b.copy_(total)
+    f = torch.zeros_like(pt)
+    es = []
+    for k in ks:
+        e = torch.zeros(1, dtype=torch.float64, device="cuda")
+        k.end(f, e)
+        es.append(e)
+    torch.cuda.synchronize()
+    dedq = np.zeros(len(pos))
+    for k in ks:
+        lo, hi = k.owned_range()
+        dedq[lo:hi] = k.dedq()[lo:hi]
+    ranges = [k.owned_range() for k in ks]
+    for k in ks:
+        k.destroy()
+    return sum(x.item() for x in es), f.cpu().numpy(), dedq, ranges
+
+
+def _e_tol(terms, rel):
+    """Energy bar relative to the terms' magnitudes: at C3 the total (~ -1e3 kJ/mol) is a
+    near-cancellation of the self (~ -7.6e6) and exclusion (~ +7.5e6) terms."""
+    return rel * np.abs(terms).sum() + 1e-8
+
+
+def _check_golden(d, e, f, q, dq, f_tol, terms=None):
+    sub = d["subset"]
+    assert abs(e - float(d["energy"])) <= _e_tol(d["terms"], 1e-12), (e, float(d["energy"]))
+    df = np.abs(f[sub] - d["forces"]).max()
+    assert df <= f_tol, df
+    # whole-system checks beyond the subset: the force sum and sum of squares
+    assert np.abs(f.sum(0) - d["force_sum"]).max() <= f_tol * np.sqrt(len(f))
+    assert abs((f ** 2).sum() - float(d["force_sq"])) <= 1e-9 * float(d["force_sq"])
+    if q is not None:
+        assert np.abs(q[sub] - d["charges"]).max() <= 1e-12
+        assert abs(q.sum() - float(d["charge_sum"])) <= 1e-9
+    scale = np.abs(d["dedq"]).max()
+    dq_rel = 1e-10 if f_tol <= 1e-8 else 1e-9   # exact k-sum / grid k-sum
+    assert np.abs(dq[sub] - d["dedq"]).max() <= dq_rel * scale + 1e-9
+    if terms is not None:
+        for a, b in zip(terms, d["terms"]):
+            assert abs(a - b) <= 1e-10 * max(abs(b), 1.0), (terms, d["terms"])
+
+
+@pytest.mark.parametrize("algo,f_tol", [(EXACT, 1e-8), (GRID, 1e-6)])
+def test_c3_vs_oracle_golden(c3, c3_golden, algo, f_tol):
+    system, force, pos, box = c3
+    k = HipCalcCoulForceKernel(kspace_algo=algo).initialize(system, force)
+    assert k.ewald_params()[1] == (31, 31, 31)
+    e, f = k.execute_host(pos, box)
+    _check_golden(c3_golden, e, f, k.charges(), k.dedq(), f_tol, k.energy_terms())
+
+
+@pytest.mark.parametrize("algo,f_tol", [(EXACT, 1e-8), (GRID, 1e-6)])
+def test_c4_eight_rank_decomposition_full_c3(c3, c3_golden, algo, f_tol):
+    """C4: the C3 box over 8 ranks; equal to the single-rank result and to the oracle."""
+    system, force, pos, box = c3
+    single = HipCalcCoulForceKernel(kspace_algo=algo).initialize(system, force)
+    e1, f1 = single.execute_host(pos, box)
+    dq1 = single.dedq()
+    t1 = single.energy_terms()
+    single.destroy()
+    e8, f8, dq8, ranges = _decomposed(system, force, pos, box, 8, algo)
+    assert ranges[0][0] == 0 and ranges[-1][1] == len(pos)
+    assert all(ranges[r][1] == ranges[r + 1][0] for r in range(7))
+    assert all(hi - lo > 0 for lo, hi in ranges)
+    assert abs(e8 - e1) <= _e_tol(t1, 1e-13), (e8, e1)
+    assert np.abs(f8 - f1).max() < 1e-8
+    assert np.abs(dq8 - dq1).max() <= 1e-11 * np.abs(dq1).max()
+    _check_golden(c3_golden, e8, f8, None, dq8, f_tol)
+
+
+def _chain_system(world):
+    """400-water box whose first 60 % of atoms are one molecule (a chain of zero-constant
+    FluxBonds between consecutive O atoms): rank 0's slice of a `world`-way partition is empty."""
+    system, force, pos, box = ts.water_box(400, cutoff=0.7, ewald_tol=1e-4)
+    n = len(pos)
+    last_o = (int(0.6 * n) // 3) * 3
+    for o in range(0, last_o, 3):
+        force.addFluxBond(o, o + 3, 0.0, 0.3)
+    return system, force, pos, box
+
+
+@pytest.mark.parametrize("algo", [0, 1, 2])
+def test_empty_rank_zero_keeps_reciprocal_energy(algo):
+    system, force, pos, box = _chain_system(4)
+    single = HipCalcCoulForceKernel(kspace_algo=algo).initialize(system, force)
+    e1, f1 = single.execute_host(pos, box)
+    terms1 = single.energy_terms()
+    assert abs(terms1[1]) > 1.0   # a reciprocal energy that would be visibly missing
+    e4, f4, _, ranges = _decomposed(system, force, pos, box, 4, algo)
+    assert ranges[0] == (0, 0), ranges          # rank 0 owns nothing
+    assert e4 == pytest.approx(e1, rel=1e-11)
+    assert np.abs(f4 - f1).max() < 1e-8
+
+
+@pytest.fixture(scope="module")
+def c5():
+    return ts.make("C5")
+
+
+def test_c5_mixed_precision_vs_fp64(c5):
+    """C5 (768k atoms, kmax 65): the mixed-precision build (fp32 pair kernel, W = 8 grid)
+    against the fp64 build (W = 14 grid) on the same positions."""
+    system, force, pos, box = c5
+    assert len(pos) == 768000
+    stream = torch.cuda.current_stream().cuda_stream
+    pt = torch.tensor(pos, dtype=torch.float64, device="cuda")
+    out = {}
+    for prec in ("double", "mixed"):
+        k = HipCalcCoulForceKernel(stream=stream, kspace_algo=GRID, precision=prec).initialize(system, force)
+        assert k.ewald_params()[1] == (65, 65, 65)
+        f = torch.zeros_like(pt)
+        e = torch.zeros(1, dtype=torch.float64, device="cuda")
+        k.execute_device(pt, box, True, True, f, e)
+        torch.cuda.synchronize()
+        out[prec] = (e.item(), f.cpu().numpy(), k.energy_terms())
+        k.destroy()
+    (ed, fd, td), (em, fm, tm) = out["double"], out["mixed"]
+    df = fm - fd
+    rms_rel = np.sqrt((df ** 2).sum(1).mean() / (fd ** 2).sum(1).mean())
+    assert rms_rel <= 1e-4, rms_rel
+    assert np.abs(df).max() <= 0.05, np.abs(df).max()
+    # energy: the total is a near-cancellation of large terms (self ~ -6e7, exclusion ~ +6e7
+    # kJ/mol at C5); the bar is relative to the sum of the terms' magnitudes
+    assert abs(em - ed) <= 1e-7 * np.abs(td).sum(), (em, ed, td)
+
+
+def test_c5_mixed_four_rank_split(c5):
+    system, force, pos, box = c5
+    k = HipCalcCoulForceKernel(kspace_algo=GRID, precision="mixed").initialize(system, force)
+    e1, f1 = k.execute_host(pos, box)
+    k.destroy()
+    e4, f4, _, ranges = _decomposed(system, force, pos, box, 4, GRID, precision="mixed")
+    assert all(hi > lo for lo, hi in ranges)
+    assert e4 == pytest.approx(e1, rel=1e-11)
+    # fp32 per-lane force sums: a rank's lanes-per-atom choice changes their rounding
+    assert np.abs(f4 - f1).max() <= 1e-6 * np.abs(f1).max()

@@ -1,8 +1,9 @@
 """GPU parity tests: the HIP path (through the C-ABI) against the oracle restatement of
 ReferenceCoulKernels.cpp on identical inputs.
 
-Tolerances (fp64 everywhere; north star: forces within 1e-5 kJ/mol/nm):
-  forces   max |dF|            <= 1e-5 kJ/mol/nm   (typically ~1e-9)
+Tolerances (fp64 everywhere; north star: forces within 1e-5 kJ/mol/nm, SURVEY §8(c)
+expects 1e-8 in practice):
+  forces   max |dF|            <= 1e-8 kJ/mol/nm   (observed ~1e-11)
   energy   |dE|                <= 1e-9 |E| + 1e-8 kJ/mol
   charges  max |dq|            <= 1e-12 e
   dE/dq    max |d(dE/dq)|      <= 1e-9 max|dE/dq| + 1e-9
@@ -19,7 +20,7 @@ from openmmcoul import HipCalcCoulForceKernel, ChargeFluxError  # noqa: E402
 from openmmcoul import testsystems as ts  # noqa: E402
 from openmmcoul.distributed import device_buffer_as_tensor  # noqa: E402
 
-F_TOL = 1e-5
+F_TOL = 1e-8
 
 
 @pytest.fixture(scope="module", autouse=True)

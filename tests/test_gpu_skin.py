@@ -57,7 +57,7 @@ def test_skin_trajectory_matches_rebuild_every_call(nw, rc, tol):
         o = Oracle(force, box).execute(x, box)
         e, f = sk.execute_host(x, box)
         assert e == pytest.approx(o["energy"], rel=1e-9)
-        assert np.abs(f - o["forces"]).max() <= 1e-5
+        assert np.abs(f - o["forces"]).max() <= 1e-8
 
 
 def test_skin_rebuilds_on_wrap_and_box_change():
@@ -92,7 +92,7 @@ def test_skin_capped_by_small_box():
     o = Oracle(force, box).execute(x, box)
     e, f = sk.execute_host(x, box)
     assert e == pytest.approx(o["energy"], rel=1e-9)
-    assert np.abs(f - o["forces"]).max() <= 1e-5
+    assert np.abs(f - o["forces"]).max() <= 1e-8
 
 
 def test_skin_two_rank_split_phase_matches_single():
