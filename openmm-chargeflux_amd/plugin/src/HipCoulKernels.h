@@ -1,0 +1,37 @@
+// HipCoulKernels.h — CalcCoulForceKernel (openmmapi/include/CoulKernels.h:15-38) on MI355X.
+//
+// Needs OpenMM's headers and the reference's openmmapi/include (CoulForce.h, CoulKernels.h):
+// built by plugin/Makefile only when OPENMM_DIR and COUL_API_DIR are set.  Everything the
+// kernel does is in coulhip::KernelCore (include/CoulHipKernelCore.h), which is compiled and
+// tested without OpenMM through tests/cpp/adapter_capi.cpp.
+#ifndef HIP_COUL_KERNELS_H_
+#define HIP_COUL_KERNELS_H_
+
+#include <string>
+
+#include "CoulHipKernelCore.h"
+#include "CoulKernels.h"
+#include "openmm/Platform.h"
+
+namespace CoulPlugin {
+
+class HipCalcCoulForceKernel : public CalcCoulForceKernel {
+public:
+    HipCalcCoulForceKernel(std::string name, const OpenMM::Platform& platform, const coulhip::Options& options)
+        : CalcCoulForceKernel(name, platform), options_(options) {}
+    // replaces ReferenceCalcCoulForceKernel::initialize (ReferenceCoulKernels.cpp:230-422)
+    void initialize(const OpenMM::System& system, const CoulForce& force) override;
+    // replaces ReferenceCalcCoulForceKernel::execute (ReferenceCoulKernels.cpp:424-636)
+    double execute(OpenMM::ContextImpl& context, bool includeForces, bool includeEnergy) override;
+    // what a CoulForce::updateParametersInContext would call (OpenMM's NonbondedForce pattern;
+    // the reference has none)
+    void copyParametersToContext(OpenMM::ContextImpl& context, const CoulForce& force);
+
+private:
+    coulhip::Options options_;
+    coulhip::KernelCore core_;
+};
+
+}  // namespace CoulPlugin
+
+#endif  // HIP_COUL_KERNELS_H_
