@@ -507,10 +507,6 @@ CF_EXPORT int cf_create(const cf_params* p, const cf_options* opt, cf_handle** o
             const cf::KGeom& g = h.kg;
             set_cells(H, std::vector<double>{p->default_box[0], p->default_box[4], p->default_box[8]}.data());
             h.erfc_tab = dupload(H, cf::erfc_table(h.alpha * h.cutoff * (1.0 + 1e-9), &h.erfc_scale, &h.erfc_m));
-            {
-                std::vector<double2> eg = cf::erfc_g_table(h.alpha * h.cutoff * (1.0 + 1e-9));
-                if (!eg.empty()) h.eg_tab = dupload(H, eg);
-            }
             if (h.mixed) {
                 h.erfc_tab_f = dupload(H, cf::erfc_table_f(h.alpha * h.cutoff * (1.0 + 1e-6), &h.erfc_scale_f, &h.erfc_m_f));
             }

@@ -6,7 +6,6 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include <functional>
 #include <string>
 #include <vector>
 
@@ -184,7 +183,6 @@ struct Handle {
     int sk_nchunk = 0;
     // energy
     double* erfc_tab = nullptr;  // erfcx interval polynomials (cf_kernels_core.hip erfc_table)
-    double2* eg_tab = nullptr;   // (erfc, G) interval polynomials (erfc_g_table), null when alpha rc > 3.2
     double erfc_scale = 0; int erfc_m = 0;
     double erfc_scale_f = 0; int erfc_m_f = 0;   // fp32 table (mixed precision): its own interval width
     float* erfc_tab_f = nullptr; // fp32 erfcx table (mixed precision)
@@ -202,9 +200,6 @@ struct Handle {
 std::vector<double> erfc_table(double xmax, double* scale, int* m);     // width 1/16, degree 7, fp64 pair kernel
 std::vector<float> erfc_table_f(double xmax, double* scale, int* m);    // degree 6, mixed-precision kernel
 std::vector<double> erfc_table_deg(double xmax, int deg, double width, int max_m, double* scale, int* m);
-std::vector<double> erfc_table_fn(double xmax, int deg, double width, int max_m, double* scale, int* m,
-                                  const std::function<long double(long double)>& fn);
-std::vector<double2> erfc_g_table(double xmax);   // (erfc, G) pairs, empty when alpha rc > 3.2
 void launch_flux_terms(Handle& h, const double* pos);
 void launch_atoms_prep(Handle& h, const double* pos, bool skin_check);   // q, self term [, skin_flag |= moved > list_skin/2]
 void launch_cell_sort(Handle& h, const double* pos);

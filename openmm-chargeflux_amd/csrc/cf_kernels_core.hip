@@ -4,8 +4,6 @@
 //
 // Reference semantics: platforms/reference/src/ReferenceCoulKernels.cpp (RCK).
 #include <algorithm>
-#include <functional>
-#include <type_traits>
 
 #include "cf_internal.h"
 
@@ -204,17 +202,9 @@ __global__ void __launch_bounds__(256) k_cell_scatter(int n, const int* __restri
 // a smaller atom index (members staged in LDS and read by broadcast)
 constexpr int kOrderLds = 1024;
 
-// Order within a cell: atoms with LJ (epsilon != 0) first, then by atom index -- a stable sort
-// on (no-LJ flag, index).  Then the waves of the pair kernel that hold only epsilon = 0 atoms
-// (water H) run without the LJ term (k_pairs).
-__device__ __forceinline__ int order_key(int v, const double2* __restrict__ lj) {
-    return v | (lj[v].y == 0.0 ? (1 << 30) : 0);
-}
-
 __global__ void __launch_bounds__(256) k_cell_order(int ncell, const int* __restrict__ flag,
                                                     const int* __restrict__ cstart, const int* __restrict__ cend,
-                                                    const int* __restrict__ tmp, const double2* __restrict__ lj,
-                                                    int* __restrict__ out) {
+                                                    const int* __restrict__ tmp, int* __restrict__ out) {
     __shared__ int mem[4][kOrderLds];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int c = blockIdx.x * 4 + w;
@@ -222,23 +212,17 @@ __global__ void __launch_bounds__(256) k_cell_order(int ncell, const int* __rest
     const int b = cstart[c], m = cend[c] - b;
     const int* src = tmp + b;
     if (m <= kOrderLds) {
-        for (int e = lane; e < m; e += 64) mem[w][e] = order_key(src[e], lj);
+        for (int e = lane; e < m; e += 64) mem[w][e] = src[e];
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        for (int e = lane; e < m; e += 64) {
-            const int kv = mem[w][e];
-            int r = 0;
-            for (int j = 0; j < m; j++) r += mem[w][j] < kv;
-            out[b + r] = kv & ((1 << 30) - 1);
-        }
-    } else {
-        for (int e = lane; e < m; e += 64) {
-            const int kv = order_key(src[e], lj);
-            int r = 0;
-            for (int j = 0; j < m; j++) r += order_key(src[j], lj) < kv;
-            out[b + r] = src[e];
-        }
+        src = mem[w];
+    }
+    for (int e = lane; e < m; e += 64) {
+        const int v = src[e];
+        int r = 0;
+        for (int j = 0; j < m; j++) r += src[j] < v;
+        out[b + r] = v;
     }
 }
 
@@ -343,14 +327,6 @@ constexpr int kErfcMaxM = 129;   // fp64 intervals of width 1/16: x = alpha r up
 constexpr int kErfcDegF = 6;     // the same in fp32 (mixed precision): relative error ~1e-7
 constexpr int kErfcMaxMF = 32;   // fp32 intervals of width 0.375: x = alpha r up to 11.6
 constexpr int kMaxLjTypes = 64;  // LJ types carried in the 6 high bits of a list entry
-// erfc(x) and G(x) = erfc(x) + (2/sqrt(pi)) x e^{-x^2} tabulated directly (no exp per pair):
-// degree-7 interpolants on intervals of width 1/32 of x = alpha r, relative error 2.2e-16 on
-// [0, 3.2] (host sweep against erfcl / expl).  Used when alpha * cutoff <= 3.2
-// (Ewald tolerances >= 1.8e-5); beyond, the erfcx table + exp path above.
-constexpr int kEgDeg = 7;
-constexpr double kEgScale = 32.0;
-constexpr double kEgXMax = 3.2;
-constexpr int kEgMaxM = 104;     // ceil(3.2 * 32) + 1 intervals
 constexpr int kSeg = 4;          // neighbour sub-lists per atom (one per scanning wave / pair lane)
 constexpr int kShiftBits = 26;
 constexpr int kBruteShift = 31;  // shift code: minimum image by floor (brute-force path)
@@ -363,7 +339,6 @@ struct DirectArgs {
     const float* erfc_tab_f;    // [erfc_m_f][kErfcDegF+1] fp32 (mixed precision), width 1/erfc_scale_f
     double erfc_scale; int erfc_m;
     double erfc_scale_f; int erfc_m_f;
-    const double2* eg_tab;      // [kEgDeg+1][kEgMaxM] (erfc, G) coefficient pairs; null: use erfc_tab
     double rl2;                 // list radius^2: (rc + list skin)^2
     int nb_cap;                 // capacity of ONE of the kSeg sub-lists
     int nlr;                    // list rows = owned atoms; row c <-> sorted slot own_slot(c)
@@ -719,56 +694,6 @@ __device__ __forceinline__ double erfc_exp(double x, const double* __restrict__ 
     return e2 * p;
 }
 
-// erfc(x) and G(x) from the (erfc, G) interval table: one ds_read_b128 per coefficient pair
-__device__ __forceinline__ void erfc_g(double x, const double2* __restrict__ tab, double& ec, double& g) {
-    const double y = x * kEgScale;
-    const int i = (int)y;
-    const double u = fma(2.0, y - (double)i, -1.0);
-    const double2* c = tab + i;
-    double2 t = c[kEgDeg * kEgMaxM];
-    double pa = t.x, pg = t.y;
-#pragma unroll
-    for (int j = kEgDeg - 1; j >= 0; j--) {
-        t = c[j * kEgMaxM];
-        pa = fma(pa, u, t.x);
-        pg = fma(pg, u, t.y);
-    }
-    ec = pa;
-    g = pg;
-}
-
-// real-space Ewald + LJ pair (RCK:567-592) from the (erfc, G) table: dEdR =
-// (q_i q_j k_e G(alpha r)/r + LJ) / r^2, dE/dq_i += k_e q_j erfc(alpha r)/r, E += q_i q_j k_e
-// erfc/r + LJ.  LJ = false: the caller knows epsilon_i = 0 for every lane of the wave (no LJ
-// term, RCK:572-577 gives 0).
-template <bool LJ>
-__device__ __forceinline__ void pair_term_eg(PairAcc& acc, const DirectArgs& a, const double2* __restrict__ tab,
-                                             double4 pi, double2 li, double4 pj, double2 lj2, double dx, double dy,
-                                             double dz, double r2) {
-    const double inv_r = rsqrt_fp64(r2);
-    double ec, g;
-    erfc_g(r2 * inv_r * a.alpha, tab, ec, g);
-    const double qj = kOne4PiEps0 * pj.w * inv_r;   // potential of j at i per unit erfc
-    const double qq = pi.w * qj;
-    double es6 = 0, sig6 = 0;
-    if (LJ) {
-        const double sig = li.x + lj2.x;
-        double s2 = inv_r * sig;
-        s2 *= s2;
-        sig6 = s2 * s2 * s2;
-        es6 = sig6 * (li.y * lj2.y);
-    }
-    if (a.include_forces) {
-        const double inv_r2 = inv_r * inv_r;
-        const double dEdR = (LJ ? fma(qq, g, es6 * fma(12.0, sig6, -6.0)) : qq * g) * inv_r2;
-        acc.fx = fma(dEdR, dx, acc.fx);
-        acc.fy = fma(dEdR, dy, acc.fy);
-        acc.fz = fma(dEdR, dz, acc.fz);
-        acc.dq = fma(qj, ec, acc.dq);
-    }
-    acc.e += LJ ? fma(qq, ec, es6 * (sig6 - 1.0)) : qq * ec;   // the pair's full energy; halved once in store_pairs
-}
-
 // real-space Ewald + LJ pair (RCK:567-592), d = pos_i - pos_j (minimum image); tab = LDS
 // copy of the erfcx table (the cutoff test r <= rc guarantees alpha r lies inside it)
 __device__ __forceinline__ void pair_term(PairAcc& acc, const DirectArgs& a, const double* __restrict__ tab,
@@ -918,23 +843,13 @@ __device__ __forceinline__ void walk_list(const v4i* __restrict__ nl4, size_t st
 // the chip): lane g walks chunks g/4, g/4 + LPA/4, ... of sub-list g%4.
 // TYPES: the partner's LJ parameters come from the per-type table (LDS) indexed by the high
 // bits of the list entry instead of a third gathered 16-B load per candidate.
-// EG: the (erfc, G) table path (alpha rc <= 3.2), else erfcx table + exp.  Waves whose atoms
-// all have epsilon = 0 (water H: the cell sort puts LJ atoms first within each cell, so most
-// such waves hold no LJ atom) run the walk without the LJ term.
-template <int LPA, bool TYPES, bool EG>
+template <int LPA, bool TYPES>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) k_pairs(DirectArgs a) {
-    constexpr int kTabD = EG ? 2 * kEgMaxM * (kEgDeg + 1) : kErfcMaxM * (kErfcDeg + 1);
-    __shared__ __attribute__((aligned(16))) double tab[kTabD];
+    __shared__ double tab[kErfcMaxM * (kErfcDeg + 1)];
     __shared__ double2 ljt[kMaxLjTypes];
     if (TYPES)
         for (int e = threadIdx.x; e < a.lj_ntypes; e += blockDim.x) ljt[e] = a.lj_tab[e];
-    if (EG) {
-        const double* src = reinterpret_cast<const double*>(a.eg_tab);
-        for (int e = threadIdx.x; e < kTabD; e += blockDim.x) tab[e] = src[e];
-        __syncthreads();
-    } else {
-        load_erfc_tab(a, tab);
-    }
+    load_erfc_tab(a, tab);
     const int gt = xcd_block() * blockDim.x + threadIdx.x;
     const int c = gt / LPA, g = gt % LPA;
     const int seg = g % kSeg, part = g / kSeg;
@@ -964,25 +879,15 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))
         // The pair vector is the minimum image d - L rint(d/L) (getDeltaRPeriodic's
         // floor(d/L + 0.5) up to exact half-box ties, which lie beyond the cutoff), so the
         // image code stored in the list is not needed.
-        auto eval_with = [&](const Cand& cd, auto lj_tag) {
-            constexpr bool LJ = decltype(lj_tag)::value;
+        auto eval = [&](const Cand& cd) {
             double dx = pi.x - cd.p.x, dy = pi.y - cd.p.y, dz = pi.z - cd.p.z;
             dx -= a.L.x * rint(dx * a.invL.x);
             dy -= a.L.y * rint(dy * a.invL.y);
             dz -= a.L.z * rint(dz * a.invL.z);
             const double r2 = dx * dx + dy * dy + dz * dz;
-            if (r2 <= a.rc2) {   // exact voxel-hash test
-                if (EG) pair_term_eg<LJ>(acc, a, reinterpret_cast<const double2*>(tab), pi, li, cd.p, cd.lj, dx, dy, dz, r2);
-                else pair_term(acc, a, tab, pi, li, cd.p, cd.lj, dx, dy, dz, r2);
-            }
+            if (r2 <= a.rc2) pair_term(acc, a, tab, pi, li, cd.p, cd.lj, dx, dy, dz, r2);  // exact voxel-hash test
         };
-        // wave-uniform: does any atom of this wave carry LJ (epsilon != 0)?
-        if (EG && __ballot(li.y != 0.0) == 0ull)
-            walk_list(nl4, a.nlr, cnt, part, LPA / kSeg, gather,
-                      [&](const Cand& cd) { eval_with(cd, std::integral_constant<bool, false>()); });
-        else
-            walk_list(nl4, a.nlr, cnt, part, LPA / kSeg, gather,
-                      [&](const Cand& cd) { eval_with(cd, std::integral_constant<bool, true>()); });
+        walk_list(nl4, a.nlr, cnt, part, LPA / kSeg, gather, eval);
     }
 #pragma unroll
     for (int m = 1; m < LPA; m <<= 1) {
@@ -1121,8 +1026,7 @@ __device__ __forceinline__ void pair_rescan(const DirectArgs& a, const double* t
     PairAcc acc;
     scan_cells(a, s, pi, a.rc2, [&](int t, int, double dx, double dy, double dz, double r2) {
         if (exc && in_excl(a.atom_sorted[t], reg, exc, a.ex_list, ex0)) return;
-        if (a.eg_tab) pair_term_eg<true>(acc, a, a.eg_tab, pi, li, a.pos4s[t], a.ljs[t], dx, dy, dz, r2);
-        else pair_term(acc, a, tab, pi, li, a.pos4s[t], a.ljs[t], dx, dy, dz, r2);
+        pair_term(acc, a, tab, pi, li, a.pos4s[t], a.ljs[t], dx, dy, dz, r2);
     });
     store_pairs(acc, a, i);
 }
@@ -1309,33 +1213,12 @@ std::vector<double> erfc_table(double xmax, double* scale, int* m) {
     return cm;
 }
 
-std::vector<double2> erfc_g_table(double xmax) {
-    if (!(xmax <= kEgXMax)) return {};
-    std::vector<double> ta, tg;
-    double scale;
-    int m;
-    const long double c2 = 2.0L / sqrtl(3.14159265358979323846264338327950288L);
-    ta = erfc_table_fn(xmax, kEgDeg, 1.0 / kEgScale, kEgMaxM, &scale, &m, [](long double x) { return erfcl(x); });
-    tg = erfc_table_fn(xmax, kEgDeg, 1.0 / kEgScale, kEgMaxM, &scale, &m,
-                       [c2](long double x) { return erfcl(x) + c2 * x * expl(-x * x); });
-    std::vector<double2> cm((size_t)(kEgDeg + 1) * kEgMaxM, make_double2(0.0, 0.0));
-    for (int i = 0; i < m; i++)
-        for (int j = 0; j <= kEgDeg; j++)
-            cm[(size_t)j * kEgMaxM + i] = make_double2(ta[(size_t)i * (kEgDeg + 1) + j], tg[(size_t)i * (kEgDeg + 1) + j]);
-    return cm;
-}
-
 std::vector<float> erfc_table_f(double xmax, double* scale, int* m) {
     std::vector<double> t = erfc_table_deg(xmax, kErfcDegF, 0.375, kErfcMaxMF, scale, m);
     return std::vector<float>(t.begin(), t.end());
 }
 
 std::vector<double> erfc_table_deg(double xmax, int deg, double width, int max_m, double* scale, int* m) {
-    return erfc_table_fn(xmax, deg, width, max_m, scale, m, [](long double x) { return erfcl(x) * expl(x * x); });
-}
-
-std::vector<double> erfc_table_fn(double xmax, int deg, double width, int max_m, double* scale, int* m,
-                                  const std::function<long double(long double)>& fn) {
     const long double w = width;
     int M = (int)std::ceil((long double)xmax / w) + 1;
     if (M > max_m) throw std::invalid_argument("alpha * cutoff too large for the erfc table");
@@ -1346,7 +1229,7 @@ std::vector<double> erfc_table_fn(double xmax, int deg, double width, int max_m,
         for (int k = 0; k < n; k++) {
             const long double t = cosl(3.14159265358979323846264338327950288L * (k + 0.5L) / n);
             const long double x = w * (i + 0.5L * (t + 1.0L));
-            f[k] = fn(x);
+            f[k] = erfcl(x) * expl(x * x);
         }
         for (int j = 0; j < n; j++) {
             long double sum = 0;
@@ -1398,7 +1281,7 @@ void launch_cell_sort(Handle& h, const double* pos) {
     hipLaunchKernelGGL(k_cell_scatter, dim3(nblk(h.n, 256)), dim3(256), 0, h.stream, h.n, f, h.cell_key, h.atom_val,
                        h.cell_start, h.atom_tmp, ncell, h.cell_cnt);
     hipLaunchKernelGGL(k_cell_order, dim3(nblk(ncell, 4)), dim3(256), 0, h.stream, ncell, f, h.cell_start,
-                       h.cell_end, h.atom_tmp, h.lj, h.key_tmp);
+                       h.cell_end, h.atom_tmp, h.key_tmp);
     if (h.own_s) {
         const int nb = nblk(h.n, kScanThreads);  // block sums live in atom_val (free after the scatter)
         hipLaunchKernelGGL(k_own_count, dim3(nb), dim3(kScanThreads), 0, h.stream, h.n, f, h.key_tmp, h.lo, h.hi,
@@ -1425,7 +1308,6 @@ static DirectArgs direct_args(Handle& h, const double* pos, int include_forces) 
     a.brute = (h.nc[0] < 3 || h.nc[1] < 3 || h.nc[2] < 3) ? 1 : 0;
     a.rc2 = h.cutoff * h.cutoff; a.alpha = h.alpha;
     a.erfc_tab = h.erfc_tab; a.erfc_scale = h.erfc_scale; a.erfc_m = h.erfc_m;
-    a.eg_tab = h.eg_tab;
     a.erfc_tab_f = h.erfc_tab_f; a.erfc_scale_f = h.erfc_scale_f; a.erfc_m_f = h.erfc_m_f;
     a.rl2 = (h.cutoff + h.list_skin) * (h.cutoff + h.list_skin);
     a.nb_cap = h.nb_cap;
@@ -1467,17 +1349,15 @@ void launch_direct(Handle& h, const double* pos, int include_forces) {
         else if ((int64_t)a.nlr * 8 >= want) { CF_PAIRS_MIXED(8); }
         else { CF_PAIRS_MIXED(16); }
 #undef CF_PAIRS_MIXED
+    } else if ((int64_t)a.nlr * 4 >= want) {
+        if (ty) hipLaunchKernelGGL((k_pairs<4, true>), dim3(nblk((int64_t)a.nlr * 4, 256)), dim3(256), 0, h.stream, a);
+        else hipLaunchKernelGGL((k_pairs<4, false>), dim3(nblk((int64_t)a.nlr * 4, 256)), dim3(256), 0, h.stream, a);
+    } else if ((int64_t)a.nlr * 8 >= want) {
+        if (ty) hipLaunchKernelGGL((k_pairs<8, true>), dim3(nblk((int64_t)a.nlr * 8, 256)), dim3(256), 0, h.stream, a);
+        else hipLaunchKernelGGL((k_pairs<8, false>), dim3(nblk((int64_t)a.nlr * 8, 256)), dim3(256), 0, h.stream, a);
     } else {
-        const int lpa = (int64_t)a.nlr * 4 >= want ? 4 : ((int64_t)a.nlr * 8 >= want ? 8 : 16);
-        const bool eg = a.eg_tab != nullptr;
-        const dim3 grid(nblk((int64_t)a.nlr * lpa, 256));
-#define CF_PAIRS(LPA_, TY_, EG_) hipLaunchKernelGGL((k_pairs<LPA_, TY_, EG_>), grid, dim3(256), 0, h.stream, a)
-#define CF_PAIRS_EG(LPA_)                                                                                         \
-    if (ty) { if (eg) CF_PAIRS(LPA_, true, true); else CF_PAIRS(LPA_, true, false); }                             \
-    else { if (eg) CF_PAIRS(LPA_, false, true); else CF_PAIRS(LPA_, false, false); }
-        if (lpa == 4) { CF_PAIRS_EG(4) } else if (lpa == 8) { CF_PAIRS_EG(8) } else { CF_PAIRS_EG(16) }
-#undef CF_PAIRS_EG
-#undef CF_PAIRS
+        if (ty) hipLaunchKernelGGL((k_pairs<16, true>), dim3(nblk((int64_t)a.nlr * 16, 256)), dim3(256), 0, h.stream, a);
+        else hipLaunchKernelGGL((k_pairs<16, false>), dim3(nblk((int64_t)a.nlr * 16, 256)), dim3(256), 0, h.stream, a);
     }
 }
 
