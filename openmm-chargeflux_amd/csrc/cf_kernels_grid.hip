@@ -526,23 +526,32 @@ __global__ void __launch_bounds__(256) k_g_dftz_inv(int rows, int ngz, int KZ, c
         if (r0 + r < nrows) grid[(size_t)(row0 + r0 + r) * ngz + z] = acc[r];
 }
 
-// Every pruned-DFT stage as one batched complex GEMM on the fp64 matrix cores:
-//   C[m][n] = sum_k A[m][k] B[k][n],  A = twiddles (complex), B complex or real, C complex or
-//   its real part.  n is split as (n1, n0) = (n / nin, n % nin) so a batch index can be folded
-//   into n.  One 16x16 output tile per wave, v_mfma_f64_16x16x4_f64 on four k per step:
-//   lane l supplies A[m0 + (l & 15)][k0 + (l >> 4)] and B[k0 + (l >> 4)][n0 + (l & 15)]
-//   straight from global memory (no LDS; the twiddles and B rows are L2-resident), the next
-//   step's operands in flight during the current step's MFMAs.  Complex products as real
-//   MFMAs: re += Ar Br + (-Ai) Bi, im += Ar Bi + Ai Br (2 MFMAs when B or C is real).
-//   Accumulator layout (CDNA4 f64 MFMA): register r of lane l is C[(l >> 4) + 4r][l & 15].
-struct ZGemm {
-    int M, N, K, nin;
-    const double2* A; long sam, sak;
-    const void* B; long sbk, sb0, sb1;
-    void* C; long scm, sc0, sc1;
-    int b_kfast;   // (unused by the MFMA kernel; kept for the call sites' layout notes)
-    // x-slab (multi-rank): which index is the grid x-plane -- 0 none, 1 m, 2 n / xdiv, 3 k.
-    // Tiles whose x-planes lie outside the slab are skipped; along k only the slab is walked.
+// Every pruned-DFT stage as one batched complex GEMM on the fp64 matrix cores,
+//   C(m, n) = sum_k A(m, k) B(k, n),
+//   A(m, k) = A[m sam + k sak]            (complex; real for the forward z stage's grid rows)
+//   B(k, n) = B[k sbk + (n / ndiv) sb1 + (n % ndiv) sb0]                       (complex)
+//   C(m, n) = C[m scm + (n / ndiv) scn1 + (n % ndiv) scn0]   (complex, or its real part)
+// n = (n / ndiv, n % ndiv) folds a batch index into the columns.  A block of 4 waves owns a
+// BM x BN output tile (64 x 64, or 32 x 32 when the big tiles would not give every CU a
+// block); K is walked in chunks of 16 staged in LDS from coalesced global loads (threads run
+// along whichever index of the operand is contiguous in memory), double-buffered: the next
+// chunk's loads are in flight in registers while the current chunk's MFMAs issue.  Each wave
+// computes a (BM/2) x (BN/2) quadrant as 16x16 v_mfma_f64_16x16x4_f64 tiles: lane l supplies
+// A[m0 + (l & 15)][k0 + (l >> 4)] and B[k0 + (l >> 4)][n0 + (l & 15)] (one ds_read_b128 each:
+// re and im), complex products as real MFMAs: re += Ar Br + (-Ai) Bi, im += Ar Bi + Ai Br.
+// Accumulator register r of lane l is C[(l >> 4) + 4r][l & 15].  Every output is summed by
+// one wave in k order: deterministic.
+// The former one-tile-per-wave kernel fetched its operands straight from global memory (16
+// cache lines per load instruction) and ran 11-23 us per stage at C3.
+struct CGemm {
+    int M, N, K;
+    const void* A; long sam, sak;
+    const double2* B; long sbk, sb1, sb0;
+    void* C; long scm, scn1, scn0;
+    int ndiv;
+    // x-slab (multi-rank): which index is the grid x-plane -- 0 none, 1 m / xdiv, 2 n / xdiv,
+    // 3 k.  Tiles whose x-planes all lie outside the slab are skipped; along k only the slab's
+    // planes are walked (k = kbase + t mod K, t < kcount).
     int xdim = 0, xdiv = 1;
     const int* xr = nullptr;
     int W = 0, ngx = 0;
@@ -554,93 +563,143 @@ __device__ __forceinline__ d4 mfma64(double a, double b, d4 c) {
     return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
 }
 
-template <bool BREAL, bool CREAL>
-__global__ void __launch_bounds__(256) k_g_zgemm(ZGemm g) {
-    const int lane = threadIdx.x & 63;
-    const int tiles_m = (g.M + 15) >> 4;
-    const int tile = blockIdx.x * 4 + wave_id();
-    const int tm = tile % tiles_m, tn = tile / tiles_m;
-    if (tn * 16 >= g.N) return;
-    const int m0 = tm * 16, n0 = tn * 16;
-    if (g.xdim == 1 && !x_range_in_slab(m0, min(m0 + 15, g.M - 1), g.xr, g.W, g.ngx)) return;
-    if (g.xdim == 2 && !x_range_in_slab(n0 / g.xdiv, min(n0 + 15, g.N - 1) / g.xdiv, g.xr, g.W, g.ngx)) return;
-    // along k (the x-plane): walk only the slab's planes, k = kbase + t (mod K), t < kcount
+constexpr int kGBK = 16;   // k per LDS chunk (4 MFMA k-steps)
+
+template <int BM, int BN, bool AREAL, bool CREAL>
+__global__ void __launch_bounds__(256) k_g_cgemm(CGemm g) {
+    constexpr int SM = BM / 32, SN = BN / 32;            // 16x16 subtiles per wave and axis
+    constexpr int AP = BM + 1, BP = BN + 1;              // padded LDS rows (conflict-free transposed stores)
+    constexpr int AE = BM * kGBK / 256, BE = BN * kGBK / 256;   // elements per thread per chunk
+    __shared__ double2 sA[2][kGBK * AP];
+    __shared__ double2 sB[2][kGBK * BP];
+    const int tiles_m = (g.M + BM - 1) / BM;
+    const int tm = blockIdx.x % tiles_m, tn = blockIdx.x / tiles_m;
+    const int m0 = tm * BM, n0 = tn * BN;
+    if (g.xdim == 1 && !x_range_in_slab(m0 / g.xdiv, min(m0 + BM - 1, g.M - 1) / g.xdiv, g.xr, g.W, g.ngx)) return;
+    if (g.xdim == 2 && !x_range_in_slab(n0 / g.xdiv, min(n0 + BN - 1, g.N - 1) / g.xdiv, g.xr, g.W, g.ngx)) return;
     int kbase = 0, kcount = g.K;
     if (g.xdim == 3 && g.xr) {
         int s0, len;
         slab_of(g.xr, g.W, g.ngx, s0, len);
         if (len < g.K) { kbase = s0; kcount = len; }
     }
-    const int r = lane & 15, kq = lane >> 4;
-    const int m = m0 + r, n = n0 + r;
-    const bool aok = m < g.M, bok = n < g.N;
-    const double2* Ap = g.A + (long)(aok ? m : 0) * g.sam;
-    const int nn = bok ? n : 0;
-    const long boff = (long)(nn / g.nin) * g.sb1 + (long)(nn % g.nin) * g.sb0;
-    // operands of step t: k = kbase + t + kq (mod K); zero beyond kcount / outside the tile
-    auto load = [&](int t, double& ar, double& ai, double& br, double& bi) {
-        int k = t + kq;
-        ar = ai = br = bi = 0.0;
-        if (k < kcount) {
-            k += kbase;
-            k -= k >= g.K ? g.K : 0;
-            if (aok) {
-                const double2 v = Ap[(long)k * g.sak];
-                ar = v.x; ai = v.y;
+    const int t = threadIdx.x;
+    const bool a_kfast = g.sak == 1, b_kfast = g.sbk == 1;
+    // element e (of AE / BE) of thread t in the chunk: (row, k) of the A tile, (k, col) of B
+    auto a_idx = [&](int e, int& mm, int& kk) {
+        const int q = t + 256 * e;
+        if (a_kfast) { kk = q % kGBK; mm = q / kGBK; } else { mm = q % BM; kk = q / BM; }
+    };
+    auto b_idx = [&](int e, int& kk, int& nn) {
+        const int q = t + 256 * e;
+        if (b_kfast) { kk = q % kGBK; nn = q / kGBK; } else { nn = q % BN; kk = q / BN; }
+    };
+    auto kmap = [&](int kt, bool& ok) {   // chunk-relative k -> operand k (slab walk)
+        ok = kt < kcount;
+        int k = kbase + kt;
+        return k >= g.K ? k - g.K : k;
+    };
+    double2 ra[AE], rb[BE];
+    auto load = [&](int c) {
+#pragma unroll
+        for (int e = 0; e < AE; e++) {
+            int mm, kk;
+            a_idx(e, mm, kk);
+            bool ok;
+            const int k = kmap(c * kGBK + kk, ok);
+            const int m = m0 + mm;
+            ra[e] = make_double2(0.0, 0.0);
+            if (ok && m < g.M) {
+                if (AREAL) ra[e].x = reinterpret_cast<const double*>(g.A)[m * g.sam + k * g.sak];
+                else ra[e] = reinterpret_cast<const double2*>(g.A)[m * g.sam + k * g.sak];
             }
-            if (bok) {
-                if (BREAL) {
-                    br = reinterpret_cast<const double*>(g.B)[boff + (long)k * g.sbk];
-                } else {
-                    const double2 v = reinterpret_cast<const double2*>(g.B)[boff + (long)k * g.sbk];
-                    br = v.x; bi = v.y;
-                }
-            }
+        }
+#pragma unroll
+        for (int e = 0; e < BE; e++) {
+            int kk, nn;
+            b_idx(e, kk, nn);
+            bool ok;
+            const int k = kmap(c * kGBK + kk, ok);
+            const int n = n0 + nn;
+            rb[e] = (ok && n < g.N) ? g.B[k * g.sbk + (long)(n / g.ndiv) * g.sb1 + (long)(n % g.ndiv) * g.sb0]
+                                    : make_double2(0.0, 0.0);
         }
     };
-    // groups of kG steps (4 k each): a group's operands are loaded together while the previous
-    // group's MFMAs issue.  Measured at C3: kG = 1 and the former VALU/LDS kernel take the same
-    // time per stage (11-23 us), kG = 4 is 15% slower (94 VGPRs): the stages are bound by the
-    // strided operand fetch (16 cache lines per load instruction), not by MFMA issue
-    constexpr int kG = 1;
-    d4 cre = {0.0, 0.0, 0.0, 0.0}, cim = {0.0, 0.0, 0.0, 0.0};
-    double ar[kG], ai[kG], br[kG], bi[kG];
+    auto store = [&](int buf) {
 #pragma unroll
-    for (int j = 0; j < kG; j++) load(4 * j, ar[j], ai[j], br[j], bi[j]);
-    for (int t = 0; t < kcount; t += 4 * kG) {
-        double nar[kG], nai[kG], nbr[kG], nbi[kG];
-        const bool more = t + 4 * kG < kcount;
-#pragma unroll
-        for (int j = 0; j < kG; j++) {
-            nar[j] = nai[j] = nbr[j] = nbi[j] = 0.0;
-            if (more) load(t + 4 * kG + 4 * j, nar[j], nai[j], nbr[j], nbi[j]);
+        for (int e = 0; e < AE; e++) {
+            int mm, kk;
+            a_idx(e, mm, kk);
+            sA[buf][kk * AP + mm] = ra[e];
         }
 #pragma unroll
-        for (int j = 0; j < kG; j++) {
-            if (BREAL) {
-                cre = mfma64(ar[j], br[j], cre);
-                cim = mfma64(ai[j], br[j], cim);
-            } else {
-                cre = mfma64(ar[j], br[j], cre);
-                cre = mfma64(-ai[j], bi[j], cre);
-                if (!CREAL) {
-                    cim = mfma64(ar[j], bi[j], cim);
-                    cim = mfma64(ai[j], br[j], cim);
+        for (int e = 0; e < BE; e++) {
+            int kk, nn;
+            b_idx(e, kk, nn);
+            sB[buf][kk * BP + nn] = rb[e];
+        }
+    };
+    const int lane = t & 63, w = wave_id();
+    const int wm = w >> 1, wn = w & 1;
+    const int r16 = lane & 15, kq = lane >> 4;
+    d4 cre[SM][SN], cim[SM][SN];
+#pragma unroll
+    for (int i = 0; i < SM; i++)
+#pragma unroll
+        for (int j = 0; j < SN; j++) {
+            cre[i][j] = d4{0.0, 0.0, 0.0, 0.0};
+            cim[i][j] = d4{0.0, 0.0, 0.0, 0.0};
+        }
+    const int nchunks = (kcount + kGBK - 1) / kGBK;
+    load(0);
+    store(0);
+    __syncthreads();
+    for (int c = 0; c < nchunks; c++) {
+        const int buf = c & 1;
+        if (c + 1 < nchunks) load(c + 1);
+#pragma unroll
+        for (int s = 0; s < kGBK / 4; s++) {
+            const int kr = 4 * s + kq;
+            double2 af[SM], bf[SN];
+#pragma unroll
+            for (int i = 0; i < SM; i++) af[i] = sA[buf][kr * AP + (wm * SM + i) * 16 + r16];
+#pragma unroll
+            for (int j = 0; j < SN; j++) bf[j] = sB[buf][kr * BP + (wn * SN + j) * 16 + r16];
+#pragma unroll
+            for (int i = 0; i < SM; i++)
+#pragma unroll
+                for (int j = 0; j < SN; j++) {
+                    if (AREAL) {
+                        cre[i][j] = mfma64(af[i].x, bf[j].x, cre[i][j]);
+                        cim[i][j] = mfma64(af[i].x, bf[j].y, cim[i][j]);
+                    } else {
+                        cre[i][j] = mfma64(af[i].x, bf[j].x, cre[i][j]);
+                        cre[i][j] = mfma64(-af[i].y, bf[j].y, cre[i][j]);
+                        if (!CREAL) {
+                            cim[i][j] = mfma64(af[i].x, bf[j].y, cim[i][j]);
+                            cim[i][j] = mfma64(af[i].y, bf[j].x, cim[i][j]);
+                        }
+                    }
                 }
-            }
         }
-#pragma unroll
-        for (int j = 0; j < kG; j++) { ar[j] = nar[j]; ai[j] = nai[j]; br[j] = nbr[j]; bi[j] = nbi[j]; }
+        if (c + 1 < nchunks) store(buf ^ 1);
+        __syncthreads();
     }
-    if (!bok) return;
-    const long coff = (long)(n / g.nin) * g.sc1 + (long)(n % g.nin) * g.sc0;
 #pragma unroll
-    for (int q = 0; q < 4; q++) {
-        const int mm = m0 + kq + 4 * q;
-        if (mm >= g.M) continue;
-        const long off = (long)mm * g.scm + coff;
-        if (CREAL) reinterpret_cast<double*>(g.C)[off] = cre[q];
-        else reinterpret_cast<double2*>(g.C)[off] = make_double2(cre[q], cim[q]);
+    for (int j = 0; j < SN; j++) {
+        const int n = n0 + (wn * SN + j) * 16 + r16;
+        if (n >= g.N) continue;
+        const long coff = (long)(n / g.ndiv) * g.scn1 + (long)(n % g.ndiv) * g.scn0;
+#pragma unroll
+        for (int i = 0; i < SM; i++)
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const int m = m0 + (wm * SM + i) * 16 + kq + 4 * q;
+                if (m >= g.M) continue;
+                const long off = (long)m * g.scm + coff;
+                if (CREAL) reinterpret_cast<double*>(g.C)[off] = cre[i][j][q];
+                else reinterpret_cast<double2*>(g.C)[off] = make_double2(cre[i][j][q], cim[i][j][q]);
+            }
     }
 }
 
@@ -939,29 +998,34 @@ void launch_grid_spread(Handle& h) {
                            h.stream, ng, nb, h.g_start, h.g_taps, h.g_grid, h.g_xrange, p.W);
 }
 
-template <bool BREAL, bool CREAL>
-static void zgemm(Handle& h, ZGemm g, int xdim = 0, int xdiv = 1) {
+template <bool AREAL, bool CREAL>
+static void cgemm(Handle& h, CGemm g, int xdim = 0, int xdiv = 1) {
     if (h.g_xrange && xdim) {
         g.xdim = xdim; g.xdiv = xdiv; g.xr = h.g_xrange; g.W = h.gp.W; g.ngx = h.gp.ng[0];
     }
-    const int tiles = ((g.M + 15) / 16) * ((g.N + 15) / 16);
-    hipLaunchKernelGGL((k_g_zgemm<BREAL, CREAL>), dim3(nblk(tiles, 4)), dim3(256), 0, h.stream, g);
+    // 64 x 64 tiles when they give every CU a block, else 32 x 32
+    const long big = (long)((g.M + 63) / 64) * ((g.N + 63) / 64);
+    if (big >= 256) {
+        hipLaunchKernelGGL((k_g_cgemm<64, 64, AREAL, CREAL>), dim3((unsigned)big), dim3(256), 0, h.stream, g);
+    } else {
+        const long small = (long)((g.M + 31) / 32) * ((g.N + 31) / 32);
+        hipLaunchKernelGGL((k_g_cgemm<32, 32, AREAL, CREAL>), dim3((unsigned)small), dim3(256), 0, h.stream, g);
+    }
 }
 
 void launch_grid_dft_fwd(Handle& h) {
     const GridPlan& p = h.gp;
     const int ngx = p.ng[0], ngy = p.ng[1], ngz = p.ng[2], KZ = p.KZ, NY = p.NY, NX = p.NX;
     const long NYKZ = (long)NY * KZ;
-    const double2* tzh = h.g_tw[2] + (size_t)(KZ - 1) * ngz;   // e^{i th nz z}, nz >= 0
-    // z (real rows -> half spectrum): t1[row][nz] = sum_z grid[row][z] Tz[nz][z]
-    zgemm<true, false>(h, ZGemm{KZ, ngx * ngy, ngz, ngx * ngy, tzh, ngz, 1, h.g_grid, 1, ngz, 0, h.g_t1, 1, KZ, 0, 1}, 2,
-                       ngy);
-    // y: t2[o][ny][i] = sum_y Ty[ny][y] t1[o][y][i]
-    zgemm<false, false>(h, ZGemm{NY, ngx * KZ, ngy, KZ, h.g_tw[1], ngy, 1, h.g_t1, KZ, 1, (long)ngy * KZ, h.g_t2, KZ, 1,
-                                 NYKZ, 0}, 2, KZ);
-    // x: b[nx][r] = sum_x Tx[nx][x] t2[x][r]
-    zgemm<false, false>(h, ZGemm{NX, (int)NYKZ, ngx, (int)NYKZ, h.g_tw[0], ngx, 1, h.g_t2, NYKZ, 1, 0, h.g_b, NYKZ, 1, 0, 0},
-                        3);
+    const double2* tzh = h.g_tw[2] + (size_t)(KZ - 1) * ngz;   // e^{i th nz z}, nz >= 0: tzh[nz * ngz + z]
+    // z (real rows -> half spectrum): t1[row][nz] = sum_z grid[row][z] Tz[nz][z], row = (x, y)
+    cgemm<true, false>(h, CGemm{ngx * ngy, KZ, ngz, h.g_grid, ngz, 1, tzh, 1, 0, ngz, h.g_t1, KZ, 0, 1, KZ}, 1, ngy);
+    // y: t2[x][ny][nz] = sum_y Ty[ny][y] t1[x][y][nz], columns n = (x, nz)
+    cgemm<false, false>(h, CGemm{NY, ngx * KZ, ngy, h.g_tw[1], ngy, 1, h.g_t1, KZ, (long)ngy * KZ, 1, h.g_t2, KZ, NYKZ,
+                                 1, KZ}, 2, KZ);
+    // x: b[nx][r] = sum_x Tx[nx][x] t2[x][r], r = (ny, nz)
+    cgemm<false, false>(h, CGemm{NX, (int)NYKZ, ngx, h.g_tw[0], ngx, 1, h.g_t2, NYKZ, 0, 1, h.g_b, NYKZ, 0, 1,
+                                 (int)NYKZ}, 3);
 }
 
 double* grid_reduce_buffer(Handle& h, int64_t* count) {
@@ -986,14 +1050,13 @@ void launch_grid_dft_inv(Handle& h) {
     const long NYKZ = (long)NY * KZ;
     const double2* tzh = h.g_tw[2] + (size_t)(KZ - 1) * ngz;
     // x: t2[x][r] = sum_nx Tx[nx][x] f[nx][r]
-    zgemm<false, false>(h, ZGemm{ngx, (int)NYKZ, NX, (int)NYKZ, h.g_tw[0], 1, ngx, h.g_b, NYKZ, 1, 0, h.g_t2, NYKZ, 1, 0, 0},
-                        1);
-    // y: t1[o][y][i] = sum_ny Ty[ny][y] t2[o][ny][i]
-    zgemm<false, false>(h, ZGemm{ngy, ngx * KZ, NY, KZ, h.g_tw[1], 1, ngy, h.g_t2, KZ, 1, NYKZ, h.g_t1, KZ, 1,
-                                 (long)ngy * KZ, 0}, 2, KZ);
-    // z (half spectrum -> real rows): grid[row][z] = Re sum_nz Tz[nz][z] t1[row][nz]
-    zgemm<false, true>(h, ZGemm{ngz, ngx * ngy, KZ, ngx * ngy, tzh, 1, ngz, h.g_t1, 1, KZ, 0, h.g_grid, 1, ngz, 0, 1}, 2,
-                       ngy);
+    cgemm<false, false>(h, CGemm{ngx, (int)NYKZ, NX, h.g_tw[0], 1, ngx, h.g_b, NYKZ, 0, 1, h.g_t2, NYKZ, 0, 1,
+                                 (int)NYKZ}, 1, 1);
+    // y: t1[x][y][nz] = sum_ny Ty[ny][y] t2[x][ny][nz], columns n = (x, nz)
+    cgemm<false, false>(h, CGemm{ngy, ngx * KZ, NY, h.g_tw[1], 1, ngy, h.g_t2, KZ, NYKZ, 1, h.g_t1, KZ,
+                                 (long)ngy * KZ, 1, KZ}, 2, KZ);
+    // z (half spectrum -> real rows): grid[row][z] = Re sum_nz t1[row][nz] Tz[nz][z], row = (x, y)
+    cgemm<false, true>(h, CGemm{ngx * ngy, ngz, KZ, h.g_t1, KZ, 1, tzh, ngz, 0, 1, h.g_grid, ngz, 0, 1, ngz}, 1, ngy);
 }
 
 void launch_grid_interp(Handle& h) {
