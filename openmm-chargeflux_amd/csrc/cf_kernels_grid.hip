@@ -749,6 +749,29 @@ __global__ void __launch_bounds__(256) k_g_coeffs(int KX, int KY, int KZ, double
 // ---------------------------------------------------------------------------------
 constexpr int kInterpThreads = 512;
 
+// Sum of v over the 64 lanes of a wave into lane 63, by DPP moves (VALU) in a fixed order:
+// quad xor 1, quad xor 2, half-row mirror, row mirror (every row of 16 then holds its sum),
+// row_bcast15 into rows 1 and 3, row_bcast31 into rows 2 and 3.  The __shfl_xor butterfly
+// this replaces costs two ds_bpermute (LDS instructions) per step and value: 48 per atom in
+// the interpolation, whose LDS issue queue is its bottleneck.
+template <int CTRL, int ROWS>
+__device__ __forceinline__ double dpp_f64(double v) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)b, CTRL, ROWS, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, ROWS, 0xF, false);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
+__device__ __forceinline__ double wave_sum_lane63(double v) {
+    v += dpp_f64<0xB1, 0xF>(v);    // quad_perm [1,0,3,2]
+    v += dpp_f64<0x4E, 0xF>(v);    // quad_perm [2,3,0,1]
+    v += dpp_f64<0x141, 0xF>(v);   // row_half_mirror
+    v += dpp_f64<0x140, 0xF>(v);   // row_mirror
+    v += dpp_f64<0x142, 0xA>(v);   // row_bcast15 -> rows 1, 3 (rows 0, 2 add 0)
+    v += dpp_f64<0x143, 0xC>(v);   // row_bcast31 -> rows 2, 3
+    return v;
+}
+
 template <int W>
 __global__ void __launch_bounds__(kInterpThreads) k_g_interp(int3 ng, int3 nb, const int* __restrict__ start,
                                                              const int4* __restrict__ g0s,
@@ -758,7 +781,7 @@ __global__ void __launch_bounds__(kInterpThreads) k_g_interp(int3 ng, int3 nb, c
     constexpr int R = 7 + W;
     constexpr int NJ = (W + 3) / 4;
     extern __shared__ double sg[];   // [R][R][R]
-    __shared__ double2 xt[kInterpThreads / 64][16];   // per wave: the current atom's x taps (v, dv)
+    __shared__ double2 tp[kInterpThreads / 64][3][16];   // per wave: the current atom's taps (v, dv) per axis
     // XCD-aware tile order (as in k_g_spread): XCD blockIdx % 8 takes a contiguous 1/8 of the
     // (y, z) tile plane over every x, so neighbouring tiles' potential halos share its L2
     const int nyz = nb.y * nb.z;
@@ -809,14 +832,15 @@ __global__ void __launch_bounds__(kInterpThreads) k_g_interp(int3 ng, int3 nb, c
         const double sd = d == 0 ? sr.x : (d == 1 ? sr.y : sr.z);
         double v = 0, dv = 0;
         if (d < 3 && m < W) es_tap(ceil(sd - 0.5 * W) + m - sd, 2.0 / W, beta, v, dv);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");   // previous atom's reads of xt done
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");   // previous atom's reads of tp done
         __builtin_amdgcn_wave_barrier();
-        if (d == 0) xt[w][m] = make_double2(v, dv);
+        if (d < 3) tp[w][d][m] = make_double2(v, dv);   // zero beyond W
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         const int rx = g.x & 7, ry = g.y & 7, rz = g.z & 7;
-        const double zt = __shfl(v, 32 + k), dzt = __shfl(dv, 32 + k);
+        const double2 zv = tp[w][2][k];
+        const double zt = zv.x, dzt = zv.y;
         double t0[NJ], t1[NJ];
 #pragma unroll
         for (int jj = 0; jj < NJ; jj++) { t0[jj] = 0; t1[jj] = 0; }
@@ -824,7 +848,7 @@ __global__ void __launch_bounds__(kInterpThreads) k_g_interp(int3 ng, int3 nb, c
         const double* base = sg + (rx * R + ry) * R + rz + kk;
 #pragma unroll
         for (int i = 0; i < W; i++) {
-            const double2 xv = xt[w][i];   // broadcast LDS read (was 4 v_readlane per i)
+            const double2 xv = tp[w][0][i];   // broadcast LDS read (was 4 v_readlane per i)
             const double xi = xv.x, dxi = xv.y;
 #pragma unroll
             for (int jj = 0; jj < NJ; jj++) {
@@ -838,21 +862,19 @@ __global__ void __launch_bounds__(kInterpThreads) k_g_interp(int3 ng, int3 nb, c
 #pragma unroll
         for (int jj = 0; jj < NJ; jj++) {
             const int j = 4 * jj + jg;
-            const int jl = 16 + (j < 16 ? j : 15);
-            double yt = __shfl(v, jl), dyt = __shfl(dv, jl);
-            if (j >= W) { yt = 0; dyt = 0; }
+            const double2 yv = tp[w][1][j < 16 ? j : 15];   // 4 addresses per wave (one per row)
+            const double yt = j < W ? yv.x : 0.0, dyt = j < W ? yv.y : 0.0;
             pv += t0[jj] * yt;
             px += t1[jj] * yt;
             py += t0[jj] * dyt;
         }
         pz = pv * dzt;
         pv *= zt; px *= zt; py *= zt;
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) {
-            pv += __shfl_xor(pv, off); px += __shfl_xor(px, off);
-            py += __shfl_xor(py, off); pz += __shfl_xor(pz, off);
-        }
-        if (lane == 0) {   // each owned atom is in exactly one bin: no other writer
+        pv = wave_sum_lane63(pv);
+        px = wave_sum_lane63(px);
+        py = wave_sum_lane63(py);
+        pz = wave_sum_lane63(pz);
+        if (lane == 63) {   // each owned atom is in exactly one bin: no other writer
             const int i = lo + g.w;
             dedq[i] += pv;
             f_part[3 * i] += -sr.w * gscale.x * px;
