@@ -421,6 +421,144 @@ __global__ void __launch_bounds__(512) k_g_spread(int3 ng, int3 nb, const int* _
     }
 }
 
+// 2'. spread, one 256-thread workgroup per 8^3 tile (the default).  The tile's source atoms
+//     (first tap in one of the NS^3 bins 0..NS-1 tiles behind it) are walked in passes of 64;
+//     each pass stages, per atom, only the three 8-tap windows this tile reads (the bin-aligned
+//     rows make a window a fixed 64-B piece: 192 B per atom instead of the 576-B row set), and
+//     the 4 waves take every 4th atom of the pass: lane (y, z) accumulates the tile's 8 x
+//     points of its (y, z) column (1 mul + 8 FMAs per atom; the x window is a broadcast LDS
+//     read).  Every wave is busy in every pass (the 2x2x2-tile kernel above leaves the waves
+//     whose tile a pass's source column does not reach waiting at the pass barrier), and the
+//     small blocks (25 KB LDS, <= 64 VGPRs) keep ~6 per CU resident, so a pass's load latency
+//     hides behind other blocks.  The 4 waves' partial tiles are summed in fixed order.
+constexpr int kSpPass = 64;        // atoms per pass
+constexpr int kSpWin = 24;         // doubles staged per atom: x, y, z windows of 8
+constexpr int kSpMaxSrc = 1024;    // source atoms whose slots are resolved per segment
+
+template <int NS>
+__global__ void __launch_bounds__(256) k_g_spread_tile(int3 ng, int3 nb, const int* __restrict__ start,
+                                                       const double* __restrict__ taps, const int4* __restrict__ g0s,
+                                                       double* __restrict__ grid, const int* __restrict__ xr, int W) {
+    constexpr int NB3 = NS * NS * NS;
+    __shared__ __attribute__((aligned(16))) double st[2 * kSpPass * kSpWin];   // 24.6 KB; reused by the reduction
+    __shared__ int bin_start[NB3], bin_pre[NB3 + 1], bin_db[NB3];
+    __shared__ int2 src[kSpMaxSrc];   // (slot, source bin) of the segment's atoms that reach this tile
+    __shared__ int wcnt[4];
+    // XCD-aware tile order (as in k_g_interp)
+    const int nyz = nb.y * nb.z;
+    int tile = blockIdx.x;
+    if (nyz % 8 == 0) {
+        const int per = nyz / 8, i = blockIdx.x / 8;
+        tile = (i / per) * nyz + (blockIdx.x % 8) * per + i % per;
+    }
+    const int tz = tile % nb.z, ty = (tile / nb.z) % nb.y, tx = tile / (nb.z * nb.y);
+    if (!x_range_in_slab(8 * tx, 8 * tx + 7, xr, W, ng.x)) return;
+    const int t = threadIdx.x;
+    if (t < NB3) {
+        const int dx = t / (NS * NS), dy = (t / NS) % NS, dz = t % NS;   // tiles behind this one
+        const int b = (wrapb(tx - dx, nb.x) * nb.y + wrapb(ty - dy, nb.y)) * nb.z + wrapb(tz - dz, nb.z);
+        const int s0 = start[b];
+        bin_start[t] = s0;
+        bin_pre[t + 1] = start[b + 1] - s0;   // counts, scanned below
+        bin_db[t] = (dx << 8) | (dy << 4) | dz;
+    }
+    __syncthreads();
+    if (t == 0) {
+        bin_pre[0] = 0;
+        for (int i = 0; i < NB3; i++) bin_pre[i + 1] += bin_pre[i];
+    }
+    __syncthreads();
+    const int total = bin_pre[NB3];
+    const int lane = t & 63, w = wave_id();
+    const int y = lane >> 3, z = lane & 7;
+    double acc[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) acc[i] = 0.0;
+    for (int seg0 = 0; seg0 < total; seg0 += kSpMaxSrc) {
+        const int nall = min(kSpMaxSrc, total - seg0);
+        __syncthreads();   // previous segment's passes done with src
+        // resolve (slot, bin) of each source atom and keep, in source order, those whose support
+        // reaches this tile: a window db tiles ahead ([8 db, 8 db + 8) of the bin-aligned row) is
+        // all zero when the taps [r, r + W) end before it (r = first tap mod 8) -- about a third
+        // of the (tile, atom) pairs at W = 14
+        int nseg = 0;
+        for (int u0 = 0; u0 < nall; u0 += 256) {
+            const int u = u0 + t;
+            bool keep = false;
+            int2 sb = make_int2(0, 0);
+            if (u < nall) {
+                const int a = seg0 + u;
+                int lo = 0, hi = NB3;   // bin i with bin_pre[i] <= a < bin_pre[i + 1]
+                while (hi - lo > 1) {
+                    const int mid = (lo + hi) >> 1;
+                    if (bin_pre[mid] <= a) lo = mid; else hi = mid;
+                }
+                sb = make_int2(bin_start[lo] + (a - bin_pre[lo]), lo);
+                const int4 g = g0s[sb.x];
+                const int db = bin_db[lo];
+                keep = (g.x & 7) + W > 8 * (db >> 8) && (g.y & 7) + W > 8 * ((db >> 4) & 15) && (g.z & 7) + W > 8 * (db & 15);
+            }
+            const unsigned long long m = __ballot(keep);
+            if ((t & 63) == 0) wcnt[t >> 6] = __popcll(m);
+            __syncthreads();
+            int off = nseg;
+            for (int q = 0; q < (t >> 6); q++) off += wcnt[q];
+            if (keep) src[off + __popcll(m & ((1ull << (t & 63)) - 1))] = sb;
+            nseg += wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
+            __syncthreads();
+        }
+        if (nseg == 0) continue;
+        // staging: 16-B piece e of the pass = atom e / 12, axis (e % 12) / 4, quarter e % 4 of the window
+        constexpr int kPieces = kSpPass * kSpWin / 2;          // 768
+        constexpr int kPer = kPieces / 256;                     // 3 per thread
+        v2d r[kPer];
+        auto fetch = [&](int base, int n) {
+#pragma unroll
+            for (int q = 0; q < kPer; q++) {
+                const int e = t + 256 * q;
+                const int a = e / 12, c = e - 12 * a, d = c >> 2, h = c & 3;
+                const int u = base + min(a, n - 1);
+                const int2 sb = src[u];
+                const int db = (bin_db[sb.y] >> (8 - 4 * d)) & 15;
+                r[q] = *reinterpret_cast<const v2d*>(taps + (size_t)sb.x * kTapStride + d * kRow + 8 * db + 2 * h);
+            }
+        };
+        auto stage = [&](double* buf) {
+#pragma unroll
+            for (int q = 0; q < kPer; q++) reinterpret_cast<v2d*>(buf)[t + 256 * q] = r[q];
+        };
+        const int npass = (nseg + kSpPass - 1) / kSpPass;
+        fetch(0, min(kSpPass, nseg));
+        stage(st);
+        __syncthreads();
+        for (int p = 0; p < npass; p++) {
+            const int base = p * kSpPass, n = min(kSpPass, nseg - base);
+            if (p + 1 < npass) fetch(base + kSpPass, min(kSpPass, nseg - base - kSpPass));
+            const double* buf = st + (p & 1) * kSpPass * kSpWin;
+            for (int a = w; a < n; a += 4) {
+                const double* rw = buf + a * kSpWin;
+                const double yz = rw[8 + y] * rw[16 + z];
+#pragma unroll
+                for (int i = 0; i < 8; i++) acc[i] = fma(rw[i], yz, acc[i]);
+            }
+            if (p + 1 < npass) stage(st + ((p + 1) & 1) * kSpPass * kSpWin);
+            __syncthreads();
+        }
+    }
+    // the 4 waves' partial tiles, summed in fixed wave order
+    __syncthreads();
+    double* red = st;   // [4][8][64]
+#pragma unroll
+    for (int i = 0; i < 8; i++) red[(w * 8 + i) * 64 + lane] = acc[i];
+    __syncthreads();
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+        const int pt = t + 256 * h, i = pt >> 6, l = pt & 63;
+        const double v = ((red[i * 64 + l] + red[(8 + i) * 64 + l]) + red[(16 + i) * 64 + l]) + red[(24 + i) * 64 + l];
+        grid[((size_t)(8 * tx + i) * ng.y + 8 * ty + (l >> 3)) * ng.z + 8 * tz + (l & 7)] = v;
+    }
+}
+
 // ---------------------------------------------------------------------------------
 // 3. pruned DFT stages (VALU)
 // ---------------------------------------------------------------------------------
@@ -1009,6 +1147,16 @@ void launch_grid_sort(Handle& h, const double* pos) {
 void launch_grid_spread(Handle& h) {
     const GridPlan& p = h.gp;
     const int3 ng = make_int3(p.ng[0], p.ng[1], p.ng[2]), nb = make_int3(p.nb[0], p.nb[1], p.nb[2]);
+    static const bool old_spread = getenv("CF_EXP_OLD_SPREAD") != nullptr;
+    if (!old_spread) {
+        if (p.W <= 9)
+            hipLaunchKernelGGL(k_g_spread_tile<2>, dim3(p.nbins), dim3(256), 0, h.stream, ng, nb, h.g_start, h.g_taps,
+                               h.g_g0s, h.g_grid, h.g_xrange, p.W);
+        else
+            hipLaunchKernelGGL(k_g_spread_tile<3>, dim3(p.nbins), dim3(256), 0, h.stream, ng, nb, h.g_start, h.g_taps,
+                               h.g_g0s, h.g_grid, h.g_xrange, p.W);
+        return;
+    }
     const int nblocks = ((p.nb[0] + 1) / 2) * ((p.nb[1] + 1) / 2) * ((p.nb[2] + 1) / 2);
     // a first tap in bin B reaches tiles B .. B + NS - 1: NS = 2 when W <= 9 (8 source bins per
     // tile instead of 27)
