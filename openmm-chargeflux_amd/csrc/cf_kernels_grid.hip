@@ -431,19 +431,19 @@ __global__ void __launch_bounds__(512) k_g_spread(int3 ng, int3 nb, const int* _
 //     whose tile a pass's source column does not reach waiting at the pass barrier), and the
 //     small blocks (25 KB LDS, <= 64 VGPRs) keep ~6 per CU resident, so a pass's load latency
 //     hides behind other blocks.  The 4 waves' partial tiles are summed in fixed order.
-constexpr int kSpPass = 64;        // atoms per pass
 constexpr int kSpWin = 24;         // doubles staged per atom: x, y, z windows of 8
 constexpr int kSpMaxSrc = 1024;    // source atoms whose slots are resolved per segment
 
-template <int NS>
+template <int NS, int kSpPass>
 __global__ void __launch_bounds__(256) k_g_spread_tile(int3 ng, int3 nb, const int* __restrict__ start,
                                                        const double* __restrict__ taps, const int4* __restrict__ g0s,
                                                        double* __restrict__ grid, const int* __restrict__ xr, int W) {
     constexpr int NB3 = NS * NS * NS;
-    __shared__ __attribute__((aligned(16))) double st[2 * kSpPass * kSpWin];   // 24.6 KB; reused by the reduction
+    constexpr int kStD = 2 * kSpPass * kSpWin > 4 * 8 * 64 ? 2 * kSpPass * kSpWin : 4 * 8 * 64;
+    __shared__ __attribute__((aligned(16))) double st[kStD];   // 2 staging buffers; reused by the reduction
     __shared__ int bin_start[NB3], bin_pre[NB3 + 1], bin_db[NB3];
-    __shared__ int2 src[kSpMaxSrc];   // (slot, source bin) of the segment's atoms that reach this tile
-    __shared__ int wcnt[4];
+    __shared__ int src[kSpMaxSrc];   // slot << 5 | source bin, of the segment's atoms that reach this tile
+    __shared__ int wcnt[4 * (kSpMaxSrc / 256)];
     // XCD-aware tile order (as in k_g_interp)
     const int nyz = nb.y * nb.z;
     int tile = blockIdx.x;
@@ -481,11 +481,13 @@ __global__ void __launch_bounds__(256) k_g_spread_tile(int3 ng, int3 nb, const i
         // reaches this tile: a window db tiles ahead ([8 db, 8 db + 8) of the bin-aligned row) is
         // all zero when the taps [r, r + W) end before it (r = first tap mod 8) -- about a third
         // of the (tile, atom) pairs at W = 14
-        int nseg = 0;
-        for (int u0 = 0; u0 < nall; u0 += 256) {
-            const int u = u0 + t;
-            bool keep = false;
-            int2 sb = make_int2(0, 0);
+        constexpr int kRounds = kSpMaxSrc / 256;
+        int2 sb[kRounds];
+        int4 g[kRounds];
+#pragma unroll
+        for (int k = 0; k < kRounds; k++) {   // every source's slot, then every g0s load in flight at once
+            const int u = 256 * k + t;
+            sb[k] = make_int2(0, 0);
             if (u < nall) {
                 const int a = seg0 + u;
                 int lo = 0, hi = NB3;   // bin i with bin_pre[i] <= a < bin_pre[i + 1]
@@ -493,39 +495,51 @@ __global__ void __launch_bounds__(256) k_g_spread_tile(int3 ng, int3 nb, const i
                     const int mid = (lo + hi) >> 1;
                     if (bin_pre[mid] <= a) lo = mid; else hi = mid;
                 }
-                sb = make_int2(bin_start[lo] + (a - bin_pre[lo]), lo);
-                const int4 g = g0s[sb.x];
-                const int db = bin_db[lo];
-                keep = (g.x & 7) + W > 8 * (db >> 8) && (g.y & 7) + W > 8 * ((db >> 4) & 15) && (g.z & 7) + W > 8 * (db & 15);
+                sb[k] = make_int2(bin_start[lo] + (a - bin_pre[lo]), lo);
             }
-            const unsigned long long m = __ballot(keep);
-            if ((t & 63) == 0) wcnt[t >> 6] = __popcll(m);
-            __syncthreads();
-            int off = nseg;
-            for (int q = 0; q < (t >> 6); q++) off += wcnt[q];
-            if (keep) src[off + __popcll(m & ((1ull << (t & 63)) - 1))] = sb;
-            nseg += wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
-            __syncthreads();
         }
+#pragma unroll
+        for (int k = 0; k < kRounds; k++) g[k] = 256 * k + t < nall ? g0s[sb[k].x] : make_int4(0, 0, 0, 0);
+        bool keep[kRounds];
+        unsigned long long m[kRounds];
+#pragma unroll
+        for (int k = 0; k < kRounds; k++) {
+            const int db = bin_db[sb[k].y];
+            keep[k] = 256 * k + t < nall && (g[k].x & 7) + W > 8 * (db >> 8) &&
+                      (g[k].y & 7) + W > 8 * ((db >> 4) & 15) && (g[k].z & 7) + W > 8 * (db & 15);
+            m[k] = __ballot(keep[k]);
+            if ((t & 63) == 0) wcnt[4 * k + (t >> 6)] = __popcll(m[k]);
+        }
+        __syncthreads();
+        int nseg = 0;
+#pragma unroll
+        for (int k = 0; k < kRounds; k++) {   // kept sources in source order: (round, wave, lane)
+            int off = nseg;
+            for (int q = 0; q < (t >> 6); q++) off += wcnt[4 * k + q];
+            if (keep[k]) src[off + __popcll(m[k] & ((1ull << (t & 63)) - 1))] = (sb[k].x << 5) | sb[k].y;
+            nseg += wcnt[4 * k] + wcnt[4 * k + 1] + wcnt[4 * k + 2] + wcnt[4 * k + 3];
+        }
+        __syncthreads();
         if (nseg == 0) continue;
         // staging: 16-B piece e of the pass = atom e / 12, axis (e % 12) / 4, quarter e % 4 of the window
-        constexpr int kPieces = kSpPass * kSpWin / 2;          // 768
-        constexpr int kPer = kPieces / 256;                     // 3 per thread
+        constexpr int kPieces = kSpPass * kSpWin / 2;          // 768 at 64 atoms per pass
+        constexpr int kPer = (kPieces + 255) / 256;             // 3 per thread at 64
         v2d r[kPer];
         auto fetch = [&](int base, int n) {
 #pragma unroll
             for (int q = 0; q < kPer; q++) {
-                const int e = t + 256 * q;
+                const int e = min(t + 256 * q, kPieces - 1);
                 const int a = e / 12, c = e - 12 * a, d = c >> 2, h = c & 3;
                 const int u = base + min(a, n - 1);
-                const int2 sb = src[u];
-                const int db = (bin_db[sb.y] >> (8 - 4 * d)) & 15;
-                r[q] = *reinterpret_cast<const v2d*>(taps + (size_t)sb.x * kTapStride + d * kRow + 8 * db + 2 * h);
+                const int sb = src[u], bin = sb & 31;
+                const int db = (bin_db[bin] >> (8 - 4 * d)) & 15;
+                r[q] = *reinterpret_cast<const v2d*>(taps + (size_t)(sb >> 5) * kTapStride + d * kRow + 8 * db + 2 * h);
             }
         };
         auto stage = [&](double* buf) {
 #pragma unroll
-            for (int q = 0; q < kPer; q++) reinterpret_cast<v2d*>(buf)[t + 256 * q] = r[q];
+            for (int q = 0; q < kPer; q++)
+                if (kPieces % 256 == 0 || t + 256 * q < kPieces) reinterpret_cast<v2d*>(buf)[t + 256 * q] = r[q];
         };
         const int npass = (nseg + kSpPass - 1) / kSpPass;
         fetch(0, min(kSpPass, nseg));
@@ -1149,12 +1163,14 @@ void launch_grid_spread(Handle& h) {
     const int3 ng = make_int3(p.ng[0], p.ng[1], p.ng[2]), nb = make_int3(p.nb[0], p.nb[1], p.nb[2]);
     static const bool old_spread = getenv("CF_EXP_OLD_SPREAD") != nullptr;
     if (!old_spread) {
-        if (p.W <= 9)
-            hipLaunchKernelGGL(k_g_spread_tile<2>, dim3(p.nbins), dim3(256), 0, h.stream, ng, nb, h.g_start, h.g_taps,
-                               h.g_g0s, h.g_grid, h.g_xrange, p.W);
-        else
-            hipLaunchKernelGGL(k_g_spread_tile<3>, dim3(p.nbins), dim3(256), 0, h.stream, ng, nb, h.g_start, h.g_taps,
-                               h.g_g0s, h.g_grid, h.g_xrange, p.W);
+        static const int pass = getenv("CF_EXP_SPREAD_PASS") ? atoi(getenv("CF_EXP_SPREAD_PASS")) : 32;
+#define CF_SPT(NS_, P_) hipLaunchKernelGGL((k_g_spread_tile<NS_, P_>), dim3(p.nbins), dim3(256), 0, h.stream, ng, nb, \
+                                           h.g_start, h.g_taps, h.g_g0s, h.g_grid, h.g_xrange, p.W)
+        if (p.W <= 9) { CF_SPT(2, 64); }
+        else if (pass == 32) { CF_SPT(3, 32); }
+        else if (pass == 128) { CF_SPT(3, 128); }
+        else { CF_SPT(3, 64); }
+#undef CF_SPT
         return;
     }
     const int nblocks = ((p.nb[0] + 1) / 2) * ((p.nb[1] + 1) / 2) * ((p.nb[2] + 1) / 2);
