@@ -158,6 +158,20 @@ void set_cells(cf_handle* H, const double L[3]) {
         h.ncell_alloc = (int)ncell;
     }
     h.nc[0] = nc[0]; h.nc[1] = nc[1]; h.nc[2] = nc[2];
+    // half neighbour list: one rank, fp64, the wave-cooperative builder (>= 4
+    // cells per axis), and cells small enough for the kernel's LDS window (14 cells <= 4096
+    // atoms) and the entry's 10-bit index within a cell -- with a margin for density variation;
+    // k_pairs_half flags the rare evaluation that does not fit and k_excl then rescans
+    const bool no_half = getenv("CF_HALF") && std::string(getenv("CF_HALF")) == "0";   // A/B and tests
+    const double per_cell = (double)h.n / (double)ncell;
+    h.half = !no_half && h.pbc && h.world == 1 && !h.mixed && nc[0] >= 4 && nc[1] >= 4 && nc[2] >= 4 &&
+             per_cell * 14.0 * 1.25 <= 4096.0 && per_cell * 2.0 < 1024.0;
+    if (h.half && ncell > h.win_cells) {
+        if (h.win_out) { (void)hipFree(h.win_out); (void)hipFree(h.win_woff); }
+        cf::check_hip(hipMalloc(&h.win_out, sizeof(unsigned long long) * 4 * 4096 * (size_t)ncell), "half-list windows");
+        cf::check_hip(hipMalloc(&h.win_woff, sizeof(int) * 14 * (size_t)ncell), "half-list windows");
+        h.win_cells = (int)ncell;
+    }
 }
 
 void set_box(cf_handle* H, const double* box9) {
@@ -531,6 +545,8 @@ CF_EXPORT int cf_create(const cf_params* p, const cf_options* opt, cf_handle** o
             h.atom_tmp = dalloc<int>(H, n);
             h.skin_flag = dalloc<int>(H, 1);
             check_hip(hipMemset(h.skin_flag, 0, sizeof(int)), "memset");
+            h.half_flag = dalloc<int>(H, 1);
+            check_hip(hipMemset(h.half_flag, 0, sizeof(int)), "memset");
             h.n_builds_dev = dalloc<long long>(H, 1);
             check_hip(hipMemset(h.n_builds_dev, 0, sizeof(long long)), "memset");
             if (h.world > 1) h.own_s = dalloc<int>(H, std::max(nown, 1));  // owned atoms, cell-sorted
@@ -609,6 +625,7 @@ CF_EXPORT int cf_destroy(cf_handle* H) {
         for (void* p : H->allocs) (void)hipFree(p);
         for (auto& v : H->ev)
             for (hipEvent_t e : v) (void)hipEventDestroy(e);
+        if (H->h.win_out) { (void)hipFree(H->h.win_out); (void)hipFree(H->h.win_woff); }
         if (H->h.cell_start) (void)hipFree(H->h.cell_start);
         if (H->h.cell_end) (void)hipFree(H->h.cell_end);
         if (H->h.cell_cnt) (void)hipFree(H->h.cell_cnt);

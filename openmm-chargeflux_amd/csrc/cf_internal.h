@@ -145,6 +145,12 @@ struct Handle {
     int nb_cap = 0;             // capacity of each of the 4 neighbour sub-lists of an atom
     int* nl = nullptr;          // [4][nb_cap][N] transposed sub-lists (sorted index | shift<<26)
     int* nl_cnt = nullptr;      // [4][N]
+    // half list: one rank, fp64, >= 4 cells per axis
+    bool half = false;
+    int* half_flag = nullptr;   // [1] device: half-list sums unusable this evaluation (fp64 rescan)
+    unsigned long long* win_out = nullptr;   // [ncell][4096][4] window partials (fixed point)
+    int* win_woff = nullptr;    // [ncell][14]
+    int win_cells = 0;          // cells win_out / win_woff are sized for
     // k-space (MFMA path)
     int npad = 0;               // owned rows of the phase tables, padded to the S-pass tile
     double2* tab_xq = nullptr;  // [Nown][KX]

@@ -330,6 +330,22 @@ constexpr int kMaxLjTypes = 64;  // LJ types carried in the 6 high bits of a lis
 constexpr int kSeg = 4;          // neighbour sub-lists per atom (one per scanning wave / pair lane)
 constexpr int kShiftBits = 26;
 constexpr int kBruteShift = 31;  // shift code: minimum image by floor (brute-force path)
+// Half neighbour list: row i keeps partner j when j's cell is i's own cell
+// (and j > i in sorted order) or one of the 13 "forward" neighbour cells, offsets d with
+// code27 = (dx+1)*9 + (dy+1)*3 + (dz+1) > 13 (lexicographically positive).  Entry = k (window
+// cell: 0 own cell, code27 - 13 forward) | j - cell_start << 4 | LJ type << 14.
+constexpr int kHalfWin = 14;          // window cells per block (own + 13 forward)
+constexpr int kHalfMaxWin = 4096;     // window atoms per block (LDS accumulators: 128 KB)
+constexpr int kHalfJBits = 10;        // atoms per cell < 1024
+constexpr int kHalfTypeShift = 4 + kHalfJBits;
+// j-side sums in 64-bit fixed point (integer adds: exact, so any order gives the same bits):
+// v -> round(v 2^34) via the 1.5 * 2^52 magic add (exact for |v 2^34| < 2^51); a contribution
+// with |v| >= 2^16 flags the evaluation for the fp64 rescan fallback
+constexpr double kFixScale = 17179869184.0;            // 2^34
+constexpr double kFixInv = 1.0 / 17179869184.0;
+constexpr double kFixMagic = 6755399441055744.0;       // 1.5 * 2^52
+constexpr long long kFixMagicBits = 0x4338000000000000LL;
+constexpr double kFixMax = 65536.0;
 
 struct DirectArgs {
     int n, lo, hi, include_forces;
@@ -354,6 +370,12 @@ struct DirectArgs {
     const double* dedq_self;
     int* nl; int* nl_cnt;
     double* dedq; double* f_part; double* e_atom;
+    // half list (single rank, fp64): pairs once, j-side summed in fixed point (k_pairs_half)
+    int half;
+    int* half_flag;             // device: 1 = the half-list evaluation cannot be used (k_excl rescans)
+    unsigned long long* win_out;// [ncell][kHalfMaxWin][4] per-cell window partials (fixed point)
+    int* win_woff;              // [ncell][kHalfWin] window offsets of the 14 window cells
+    const int* key_s;           // cell key per sorted slot
 };
 
 __device__ __forceinline__ int own_slot(const DirectArgs& a, int c) { return a.own_s ? a.own_s[c] : c; }
@@ -496,7 +518,7 @@ __global__ void __launch_bounds__(kWaveNL * kSeg) k_nlist_wave(DirectArgs a) {
     const int c0[3] = {key0 / (a.nc.y * a.nc.z), (key0 / a.nc.z) % a.nc.y, key0 % a.nc.z};
     const int ncs[3] = {a.nc.x, a.nc.y, a.nc.z};
     const double Ls[3] = {a.L.x, a.L.y, a.L.z};
-    int lo3[3], hi3[3], lsh[3];
+    int lo3[3], hi3[3], lsh[3], ucell[3];
     bool fits = true;
 #pragma unroll
     for (int d = 0; d < 3; d++) {
@@ -504,6 +526,7 @@ __global__ void __launch_bounds__(kWaveNL * kSeg) k_nlist_wave(DirectArgs a) {
         if (dd > ncs[d] / 2) dd -= ncs[d];
         if (dd < -(ncs[d] / 2)) dd += ncs[d];
         int u = c0[d] + dd;  // unwrapped cell coordinate of this lane in the block frame
+        ucell[d] = u;
         lsh[d] = u < 0 ? -1 : (u >= ncs[d] ? 1 : 0);  // image of this lane's (wrapped) position
         int mn = u, mx = u;
         for (int off = 32; off > 0; off >>= 1) {
@@ -527,6 +550,11 @@ __global__ void __launch_bounds__(kWaveNL * kSeg) k_nlist_wave(DirectArgs a) {
         cnt++;
     };
     if (!fits) {  // wave-uniform (and block-uniform: every wave sees the same 64 atoms)
+        if (a.half) {   // half lists need the block frame: hand the evaluation to the fp64 rescan
+            if (active) a.nl_cnt[(size_t)seg * a.nlr + c] = 0;
+            if (lane == 0) atomicOr(a.half_flag, 1);
+            return;
+        }
         if (active)
             scan_cells(a, s, pi, a.rl2, [&](int t, int code, double, double, double, double) {
                 emit(t, a.atom_sorted[t], a.typ_s ? a.typ_s[t] : code);
@@ -534,6 +562,12 @@ __global__ void __launch_bounds__(kWaveNL * kSeg) k_nlist_wave(DirectArgs a) {
         if (active) a.nl_cnt[(size_t)seg * a.nlr + c] = cnt;
         return;
     }
+    bool jbig = false;   // half mode: an atom index within its cell beyond kHalfJBits
+    auto emit_half = [&](int entry, int j) {
+        if (j >= ex_min && j <= ex_max && in_excl(j, reg, exc, a.ex_list, ex0)) return;
+        if (cnt < a.nb_cap) a.nl[nl_index(a, seg, cnt, c)] = entry;
+        cnt++;
+    };
 
     // block frame: every lane's position moved to the image of its unwrapped cell; origin =
     // lane 0 (lsh = 0 there), so frame coordinates stay within a few cells of 0
@@ -544,6 +578,14 @@ __global__ void __launch_bounds__(kWaveNL * kSeg) k_nlist_wave(DirectArgs a) {
 
     const int by = hi3[1] - lo3[1] + 1, bz = hi3[2] - lo3[2] + 1;
     const int ncell = (hi3[0] - lo3[0] + 1) * by * bz;
+    // half mode: window cell index of box cell q for this lane (0 own cell, 1..13 forward,
+    // negative: backward or not adjacent -- no entries)
+    auto half_k = [&](int q) {
+        const int w[3] = {lo3[0] + q / (by * bz), lo3[1] + (q / bz) % by, lo3[2] + q % bz};
+        const int dx = w[0] - ucell[0], dy = w[1] - ucell[1], dz = w[2] - ucell[2];
+        if (dx < -1 || dx > 1 || dy < -1 || dy > 1 || dz < -1 || dz > 1) return -1;
+        return (dx + 1) * 9 + (dy + 1) * 3 + (dz + 1) - 13;
+    };
     // cell q of the box -> storage index, image code, frame offset (shift - origin)
     auto cell_of = [&](int q, int& code, double3& off) {
         int w[3] = {lo3[0] + q / (by * bz), lo3[1] + (q / bz) % by, lo3[2] + q % bz}, k[3];
@@ -585,8 +627,9 @@ __global__ void __launch_bounds__(kWaveNL * kSeg) k_nlist_wave(DirectArgs a) {
     // count over the wave's lanes)
     typedef float v2f __attribute__((ext_vector_type(2)));
     typedef float v4f __attribute__((ext_vector_type(4)));
-    auto test = [&](int t0, int m, int code) {
+    auto test = [&](int t0, int m, int code, int hk, int cst) {
         if (!active) return;
+        if (a.half && hk < 0) return;   // backward cell: its pairs belong to the partner's row
         const v2f px = {pf.x, pf.x}, py = {pf.y, pf.y}, pz = {pf.z, pf.z};
         for (int u0 = 0; u0 < m; u0 += 16) {
             unsigned bits = 0;
@@ -604,11 +647,26 @@ __global__ void __launch_bounds__(kWaveNL * kSeg) k_nlist_wave(DirectArgs a) {
                 }
             }
             if (m - u0 < 16) bits &= (1u << (m - u0)) - 1u;
-            if (s >= t0 + u0 && s < t0 + u0 + 16) bits &= ~(1u << (s - t0 - u0));
-            while (bits) {
-                int v = __builtin_ctz(bits);
-                bits &= bits - 1;
-                emit(t0 + u0 + v, cand_j[u0 + v], a.typ_s ? ctp[u0 + v] : code);
+            if (!a.half) {
+                if (s >= t0 + u0 && s < t0 + u0 + 16) bits &= ~(1u << (s - t0 - u0));
+                while (bits) {
+                    int v = __builtin_ctz(bits);
+                    bits &= bits - 1;
+                    emit(t0 + u0 + v, cand_j[u0 + v], a.typ_s ? ctp[u0 + v] : code);
+                }
+            } else {
+                if (hk == 0) {   // own cell: partners after this atom in sorted order
+                    const int lim = s - (t0 + u0);
+                    if (lim >= 15) bits = 0;
+                    else if (lim >= 0) bits &= ~((2u << lim) - 1u);
+                }
+                while (bits) {
+                    int v = __builtin_ctz(bits);
+                    bits &= bits - 1;
+                    const int jj = t0 + u0 + v - cst;
+                    jbig |= jj >= (1 << kHalfJBits);
+                    emit_half(hk | (jj << 4) | ((a.typ_s ? ctp[u0 + v] : 0) << kHalfTypeShift), cand_j[u0 + v]);
+                }
             }
         }
     };
@@ -631,6 +689,8 @@ __global__ void __launch_bounds__(kWaveNL * kSeg) k_nlist_wave(DirectArgs a) {
     for (int q = 0; q < ncell; q++) {
         const int code = code_n, t0 = t0_n, t1 = t1_n, cend = end_n;
         const double3 off = off_n;
+        const int hk = a.half ? half_k(q) : 0;
+        const int cst = a.half ? a.cstart[cc] : 0;
         __builtin_amdgcn_wave_barrier();
         stage(t0, t1, off);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -642,7 +702,7 @@ __global__ void __launch_bounds__(kWaveNL * kSeg) k_nlist_wave(DirectArgs a) {
             t1_n = min(end_n, t0_n + kStage);
             fetch(t0_n, t1_n);
         }
-        test(t0, t1 - t0, code);
+        test(t0, t1 - t0, code, hk, cst);
         // rare: a quarter cell with more than kStage atoms (synchronous remainder)
         for (int tb = t0 + kStage; tb < cend; tb += kStage) {
             const int te = min(cend, tb + kStage);
@@ -664,11 +724,12 @@ __global__ void __launch_bounds__(kWaveNL * kSeg) k_nlist_wave(DirectArgs a) {
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            test(tb, te - tb, code);
+            test(tb, te - tb, code, hk, cst);
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     }
     if (active) a.nl_cnt[(size_t)seg * a.nlr + c] = cnt;
+    if (a.half && __ballot(jbig) && lane == 0) atomicOr(a.half_flag, 1);
 }
 
 struct PairAcc {
@@ -899,6 +960,179 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))
 }
 
 // ---------------------------------------------------------------------------------
+// 4b'' half list: one 1024-thread workgroup per cell, 4 lanes per row
+//     (passes of 256 rows).  Each pair is evaluated once, by the row of the lower (cell,
+//     sorted index): the i side accumulates in fp64 registers as in k_pairs; the j side (force
+//     -F_ij and dE/dq_j += k_e q_i erfc/r) is added in 64-bit fixed point to the block's LDS
+//     window -- the atoms of the row cell and its 13 forward cells -- with integer LDS atomics
+//     (exact: the sum does not depend on the order).  The window is then written to
+//     win_out[cell] and k_half_gather adds, per atom, the 14 windows that contain it.  The
+//     pair energy goes wholly to row i (no halving).  Any row whose list overflowed, any
+//     j-side contribution too large for the fixed point, or a builder that could not encode
+//     its block sets half_flag: k_half_gather then does nothing and k_excl recomputes every
+//     atom's pair sums with the fp64 cell rescan.
+// ---------------------------------------------------------------------------------
+__device__ __forceinline__ unsigned long long to_fix(double v) {
+    return (unsigned long long)(__double_as_longlong(fma(v, kFixScale, kFixMagic)) - kFixMagicBits);
+}
+
+__device__ __forceinline__ int3 half_offset(int k) {   // window cell k -> cell offset
+    if (k == 0) return make_int3(0, 0, 0);
+    const int c27 = k + 13;
+    return make_int3(c27 / 9 - 1, (c27 / 3) % 3 - 1, c27 % 3 - 1);
+}
+
+__device__ __forceinline__ int wrap_cell(int v, int n) { return v < 0 ? v + n : (v >= n ? v - n : v); }
+
+template <bool TYPES>
+__global__ void __launch_bounds__(1024) k_pairs_half(DirectArgs a) {
+    __shared__ double tab[kErfcMaxM * (kErfcDeg + 1)];
+    __shared__ double2 ljt[kMaxLjTypes];
+    __shared__ int2 win[kHalfWin];                     // (first sorted slot, window offset) per window cell
+    __shared__ unsigned long long accw[4][kHalfMaxWin];   // j-side fx, fy, fz, dE/dq (fixed point)
+    __shared__ int wtot;
+    const int cell = xcd_block();
+    const int3 nc = a.nc;
+    const int cz = cell % nc.z, cy = (cell / nc.z) % nc.y, cx = cell / (nc.y * nc.z);
+    if (threadIdx.x < kHalfWin) {
+        const int3 o = half_offset(threadIdx.x);
+        const int w = (wrap_cell(cx + o.x, nc.x) * nc.y + wrap_cell(cy + o.y, nc.y)) * nc.z + wrap_cell(cz + o.z, nc.z);
+        const int b = a.cstart[w];
+        win[threadIdx.x] = make_int2(b, a.cend[w] - b);
+    }
+    if (TYPES)
+        for (int e = threadIdx.x; e < a.lj_ntypes; e += blockDim.x) ljt[e] = a.lj_tab[e];
+    for (int e = threadIdx.x; e < kErfcMaxM * (kErfcDeg + 1); e += blockDim.x) tab[e] = a.erfc_tab[e];
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int off = 0;
+        for (int k = 0; k < kHalfWin; k++) {
+            const int n = win[k].y;
+            win[k].y = off;
+            off += n;
+        }
+        wtot = off;
+        if (off > kHalfMaxWin) atomicOr(a.half_flag, 1);
+    }
+    __syncthreads();
+    const int nw = wtot;
+    if (nw > kHalfMaxWin) return;   // block-uniform; k_excl recomputes everything
+    if (threadIdx.x < kHalfWin) a.win_woff[cell * kHalfWin + threadIdx.x] = win[threadIdx.x].y;
+    for (int e = threadIdx.x; e < nw; e += blockDim.x) {
+        accw[0][e] = 0; accw[1][e] = 0; accw[2][e] = 0; accw[3][e] = 0;
+    }
+    __syncthreads();
+    const int r0 = win[0].x, nrows = a.cend[cell] - r0;
+    const int g = threadIdx.x & 3;   // sub-list walked by this lane
+    bool bad = false;
+    for (int rb = 0; rb < nrows; rb += 256) {
+        const int rr = rb + (threadIdx.x >> 2);
+        bool active = rr < nrows;
+        const int row = r0 + (active ? rr : 0);
+        const int cnt = active ? a.nl_cnt[(size_t)g * a.nlr + row] : 0;
+        if (cnt > a.nb_cap) { bad = true; active = false; }
+        PairAcc acc;
+        if (active) {
+            const double4 pi = a.pos4s[row];
+            const double2 li = a.ljs[row];
+            const double kqi = kOne4PiEps0 * pi.w;
+            const v4i* nl4 = reinterpret_cast<const v4i*>(a.nl) + (size_t)g * (a.nb_cap / kChunk) * a.nlr + row;
+            struct Cand { double4 p; double2 lj; int slot; };
+            auto gather = [&](int e, bool ok) {
+                const int k = ok ? (e & 15) : 0, jj = ok ? ((e >> 4) & ((1 << kHalfJBits) - 1)) : 0;
+                const int2 wk = win[k];
+                Cand cd;
+                cd.p = a.pos4s[wk.x + jj];
+                cd.lj = TYPES ? ljt[(unsigned)e >> kHalfTypeShift] : a.ljs[wk.x + jj];
+                cd.slot = wk.y + jj;
+                return cd;
+            };
+            auto eval = [&](const Cand& cd) {
+                double dx = pi.x - cd.p.x, dy = pi.y - cd.p.y, dz = pi.z - cd.p.z;
+                dx -= a.L.x * rint(dx * a.invL.x);
+                dy -= a.L.y * rint(dy * a.invL.y);
+                dz -= a.L.z * rint(dz * a.invL.z);
+                const double r2 = dx * dx + dy * dy + dz * dz;
+                if (r2 <= a.rc2) {   // exact voxel-hash test
+                    const double ke = kOne4PiEps0;
+                    const double two_over_sqrtpi = 1.1283791670955126;
+                    const double inv_r = rsqrt_fp64(r2);
+                    const double ar = a.alpha * (r2 * inv_r);
+                    double e2;
+                    const double ec = erfc_exp(ar, tab, a.erfc_scale, e2);
+                    const double sig = li.x + cd.lj.x;
+                    double s2 = inv_r * sig;
+                    s2 *= s2;
+                    const double sig6 = s2 * s2 * s2;
+                    const double es6 = sig6 * li.y * cd.lj.y;
+                    const double qj = ke * cd.p.w * inv_r;
+                    const double qq = pi.w * qj;
+                    if (a.include_forces) {
+                        const double dEdR = fma(qq, ec + ar * e2 * two_over_sqrtpi, es6 * (12 * sig6 - 6)) * (inv_r * inv_r);
+                        const double fx = dEdR * dx, fy = dEdR * dy, fz = dEdR * dz;
+                        const double dqj = kqi * inv_r * ec;
+                        acc.fx += fx; acc.fy += fy; acc.fz += fz;
+                        acc.dq += qj * ec;
+                        bad |= !(fmax(fmax(fabs(fx), fabs(fy)), fmax(fabs(fz), fabs(dqj))) < kFixMax);
+                        atomicAdd(&accw[0][cd.slot], to_fix(-fx));
+                        atomicAdd(&accw[1][cd.slot], to_fix(-fy));
+                        atomicAdd(&accw[2][cd.slot], to_fix(-fz));
+                        atomicAdd(&accw[3][cd.slot], to_fix(dqj));
+                    }
+                    acc.e += qq * ec + es6 * (sig6 - 1);   // the whole pair energy: each pair once
+                }
+            };
+            walk_list(nl4, a.nlr, cnt, 0, 1, gather, eval);
+        }
+#pragma unroll
+        for (int m = 1; m < 4; m <<= 1) {
+            acc.fx += __shfl_xor(acc.fx, m); acc.fy += __shfl_xor(acc.fy, m); acc.fz += __shfl_xor(acc.fz, m);
+            acc.dq += __shfl_xor(acc.dq, m); acc.e += __shfl_xor(acc.e, m);
+        }
+        if (active && g == 0) {
+            const int i = a.atom_sorted[row];
+            a.e_atom[3 * i + 1] = acc.e;
+            if (a.include_forces) {
+                a.dedq[i] = acc.dq;
+                a.f_part[3 * i] = acc.fx;
+                a.f_part[3 * i + 1] = acc.fy;
+                a.f_part[3 * i + 2] = acc.fz;
+            }
+        }
+    }
+    if (__ballot(bad) && (threadIdx.x & 63) == 0) atomicOr(a.half_flag, 1);
+    if (!a.include_forces) return;
+    __syncthreads();
+    unsigned long long* out = a.win_out + (size_t)cell * kHalfMaxWin * 4;
+    for (int e = threadIdx.x; e < nw; e += blockDim.x)
+        reinterpret_cast<ulonglong4*>(out)[e] = make_ulonglong4(accw[0][e], accw[1][e], accw[2][e], accw[3][e]);
+}
+
+// per sorted slot s: the j-side sums of the 14 windows holding s (its own cell's and those of
+// the 13 cells behind it), converted from fixed point once and added to the i-side values
+__global__ void __launch_bounds__(256) k_half_gather(DirectArgs a) {
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= a.n || *a.half_flag) return;
+    const int key = a.key_s[s];
+    const int3 nc = a.nc;
+    const int cz = key % nc.z, cy = (key / nc.z) % nc.y, cx = key / (nc.y * nc.z);
+    const int jj = s - a.cstart[key];
+    long long sx = 0, sy = 0, sz = 0, sq = 0;
+    for (int k = 0; k < kHalfWin; k++) {
+        const int3 o = half_offset(k);
+        const int b = (wrap_cell(cx - o.x, nc.x) * nc.y + wrap_cell(cy - o.y, nc.y)) * nc.z + wrap_cell(cz - o.z, nc.z);
+        const int slot = a.win_woff[b * kHalfWin + k] + jj;
+        const ulonglong4 v = reinterpret_cast<const ulonglong4*>(a.win_out)[(size_t)b * kHalfMaxWin + slot];
+        sx += (long long)v.x; sy += (long long)v.y; sz += (long long)v.z; sq += (long long)v.w;
+    }
+    const int i = a.atom_sorted[s];
+    a.f_part[3 * i] += (double)sx * kFixInv;
+    a.f_part[3 * i + 1] += (double)sy * kFixInv;
+    a.f_part[3 * i + 2] += (double)sz * kFixInv;
+    a.dedq[i] += (double)sq * kFixInv;
+}
+
+// ---------------------------------------------------------------------------------
 // 4b' mixed precision (CF_PRECISION_MIXED): the same list walk with the pair term in fp32.
 //     Pair vectors are formed and minimum-imaged in fp64 from the sorted coordinates and then
 //     rounded to fp32; r^2 and the cutoff test in fp32; erfc(alpha r) = e^{-x^2} erfcx(x) with erfcx from a
@@ -1040,8 +1274,12 @@ __global__ void __launch_bounds__(256) k_excl(DirectArgs a) {
     const int s = own_slot(a, c);
     const int i = a.atom_sorted[s];
     bool over = false;
+    if (a.half) {
+        over = *a.half_flag != 0;   // the half-list sums are unusable: every atom is rescanned
+    } else {
 #pragma unroll
-    for (int g = 0; g < kSeg; g++) over = over || a.nl_cnt[(size_t)g * a.nlr + c] > a.nb_cap;
+        for (int g = 0; g < kSeg; g++) over = over || a.nl_cnt[(size_t)g * a.nlr + c] > a.nb_cap;
+    }
     if (over) pair_rescan(a, a.erfc_tab, s, i);   // rare: erfcx table read from global memory
     excl_atom(a, i);
 }
@@ -1147,7 +1385,8 @@ __global__ void __launch_bounds__(kEChunk) k_assemble_energy(int lo, int hi, con
                                                              const double* __restrict__ e_rec_part, int nrec, int pbc,
                                                              double* __restrict__ terms, double* __restrict__ energy_out,
                                                              double* __restrict__ energy_int, int* __restrict__ ticket,
-                                                             int* __restrict__ flag, int* __restrict__ xrange) {
+                                                             int* __restrict__ flag, int* __restrict__ xrange,
+                                                             int* __restrict__ half_flag) {
     __shared__ double red[3][256];
     const int b = lo + blockIdx.x * kEChunk + threadIdx.x;
     double a0 = 0, a1 = 0, a2 = 0;
@@ -1191,6 +1430,7 @@ __global__ void __launch_bounds__(kEChunk) k_assemble_energy(int lo, int hi, con
         *energy_int = e;
         if (energy_out) *energy_out = e;
         if (flag) *flag = 0;
+        if (half_flag) *half_flag = 0;
         if (xrange) { xrange[0] = INT_MAX; xrange[1] = INT_MIN; }   // re-arm the grid x-slab
     }
 }
@@ -1323,6 +1563,11 @@ static DirectArgs direct_args(Handle& h, const double* pos, int include_forces) 
     a.nl = h.nl; a.nl_cnt = h.nl_cnt;
     a.dedq = h.dedq; a.f_part = h.f_part; a.e_atom = h.e_atom;
     a.pos = pos;
+    a.half = h.half ? 1 : 0;
+    a.half_flag = h.half_flag;
+    a.win_out = h.win_out;
+    a.win_woff = h.win_woff;
+    a.key_s = h.cell_key_sorted;
     return a;
 }
 
@@ -1336,6 +1581,13 @@ void launch_nlist(Handle& h, const double* pos) {
 
 void launch_direct(Handle& h, const double* pos, int include_forces) {
     DirectArgs a = direct_args(h, pos, include_forces);
+    if (a.half) {
+        const int ncell = h.nc[0] * h.nc[1] * h.nc[2];
+        if (a.typ_s) hipLaunchKernelGGL((k_pairs_half<true>), dim3(ncell), dim3(1024), 0, h.stream, a);
+        else hipLaunchKernelGGL((k_pairs_half<false>), dim3(ncell), dim3(1024), 0, h.stream, a);
+        if (include_forces) hipLaunchKernelGGL(k_half_gather, dim3(nblk(a.n, 256)), dim3(256), 0, h.stream, a);
+        return;
+    }
     // lanes per atom: enough threads for ~2 waves per SIMD on 256 CUs
     const int64_t want = 256LL * 4 * 2 * 64;   // (LPA 4 measured best at C3: 0.296 vs 0.299 / 0.322 ms for 8 / 16)
     const bool ty = a.typ_s != nullptr;
@@ -1387,7 +1639,8 @@ void launch_assemble_energy(Handle& h, double* forces_out, int include_energy, d
     const int nparts = std::max(1, nblk(nown, kEChunk));
     hipLaunchKernelGGL(k_assemble_energy, dim3(nparts), dim3(kEChunk), 0, h.stream, h.lo, h.hi, h.ccsr_start,
                        h.ccsr_ent, h.dedq, h.dqdx, h.f_part, forces_out, h.e_atom, h.e_part, h.e_rec_part, nrec, h.pbc,
-                       h.terms_dev, energy_out, h.energy_dev, h.e_ticket + kTicketEnergy, h.skin_flag, h.g_xrange);
+                       h.terms_dev, energy_out, h.energy_dev, h.e_ticket + kTicketEnergy, h.skin_flag, h.g_xrange,
+                       h.half ? h.half_flag : nullptr);
 }
 
 }  // namespace cf

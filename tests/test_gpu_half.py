@@ -1,0 +1,106 @@
+"""The half neighbour list (k_pairs_half + k_half_gather): every pair
+evaluated once, the partner's share summed in 64-bit fixed point.  Used on one rank in fp64
+when the box has >= 4 cells per axis; CF_HALF=0 (read when a handle builds its cells) selects
+the full two-sided list for comparison.
+
+Tolerances (written here): against the oracle forces <= 1e-8 kJ/mol/nm, energy <= 1e-9 |E| +
+1e-8; half vs full list forces <= 1e-9 (the fixed point rounds each j-side term to 2^-34).
+The fallbacks -- an overflowed list, a j-side term too large for the fixed point -- hand the
+evaluation to the fp64 cell rescan, which must give the same answer.
+"""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+from oracle import Oracle  # noqa: E402
+from openmmcoul import HipCalcCoulForceKernel  # noqa: E402
+from openmmcoul import testsystems as ts  # noqa: E402
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+
+
+def _kernel(system, force, half, algo=0, skin=0.0):
+    old = os.environ.get("CF_HALF")
+    os.environ["CF_HALF"] = "1" if half else "0"
+    try:
+        k = HipCalcCoulForceKernel(kspace_algo=algo).initialize(system, force)
+        if skin:
+            k.set_neighbor_skin(skin)
+    finally:
+        if old is None:
+            del os.environ["CF_HALF"]
+        else:
+            os.environ["CF_HALF"] = old
+    return k
+
+
+def _eval(k, pos, box):
+    e, f = k.execute_host(pos, box)   # the first evaluation builds the cells (and picks the list kind)
+    return e, f, k.dedq(), k.energy_terms()
+
+
+@pytest.mark.parametrize("nw,algo", [(4000, 0), (7000, 2)])
+def test_half_list_matches_full_list_and_oracle(nw, algo):
+    system, force, pos, box = ts.water_box(nw, cutoff=1.0, ewald_tol=1e-4, every_bond_angle=5)
+    eh, fh, dh, th = _eval(_kernel(system, force, True, algo), pos, box)
+    ef, ff, df, tf = _eval(_kernel(system, force, False, algo), pos, box)
+    assert np.abs(fh - ff).max() <= 1e-9, np.abs(fh - ff).max()
+    assert np.abs(dh - df).max() <= 1e-10 * np.abs(df).max()
+    assert abs(th[2] - tf[2]) <= 1e-11 * abs(tf[2]) + 1e-9
+    ref = Oracle(force, box).execute(pos, box)
+    tol = 1e-8 if algo == 0 else 1e-6
+    assert np.abs(fh - ref["forces"]).max() <= tol
+    assert abs(eh - ref["energy"]) <= 1e-9 * np.abs(ref["terms"]).sum() + 1e-8
+
+
+def test_half_list_bitwise_reproducible_with_skin():
+    system, force, pos, box = ts.water_box(4000, cutoff=1.0, ewald_tol=1e-3)
+    k = _kernel(system, force, True, skin=0.1)
+    rng = np.random.default_rng(5)
+    x = pos.copy()
+    outs = []
+    for _ in range(3):
+        outs.append(k.execute_host(x, box))
+        x = x + rng.normal(scale=0.003, size=x.shape)
+    k2 = _kernel(system, force, True, skin=0.1)
+    x = pos.copy()
+    rng = np.random.default_rng(5)
+    for e, f in outs:
+        e2, f2 = k2.execute_host(x, box)
+        assert e2 == e and np.array_equal(f2, f)
+        x = x + rng.normal(scale=0.003, size=x.shape)
+
+
+def test_half_list_fallback_on_list_overflow():
+    # a default box 2.5x wider sizes the list capacity for a 16x lower density: every list
+    # overflows, the half-list evaluation is flagged and k_excl rescans every atom in fp64
+    system, force, pos, box = ts.water_box(4000, cutoff=1.0, ewald_tol=1e-4)
+    big = [[2.5 * box[i][j] for j in range(3)] for i in range(3)]
+    system.setDefaultPeriodicBoxVectors(*big)
+    k = _kernel(system, force, True)
+    ref = Oracle(force, big).execute(pos, box)
+    for _ in range(2):
+        e, f = k.execute_host(pos, box)
+        assert np.abs(f - ref["forces"]).max() <= 1e-8
+        assert abs(e - ref["energy"]) <= 1e-9 * np.abs(ref["terms"]).sum() + 1e-8
+
+
+def test_half_list_fallback_on_fixed_point_range():
+    # two waters 0.02 nm apart: a pair force of ~1e5 kJ/mol/nm exceeds the fixed point's 2^16
+    system, force, pos, box = ts.water_box(4000, cutoff=1.0, ewald_tol=1e-4)
+    p = pos.copy()
+    p[3:6] = p[0:3] + np.array([0.02, 0.0, 0.0])
+    k = _kernel(system, force, True)
+    e, f = k.execute_host(p, box)
+    ref = Oracle(force, box).execute(p, box)
+    assert np.abs(f - ref["forces"]).max() <= 1e-8 * max(1.0, np.abs(ref["forces"]).max() / 1e3)
+    assert abs(e - ref["energy"]) <= 1e-9 * np.abs(ref["terms"]).sum() + 1e-8
