@@ -117,7 +117,7 @@ def cpu_baseline(force, pos, box, k_sample):
 
 # rocprofv3 kernel names of the library's timing phases at C3
 PMC_KERNEL = {"kspace_force": "cf::k_force<2>", "kspace_sfac": "cf::k_sfac<4, 32>",
-              "direct_pairs": "cf::k_pairs<4, true>", "grid_spread": "cf::k_g_spread<3>",
+              "direct_pairs": "cf::k_pairs_half<true>", "grid_spread": "cf::k_g_spread_tile<3, 32>",
               "grid_interp": "cf::k_g_interp<14>"}
 
 
@@ -282,8 +282,9 @@ def main():
     n_own = hi - lo
     # algorithmic work per launch of each hot phase: (HBM bytes,
     # flops, compute pipe, its peak)
-    #  direct_pairs  (k_pairs alone) bytes 4 P_c + 80 N (int32 half list + per-atom in/out), flops 80 P_c
-    #                on the fp64 VALU (fp32 VALU for the mixed-precision kernel)
+    #  direct_pairs  (k_pairs_half + k_half_gather on one fp64 rank, k_pairs otherwise) bytes 4 P_c + 80 N
+    #                (int32 half list + per-atom in/out), flops 80 P_c on the fp64 VALU (fp32 VALU for
+    #                the mixed-precision kernel); P_c counts each pair once
     #  grid_spread   2 N W^3 fp64 VALU flops (one FMA per atom x grid point of its support), bytes 24 N W
     #                (the atom's three tap rows) + 8 ng^3 (grid out)
     #  grid_interp   4 N W^3 fp64 VALU flops (two FMAs per grid value), bytes 8 ng^3 + 24 N W + 32 N

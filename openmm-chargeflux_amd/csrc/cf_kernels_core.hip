@@ -330,14 +330,22 @@ constexpr int kMaxLjTypes = 64;  // LJ types carried in the 6 high bits of a lis
 constexpr int kSeg = 4;          // neighbour sub-lists per atom (one per scanning wave / pair lane)
 constexpr int kShiftBits = 26;
 constexpr int kBruteShift = 31;  // shift code: minimum image by floor (brute-force path)
-// Half neighbour list: row i keeps partner j when j's cell is i's own cell
-// (and j > i in sorted order) or one of the 13 "forward" neighbour cells, offsets d with
-// code27 = (dx+1)*9 + (dy+1)*3 + (dz+1) > 13 (lexicographically positive).  Entry = k (window
-// cell: 0 own cell, code27 - 13 forward) | j - cell_start << 4 | LJ type << 14.
-constexpr int kHalfWin = 14;          // window cells per block (own + 13 forward)
+// Half neighbour list, split by x (a half-space rule): the pair (i, j) is
+// kept by the atom of the lower x cell when their cells differ in x, and otherwise by the
+// atom with the smaller wrapped x (rounded to fp32, a per-atom key that both sides see
+// identically; ties: the lower sorted slot).  Every atom so keeps about half of its partners
+// wherever it sits in its cell (a cell-index rule -- own cell "later" partners plus 13
+// forward cells -- gives the first rows of a cell ~2x the partners of the last ones and skews
+// the sub-lists, ~0.66 lane efficiency against ~0.84).  A row's partners lie in the 18 cells
+// at x offset 0 or +1: the row cell's window.  Entry = sorted slot of j | k << 21 (window
+// cell k = ox*9 + (oy+1)*3 + (oz+1)) | LJ type << 26: the partner's address needs no table
+// lookup (the gather is not queued behind LDS work).
+constexpr int kHalfWin = 18;          // window cells per block: x offsets 0 and +1
+constexpr int kHalfOwn = 4;           // the row cell's own window index (0, 0, 0)
 constexpr int kHalfMaxWin = 4096;     // window atoms per block (LDS accumulators: 128 KB)
-constexpr int kHalfJBits = 10;        // atoms per cell < 1024
-constexpr int kHalfTypeShift = 4 + kHalfJBits;
+constexpr int kHalfSlotBits = 21;     // sorted slots < 2^21 (cf_api.hip enables half lists below)
+constexpr int kHalfSlotMask = (1 << kHalfSlotBits) - 1;
+static_assert(kHalfSlotBits + 5 <= kShiftBits, "window cell bits overlap the LJ type bits");
 // j-side sums in 64-bit fixed point (integer adds: exact, so any order gives the same bits):
 // v -> round(v 2^34) via the 1.5 * 2^52 magic add (exact for |v 2^34| < 2^51); a contribution
 // with |v| >= 2^16 flags the evaluation for the fp64 rescan fallback
@@ -374,7 +382,7 @@ struct DirectArgs {
     int half;
     int* half_flag;             // device: 1 = the half-list evaluation cannot be used (k_excl rescans)
     unsigned long long* win_out;// [ncell][kHalfMaxWin][4] per-cell window partials (fixed point)
-    int* win_woff;              // [ncell][kHalfWin] window offsets of the 14 window cells
+    int* win_woff;              // [ncell][kHalfWin] window offsets of the 18 window cells
     const int* key_s;           // cell key per sorted slot
 };
 
@@ -495,8 +503,8 @@ constexpr int kStage = kStageU * kWaveNL;
 
 __global__ void __launch_bounds__(kWaveNL * kSeg) k_nlist_wave(DirectArgs a) {
     // staged candidates, SoA so that one ds_read_b128 gives 4 candidates' x (two packed-fp32
-    // operands): x, y, z in the block frame, LJ type bits, atom index
-    __shared__ __attribute__((aligned(16))) float cand_all[kSeg][4][kStage + 16];
+    // operands): x, y, z in the block frame, LJ type bits, (half lists) the x key; atom index
+    __shared__ __attribute__((aligned(16))) float cand_all[kSeg][5][kStage + 16];
     __shared__ int cand_j_all[kSeg][kStage + 16];
     const int lane = threadIdx.x & 63;
     const int seg = threadIdx.x >> 6;   // this wave's share of the cell box and its sub-list
@@ -504,6 +512,7 @@ __global__ void __launch_bounds__(kWaveNL * kSeg) k_nlist_wave(DirectArgs a) {
     float* cy = cand_all[seg][1];
     float* cz = cand_all[seg][2];
     int* ctp = reinterpret_cast<int*>(cand_all[seg][3]);
+    float* cxk = cand_all[seg][4];
     int* cand_j = cand_j_all[seg];
     if (!*a.flag) return;  // list still valid (skin): nothing to build
     const int base = xcd_block() * kWaveNL;
@@ -562,7 +571,6 @@ __global__ void __launch_bounds__(kWaveNL * kSeg) k_nlist_wave(DirectArgs a) {
         if (active) a.nl_cnt[(size_t)seg * a.nlr + c] = cnt;
         return;
     }
-    bool jbig = false;   // half mode: an atom index within its cell beyond kHalfJBits
     auto emit_half = [&](int entry, int j) {
         if (j >= ex_min && j <= ex_max && in_excl(j, reg, exc, a.ex_list, ex0)) return;
         if (cnt < a.nb_cap) a.nl[nl_index(a, seg, cnt, c)] = entry;
@@ -578,14 +586,15 @@ __global__ void __launch_bounds__(kWaveNL * kSeg) k_nlist_wave(DirectArgs a) {
 
     const int by = hi3[1] - lo3[1] + 1, bz = hi3[2] - lo3[2] + 1;
     const int ncell = (hi3[0] - lo3[0] + 1) * by * bz;
-    // half mode: window cell index of box cell q for this lane (0 own cell, 1..13 forward,
-    // negative: backward or not adjacent -- no entries)
+    // half mode: window cell index of box cell q for this lane (x offset 0: 0..8, +1: 9..17;
+    // negative: x offset -1 or not adjacent -- no entries)
     auto half_k = [&](int q) {
         const int w[3] = {lo3[0] + q / (by * bz), lo3[1] + (q / bz) % by, lo3[2] + q % bz};
         const int dx = w[0] - ucell[0], dy = w[1] - ucell[1], dz = w[2] - ucell[2];
-        if (dx < -1 || dx > 1 || dy < -1 || dy > 1 || dz < -1 || dz > 1) return -1;
-        return (dx + 1) * 9 + (dy + 1) * 3 + (dz + 1) - 13;
+        if (dx < 0 || dx > 1 || dy < -1 || dy > 1 || dz < -1 || dz > 1) return -1;
+        return dx * 9 + (dy + 1) * 3 + (dz + 1);
     };
+    const float xki = (float)pi.x;   // this row's x key (wrapped coordinate, as stored)
     // cell q of the box -> storage index, image code, frame offset (shift - origin)
     auto cell_of = [&](int q, int& code, double3& off) {
         int w[3] = {lo3[0] + q / (by * bz), lo3[1] + (q / bz) % by, lo3[2] + q % bz}, k[3];
@@ -598,46 +607,62 @@ __global__ void __launch_bounds__(kWaveNL * kSeg) k_nlist_wave(DirectArgs a) {
         off = make_double3((k[0] - 1) * Ls[0] - org.x, (k[1] - 1) * Ls[1] - org.y, (k[2] - 1) * Ls[2] - org.z);
         return (w[0] * a.nc.y + w[1]) * a.nc.z + w[2];
     };
+    // This wave's candidates of a cell are the atoms whose index in the cell, in groups of 4
+    // (one 128-B line of pos4s), is this wave's group mod 4: candidate u of cell [cb, ce) is
+    // slot cb + 16 (u / 4) + 4 seg + u % 4.  Interleaved because cells are sorted by atom
+    // index, which follows space: contiguous quarters would give the sub-lists of a half list
+    // very different lengths (lane efficiency 0.66 -> 0.83 at C3; 0.85 -> 0.88 full lists).
+    static_assert(kSeg == 4, "the interleave below uses shifts");
+    auto slot_of = [&](int cb, int u) { return cb + ((u >> 2) << 4) + (seg << 2) + (u & 3); };
+    auto count_of = [&](int cb, int ce) {   // this wave's candidates in the cell
+        const int n = ce - cb;
+        return ((n >> 4) << 2) + min(4, max(0, (n & 15) - (seg << 2)));
+    };
     double4 rp[kStageU];
     int rj[kStageU], rt[kStageU];
-    auto fetch = [&](int t0, int t1) {
+    auto fetch = [&](int cb, int nu) {   // candidates u = 0 .. kStage-1 of the cell
 #pragma unroll
         for (int v = 0; v < kStageU; v++) {
-            int t = t0 + v * kWaveNL + lane;
-            if (t < t1) { rp[v] = a.pos4s[t]; rj[v] = a.atom_sorted[t]; rt[v] = a.typ_s ? a.typ_s[t] : 0; }
+            const int u = v * kWaveNL + lane;
+            if (u < nu) {
+                const int t = slot_of(cb, u);
+                rp[v] = a.pos4s[t]; rj[v] = a.atom_sorted[t]; rt[v] = a.typ_s ? a.typ_s[t] : 0;
+            }
         }
     };
-    // staged candidate: fp32 block-frame position, LJ type bits in .w
-    auto stage = [&](int t0, int t1, double3 off) {
+    // staged candidate: fp32 block-frame position, LJ type bits, x key
+    auto put = [&](int u, const double4& pj, int j, int tp, double3 off) {
+        cx[u] = (float)(pj.x + off.x);
+        cy[u] = (float)(pj.y + off.y);
+        cz[u] = (float)(pj.z + off.z);
+        ctp[u] = tp;
+        cxk[u] = (float)pj.x;
+        cand_j[u] = j;
+    };
+    auto stage = [&](int nu, double3 off) {
 #pragma unroll
         for (int v = 0; v < kStageU; v++) {
             int u = v * kWaveNL + lane;
-            if (t0 + u < t1) {
-                cx[u] = (float)(rp[v].x + off.x);
-                cy[u] = (float)(rp[v].y + off.y);
-                cz[u] = (float)(rp[v].z + off.z);
-                ctp[u] = rt[v];
-                cand_j[u] = rj[v];
-            }
+            if (u < nu) put(u, rp[v], rj[v], rt[v], off);
         }
     };
     // 16 candidates per chunk, tested two at a time in packed fp32 (v_pk_add/mul/fma_f32: half
     // the VALU instructions of scalar fp32), then the lane's hits of the chunk are emitted
     // (a longer chunk amortizes the divergent emit loop: its trip count is the maximum hit
-    // count over the wave's lanes)
+    // count over the wave's lanes).  Staged candidate u is candidate u0 + u of cell cb.
     typedef float v2f __attribute__((ext_vector_type(2)));
     typedef float v4f __attribute__((ext_vector_type(4)));
-    auto test = [&](int t0, int m, int code, int hk, int cst) {
+    auto test = [&](int cb, int u0, int m, int code, int hk) {
         if (!active) return;
-        if (a.half && hk < 0) return;   // backward cell: its pairs belong to the partner's row
+        if (a.half && hk < 0) return;   // x offset -1: those pairs belong to the partner's row
         const v2f px = {pf.x, pf.x}, py = {pf.y, pf.y}, pz = {pf.z, pf.z};
-        for (int u0 = 0; u0 < m; u0 += 16) {
+        for (int c0 = 0; c0 < m; c0 += 16) {
             unsigned bits = 0;
 #pragma unroll
             for (int v = 0; v < 16; v += 4) {
-                const v4f X = *reinterpret_cast<const v4f*>(cx + u0 + v);
-                const v4f Y = *reinterpret_cast<const v4f*>(cy + u0 + v);
-                const v4f Z = *reinterpret_cast<const v4f*>(cz + u0 + v);
+                const v4f X = *reinterpret_cast<const v4f*>(cx + c0 + v);
+                const v4f Y = *reinterpret_cast<const v4f*>(cy + c0 + v);
+                const v4f Z = *reinterpret_cast<const v4f*>(cz + c0 + v);
 #pragma unroll
                 for (int h = 0; h < 2; h++) {
                     const v2f dx = px - (h ? X.zw : X.xy), dy = py - (h ? Y.zw : Y.xy), dz = pz - (h ? Z.zw : Z.xy);
@@ -646,90 +671,75 @@ __global__ void __launch_bounds__(kWaveNL * kSeg) k_nlist_wave(DirectArgs a) {
                     bits |= (r2.y <= rc2f ? 1u : 0u) << (v + 2 * h + 1);
                 }
             }
-            if (m - u0 < 16) bits &= (1u << (m - u0)) - 1u;
+            if (m - c0 < 16) bits &= (1u << (m - c0)) - 1u;
             if (!a.half) {
-                if (s >= t0 + u0 && s < t0 + u0 + 16) bits &= ~(1u << (s - t0 - u0));
+                const int ds = s - cb;   // this atom itself, if it is one of the chunk's candidates
+                if (ds >= 0 && ((ds >> 2) & 3) == seg) {
+                    const int us = (((ds >> 4) << 2) | (ds & 3)) - (u0 + c0);
+                    if (us >= 0 && us < 16) bits &= ~(1u << us);
+                }
                 while (bits) {
                     int v = __builtin_ctz(bits);
                     bits &= bits - 1;
-                    emit(t0 + u0 + v, cand_j[u0 + v], a.typ_s ? ctp[u0 + v] : code);
+                    emit(slot_of(cb, u0 + c0 + v), cand_j[c0 + v], a.typ_s ? ctp[c0 + v] : code);
                 }
             } else {
-                if (hk == 0) {   // own cell: partners after this atom in sorted order
-                    const int lim = s - (t0 + u0);
-                    if (lim >= 15) bits = 0;
-                    else if (lim >= 0) bits &= ~((2u << lim) - 1u);
-                }
                 while (bits) {
                     int v = __builtin_ctz(bits);
                     bits &= bits - 1;
-                    const int jj = t0 + u0 + v - cst;
-                    jbig |= jj >= (1 << kHalfJBits);
-                    emit_half(hk | (jj << 4) | ((a.typ_s ? ctp[u0 + v] : 0) << kHalfTypeShift), cand_j[u0 + v]);
+                    const int t = slot_of(cb, u0 + c0 + v);
+                    if (hk < 9) {   // same x cell: the smaller x key keeps the pair (ties: lower slot)
+                        const float xk = cxk[c0 + v];
+                        if (!(xk > xki || (xk == xki && t > s))) continue;
+                    }
+                    emit_half(t | (hk << kHalfSlotBits) | ((a.typ_s ? ctp[c0 + v] : 0) << kShiftBits), cand_j[c0 + v]);
                 }
             }
         }
     };
 
-    // every wave visits every cell of the box but takes only its contiguous quarter of the
-    // cell's atoms, so the kSeg sub-lists of an atom are statistically balanced.
+    // every wave visits every cell of the box (its interleaved quarter of the atoms).
     // (LDS regions are per wave: wave barriers only.)
-    auto quarter = [&](int cc_, int& t0_, int& t1_) {
-        int b = a.cstart[cc_], e = a.cend[cc_];
-        int qs = (e - b + kSeg - 1) / kSeg;
-        t0_ = min(e, b + seg * qs);
-        t1_ = min(e, t0_ + qs);
-    };
     int code_n; double3 off_n;
     int cc = cell_of(0, code_n, off_n);
-    int t0_n, end_n;
-    quarter(cc, t0_n, end_n);
-    int t1_n = min(end_n, t0_n + kStage);
-    fetch(t0_n, t1_n);
+    int cb_n = a.cstart[cc], nu_n = count_of(cb_n, a.cend[cc]);
+    fetch(cb_n, nu_n);
     for (int q = 0; q < ncell; q++) {
-        const int code = code_n, t0 = t0_n, t1 = t1_n, cend = end_n;
+        const int code = code_n, cb = cb_n, nu = nu_n;
         const double3 off = off_n;
         const int hk = a.half ? half_k(q) : 0;
-        const int cst = a.half ? a.cstart[cc] : 0;
         __builtin_amdgcn_wave_barrier();
-        stage(t0, t1, off);
+        stage(nu, off);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         if (q + 1 < ncell) {  // prefetch the next cell while this one is tested
             cc = cell_of(q + 1, code_n, off_n);
-            quarter(cc, t0_n, end_n);
-            t1_n = min(end_n, t0_n + kStage);
-            fetch(t0_n, t1_n);
+            cb_n = a.cstart[cc];
+            nu_n = count_of(cb_n, a.cend[cc]);
+            fetch(cb_n, nu_n);
         }
-        test(t0, t1 - t0, code, hk, cst);
-        // rare: a quarter cell with more than kStage atoms (synchronous remainder)
-        for (int tb = t0 + kStage; tb < cend; tb += kStage) {
-            const int te = min(cend, tb + kStage);
+        test(cb, 0, min(nu, kStage), code, hk);
+        // rare: more than kStage candidates per wave in a cell (synchronous remainder)
+        for (int u0 = kStage; u0 < nu; u0 += kStage) {
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
 #pragma unroll
             for (int v = 0; v < kStageU; v++) {
-                int t = tb + v * kWaveNL + lane;
-                if (t < te) {
-                    double4 pj = a.pos4s[t];
-                    const int u = v * kWaveNL + lane;
-                    cx[u] = (float)(pj.x + off.x);
-                    cy[u] = (float)(pj.y + off.y);
-                    cz[u] = (float)(pj.z + off.z);
-                    ctp[u] = a.typ_s ? a.typ_s[t] : 0;
-                    cand_j[u] = a.atom_sorted[t];
+                const int u = v * kWaveNL + lane;
+                if (u0 + u < nu) {
+                    const int t = slot_of(cb, u0 + u);
+                    put(u, a.pos4s[t], a.atom_sorted[t], a.typ_s ? a.typ_s[t] : 0, off);
                 }
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            test(tb, te - tb, code, hk, cst);
+            test(cb, u0, min(nu - u0, kStage), code, hk);
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     }
     if (active) a.nl_cnt[(size_t)seg * a.nlr + c] = cnt;
-    if (a.half && __ballot(jbig) && lane == 0) atomicOr(a.half_flag, 1);
 }
 
 struct PairAcc {
@@ -961,12 +971,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))
 
 // ---------------------------------------------------------------------------------
 // 4b'' half list: one 1024-thread workgroup per cell, 4 lanes per row
-//     (passes of 256 rows).  Each pair is evaluated once, by the row of the lower (cell,
-//     sorted index): the i side accumulates in fp64 registers as in k_pairs; the j side (force
-//     -F_ij and dE/dq_j += k_e q_i erfc/r) is added in 64-bit fixed point to the block's LDS
-//     window -- the atoms of the row cell and its 13 forward cells -- with integer LDS atomics
-//     (exact: the sum does not depend on the order).  The window is then written to
-//     win_out[cell] and k_half_gather adds, per atom, the 14 windows that contain it.  The
+//     (passes of 256 rows).  Each pair is evaluated once, by the row that keeps it (the x
+//     half-space rule above): the i side accumulates in fp64 registers as in k_pairs; the j
+//     side (force -F_ij and dE/dq_j += k_e q_i erfc/r) is added in 64-bit fixed point to the
+//     block's LDS window -- the atoms of the 18 cells at x offset 0 and +1 -- with integer LDS
+//     atomics (exact: the sum does not depend on the order).  The window is then written to
+//     win_out[cell] and k_half_gather adds, per atom, the 18 windows that contain it.  The
 //     pair energy goes wholly to row i (no halving).  Any row whose list overflowed, any
 //     j-side contribution too large for the fixed point, or a builder that could not encode
 //     its block sets half_flag: k_half_gather then does nothing and k_excl recomputes every
@@ -977,9 +987,7 @@ __device__ __forceinline__ unsigned long long to_fix(double v) {
 }
 
 __device__ __forceinline__ int3 half_offset(int k) {   // window cell k -> cell offset
-    if (k == 0) return make_int3(0, 0, 0);
-    const int c27 = k + 13;
-    return make_int3(c27 / 9 - 1, (c27 / 3) % 3 - 1, c27 % 3 - 1);
+    return make_int3(k / 9, (k / 3) % 3 - 1, k % 3 - 1);
 }
 
 __device__ __forceinline__ int wrap_cell(int v, int n) { return v < 0 ? v + n : (v >= n ? v - n : v); }
@@ -989,6 +997,7 @@ __global__ void __launch_bounds__(1024) k_pairs_half(DirectArgs a) {
     __shared__ double tab[kErfcMaxM * (kErfcDeg + 1)];
     __shared__ double2 ljt[kMaxLjTypes];
     __shared__ int2 win[kHalfWin];                     // (first sorted slot, window offset) per window cell
+    __shared__ int wdel[kHalfWin];                     // window offset - first sorted slot
     __shared__ unsigned long long accw[4][kHalfMaxWin];   // j-side fx, fy, fz, dE/dq (fixed point)
     __shared__ int wtot;
     const int cell = xcd_block();
@@ -1009,6 +1018,7 @@ __global__ void __launch_bounds__(1024) k_pairs_half(DirectArgs a) {
         for (int k = 0; k < kHalfWin; k++) {
             const int n = win[k].y;
             win[k].y = off;
+            wdel[k] = off - win[k].x;
             off += n;
         }
         wtot = off;
@@ -1022,7 +1032,7 @@ __global__ void __launch_bounds__(1024) k_pairs_half(DirectArgs a) {
         accw[0][e] = 0; accw[1][e] = 0; accw[2][e] = 0; accw[3][e] = 0;
     }
     __syncthreads();
-    const int r0 = win[0].x, nrows = a.cend[cell] - r0;
+    const int r0 = win[kHalfOwn].x, nrows = a.cend[cell] - r0;
     const int g = threadIdx.x & 3;   // sub-list walked by this lane
     bool bad = false;
     for (int rb = 0; rb < nrows; rb += 256) {
@@ -1039,12 +1049,11 @@ __global__ void __launch_bounds__(1024) k_pairs_half(DirectArgs a) {
             const v4i* nl4 = reinterpret_cast<const v4i*>(a.nl) + (size_t)g * (a.nb_cap / kChunk) * a.nlr + row;
             struct Cand { double4 p; double2 lj; int slot; };
             auto gather = [&](int e, bool ok) {
-                const int k = ok ? (e & 15) : 0, jj = ok ? ((e >> 4) & ((1 << kHalfJBits) - 1)) : 0;
-                const int2 wk = win[k];
+                const int t = ok ? (e & kHalfSlotMask) : 0;
                 Cand cd;
-                cd.p = a.pos4s[wk.x + jj];
-                cd.lj = TYPES ? ljt[(unsigned)e >> kHalfTypeShift] : a.ljs[wk.x + jj];
-                cd.slot = wk.y + jj;
+                cd.p = a.pos4s[t];
+                cd.lj = TYPES ? ljt[(unsigned)e >> kShiftBits] : a.ljs[t];
+                cd.slot = wdel[ok ? (e >> kHalfSlotBits) & 31 : 0] + t;
                 return cd;
             };
             auto eval = [&](const Cand& cd) {
@@ -1108,8 +1117,8 @@ __global__ void __launch_bounds__(1024) k_pairs_half(DirectArgs a) {
         reinterpret_cast<ulonglong4*>(out)[e] = make_ulonglong4(accw[0][e], accw[1][e], accw[2][e], accw[3][e]);
 }
 
-// per sorted slot s: the j-side sums of the 14 windows holding s (its own cell's and those of
-// the 13 cells behind it), converted from fixed point once and added to the i-side values
+// per sorted slot s: the j-side sums of the 18 windows holding s (those of the cells at x offset
+// 0 and -1 from its own), converted from fixed point once and added to the i-side values
 __global__ void __launch_bounds__(256) k_half_gather(DirectArgs a) {
     const int s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= a.n || *a.half_flag) return;
