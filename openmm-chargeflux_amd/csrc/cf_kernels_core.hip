@@ -329,6 +329,7 @@ constexpr int kErfcMaxMF = 32;   // fp32 intervals of width 0.375: x = alpha r u
 constexpr int kMaxLjTypes = 64;  // LJ types carried in the 6 high bits of a list entry
 constexpr int kSeg = 4;          // neighbour sub-lists per atom (one per scanning wave / pair lane)
 constexpr int kShiftBits = 26;
+constexpr int kJMask = (1 << kShiftBits) - 1;   // atom / slot index bits of a packed entry
 constexpr int kBruteShift = 31;  // shift code: minimum image by floor (brute-force path)
 // Half neighbour list, split by x (a half-space rule): the pair (i, j) is
 // kept by the atom of the lower x cell when their cells differ in x, and otherwise by the
@@ -503,16 +504,15 @@ constexpr int kStage = kStageU * kWaveNL;
 
 __global__ void __launch_bounds__(kWaveNL * kSeg) k_nlist_wave(DirectArgs a) {
     // staged candidates, SoA so that one ds_read_b128 gives 4 candidates' x (two packed-fp32
-    // operands): x, y, z in the block frame, LJ type bits, (half lists) the x key; atom index
-    __shared__ __attribute__((aligned(16))) float cand_all[kSeg][5][kStage + 16];
+    // operands): x, y, z in the block frame, (half lists) the x key; atom index | LJ type << 26
+    __shared__ __attribute__((aligned(16))) float cand_all[kSeg][4][kStage + 16];
     __shared__ int cand_j_all[kSeg][kStage + 16];
     const int lane = threadIdx.x & 63;
     const int seg = threadIdx.x >> 6;   // this wave's share of the cell box and its sub-list
     float* cx = cand_all[seg][0];
     float* cy = cand_all[seg][1];
     float* cz = cand_all[seg][2];
-    int* ctp = reinterpret_cast<int*>(cand_all[seg][3]);
-    float* cxk = cand_all[seg][4];
+    float* cxk = cand_all[seg][3];
     int* cand_j = cand_j_all[seg];
     if (!*a.flag) return;  // list still valid (skin): nothing to build
     const int base = xcd_block() * kWaveNL;
@@ -544,6 +544,8 @@ __global__ void __launch_bounds__(kWaveNL * kSeg) k_nlist_wave(DirectArgs a) {
         }
         lo3[d] = mn - 1; hi3[d] = mx + 1;
         if (hi3[d] - lo3[d] + 1 > ncs[d]) fits = false;
+        // half lists: partners only at x offset 0 or +1, so the box starts at the lowest row cell
+        if (d == 0 && a.half) lo3[d] = mn;
     }
     const int ex0 = a.ex_start[i], exc = a.ex_start[i + 1] - ex0;
     int reg[kMaxRegExcl];
@@ -552,12 +554,16 @@ __global__ void __launch_bounds__(kWaveNL * kSeg) k_nlist_wave(DirectArgs a) {
     // exclusion lists are sorted: a candidate outside [ex_min, ex_max] needs no lookup
     const int ex_min = exc ? a.ex_list[ex0] : 1, ex_max = exc ? a.ex_list[ex0 + exc - 1] : 0;
     int cnt = 0;
-    // high bits of a list entry: the partner's LJ type when types are used, else the image code
-    auto emit = [&](int t, int j, int hb) {
-        if (j >= ex_min && j <= ex_max && in_excl(j, reg, exc, a.ex_list, ex0)) return;
-        if (cnt < a.nb_cap) a.nl[nl_index(a, seg, cnt, c)] = t | (hb << kShiftBits);
-        cnt++;
+    int* const nl_row = a.nl + ((size_t)seg * (a.nb_cap / kChunk) * a.nlr + c) * kChunk;   // = nl_index(a, seg, 0, c)
+    const size_t nl_qstride = (size_t)a.nlr * kChunk;
+    // store list entry `entry` unless partner j is excluded (one branch: the store)
+    auto put_entry = [&](int entry, int j) {
+        const bool keep = !(j >= ex_min && j <= ex_max && in_excl(j, reg, exc, a.ex_list, ex0));
+        if (keep && cnt < a.nb_cap) nl_row[(size_t)(cnt >> 2) * nl_qstride + (cnt & 3)] = entry;
+        cnt += keep;
     };
+    // high bits of a list entry: the partner's LJ type when types are used, else the image code
+    auto emit = [&](int t, int j, int hb) { put_entry(t | (hb << kShiftBits), j); };
     if (!fits) {  // wave-uniform (and block-uniform: every wave sees the same 64 atoms)
         if (a.half) {   // half lists need the block frame: hand the evaluation to the fp64 rescan
             if (active) a.nl_cnt[(size_t)seg * a.nlr + c] = 0;
@@ -571,11 +577,6 @@ __global__ void __launch_bounds__(kWaveNL * kSeg) k_nlist_wave(DirectArgs a) {
         if (active) a.nl_cnt[(size_t)seg * a.nlr + c] = cnt;
         return;
     }
-    auto emit_half = [&](int entry, int j) {
-        if (j >= ex_min && j <= ex_max && in_excl(j, reg, exc, a.ex_list, ex0)) return;
-        if (cnt < a.nb_cap) a.nl[nl_index(a, seg, cnt, c)] = entry;
-        cnt++;
-    };
 
     // block frame: every lane's position moved to the image of its unwrapped cell; origin =
     // lane 0 (lsh = 0 there), so frame coordinates stay within a few cells of 0
@@ -630,14 +631,13 @@ __global__ void __launch_bounds__(kWaveNL * kSeg) k_nlist_wave(DirectArgs a) {
             }
         }
     };
-    // staged candidate: fp32 block-frame position, LJ type bits, x key
+    // staged candidate: fp32 block-frame position, x key, atom index | LJ type bits
     auto put = [&](int u, const double4& pj, int j, int tp, double3 off) {
         cx[u] = (float)(pj.x + off.x);
         cy[u] = (float)(pj.y + off.y);
         cz[u] = (float)(pj.z + off.z);
-        ctp[u] = tp;
         cxk[u] = (float)pj.x;
-        cand_j[u] = j;
+        cand_j[u] = j | (tp << kShiftBits);
     };
     auto stage = [&](int nu, double3 off) {
 #pragma unroll
@@ -672,6 +672,25 @@ __global__ void __launch_bounds__(kWaveNL * kSeg) k_nlist_wave(DirectArgs a) {
                 }
             }
             if (m - c0 < 16) bits &= (1u << (m - c0)) - 1u;
+            if (a.half && hk < 9 && bits) {
+                // same x cell: the smaller x key keeps the pair (ties: the lower slot)
+                unsigned ahead = 0, tie = 0;
+#pragma unroll
+                for (int v = 0; v < 16; v += 4) {
+                    const v4f K = *reinterpret_cast<const v4f*>(cxk + c0 + v);
+                    ahead |= ((K.x > xki ? 1u : 0u) | (K.y > xki ? 2u : 0u) | (K.z > xki ? 4u : 0u) |
+                              (K.w > xki ? 8u : 0u)) << v;
+                    tie |= ((K.x == xki ? 1u : 0u) | (K.y == xki ? 2u : 0u) | (K.z == xki ? 4u : 0u) |
+                            (K.w == xki ? 8u : 0u)) << v;
+                }
+                tie &= bits;
+                while (tie) {   // rare (and the row atom itself, which is dropped)
+                    const int v = __builtin_ctz(tie);
+                    tie &= tie - 1;
+                    if (slot_of(cb, u0 + c0 + v) > s) ahead |= 1u << v;
+                }
+                bits &= ahead;
+            }
             if (!a.half) {
                 const int ds = s - cb;   // this atom itself, if it is one of the chunk's candidates
                 if (ds >= 0 && ((ds >> 2) & 3) == seg) {
@@ -681,18 +700,15 @@ __global__ void __launch_bounds__(kWaveNL * kSeg) k_nlist_wave(DirectArgs a) {
                 while (bits) {
                     int v = __builtin_ctz(bits);
                     bits &= bits - 1;
-                    emit(slot_of(cb, u0 + c0 + v), cand_j[c0 + v], a.typ_s ? ctp[c0 + v] : code);
+                    const int cj = cand_j[c0 + v];
+                    emit(slot_of(cb, u0 + c0 + v), cj & kJMask, a.typ_s ? (int)((unsigned)cj >> kShiftBits) : code);
                 }
             } else {
                 while (bits) {
                     int v = __builtin_ctz(bits);
                     bits &= bits - 1;
-                    const int t = slot_of(cb, u0 + c0 + v);
-                    if (hk < 9) {   // same x cell: the smaller x key keeps the pair (ties: lower slot)
-                        const float xk = cxk[c0 + v];
-                        if (!(xk > xki || (xk == xki && t > s))) continue;
-                    }
-                    emit_half(t | (hk << kHalfSlotBits) | ((a.typ_s ? ctp[c0 + v] : 0) << kShiftBits), cand_j[c0 + v]);
+                    const int cj = cand_j[c0 + v];
+                    put_entry(slot_of(cb, u0 + c0 + v) | (hk << kHalfSlotBits) | (cj & ~kJMask), cj & kJMask);
                 }
             }
         }
