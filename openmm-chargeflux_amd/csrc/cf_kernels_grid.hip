@@ -444,6 +444,7 @@ __global__ void __launch_bounds__(256) k_g_spread_tile(int3 ng, int3 nb, const i
     __shared__ int bin_start[NB3], bin_pre[NB3 + 1], bin_db[NB3];
     __shared__ int src[kSpMaxSrc];   // slot << 5 | source bin, of the segment's atoms that reach this tile
     __shared__ int wcnt[4 * (kSpMaxSrc / 256)];
+    __shared__ int xoff[2][kSpPass];   // offset in taps of each staged atom's x window
     // XCD-aware tile order (as in k_g_interp)
     const int nyz = nb.y * nb.z;
     int tile = blockIdx.x;
@@ -522,9 +523,12 @@ __global__ void __launch_bounds__(256) k_g_spread_tile(int3 ng, int3 nb, const i
         __syncthreads();
         if (nseg == 0) continue;
         // staging: 16-B piece e of the pass = atom e / 12, axis (e % 12) / 4, quarter e % 4 of the window
+        // (the x window is staged too although the FMAs read it from memory with scalar loads: those
+        // vector loads bring it into L2 ahead of them, 0.110 -> 0.100 ms at C3)
         constexpr int kPieces = kSpPass * kSpWin / 2;          // 768 at 64 atoms per pass
         constexpr int kPer = (kPieces + 255) / 256;             // 3 per thread at 64
         v2d r[kPer];
+        int xo_r[kPer];
         auto fetch = [&](int base, int n) {
 #pragma unroll
             for (int q = 0; q < kPer; q++) {
@@ -533,29 +537,51 @@ __global__ void __launch_bounds__(256) k_g_spread_tile(int3 ng, int3 nb, const i
                 const int u = base + min(a, n - 1);
                 const int sb = src[u], bin = sb & 31;
                 const int db = (bin_db[bin] >> (8 - 4 * d)) & 15;
-                r[q] = *reinterpret_cast<const v2d*>(taps + (size_t)(sb >> 5) * kTapStride + d * kRow + 8 * db + 2 * h);
+                const int off = (sb >> 5) * kTapStride + d * kRow + 8 * db;
+                xo_r[q] = off;
+                r[q] = *reinterpret_cast<const v2d*>(taps + off + 2 * h);
             }
         };
-        auto stage = [&](double* buf) {
+        auto stage = [&](double* buf, int* xb) {
 #pragma unroll
-            for (int q = 0; q < kPer; q++)
-                if (kPieces % 256 == 0 || t + 256 * q < kPieces) reinterpret_cast<v2d*>(buf)[t + 256 * q] = r[q];
+            for (int q = 0; q < kPer; q++) {
+                const int e = t + 256 * q;
+                if (kPieces % 256 == 0 || e < kPieces) {
+                    reinterpret_cast<v2d*>(buf)[e] = r[q];
+                    if (e % 12 == 0) xb[e / 12] = xo_r[q];
+                }
+            }
         };
         const int npass = (nseg + kSpPass - 1) / kSpPass;
         fetch(0, min(kSpPass, nseg));
-        stage(st);
+        stage(st, xoff[0]);
         __syncthreads();
         for (int p = 0; p < npass; p++) {
             const int base = p * kSpPass, n = min(kSpPass, nseg - base);
             if (p + 1 < npass) fetch(base + kSpPass, min(kSpPass, nseg - base - kSpPass));
             const double* buf = st + (p & 1) * kSpPass * kSpWin;
-            for (int a = w; a < n; a += 4) {
-                const double* rw = buf + a * kSpWin;
-                const double yz = rw[8 + y] * rw[16 + z];
+            const int* xb = xoff[p & 1];
+            // the x window is the same for every lane: scalar loads (SGPR operands of the FMAs),
+            // so the LDS serves only the per-lane y and z taps (2 of the 6 reads per atom)
+            // (two atoms per iteration: one wait covers both windows' scalar loads; four measured
+            // slower, 0.100 -> 0.110 ms at C3)
+            for (int a = w; a < n; a += 8) {
+                const bool two = a + 4 < n;
+                const double* rw0 = buf + a * kSpWin;
+                const double* rw1 = buf + (two ? a + 4 : a) * kSpWin;
+                const double* xw0 = taps + __builtin_amdgcn_readfirstlane(xb[a]);
+                const double* xw1 = taps + __builtin_amdgcn_readfirstlane(xb[two ? a + 4 : a]);
+                const double yz0 = rw0[8 + y] * rw0[16 + z];
+                const double yz1 = two ? rw1[8 + y] * rw1[16 + z] : 0.0;   // + 0 x: the same sums
+                double x0[8], x1[8];
 #pragma unroll
-                for (int i = 0; i < 8; i++) acc[i] = fma(rw[i], yz, acc[i]);
+                for (int i = 0; i < 8; i++) { x0[i] = xw0[i]; x1[i] = xw1[i]; }
+#pragma unroll
+                for (int i = 0; i < 8; i++) acc[i] = fma(x0[i], yz0, acc[i]);
+#pragma unroll
+                for (int i = 0; i < 8; i++) acc[i] = fma(x1[i], yz1, acc[i]);
             }
-            if (p + 1 < npass) stage(st + ((p + 1) & 1) * kSpPass * kSpWin);
+            if (p + 1 < npass) stage(st + ((p + 1) & 1) * kSpPass * kSpWin, xoff[(p + 1) & 1]);
             __syncthreads();
         }
     }
