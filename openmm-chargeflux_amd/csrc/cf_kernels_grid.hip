@@ -1002,9 +1002,17 @@ __global__ void __launch_bounds__(kInterpThreads) k_g_interp(int3 ng, int3 nb, c
     const int lane = threadIdx.x & 63, w = wave_id();
     const int d = lane >> 4, m = lane & 15;
     const int k = lane & 15, jg = lane >> 4;
+    // the next atom's bin entry and coordinates are loaded while this one is evaluated (the
+    // two dependent loads are otherwise the head of every atom's latency chain)
+    int4 g_n = s0 + w < s1 ? g0s[s0 + w] : make_int4(0, 0, 0, 0);
+    double4 sr_n = srec[g_n.w];
     for (int s = s0 + w; s < s1; s += kInterpThreads / 64) {
-        const int4 g = g0s[s];
-        const double4 sr = srec[g.w];
+        const int4 g = g_n;
+        const double4 sr = sr_n;
+        if (s + kInterpThreads / 64 < s1) {
+            g_n = g0s[s + kInterpThreads / 64];
+            sr_n = srec[g_n.w];
+        }
         // taps: lane (d, m)
         // tap m at t = g0 + m - s, g0 = ceil(s - W/2) (the unwrapped first tap of k_g_bin)
         const double sd = d == 0 ? sr.x : (d == 1 ? sr.y : sr.z);
