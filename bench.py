@@ -116,9 +116,10 @@ def cpu_baseline(force, pos, box, k_sample):
 
 
 # rocprofv3 kernel names of the library's timing phases at C3
-PMC_KERNEL = {"kspace_force": "cf::k_force<2>", "kspace_sfac": "cf::k_sfac<4, 32>",
-              "direct_pairs": "cf::k_pairs_half<true>", "grid_spread": "cf::k_g_spread_tile<3, 32>",
-              "grid_interp": "cf::k_g_interp<14>"}
+# (a phase timed as one bracket may be several launches: their bytes are summed)
+PMC_KERNEL = {"kspace_force": ["cf::k_force<2>"], "kspace_sfac": ["cf::k_sfac<4, 32>"],
+              "direct_pairs": ["cf::k_pairs_half<true>", "cf::k_half_gather"],
+              "grid_spread": ["cf::k_g_spread_tile<3, 32>"], "grid_interp": ["cf::k_g_interp<14>"]}
 
 
 def pair_count(force, pos, box):
@@ -151,10 +152,14 @@ def pmc_traffic(config, world, phase, precision):
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_c3_pmc_summary_*.json")))
     if not files:
         return None, None
-    e = json.load(open(files[-1])).get(PMC_KERNEL[phase], {})
-    if "hbm_read_bytes_est" not in e or "hbm_write_bytes" not in e:
-        return None, None
-    return int(e["hbm_read_bytes_est"] + e["hbm_write_bytes"]), os.path.relpath(files[-1], ROOT)
+    summary = json.load(open(files[-1]))
+    total = 0
+    for name in PMC_KERNEL[phase]:
+        e = summary.get(name, {})
+        if "hbm_read_bytes_est" not in e or "hbm_write_bytes" not in e:
+            return None, None
+        total += e["hbm_read_bytes_est"] + e["hbm_write_bytes"]
+    return int(total), os.path.relpath(files[-1], ROOT)
 
 
 def main():
