@@ -233,201 +233,17 @@ __global__ void __launch_bounds__(256) k_g_order_taps(int nbins, const int* __re
 }
 
 // ---------------------------------------------------------------------------------
-// 2. spread: a gather per 8^3 grid tile.  A workgroup of 8 waves owns a 2x2x2 block of
-//    tiles, one per wave.  The block's 4x4x4 source bins (a first tap in bin B reaches
-//    tiles B..B+2 for W <= 17) are walked as 16 (x, y) columns of 4 z-bins whose tap rows
-//    are staged in LDS (shared by the 8 tiles), double-buffered: the next pass's global
-//    loads are in flight in registers while the current pass is computed.  Each wave takes
-//    the 27 bins within 0..2 tiles behind its own tile, 8 atoms at a time: lane (a, k)
-//    holds atom a's x and y windows and z tap k and accumulates the 8x8 (i, j) points of
-//    its z column (8 muls + 64 FMAs per atom).  The 8 atom lanes of a column are summed
-//    in fixed order through LDS at the end -> deterministic.
+// 2. spread (a gather per 8^3 grid tile)
 // ---------------------------------------------------------------------------------
-constexpr int kSpreadCap = 56;                          // atoms staged per pass (31.5 KB)
-constexpr int kSpreadU = (kSpreadCap * (kTapStride / 2) + 511) / 512;   // double2 per thread
-
-struct SpreadPass {
-    int col;          // (sx, sy) = (col >> 2, col & 3); 16 = done
-    int base, nst;    // atoms [base, base + nst) of the column's concatenated z-bins
-    int cs[4], cn[4];
-};
-
 __device__ __forceinline__ int wrapb(int b, int n) { return b < 0 ? b + n : (b >= n ? b - n : b); }
 
-// NS = source bins per axis that reach a tile (3 for W <= 17, 2 for W <= 9); the 2x2x2-tile
-// block reads a window of NW = NS + 1 bins per axis, starting NS - 1 bins before the block
-// ws / wn: lane l of every wave holds (first slot, count) of bin l of the block's NW^3 window
-// ([col * NW + sz]), loaded once per block; a pass reads them with readlane (no memory access
-// on the pass-to-pass critical path)
-template <int NS>
-__device__ __forceinline__ void spread_column(SpreadPass& p, int ws, int wn) {
-    constexpr int NW = NS + 1;
-#pragma unroll
-    for (int sz = 0; sz < 4; sz++) {
-        if (sz >= NW) { p.cs[sz] = 0; p.cn[sz] = 0; continue; }
-        const int l = __builtin_amdgcn_readfirstlane(p.col * NW + sz);
-        p.cs[sz] = __builtin_amdgcn_readlane(ws, l);
-        p.cn[sz] = __builtin_amdgcn_readlane(wn, l);
-    }
-}
-
-// advance to the next non-empty pass; false when the columns are exhausted
-template <int NS>
-__device__ __forceinline__ bool spread_next(SpreadPass& p, int ws, int wn) {
-    constexpr int NCOL = (NS + 1) * (NS + 1);
-    int tot = p.cn[0] + p.cn[1] + p.cn[2] + p.cn[3];
-    if (p.col < NCOL && p.base + kSpreadCap < tot) {
-        p.base += kSpreadCap;
-    } else {
-        do {
-            if (++p.col >= NCOL) return false;
-            spread_column<NS>(p, ws, wn);
-            tot = p.cn[0] + p.cn[1] + p.cn[2] + p.cn[3];
-        } while (tot == 0);
-        p.base = 0;
-    }
-    p.nst = min(kSpreadCap, tot - p.base);
-    return true;
-}
-
-__device__ __forceinline__ void spread_fetch(const SpreadPass& p, const double* __restrict__ taps,
-                                             v2d (&r)[kSpreadU]) {
-    const int c1 = p.cn[0], c2 = c1 + p.cn[1], c3 = c2 + p.cn[2];
-#pragma unroll
-    for (int q = 0; q < kSpreadU; q++) {
-        const int e = threadIdx.x + 512 * q;
-        const int a = e / (kTapStride / 2), c = e - a * (kTapStride / 2);
-        const int u = p.base + min(a, p.nst - 1);
-        const int slot = u < c1 ? p.cs[0] + u : (u < c2 ? p.cs[1] + u - c1 : (u < c3 ? p.cs[2] + u - c2 : p.cs[3] + u - c3));
-        r[q] = reinterpret_cast<const v2d*>(taps + (size_t)slot * kTapStride)[c];
-    }
-}
-
-__device__ __forceinline__ void spread_store(const SpreadPass& p, double* __restrict__ buf, const v2d (&r)[kSpreadU]) {
-#pragma unroll
-    for (int q = 0; q < kSpreadU; q++) {
-        const int e = threadIdx.x + 512 * q;
-        if (e < p.nst * (kTapStride / 2)) reinterpret_cast<v2d*>(buf)[e] = r[q];
-    }
-}
-
-template <int NS>
-__global__ void __launch_bounds__(512) k_g_spread(int3 ng, int3 nb, const int* __restrict__ start,
-                                                  const double* __restrict__ taps, double* __restrict__ grid,
-                                                  const int* __restrict__ xr, int W) {
-    constexpr int NW = NS + 1;
-    extern __shared__ double st[];   // 2 x [kSpreadCap][kTapStride]
-    const int lane = threadIdx.x & 63, w = wave_id();
-    const int ka = lane >> 4, jh = (lane >> 3) & 1, k = lane & 7;   // atom-in-group, y half, z column
-    const int nbbz = (nb.z + 1) >> 1, nbby = (nb.y + 1) >> 1;
-    // XCD-aware block order: the hardware deals workgroups to the 8 XCDs round-robin, so XCD
-    // blockIdx % 8 is given a contiguous 1/8 of the (y, z) block plane over every x -- the blocks
-    // that share source bins then share that XCD's L2, and an x-slab (multi-rank run) still
-    // spreads over all 8 XCDs.  Plain order when the (y, z) plane does not split by 8.
-    const int nyz = nbby * nbbz;
-    int BX, yz;
-    if (nyz % 8 == 0) {
-        const int per = nyz / 8, i = blockIdx.x / 8;
-        yz = (blockIdx.x % 8) * per + i % per;
-        BX = i / per;
-    } else {
-        yz = blockIdx.x % nyz;
-        BX = blockIdx.x / nyz;
-    }
-    const int BY = yz / nbbz, BZ = yz % nbbz;
-    if (!x_range_in_slab(16 * BX, min(16 * BX + 15, ng.x - 1), xr, W, ng.x)) return;
-    const int wx = (w >> 2) & 1, wy = (w >> 1) & 1, wz = w & 1;
-    const int tx = 2 * BX + wx, ty = 2 * BY + wy, tz = 2 * BZ + wz;
-    const bool active = tx < nb.x && ty < nb.y && tz < nb.z;
-    double acc[8][4];
-#pragma unroll
-    for (int i = 0; i < 8; i++)
-#pragma unroll
-        for (int jj = 0; jj < 4; jj++) acc[i][jj] = 0.0;
-    int ws = 0, wn = 0;
-    if (lane < NW * NW * NW) {
-        const int col = lane / NW, sz = lane - NW * col;
-        const int bx = wrapb(2 * BX - (NS - 1) + col / NW, nb.x), by = wrapb(2 * BY - (NS - 1) + col % NW, nb.y);
-        const int b = (bx * nb.y + by) * nb.z + wrapb(2 * BZ - (NS - 1) + sz, nb.z);
-        ws = start[b];
-        wn = start[b + 1] - ws;
-    }
-    SpreadPass p;
-    p.col = -1; p.base = 0;
-    p.cn[0] = p.cn[1] = p.cn[2] = p.cn[3] = 0;
-    bool have = spread_next<NS>(p, ws, wn);
-    v2d r[kSpreadU];
-    int cur = 0;
-    if (have) {
-        spread_fetch(p, taps, r);
-        spread_store(p, st, r);
-    }
-    __syncthreads();
-    while (have) {
-        SpreadPass pn = p;
-        const bool more = spread_next<NS>(pn, ws, wn);
-        if (more) spread_fetch(pn, taps, r);   // in flight during the compute below
-        const double* buf = st + (size_t)cur * kSpreadCap * kTapStride;
-        const int dbx = wx + (NS - 1) - p.col / NW, dby = wy + (NS - 1) - p.col % NW;
-        if (active && dbx >= 0 && dbx < NS && dby >= 0 && dby < NS) {
-            const int ox = 8 * dbx, oy = kRow + 8 * dby + 4 * jh;
-            int off = 0;
-#pragma unroll
-            for (int sz = 0; sz < 4; sz++) {
-                if (sz >= NW) break;
-                const int dbz = wz + (NS - 1) - sz;
-                const int lo = max(off, p.base) - p.base, hi = min(off + p.cn[sz], p.base + p.nst) - p.base;
-                off += p.cn[sz];
-                if (dbz < 0 || dbz >= NS || lo >= hi) continue;
-                const int oz = 2 * kRow + 8 * dbz + k;
-                for (int u0 = lo; u0 < hi; u0 += 4) {
-                    const int u = min(u0 + ka, hi - 1);
-                    const double* rr = buf + (size_t)u * kTapStride;
-                    const double zq = u0 + ka < hi ? rr[oz] : 0.0;
-                    double yz[4];
-#pragma unroll
-                    for (int jj = 0; jj < 4; jj++) yz[jj] = rr[oy + jj] * zq;
-#pragma unroll
-                    for (int i = 0; i < 8; i++) {
-                        const double xi = rr[ox + i];
-#pragma unroll
-                        for (int jj = 0; jj < 4; jj++) acc[i][jj] += xi * yz[jj];
-                    }
-                }
-            }
-        }
-        if (!more) break;
-        cur ^= 1;
-        spread_store(pn, st + (size_t)cur * kSpreadCap * kTapStride, r);
-        p = pn;
-        __syncthreads();
-    }
-    // sum the 4 atom lanes of each (j, k) point in fixed order through LDS, one x row at a time
-    __syncthreads();
-    double* red = st + (size_t)w * 256;   // [ka][jh*4+jj][k] of this wave
-#pragma unroll
-    for (int i = 0; i < 8; i++) {
-#pragma unroll
-        for (int jj = 0; jj < 4; jj++) red[(ka * 8 + jh * 4 + jj) * 8 + k] = acc[i][jj];
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        const int jl = lane >> 3;   // lane = (jl, k) sums the 4 atom partials of point (i, jl, k)
-        const double v = ((red[jl * 8 + k] + red[(8 + jl) * 8 + k]) + red[(16 + jl) * 8 + k]) + red[(24 + jl) * 8 + k];
-        if (active) grid[((size_t)(8 * tx + i) * ng.y + 8 * ty + jl) * ng.z + 8 * tz + k] = v;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    }
-}
-
-// 2'. spread, one 256-thread workgroup per 8^3 tile (the default).  The tile's source atoms
+// One 256-thread workgroup per 8^3 tile.  The tile's source atoms
 //     (first tap in one of the NS^3 bins 0..NS-1 tiles behind it) are walked in passes of 64;
 //     each pass stages, per atom, only the three 8-tap windows this tile reads (the bin-aligned
 //     rows make a window a fixed 64-B piece: 192 B per atom instead of the 576-B row set), and
 //     the 4 waves take every 4th atom of the pass: lane (y, z) accumulates the tile's 8 x
 //     points of its (y, z) column (1 mul + 8 FMAs per atom; the x window is a broadcast LDS
-//     read).  Every wave is busy in every pass (the 2x2x2-tile kernel above leaves the waves
+//     read).  Every wave is busy in every pass (a 2x2x2-tile workgroup, round 1, left the waves
 //     whose tile a pass's source column does not reach waiting at the pass barrier), and the
 //     small blocks (25 KB LDS, <= 64 VGPRs) keep ~6 per CU resident, so a pass's load latency
 //     hides behind other blocks.  The 4 waves' partial tiles are summed in fixed order.
@@ -600,109 +416,9 @@ __global__ void __launch_bounds__(256) k_g_spread_tile(int3 ng, int3 nb, const i
 }
 
 // ---------------------------------------------------------------------------------
-// 3. pruned DFT stages (VALU)
+// 3. pruned DFT stages
 // ---------------------------------------------------------------------------------
-// z, real -> half spectrum:  t1[row][nz] = sum_z grid[row][z] e^{i th nz z}, nz < KZ.
-// lane = row; twiddles (uniform) from twz[z][KZP].
-constexpr int kNZB = 4;
-
-__global__ void __launch_bounds__(256) k_g_dftz_fwd(int rows, int ngz, int KZ, int KZP, const double* __restrict__ grid,
-                                                    const double2* __restrict__ twz, double2* __restrict__ t1) {
-    const int row = blockIdx.x * blockDim.x + threadIdx.x;
-    const int nz0 = blockIdx.y * kNZB;
-    const bool ok = row < rows;
-    const double* gr = grid + (size_t)(ok ? row : 0) * ngz;
-    double re[kNZB], im[kNZB];
-#pragma unroll
-    for (int u = 0; u < kNZB; u++) { re[u] = 0; im[u] = 0; }
-#pragma unroll 8
-    for (int z = 0; z < ngz; z++) {
-        const double gv = gr[z];
-        const double2* w = twz + (size_t)z * KZP + nz0;
-#pragma unroll
-        for (int u = 0; u < kNZB; u++) {
-            const double2 c = w[u];
-            re[u] += gv * c.x;
-            im[u] += gv * c.y;
-        }
-    }
-    if (!ok) return;
-#pragma unroll
-    for (int u = 0; u < kNZB; u++)
-        if (nz0 + u < KZ) t1[(size_t)row * KZ + nz0 + u] = make_double2(re[u], im[u]);
-}
-
-// middle-axis complex contraction: out[o][ap][i] = sum_a in[o][a][i] * tw[ap*sap + a*sa]
-// lanes over the flattened (o, i) pairs, kAP consecutive ap per thread (uniform twiddles)
-constexpr int kAP = 2;
-
-__global__ void __launch_bounds__(256) k_g_contract(int O, int A, int APn, int inner, const double2* __restrict__ in,
-                                                    const double2* __restrict__ tw, int sap, int sa,
-                                                    double2* __restrict__ out) {
-    const int p = blockIdx.x * blockDim.x + threadIdx.x;
-    const int ap0 = blockIdx.y * kAP;
-    const bool ok = p < O * inner;
-    const int o = ok ? p / inner : 0, i = ok ? p % inner : 0;
-    const double2* src = in + (size_t)o * A * inner + i;
-    double re[kAP], im[kAP];
-    const double2* twp[kAP];
-#pragma unroll
-    for (int u = 0; u < kAP; u++) {
-        re[u] = 0; im[u] = 0;
-        twp[u] = tw + (size_t)min(ap0 + u, APn - 1) * sap;
-    }
-#pragma unroll 8
-    for (int a = 0; a < A; a++) {
-        const double2 v = src[(size_t)a * inner];
-#pragma unroll
-        for (int u = 0; u < kAP; u++) {
-            const double2 w = twp[u][(size_t)a * sa];
-            re[u] += v.x * w.x - v.y * w.y;
-            im[u] += v.x * w.y + v.y * w.x;
-        }
-    }
-    if (!ok) return;
-#pragma unroll
-    for (int u = 0; u < kAP; u++)
-        if (ap0 + u < APn) out[((size_t)o * APn + ap0 + u) * inner + i] = make_double2(re[u], im[u]);
-}
-
-// half spectrum -> real z rows: grid[row][z] = sum_{nz<KZ} Re(u2[row][nz] e^{i th nz z})
-// (the x2 weight of nz > 0 is folded into the coefficients).  lane = z (64-wide chunk),
-// 4 waves x kRW rows; the block's rows of u2 are staged in LDS (broadcast reads).
-constexpr int kRW = 8;
-
-__global__ void __launch_bounds__(256) k_g_dftz_inv(int rows, int ngz, int KZ, const double2* __restrict__ u2,
-                                                    const double2* __restrict__ twnz, double* __restrict__ grid) {
-    extern __shared__ double2 su[];   // [4*kRW][KZ]
-    const int zchunks = (ngz + 63) / 64;
-    const int rb = blockIdx.x / zchunks, zc = blockIdx.x % zchunks;
-    const int row0 = rb * 4 * kRW;
-    const int nrows = min(4 * kRW, rows - row0);
-    for (int e = threadIdx.x; e < nrows * KZ; e += 256) su[e] = u2[(size_t)row0 * KZ + e];
-    __syncthreads();
-    const int lane = threadIdx.x & 63, w = wave_id();
-    const int z = zc * 64 + lane;
-    const int zz = z < ngz ? z : 0;
-    const int r0 = w * kRW;
-    if (r0 >= nrows) return;
-    double acc[kRW];
-#pragma unroll
-    for (int r = 0; r < kRW; r++) acc[r] = 0;
-#pragma unroll 4
-    for (int nz = 0; nz < KZ; nz++) {
-        const double2 t = twnz[(size_t)nz * ngz + zz];
-#pragma unroll
-        for (int r = 0; r < kRW; r++) {
-            const double2 uv = su[min(r0 + r, nrows - 1) * KZ + nz];
-            acc[r] += uv.x * t.x - uv.y * t.y;
-        }
-    }
-    if (z >= ngz) return;
-#pragma unroll
-    for (int r = 0; r < kRW; r++)
-        if (r0 + r < nrows) grid[(size_t)(row0 + r0 + r) * ngz + z] = acc[r];
-}
+constexpr int kNZB = 4;   // KZ padding unit of the plan's KZP
 
 // Every pruned-DFT stage as one batched complex GEMM on the fp64 matrix cores,
 //   C(m, n) = sum_k A(m, k) B(k, n),
@@ -1195,27 +911,13 @@ void launch_grid_sort(Handle& h, const double* pos) {
 void launch_grid_spread(Handle& h) {
     const GridPlan& p = h.gp;
     const int3 ng = make_int3(p.ng[0], p.ng[1], p.ng[2]), nb = make_int3(p.nb[0], p.nb[1], p.nb[2]);
-    static const bool old_spread = getenv("CF_EXP_OLD_SPREAD") != nullptr;
-    if (!old_spread) {
-        static const int pass = getenv("CF_EXP_SPREAD_PASS") ? atoi(getenv("CF_EXP_SPREAD_PASS")) : 32;
 #define CF_SPT(NS_, P_) hipLaunchKernelGGL((k_g_spread_tile<NS_, P_>), dim3(p.nbins), dim3(256), 0, h.stream, ng, nb, \
                                            h.g_start, h.g_taps, h.g_g0s, h.g_grid, h.g_xrange, p.W)
-        if (p.W <= 9) { CF_SPT(2, 64); }
-        else if (pass == 32) { CF_SPT(3, 32); }
-        else if (pass == 128) { CF_SPT(3, 128); }
-        else { CF_SPT(3, 64); }
-#undef CF_SPT
-        return;
-    }
-    const int nblocks = ((p.nb[0] + 1) / 2) * ((p.nb[1] + 1) / 2) * ((p.nb[2] + 1) / 2);
     // a first tap in bin B reaches tiles B .. B + NS - 1: NS = 2 when W <= 9 (8 source bins per
-    // tile instead of 27)
-    if (p.W <= 9)
-        hipLaunchKernelGGL(k_g_spread<2>, dim3(nblocks), dim3(512), sizeof(double) * 2 * kSpreadCap * kTapStride,
-                           h.stream, ng, nb, h.g_start, h.g_taps, h.g_grid, h.g_xrange, p.W);
-    else
-        hipLaunchKernelGGL(k_g_spread<3>, dim3(nblocks), dim3(512), sizeof(double) * 2 * kSpreadCap * kTapStride,
-                           h.stream, ng, nb, h.g_start, h.g_taps, h.g_grid, h.g_xrange, p.W);
+    // tile instead of 27).  Passes of 32 atoms at W = 14 (64 / 128 measured slower at C3)
+    if (p.W <= 9) { CF_SPT(2, 64); }
+    else { CF_SPT(3, 32); }
+#undef CF_SPT
 }
 
 template <bool AREAL, bool CREAL>
