@@ -1002,6 +1002,11 @@ __device__ __forceinline__ unsigned long long to_fix(double v) {
     return (unsigned long long)(__double_as_longlong(fma(v, kFixScale, kFixMagic)) - kFixMagicBits);
 }
 
+// the same for a value already scaled by 2^34: one add (literal operand) + one integer add
+__device__ __forceinline__ unsigned long long scaled_to_fix(double vs) {
+    return (unsigned long long)(__double_as_longlong(vs + kFixMagic) - kFixMagicBits);
+}
+
 __device__ __forceinline__ int3 half_offset(int k) {   // window cell k -> cell offset
     return make_int3(k / 9, (k / 3) % 3 - 1, k % 3 - 1);
 }
@@ -1061,7 +1066,7 @@ __global__ void __launch_bounds__(1024) k_pairs_half(DirectArgs a) {
         if (active) {
             const double4 pi = a.pos4s[row];
             const double2 li = a.ljs[row];
-            const double kqi = kOne4PiEps0 * pi.w;
+            const double kqis = kOne4PiEps0 * pi.w * kFixScale;   // k_e q_i in fixed-point units
             const v4i* nl4 = reinterpret_cast<const v4i*>(a.nl) + (size_t)g * (a.nb_cap / kChunk) * a.nlr + row;
             struct Cand { double4 p; double2 lj; int slot; };
             auto gather = [&](int e, bool ok) {
@@ -1093,16 +1098,20 @@ __global__ void __launch_bounds__(1024) k_pairs_half(DirectArgs a) {
                     const double qj = ke * cd.p.w * inv_r;
                     const double qq = pi.w * qj;
                     if (a.include_forces) {
-                        const double dEdR = fma(qq, ec + ar * e2 * two_over_sqrtpi, es6 * (12 * sig6 - 6)) * (inv_r * inv_r);
-                        const double fx = dEdR * dx, fy = dEdR * dy, fz = dEdR * dz;
-                        const double dqj = kqi * inv_r * ec;
-                        acc.fx += fx; acc.fy += fy; acc.fz += fz;
+                        // the force on j, -F_ij, in fixed-point units (x -2^34: exact), which the
+                        // i side also accumulates (negated and unscaled once at the end: the same
+                        // bits as summing F_ij) -- the conversion is then one add per value
+                        const double ndEdRs = fma(qq, ec + ar * e2 * two_over_sqrtpi, es6 * (12 * sig6 - 6)) *
+                                              ((inv_r * inv_r) * -kFixScale);
+                        const double nfx = ndEdRs * dx, nfy = ndEdRs * dy, nfz = ndEdRs * dz;
+                        const double dqjs = kqis * inv_r * ec;
+                        acc.fx += nfx; acc.fy += nfy; acc.fz += nfz;
                         acc.dq += qj * ec;
-                        bad |= !(fmax(fmax(fabs(fx), fabs(fy)), fmax(fabs(fz), fabs(dqj))) < kFixMax);
-                        atomicAdd(&accw[0][cd.slot], to_fix(-fx));
-                        atomicAdd(&accw[1][cd.slot], to_fix(-fy));
-                        atomicAdd(&accw[2][cd.slot], to_fix(-fz));
-                        atomicAdd(&accw[3][cd.slot], to_fix(dqj));
+                        bad |= !(fmax(fmax(fabs(nfx), fabs(nfy)), fmax(fabs(nfz), fabs(dqjs))) < kFixMax * kFixScale);
+                        atomicAdd(&accw[0][cd.slot], scaled_to_fix(nfx));
+                        atomicAdd(&accw[1][cd.slot], scaled_to_fix(nfy));
+                        atomicAdd(&accw[2][cd.slot], scaled_to_fix(nfz));
+                        atomicAdd(&accw[3][cd.slot], scaled_to_fix(dqjs));
                     }
                     acc.e += qq * ec + es6 * (sig6 - 1);   // the whole pair energy: each pair once
                 }
@@ -1119,9 +1128,9 @@ __global__ void __launch_bounds__(1024) k_pairs_half(DirectArgs a) {
             a.e_atom[3 * i + 1] = acc.e;
             if (a.include_forces) {
                 a.dedq[i] = acc.dq;
-                a.f_part[3 * i] = acc.fx;
-                a.f_part[3 * i + 1] = acc.fy;
-                a.f_part[3 * i + 2] = acc.fz;
+                a.f_part[3 * i] = acc.fx * -kFixInv;
+                a.f_part[3 * i + 1] = acc.fy * -kFixInv;
+                a.f_part[3 * i + 2] = acc.fz * -kFixInv;
             }
         }
     }
