@@ -925,13 +925,27 @@ static void cgemm(Handle& h, CGemm g, int xdim = 0, int xdiv = 1) {
     if (h.g_xrange && xdim) {
         g.xdim = xdim; g.xdiv = xdiv; g.xr = h.g_xrange; g.W = h.gp.W; g.ngx = h.gp.ng[0];
     }
-    // 64 x 64 tiles when they give every CU a block, else 32 x 32
-    const long big = (long)((g.M + 63) / 64) * ((g.N + 63) / 64);
-    if (big >= 256) {
-        hipLaunchKernelGGL((k_g_cgemm<64, 64, AREAL, CREAL>), dim3((unsigned)big), dim3(256), 0, h.stream, g);
-    } else {
-        const long small = (long)((g.M + 31) / 32) * ((g.N + 31) / 32);
-        hipLaunchKernelGGL((k_g_cgemm<32, 32, AREAL, CREAL>), dim3((unsigned)small), dim3(256), 0, h.stream, g);
+    // block tile: the least padded work among 64x64, 64x32, 32x64 and 32x32 (kmax = 31 or 65
+    // pads a 64-wide tile to twice its width) among the shapes that give every CU a block, or
+    // the shape with the most blocks when none does
+    const int bms[4] = {64, 64, 32, 32}, bns[4] = {64, 32, 64, 32};
+    int best = -1;
+    long best_work = 0, best_blocks = 0;
+    for (int c = 0; c < 4; c++) {
+        const long tm = (g.M + bms[c] - 1) / bms[c], tn = (g.N + bns[c] - 1) / bns[c];
+        const long blocks = tm * tn, work = tm * bms[c] * tn * bns[c];
+        const bool ok = blocks >= 256, best_ok = best >= 0 && best_blocks >= 256;
+        if (best < 0 || (ok && !best_ok) || (ok && best_ok && work < best_work) ||
+            (!ok && !best_ok && blocks > best_blocks)) {
+            best = c; best_work = work; best_blocks = blocks;
+        }
+    }
+    const dim3 grid((unsigned)best_blocks);
+    switch (best) {
+        case 0: hipLaunchKernelGGL((k_g_cgemm<64, 64, AREAL, CREAL>), grid, dim3(256), 0, h.stream, g); break;
+        case 1: hipLaunchKernelGGL((k_g_cgemm<64, 32, AREAL, CREAL>), grid, dim3(256), 0, h.stream, g); break;
+        case 2: hipLaunchKernelGGL((k_g_cgemm<32, 64, AREAL, CREAL>), grid, dim3(256), 0, h.stream, g); break;
+        default: hipLaunchKernelGGL((k_g_cgemm<32, 32, AREAL, CREAL>), grid, dim3(256), 0, h.stream, g); break;
     }
 }
 
