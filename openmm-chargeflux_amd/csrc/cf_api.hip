@@ -151,10 +151,16 @@ void set_cells(cf_handle* H, const double L[3]) {
     if (ncell > h.ncell_alloc) {
         // grow (not graph-capture safe; only happens when the box grows past the initial grid)
         if (h.cell_start) { (void)hipFree(h.cell_start); (void)hipFree(h.cell_end); (void)hipFree(h.cell_cnt); }
+        if (h.own_cnt) { (void)hipFree(h.own_cnt); (void)hipFree(h.own_start); h.own_cnt = h.own_start = nullptr; }
         cf::check_hip(hipMalloc(&h.cell_start, sizeof(int) * ncell), "cells");
         cf::check_hip(hipMalloc(&h.cell_end, sizeof(int) * ncell), "cells");
         cf::check_hip(hipMalloc(&h.cell_cnt, sizeof(int) * ncell), "cells");
         cf::check_hip(hipMemset(h.cell_cnt, 0, sizeof(int) * ncell), "cells");   // re-zeroed by each build
+        if (h.world > 1) {   // owned atoms per cell and their scan (list rows of a multi-rank run)
+            cf::check_hip(hipMalloc(&h.own_cnt, sizeof(int) * ncell), "cells");
+            cf::check_hip(hipMalloc(&h.own_start, sizeof(int) * (ncell + 1)), "cells");
+            cf::check_hip(hipMemset(h.own_cnt, 0, sizeof(int) * ncell), "cells");
+        }
         h.ncell_alloc = (int)ncell;
     }
     h.nc[0] = nc[0]; h.nc[1] = nc[1]; h.nc[2] = nc[2];
@@ -629,6 +635,7 @@ CF_EXPORT int cf_destroy(cf_handle* H) {
         if (H->h.cell_start) (void)hipFree(H->h.cell_start);
         if (H->h.cell_end) (void)hipFree(H->h.cell_end);
         if (H->h.cell_cnt) (void)hipFree(H->h.cell_cnt);
+        if (H->h.own_cnt) { (void)hipFree(H->h.own_cnt); (void)hipFree(H->h.own_start); }
         if (H->h.own_stream) (void)hipStreamDestroy(H->h.stream);
         delete H;
     });

@@ -142,6 +142,8 @@ struct Handle {
     int* key_tmp = nullptr; int* atom_tmp = nullptr;
     // multi-rank: owned atoms compacted in cell-sorted order (list rows)
     int* own_s = nullptr;       // [N_own] (null on one rank: identity)
+    int* own_cnt = nullptr;     // [ncell] owned atoms per cell (multi-rank; re-zeroed by k_cell_scatter)
+    int* own_start = nullptr;   // [ncell + 1] their exclusive scan: first list row of each cell
     int nb_cap = 0;             // capacity of each of the 4 neighbour sub-lists of an atom
     int* nl = nullptr;          // [4][nb_cap][N] transposed sub-lists (sorted index | shift<<26)
     int* nl_cnt = nullptr;      // [4][N]
@@ -149,7 +151,7 @@ struct Handle {
     bool half = false;
     int* half_flag = nullptr;   // [1] device: half-list sums unusable this evaluation (fp64 rescan)
     unsigned long long* win_out = nullptr;   // [ncell][4096][4] window partials (fixed point)
-    int* win_woff = nullptr;    // [ncell][14]
+    int* win_woff = nullptr;    // [ncell][18]
     int win_cells = 0;          // cells win_out / win_woff are sized for
     // k-space (MFMA path)
     int npad = 0;               // owned rows of the phase tables, padded to the S-pass tile
@@ -306,11 +308,11 @@ constexpr int kTicketEnergy = 0, kTicketCells = 1, kTicketGrid = 2, kNumTickets 
 // ordered atoms put long runs of a wave in one cell or bin, whose counter would otherwise
 // serialize up to 64 atomics): the first lane of each run adds the run length, all runs'
 // atomics in flight at once (one round trip), and the run's lanes take consecutive ranks.
-// The valid lanes must be a prefix of the wave (i < n).  Returns a provisional rank within
-// the key; the sorts fix the final order in a separate, deterministic pass.
+// Any set of lanes may be valid (a run starts after an invalid lane).  Returns a provisional
+// rank within the key; the sorts fix the final order in a separate, deterministic pass.
 __device__ __forceinline__ int wave_agg_inc(int* cnt, int key, bool valid) {
     const int lane = threadIdx.x & 63;
-    const int prev = __shfl_up(key, 1);
+    const int prev = __shfl_up(valid ? key : -1, 1);   // -1: no key (keys are >= 0)
     const bool head = valid && (lane == 0 || prev != key);
     const unsigned long long cut = __ballot(head || !valid);        // run starts + invalid lanes
     const unsigned long long upto = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);   // bits 0..lane

@@ -153,11 +153,14 @@ __global__ void __launch_bounds__(256) k_atoms_prep(int n, const double* __restr
 // ---------------------------------------------------------------------------------
 
 // keys + histogram (wave-aggregated atomics: provisional ranks), then the block that
-// finishes last turns the counts into cell bounds (no separate scan launch)
+// finishes last turns the counts into cell bounds (no separate scan launch).  Multi-rank
+// (own_cnt != null): also the owned atoms per cell and their scan, the first list row of each
+// cell, from which k_cell_order writes the owned rows in cell-sorted order.
 __global__ void __launch_bounds__(256) k_cell_hist(int n, const int* __restrict__ flag, const double* __restrict__ pos,
                                                    double3 L, int3 nc, int* __restrict__ key, int* __restrict__ rank,
                                                    int* __restrict__ cnt, int* __restrict__ ticket,
-                                                   int* __restrict__ cstart, int* __restrict__ cend) {
+                                                   int* __restrict__ cstart, int* __restrict__ cend, int lo, int hi,
+                                                   int* __restrict__ own_cnt, int* __restrict__ own_start) {
     __shared__ int sh[256];
     if (!*flag) return;   // uniform over the grid
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -179,32 +182,40 @@ __global__ void __launch_bounds__(256) k_cell_hist(int n, const int* __restrict_
     }
     const int r = wave_agg_inc(cnt, k, valid);   // provisional slot; k_cell_order fixes the order
     if (valid) rank[i] = r;
+    if (own_cnt) (void)wave_agg_inc(own_cnt, k, valid && i >= lo && i < hi);
     if (!last_block_done(ticket)) return;
     block_counts_to_bounds<256>(nc.x * nc.y * nc.z, cnt, cstart, cend, false, sh);
+    if (own_cnt) {
+        __syncthreads();
+        block_counts_to_bounds<256>(nc.x * nc.y * nc.z, own_cnt, own_start, nullptr, true, sh);
+    }
 }
-
-// one workgroup: exclusive scan of m counts (chunked per thread); bounds -> start/end
-constexpr int kScanThreads = 1024;
 
 // also re-zeroes the per-cell counts (consumed by k_cell_hist's bounds) for the next build, so no
 // separate zeroing launch precedes k_cell_hist
 __global__ void __launch_bounds__(256) k_cell_scatter(int n, const int* __restrict__ flag, const int* __restrict__ key,
                                                       const int* __restrict__ rank, const int* __restrict__ cstart,
-                                                      int* __restrict__ tmp, int ncell, int* __restrict__ cnt) {
+                                                      int* __restrict__ tmp, int ncell, int* __restrict__ cnt,
+                                                      int* __restrict__ own_cnt) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (!*flag) return;
-    for (int c = i; c < ncell; c += gridDim.x * blockDim.x) cnt[c] = 0;
+    for (int c = i; c < ncell; c += gridDim.x * blockDim.x) {
+        cnt[c] = 0;
+        if (own_cnt) own_cnt[c] = 0;
+    }
     if (i >= n) return;
     tmp[cstart[key[i]] + rank[i]] = i;
 }
 
 // one wave per cell: final position of each member = cell start + number of members with
-// a smaller atom index (members staged in LDS and read by broadcast)
+// a smaller atom index (members staged in LDS and read by broadcast); multi-rank: an owned
+// member's list row = the cell's first row + number of owned members with a smaller index
 constexpr int kOrderLds = 1024;
 
 __global__ void __launch_bounds__(256) k_cell_order(int ncell, const int* __restrict__ flag,
                                                     const int* __restrict__ cstart, const int* __restrict__ cend,
-                                                    const int* __restrict__ tmp, int* __restrict__ out) {
+                                                    const int* __restrict__ tmp, int* __restrict__ out, int lo, int hi,
+                                                    const int* __restrict__ own_start, int* __restrict__ own_s) {
     __shared__ int mem[4][kOrderLds];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int c = blockIdx.x * 4 + w;
@@ -220,57 +231,19 @@ __global__ void __launch_bounds__(256) k_cell_order(int ncell, const int* __rest
     }
     for (int e = lane; e < m; e += 64) {
         const int v = src[e];
-        int r = 0;
-        for (int j = 0; j < m; j++) r += src[j] < v;
+        int r = 0, ro = 0;
+        if (own_s) {
+            for (int j = 0; j < m; j++) {
+                const int u = src[j];
+                r += u < v;
+                ro += u < v && u >= lo && u < hi;
+            }
+        } else {
+            for (int j = 0; j < m; j++) r += src[j] < v;
+        }
         out[b + r] = v;
+        if (own_s && v >= lo && v < hi) own_s[own_start[c] + ro] = b + r;
     }
-}
-
-// multi-rank: owned atoms of the new order compacted, in cell-sorted order.  Three
-// coalesced passes over 1024-slot blocks: owned count per block, exclusive scan of the
-// block counts (one workgroup), in-block ballot prefix + write.
-__global__ void __launch_bounds__(kScanThreads) k_own_count(int n, const int* __restrict__ flag,
-                                                            const int* __restrict__ idx, int lo, int hi,
-                                                            int* __restrict__ bsum) {
-    if (!*flag) return;
-    int s = blockIdx.x * kScanThreads + threadIdx.x;
-    int i = s < n ? idx[s] : -1;
-    int c = __syncthreads_count(i >= lo && i < hi);
-    if (threadIdx.x == 0) bsum[blockIdx.x] = c;
-}
-
-__global__ void __launch_bounds__(kScanThreads) k_own_scan(int nb, const int* __restrict__ flag,
-                                                           int* __restrict__ bsum) {
-    __shared__ int sh[kScanThreads];
-    if (!*flag) return;
-    const int per = (nb + kScanThreads - 1) / kScanThreads;
-    const int b0 = min(nb, threadIdx.x * per), b1 = min(nb, b0 + per);
-    int sum = 0;
-    for (int b = b0; b < b1; b++) sum += bsum[b];
-    int run = block_exclusive_scan_t<kScanThreads>(sum, sh);
-    for (int b = b0; b < b1; b++) {
-        int v = bsum[b];
-        bsum[b] = run;  // in place: counts -> offsets
-        run += v;
-    }
-}
-
-__global__ void __launch_bounds__(kScanThreads) k_own_write(int n, const int* __restrict__ flag,
-                                                            const int* __restrict__ idx, int lo, int hi,
-                                                            const int* __restrict__ boff, int* __restrict__ own_s) {
-    __shared__ int wsum[kScanThreads / 64];
-    if (!*flag) return;
-    const int s = blockIdx.x * kScanThreads + threadIdx.x;
-    const int i = s < n ? idx[s] : -1;
-    const bool own = i >= lo && i < hi;
-    const unsigned long long m = __ballot(own);
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int pre = __popcll(m & ((1ull << lane) - 1));
-    if (lane == 0) wsum[w] = __popcll(m);
-    __syncthreads();
-    int off = boff[blockIdx.x];
-    for (int k = 0; k < w; k++) off += wsum[k];
-    if (own) own_s[off + pre] = s;
 }
 
 // rebuild (flag set): commit the new order (scratch -> live), sorted wrapped (x,y,z,q) +
@@ -1550,20 +1523,15 @@ void launch_cell_sort(Handle& h, const double* pos) {
     const int* f = h.skin_flag;
     // scratch: cell_key = per-atom key, atom_val = provisional rank, key_tmp = per-cell
     // counts, atom_tmp = scattered order, cell_key_sorted's partner atom_new = final order
+    // multi-rank: the owned rows in cell-sorted order come out of the same three launches
+    int* oc = h.own_s ? h.own_cnt : nullptr;
     hipLaunchKernelGGL(k_cell_hist, dim3(nblk(h.n, 256)), dim3(256), 0, h.stream, h.n, f, pos, L, nc, h.cell_key,
-                       h.atom_val, h.cell_cnt, h.e_ticket + kTicketCells, h.cell_start, h.cell_end);
+                       h.atom_val, h.cell_cnt, h.e_ticket + kTicketCells, h.cell_start, h.cell_end, h.lo, h.hi, oc,
+                       h.own_start);
     hipLaunchKernelGGL(k_cell_scatter, dim3(nblk(h.n, 256)), dim3(256), 0, h.stream, h.n, f, h.cell_key, h.atom_val,
-                       h.cell_start, h.atom_tmp, ncell, h.cell_cnt);
+                       h.cell_start, h.atom_tmp, ncell, h.cell_cnt, oc);
     hipLaunchKernelGGL(k_cell_order, dim3(nblk(ncell, 4)), dim3(256), 0, h.stream, ncell, f, h.cell_start,
-                       h.cell_end, h.atom_tmp, h.key_tmp);
-    if (h.own_s) {
-        const int nb = nblk(h.n, kScanThreads);  // block sums live in atom_val (free after the scatter)
-        hipLaunchKernelGGL(k_own_count, dim3(nb), dim3(kScanThreads), 0, h.stream, h.n, f, h.key_tmp, h.lo, h.hi,
-                           h.atom_val);
-        hipLaunchKernelGGL(k_own_scan, dim3(1), dim3(kScanThreads), 0, h.stream, nb, f, h.atom_val);
-        hipLaunchKernelGGL(k_own_write, dim3(nb), dim3(kScanThreads), 0, h.stream, h.n, f, h.key_tmp, h.lo, h.hi,
-                           h.atom_val, h.own_s);
-    }
+                       h.cell_end, h.atom_tmp, h.key_tmp, h.lo, h.hi, h.own_start, oc ? h.own_s : nullptr);
     hipLaunchKernelGGL(k_cell_commit, dim3(nblk(h.n, 256)), dim3(256), 0, h.stream, h.n, f, h.cell_key, h.key_tmp,
                        pos, h.q, h.lj, L, h.cell_key_sorted, h.atom_sorted, h.pos4s, h.ljs, h.atom_type, h.typ_s,
                        h.pos_ref, h.n_builds_dev);

@@ -922,8 +922,13 @@ void launch_grid_spread(Handle& h) {
 
 template <bool AREAL, bool CREAL>
 static void cgemm(Handle& h, CGemm g, int xdim = 0, int xdiv = 1) {
+    // multi-rank: tiles outside the rank's x-slab exit at once, so only about the slab's share
+    // of the blocks (its owned fraction of the planes plus the W - 1 halo) counts as work
+    double active = 1.0;
     if (h.g_xrange && xdim) {
         g.xdim = xdim; g.xdiv = xdiv; g.xr = h.g_xrange; g.W = h.gp.W; g.ngx = h.gp.ng[0];
+        if (xdim != 3 && h.n > 0)
+            active = std::min(1.0, (double)(h.hi - h.lo) / h.n + (double)(h.gp.W - 1) / h.gp.ng[0]);
     }
     // block tile: the least padded work among 64x64, 64x32, 32x64 and 32x32 (kmax = 31 or 65
     // pads a 64-wide tile to twice its width) among the shapes that give every CU a block, or
@@ -934,7 +939,7 @@ static void cgemm(Handle& h, CGemm g, int xdim = 0, int xdiv = 1) {
     for (int c = 0; c < 4; c++) {
         const long tm = (g.M + bms[c] - 1) / bms[c], tn = (g.N + bns[c] - 1) / bns[c];
         const long blocks = tm * tn, work = tm * bms[c] * tn * bns[c];
-        const bool ok = blocks >= 256, best_ok = best >= 0 && best_blocks >= 256;
+        const bool ok = blocks * active >= 256, best_ok = best >= 0 && best_blocks * active >= 256;
         if (best < 0 || (ok && !best_ok) || (ok && best_ok && work < best_work) ||
             (!ok && !best_ok && blocks > best_blocks)) {
             best = c; best_work = work; best_blocks = blocks;
