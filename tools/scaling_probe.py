@@ -24,7 +24,7 @@ from openmmcoul import testsystems as ts  # noqa: E402
 from openmmcoul.distributed import ShardedCoulKernel  # noqa: E402
 
 
-def probe(system, force, pos_np, box, world, steps, skin, algo=2):
+def probe(system, force, pos_np, box, world, steps, skin, algo=2, timing=True):
     dev = torch.device("cuda", 0)
     stream = torch.cuda.current_stream(dev).cuda_stream
     k = HipCalcCoulForceKernel(device=0, stream=stream, rank=0, world_size=world, kspace_algo=algo).initialize(system, force)
@@ -55,7 +55,7 @@ def probe(system, force, pos_np, box, world, steps, skin, algo=2):
     for _ in range(5):
         step()
     torch.cuda.synchronize()
-    k.set_timing(True)
+    k.set_timing(timing)
     host = 0.0
     t0 = time.perf_counter()
     for _ in range(steps):
@@ -80,10 +80,12 @@ def main():
     ap.add_argument("--config", default="C3")
     ap.add_argument("--neighbor-skin", type=float, default=0.1)
     ap.add_argument("--kspace-algo", type=int, default=2)
+    ap.add_argument("--no-timing", action="store_true", help="no per-phase events (clean wall time)")
     args = ap.parse_args()
     system, force, pos_np, box = ts.make(args.config)
     for w in args.worlds:
-        print(json.dumps(probe(system, force, pos_np, box, w, args.steps, args.neighbor_skin, args.kspace_algo)), flush=True)
+        print(json.dumps(probe(system, force, pos_np, box, w, args.steps, args.neighbor_skin, args.kspace_algo,
+                               not args.no_timing)), flush=True)
 
 
 if __name__ == "__main__":
