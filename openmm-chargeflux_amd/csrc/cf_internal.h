@@ -352,21 +352,34 @@ __device__ __forceinline__ void st_agent(T* p, T v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// exclusive scan of one int per thread over a block of NT threads (sh: NT ints of LDS)
+// exclusive scan of one int per thread over a block of NT threads (NT a multiple of 64, at
+// most 1024; sh: NT ints of LDS, left holding the block total in sh[NT - 1]): wave scans by
+// shuffles, then the wave totals -- 4 barriers (a Hillis-Steele scan over LDS takes 2 log2 NT)
 template <int NT>
 __device__ __forceinline__ int block_exclusive_scan_t(int v, int* sh) {
-    const int t = threadIdx.x;
-    sh[t] = v;
-    __syncthreads();
-    for (int off = 1; off < NT; off <<= 1) {
-        int u = t >= off ? sh[t - off] : 0;
-        __syncthreads();
-        sh[t] += u;
-        __syncthreads();
+    constexpr int NW = NT / 64;
+    static_assert(NT % 64 == 0 && NW <= 16, "block scan: NT must be a multiple of 64, at most 1024");
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    int x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(x, o);
+        if (lane >= o) x += y;
     }
-    int incl = sh[t];
+    __syncthreads();   // a previous scan's readers of sh are done
+    if (lane == 63) sh[w] = x;
     __syncthreads();
-    return incl - v;
+    int before = 0, total = 0;
+#pragma unroll
+    for (int k = 0; k < NW; k++) {
+        const int s = sh[k];
+        before += k < w ? s : 0;
+        total += s;
+    }
+    __syncthreads();
+    if (t == NT - 1) sh[NT - 1] = total;
+    __syncthreads();
+    return before + x - v;
 }
 
 // counts cnt[0..m) (device-scope atomics of other blocks: read with ld_agent) -> start[c]
