@@ -30,88 +30,98 @@ __device__ __forceinline__ double3 ld3(const double* p, int i) {
 //    block in the reference's entry order.  Bonds RCK:42-80, angles RCK:81-162,
 //    waters RCK:163-227.
 // ---------------------------------------------------------------------------------
+// first dq/dx double of term t: bonds (12 doubles each), then angles (27), then waters (27) --
+// the terms of a block write one contiguous range
+__device__ __forceinline__ long dqdx_start(int t, int nb, int na) {
+    const int b = min(t, nb), an = max(0, min(t, nb + na) - nb), w = max(0, t - nb - na);
+    return 3L * (4L * b + 9L * an + 9L * w);
+}
+
 __global__ void __launch_bounds__(256) k_flux_terms(int nterms, int nb, int na, const int4* __restrict__ tidx,
                                                     const double* __restrict__ tpar, const double* __restrict__ pos,
                                                     double3 L, int pbc, double* __restrict__ dq_slot,
                                                     double* __restrict__ dqdx) {
-    int t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= nterms) return;
-    int4 ti = tidx[t];
-    const double* p = tpar + 5 * t;
-    if (ti.x == 0) {  // bond p1-p2
-        double3 d = delta_r(ld3(pos, ti.y), ld3(pos, ti.z), L, pbc);
-        double r = sqrt(d.x * d.x + d.y * d.y + d.z * d.z);
-        double k = p[0], dq = k * (r - p[1]);
-        dq_slot[2 * t] = dq;
-        dq_slot[2 * t + 1] = -dq;
-        double c = k / r;
-        double v[3] = {c * d.x, c * d.y, c * d.z};
-        double* o = dqdx + 3 * (4 * t);
+    // the block's dq/dx blocks are staged in LDS and written out as one coalesced run (each
+    // lane's 12 or 27 doubles written straight to memory spread every store instruction over
+    // ~100 cache lines)
+    __shared__ double st[256 * 27];
+    const int t0 = blockIdx.x * blockDim.x;
+    const int t = t0 + threadIdx.x;
+    const long base = dqdx_start(t0, nb, na);
+    if (t < nterms) {
+        int4 ti = tidx[t];
+        const double* p = tpar + 5 * t;
+        double* o = st + (dqdx_start(t, nb, na) - base);
+        if (ti.x == 0) {  // bond p1-p2
+            double3 d = delta_r(ld3(pos, ti.y), ld3(pos, ti.z), L, pbc);
+            double r = sqrt(d.x * d.x + d.y * d.y + d.z * d.z);
+            double k = p[0], dq = k * (r - p[1]);
+            dq_slot[2 * t] = dq;
+            dq_slot[2 * t + 1] = -dq;
+            double c = k / r;
+            double v[3] = {c * d.x, c * d.y, c * d.z};
 #pragma unroll
-        for (int j = 0; j < 3; j++) { o[j] = -v[j]; o[3 + j] = v[j]; o[6 + j] = v[j]; o[9 + j] = -v[j]; }
-    } else if (ti.x == 1) {  // angle p1-p2-p3, p2 central
-        int a = t - nb;
-        double3 x1 = ld3(pos, ti.y), x2 = ld3(pos, ti.z), x3 = ld3(pos, ti.w);
-        double3 d21 = delta_r(x2, x1, L, pbc), d23 = delta_r(x2, x3, L, pbc), d13 = delta_r(x1, x3, L, pbc);
-        double r21_2 = d21.x * d21.x + d21.y * d21.y + d21.z * d21.z;
-        double r23_2 = d23.x * d23.x + d23.y * d23.y + d23.z * d23.z;
-        double r13_2 = d13.x * d13.x + d13.y * d13.y + d13.z * d13.z;
-        double r21 = sqrt(r21_2), r23 = sqrt(r23_2);
-        double cost = (r23_2 + r21_2 - r13_2) / 2 / r21 / r23;
-        double k = p[0];
-        double dq = k * (acos(cost) - p[1]);
-        int s = 2 * nb + 3 * a;
-        dq_slot[s] = dq; dq_slot[s + 1] = -2 * dq; dq_slot[s + 2] = dq;
-        double inv_s = 1 / sqrt(1 - cost * cost);
-        double c1 = k * (1.0 / r21 / r23) * inv_s;
-        double c21 = k * cost * inv_s / r21_2;
-        double c23 = k * cost * inv_s / r23_2;
-        double a21[3] = {d21.x, d21.y, d21.z}, a23[3] = {d23.x, d23.y, d23.z};
-        double* o = dqdx + 3 * (4 * nb + 9 * a);
+            for (int j = 0; j < 3; j++) { o[j] = -v[j]; o[3 + j] = v[j]; o[6 + j] = v[j]; o[9 + j] = -v[j]; }
+        } else if (ti.x == 1) {  // angle p1-p2-p3, p2 central
+            int a = t - nb;
+            double3 x1 = ld3(pos, ti.y), x2 = ld3(pos, ti.z), x3 = ld3(pos, ti.w);
+            double3 d21 = delta_r(x2, x1, L, pbc), d23 = delta_r(x2, x3, L, pbc), d13 = delta_r(x1, x3, L, pbc);
+            double r21_2 = d21.x * d21.x + d21.y * d21.y + d21.z * d21.z;
+            double r23_2 = d23.x * d23.x + d23.y * d23.y + d23.z * d23.z;
+            double r13_2 = d13.x * d13.x + d13.y * d13.y + d13.z * d13.z;
+            double r21 = sqrt(r21_2), r23 = sqrt(r23_2);
+            double cost = (r23_2 + r21_2 - r13_2) / 2 / r21 / r23;
+            double k = p[0];
+            double dq = k * (acos(cost) - p[1]);
+            int s = 2 * nb + 3 * a;
+            dq_slot[s] = dq; dq_slot[s + 1] = -2 * dq; dq_slot[s + 2] = dq;
+            double inv_s = 1 / sqrt(1 - cost * cost);
+            double c1 = k * (1.0 / r21 / r23) * inv_s;
+            double c21 = k * cost * inv_s / r21_2;
+            double c23 = k * cost * inv_s / r23_2;
+            double a21[3] = {d21.x, d21.y, d21.z}, a23[3] = {d23.x, d23.y, d23.z};
 #pragma unroll
-        for (int j = 0; j < 3; j++) {
-            double v1 = -c1 * a23[j] + c21 * a21[j];
-            double v3 = -c1 * a21[j] + c23 * a23[j];
-            double v2 = -v1 - v3;
-            o[j] = v1; o[3 + j] = v2; o[6 + j] = v3;
-            o[9 + j] = -2 * v1; o[12 + j] = -2 * v2; o[15 + j] = -2 * v3;
-            o[18 + j] = v1; o[21 + j] = v2; o[24 + j] = v3;
-        }
-    } else {  // water O,H1,H2
-        int w = t - nb - na;
-        double3 x1 = ld3(pos, ti.y), x2 = ld3(pos, ti.z), x3 = ld3(pos, ti.w);
-        double3 d12 = delta_r(x1, x2, L, pbc), d13 = delta_r(x1, x3, L, pbc), d23 = delta_r(x2, x3, L, pbc);
-        double r12 = sqrt(d12.x * d12.x + d12.y * d12.y + d12.z * d12.z);
-        double r13 = sqrt(d13.x * d13.x + d13.y * d13.y + d13.z * d13.z);
-        double r23 = sqrt(d23.x * d23.x + d23.y * d23.y + d23.z * d23.z);
-        double k1 = p[0], k2 = p[1], kub = p[2], b0 = p[3], ub0 = p[4];
-        double dq2 = k1 * (r12 - b0) + k2 * (r13 - b0) + kub * (r23 - ub0);
-        double dq3 = k1 * (r13 - b0) + k2 * (r12 - b0) + kub * (r23 - ub0);
-        int s = 2 * nb + 3 * na + 3 * w;
-        dq_slot[s] = -dq2 - dq3; dq_slot[s + 1] = dq2; dq_slot[s + 2] = dq3;
-        double e12[3] = {d12.x, d12.y, d12.z}, e13[3] = {d13.x, d13.y, d13.z}, e23[3] = {d23.x, d23.y, d23.z};
-        double* o = dqdx + 3 * (4 * nb + 9 * na + 9 * w);
+            for (int j = 0; j < 3; j++) {
+                double v1 = -c1 * a23[j] + c21 * a21[j];
+                double v3 = -c1 * a21[j] + c23 * a23[j];
+                double v2 = -v1 - v3;
+                o[j] = v1; o[3 + j] = v2; o[6 + j] = v3;
+                o[9 + j] = -2 * v1; o[12 + j] = -2 * v2; o[15 + j] = -2 * v3;
+                o[18 + j] = v1; o[21 + j] = v2; o[24 + j] = v3;
+            }
+        } else {  // water O,H1,H2
+            int w = t - nb - na;
+            double3 x1 = ld3(pos, ti.y), x2 = ld3(pos, ti.z), x3 = ld3(pos, ti.w);
+            double3 d12 = delta_r(x1, x2, L, pbc), d13 = delta_r(x1, x3, L, pbc), d23 = delta_r(x2, x3, L, pbc);
+            double r12 = sqrt(d12.x * d12.x + d12.y * d12.y + d12.z * d12.z);
+            double r13 = sqrt(d13.x * d13.x + d13.y * d13.y + d13.z * d13.z);
+            double r23 = sqrt(d23.x * d23.x + d23.y * d23.y + d23.z * d23.z);
+            double k1 = p[0], k2 = p[1], kub = p[2], b0 = p[3], ub0 = p[4];
+            double dq2 = k1 * (r12 - b0) + k2 * (r13 - b0) + kub * (r23 - ub0);
+            double dq3 = k1 * (r13 - b0) + k2 * (r12 - b0) + kub * (r23 - ub0);
+            int s = 2 * nb + 3 * na + 3 * w;
+            dq_slot[s] = -dq2 - dq3; dq_slot[s + 1] = dq2; dq_slot[s + 2] = dq3;
+            double e12[3] = {d12.x, d12.y, d12.z}, e13[3] = {d13.x, d13.y, d13.z}, e23[3] = {d23.x, d23.y, d23.z};
 #pragma unroll
-        for (int j = 0; j < 3; j++) {
-            double n12 = e12[j] / r12, n13 = e13[j] / r13, n23 = e23[j] / r23;
-            double a12k1 = k1 * n12, a12k2 = k2 * n12, a13k1 = k1 * n13, a13k2 = k2 * n13, ub = kub * n23;
-            o[0 + j] = a12k1 + a12k2 + a13k1 + a13k2;
-            o[3 + j] = -a12k1 - a12k2 + 2 * ub;
-            o[6 + j] = -a13k2 - a13k1 - 2 * ub;
-            o[9 + j] = -a12k1 - a13k2;
-            o[12 + j] = a12k1 - ub;
-            o[15 + j] = a13k2 + ub;
-            o[18 + j] = -a12k2 - a13k1;
-            o[21 + j] = a12k2 - ub;
-            o[24 + j] = a13k1 + ub;
+            for (int j = 0; j < 3; j++) {
+                double n12 = e12[j] / r12, n13 = e13[j] / r13, n23 = e23[j] / r23;
+                double a12k1 = k1 * n12, a12k2 = k2 * n12, a13k1 = k1 * n13, a13k2 = k2 * n13, ub = kub * n23;
+                o[0 + j] = a12k1 + a12k2 + a13k1 + a13k2;
+                o[3 + j] = -a12k1 - a12k2 + 2 * ub;
+                o[6 + j] = -a13k2 - a13k1 - 2 * ub;
+                o[9 + j] = -a12k1 - a13k2;
+                o[12 + j] = a12k1 - ub;
+                o[15 + j] = a13k2 + ub;
+                o[18 + j] = -a12k2 - a13k1;
+                o[21 + j] = a12k2 - ub;
+                o[24 + j] = a13k1 + ub;
+            }
         }
     }
+    __syncthreads();
+    const int len = (int)(dqdx_start(min(t0 + (int)blockDim.x, nterms), nb, na) - base);
+    for (int e = threadIdx.x; e < len; e += blockDim.x) dqdx[base + e] = st[e];
 }
-
-// 2. per-atom charges q_i = q0_i + sum of its slots (term order), self term
-//    (RCK:38-40, 507-510).  With skin_flag set, the same launch also does the neighbour-
-//    list validity check: flag = 1 if any atom moved more than half the skin since the
-//    last build (one launch fewer per step than a separate check kernel).
 __global__ void __launch_bounds__(256) k_atoms_prep(int n, const double* __restrict__ q0,
                                                     const int* __restrict__ qs, const int* __restrict__ qslot,
                                                     const double* __restrict__ dq_slot, int pbc, double alpha,
