@@ -118,7 +118,7 @@ def cpu_baseline(force, pos, box, k_sample):
 # rocprofv3 kernel names of the library's timing phases at C3
 # (a phase timed as one bracket may be several launches: their bytes are summed)
 PMC_KERNEL = {"kspace_force": ["cf::k_force<2>"], "kspace_sfac": ["cf::k_sfac<4, 32>"],
-              "direct_pairs": ["cf::k_pairs_half<true>", "cf::k_half_gather"],
+              "direct_pairs": ["cf::k_pairs_half<true>"],
               "grid_spread": ["cf::k_g_spread_tile<3, 32>"], "grid_interp": ["cf::k_g_interp<14>"]}
 
 
@@ -287,7 +287,7 @@ def main():
     n_own = hi - lo
     # algorithmic work per launch of each hot phase: (HBM bytes,
     # flops, compute pipe, its peak)
-    #  direct_pairs  (k_pairs_half + k_half_gather on one fp64 rank, k_pairs otherwise) bytes 4 P_c + 80 N
+    #  direct_pairs  (k_pairs_half on one fp64 rank, k_pairs otherwise) bytes 4 P_c + 80 N
     #                (int32 half list + per-atom in/out), flops 80 P_c on the fp64 VALU (fp32 VALU for
     #                the mixed-precision kernel); P_c counts each pair once
     #  grid_spread   2 N W^3 fp64 VALU flops (one FMA per atom x grid point of its support), bytes 24 N W

@@ -816,12 +816,17 @@ __device__ __forceinline__ void store_pairs(const PairAcc& acc, const DirectArgs
 // (VGPRs -> occupancy).  The
 // operation order per atom is that of one fused loop: pair sums, then exclusions in list
 // order, then dE/dq_self + sum.
-__device__ __forceinline__ void excl_atom(const DirectArgs& a, int i) {
+// (add_f, add_dq: the half list's partner-side sums of the atom, added to the stored pair sums)
+__device__ __forceinline__ void excl_atom(const DirectArgs& a, int i, double3 add_f = make_double3(0.0, 0.0, 0.0),
+                                          double add_dq = 0.0) {
     const double ke = kOne4PiEps0;
     const double two_over_sqrtpi = 1.1283791670955126;
     const int ex0 = a.ex_start[i], exc = a.ex_start[i + 1] - ex0;
     double fx = 0, fy = 0, fz = 0, dq = 0, ex_e = 0;
-    if (a.include_forces) { fx = a.f_part[3 * i]; fy = a.f_part[3 * i + 1]; fz = a.f_part[3 * i + 2]; dq = a.dedq[i]; }
+    if (a.include_forces) {
+        fx = a.f_part[3 * i] + add_f.x; fy = a.f_part[3 * i + 1] + add_f.y; fz = a.f_part[3 * i + 2] + add_f.z;
+        dq = a.dedq[i] + add_dq;
+    }
     if (exc) {
         double3 xi = ld3(a.pos, i);
         double qi = a.q[i];
@@ -975,10 +980,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))
 //     side (force -F_ij and dE/dq_j += k_e q_i erfc/r) is added in 64-bit fixed point to the
 //     block's LDS window -- the atoms of the 18 cells at x offset 0 and +1 -- with integer LDS
 //     atomics (exact: the sum does not depend on the order).  The window is then written to
-//     win_out[cell] and k_half_gather adds, per atom, the 18 windows that contain it.  The
+//     win_out[cell] and k_excl adds, per atom, the 18 windows that contain it.  The
 //     pair energy goes wholly to row i (no halving).  Any row whose list overflowed, any
 //     j-side contribution too large for the fixed point, or a builder that could not encode
-//     its block sets half_flag: k_half_gather then does nothing and k_excl recomputes every
+//     its block sets half_flag: k_excl then skips the windows and recomputes every
 //     atom's pair sums with the fp64 cell rescan.
 // ---------------------------------------------------------------------------------
 __device__ __forceinline__ unsigned long long to_fix(double v) {
@@ -1125,11 +1130,9 @@ __global__ void __launch_bounds__(1024) k_pairs_half(DirectArgs a) {
         reinterpret_cast<ulonglong4*>(out)[e] = make_ulonglong4(accw[0][e], accw[1][e], accw[2][e], accw[3][e]);
 }
 
-// per sorted slot s: the j-side sums of the 18 windows holding s (those of the cells at x offset
-// 0 and -1 from its own), converted from fixed point once and added to the i-side values
-__global__ void __launch_bounds__(256) k_half_gather(DirectArgs a) {
-    const int s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= a.n || *a.half_flag) return;
+// sorted slot s: the j-side sums of the 18 windows holding s (those of the cells at x offset
+// 0 and -1 from its own), converted from fixed point once (k_excl, before the exclusions)
+__device__ __forceinline__ void half_window_sums(const DirectArgs& a, int s, double3& f, double& dq) {
     const int key = a.key_s[s];
     const int3 nc = a.nc;
     const int cz = key % nc.z, cy = (key / nc.z) % nc.y, cx = key / (nc.y * nc.z);
@@ -1142,11 +1145,8 @@ __global__ void __launch_bounds__(256) k_half_gather(DirectArgs a) {
         const ulonglong4 v = reinterpret_cast<const ulonglong4*>(a.win_out)[(size_t)b * kHalfMaxWin + slot];
         sx += (long long)v.x; sy += (long long)v.y; sz += (long long)v.z; sq += (long long)v.w;
     }
-    const int i = a.atom_sorted[s];
-    a.f_part[3 * i] += (double)sx * kFixInv;
-    a.f_part[3 * i + 1] += (double)sy * kFixInv;
-    a.f_part[3 * i + 2] += (double)sz * kFixInv;
-    a.dedq[i] += (double)sq * kFixInv;
+    f = make_double3((double)sx * kFixInv, (double)sy * kFixInv, (double)sz * kFixInv);
+    dq = (double)sq * kFixInv;
 }
 
 // ---------------------------------------------------------------------------------
@@ -1298,7 +1298,14 @@ __global__ void __launch_bounds__(256) k_excl(DirectArgs a) {
         for (int g = 0; g < kSeg; g++) over = over || a.nl_cnt[(size_t)g * a.nlr + c] > a.nb_cap;
     }
     if (over) pair_rescan(a, a.erfc_tab, s, i);   // rare: erfcx table read from global memory
-    excl_atom(a, i);
+    if (a.half && !over && a.include_forces) {    // the partner-side sums of the half list
+        double3 f;
+        double dq;
+        half_window_sums(a, s, f, dq);
+        excl_atom(a, i, f, dq);
+    } else {
+        excl_atom(a, i);
+    }
 }
 
 // ---------------------------------------------------------------------------------
@@ -1597,7 +1604,6 @@ void launch_direct(Handle& h, const double* pos, int include_forces) {
         const int ncell = h.nc[0] * h.nc[1] * h.nc[2];
         if (a.typ_s) hipLaunchKernelGGL((k_pairs_half<true>), dim3(ncell), dim3(1024), 0, h.stream, a);
         else hipLaunchKernelGGL((k_pairs_half<false>), dim3(ncell), dim3(1024), 0, h.stream, a);
-        if (include_forces) hipLaunchKernelGGL(k_half_gather, dim3(nblk(a.n, 256)), dim3(256), 0, h.stream, a);
         return;
     }
     // lanes per atom: enough threads for ~2 waves per SIMD on 256 CUs

@@ -1,4 +1,4 @@
-"""The half neighbour list (k_pairs_half + k_half_gather): every pair
+"""The half neighbour list (k_pairs_half, window sums in k_excl): every pair
 evaluated once (kept by the atom of the lower x cell, or within one x cell by the smaller x),
 the partner's share summed in 64-bit fixed point.  Used on one rank in fp64
 when the box has >= 4 cells per axis; CF_HALF=0 (read when a handle builds its cells) selects
