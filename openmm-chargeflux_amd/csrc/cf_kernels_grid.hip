@@ -459,9 +459,14 @@ __device__ __forceinline__ d4 mfma64(double a, double b, d4 c) {
 
 constexpr int kGBK = 16;   // k per LDS chunk (4 MFMA k-steps)
 
-template <int BM, int BN, bool AREAL, bool CREAL>
+// WM x (4 / WM) waves over the block tile (2 x 2, or 4 x 1 for the 64 x 80 tile that fits
+// kmax = 65's 65 output columns with less padding)
+template <int BM, int BN, int WM, bool AREAL, bool CREAL>
 __global__ void __launch_bounds__(256) k_g_cgemm(CGemm g) {
-    constexpr int SM = BM / 32, SN = BN / 32;            // 16x16 subtiles per wave and axis
+    constexpr int WN = 4 / WM;
+    constexpr int SM = BM / (16 * WM), SN = BN / (16 * WN);   // 16x16 subtiles per wave and axis
+    static_assert(SM * 16 * WM == BM && SN * 16 * WN == BN && (BM * kGBK) % 256 == 0 && (BN * kGBK) % 256 == 0,
+                  "cgemm tile shape");
     constexpr int AP = BM + 1, BP = BN + 1;              // padded LDS rows (conflict-free transposed stores)
     constexpr int AE = BM * kGBK / 256, BE = BN * kGBK / 256;   // elements per thread per chunk
     __shared__ double2 sA[2][kGBK * AP];
@@ -534,7 +539,7 @@ __global__ void __launch_bounds__(256) k_g_cgemm(CGemm g) {
         }
     };
     const int lane = t & 63, w = wave_id();
-    const int wm = w >> 1, wn = w & 1;
+    const int wm = w / WN, wn = w % WN;
     const int r16 = lane & 15, kq = lane >> 4;
     d4 cre[SM][SN], cim[SM][SN];
 #pragma unroll
@@ -930,13 +935,15 @@ static void cgemm(Handle& h, CGemm g, int xdim = 0, int xdiv = 1) {
         if (xdim != 3 && h.n > 0)
             active = std::min(1.0, (double)(h.hi - h.lo) / h.n + (double)(h.gp.W - 1) / h.gp.ng[0]);
     }
-    // block tile: the least padded work among 64x64, 64x32, 32x64 and 32x32 (kmax = 31 or 65
-    // pads a 64-wide tile to twice its width) among the shapes that give every CU a block, or
-    // the shape with the most blocks when none does
-    const int bms[4] = {64, 64, 32, 32}, bns[4] = {64, 32, 64, 32};
+    // block tile: the least padded work among the shapes below (kmax = 31 or 65 pads a 64-wide
+    // tile to twice its width; 80 fits 65 closely) among the shapes that give every CU a block,
+    // or the shape with the most blocks when none does.  (A 48 x 64 tile of 1 x 4 waves for the
+    // 129-row stages: less padding than 32 x 32 but slower, 100 against 92 us at C5.)
+    constexpr int kShapes = 5;
+    const int bms[kShapes] = {64, 64, 32, 32, 64}, bns[kShapes] = {64, 32, 64, 32, 80};
     int best = -1;
     long best_work = 0, best_blocks = 0;
-    for (int c = 0; c < 4; c++) {
+    for (int c = 0; c < kShapes; c++) {
         const long tm = (g.M + bms[c] - 1) / bms[c], tn = (g.N + bns[c] - 1) / bns[c];
         const long blocks = tm * tn, work = tm * bms[c] * tn * bns[c];
         const bool ok = blocks * active >= 256, best_ok = best >= 0 && best_blocks * active >= 256;
@@ -947,10 +954,11 @@ static void cgemm(Handle& h, CGemm g, int xdim = 0, int xdiv = 1) {
     }
     const dim3 grid((unsigned)best_blocks);
     switch (best) {
-        case 0: hipLaunchKernelGGL((k_g_cgemm<64, 64, AREAL, CREAL>), grid, dim3(256), 0, h.stream, g); break;
-        case 1: hipLaunchKernelGGL((k_g_cgemm<64, 32, AREAL, CREAL>), grid, dim3(256), 0, h.stream, g); break;
-        case 2: hipLaunchKernelGGL((k_g_cgemm<32, 64, AREAL, CREAL>), grid, dim3(256), 0, h.stream, g); break;
-        default: hipLaunchKernelGGL((k_g_cgemm<32, 32, AREAL, CREAL>), grid, dim3(256), 0, h.stream, g); break;
+        case 0: hipLaunchKernelGGL((k_g_cgemm<64, 64, 2, AREAL, CREAL>), grid, dim3(256), 0, h.stream, g); break;
+        case 1: hipLaunchKernelGGL((k_g_cgemm<64, 32, 2, AREAL, CREAL>), grid, dim3(256), 0, h.stream, g); break;
+        case 2: hipLaunchKernelGGL((k_g_cgemm<32, 64, 2, AREAL, CREAL>), grid, dim3(256), 0, h.stream, g); break;
+        case 3: hipLaunchKernelGGL((k_g_cgemm<32, 32, 2, AREAL, CREAL>), grid, dim3(256), 0, h.stream, g); break;
+        default: hipLaunchKernelGGL((k_g_cgemm<64, 80, 4, AREAL, CREAL>), grid, dim3(256), 0, h.stream, g); break;
     }
 }
 
