@@ -164,13 +164,13 @@ void set_cells(cf_handle* H, const double L[3]) {
         h.ncell_alloc = (int)ncell;
     }
     h.nc[0] = nc[0]; h.nc[1] = nc[1]; h.nc[2] = nc[2];
-    // half neighbour list: one rank, fp64, the wave-cooperative builder (>= 4
+    // half neighbour list: one rank (fp64 or mixed), the wave-cooperative builder (>= 4
     // cells per axis), cells small enough for the kernel's LDS window (18 cells <= 4096 atoms,
     // with a margin for density variation: k_pairs_half flags the rare evaluation that does not
     // fit and k_excl then rescans) and sorted slots that fit the entry's 21 bits
     const bool no_half = getenv("CF_HALF") && std::string(getenv("CF_HALF")) == "0";   // A/B and tests
     const double per_cell = (double)h.n / (double)ncell;
-    h.half = !no_half && h.pbc && h.world == 1 && !h.mixed && nc[0] >= 4 && nc[1] >= 4 && nc[2] >= 4 &&
+    h.half = !no_half && h.pbc && h.world == 1 && nc[0] >= 4 && nc[1] >= 4 && nc[2] >= 4 &&
              per_cell * 18.0 * 1.15 <= 4096.0 && h.n < (1 << 21);
     if (h.half && ncell > h.win_cells) {
         if (h.win_out) { (void)hipFree(h.win_out); (void)hipFree(h.win_woff); }

@@ -4,6 +4,7 @@
 //
 // Reference semantics: platforms/reference/src/ReferenceCoulKernels.cpp (RCK).
 #include <algorithm>
+#include <type_traits>
 
 #include "cf_internal.h"
 
@@ -745,6 +746,11 @@ struct PairAcc {
     double fx = 0, fy = 0, fz = 0, dq = 0, e = 0;
 };
 
+struct PairAccF {   // mixed precision: fp32 forces / dE/dq, fp64 energy
+    float fx = 0, fy = 0, fz = 0, dq = 0;
+    double e = 0;
+};
+
 // erfc(x) = e^{-x^2} erfcx(x): erfcx from a piecewise degree-7 polynomial (interval table
 // in LDS, fitted at cf_create in long double, relative error ~4e-16 over [0, alpha*rc]),
 // and e^{-x^2} is shared with the force term -> one exp per pair instead of erfc + exp.
@@ -1001,10 +1007,15 @@ __device__ __forceinline__ int3 half_offset(int k) {   // window cell k -> cell 
 
 __device__ __forceinline__ int wrap_cell(int v, int n) { return v < 0 ? v + n : (v >= n ? v - n : v); }
 
-template <bool TYPES>
+// MIXED: the pair term in fp32 as in k_pairs_mixed (pair vector minimum-imaged in fp64, then
+// rounded; fp32 forces and dE/dq per lane, fp64 energy), the partner side in the same fixed
+// point (an fp32 value times 2^34 is exact in fp64)
+template <bool TYPES, bool MIXED>
 __global__ void __launch_bounds__(1024) k_pairs_half(DirectArgs a) {
-    __shared__ double tab[kErfcMaxM * (kErfcDeg + 1)];
-    __shared__ double2 ljt[kMaxLjTypes];
+    __shared__ double tab[MIXED ? 1 : kErfcMaxM * (kErfcDeg + 1)];
+    __shared__ float tabf[MIXED ? kErfcMaxMF * (kErfcDegF + 1) : 1];
+    __shared__ double2 ljt[(TYPES && !MIXED) ? kMaxLjTypes : 1];
+    __shared__ float2 ljtf[(TYPES && MIXED) ? kMaxLjTypes : 1];
     __shared__ int2 win[kHalfWin];                     // (first sorted slot, window offset) per window cell
     __shared__ int wdel[kHalfWin];                     // window offset - first sorted slot
     __shared__ unsigned long long accw[4][kHalfMaxWin];   // j-side fx, fy, fz, dE/dq (fixed point)
@@ -1018,9 +1029,17 @@ __global__ void __launch_bounds__(1024) k_pairs_half(DirectArgs a) {
         const int b = a.cstart[w];
         win[threadIdx.x] = make_int2(b, a.cend[w] - b);
     }
-    if (TYPES)
-        for (int e = threadIdx.x; e < a.lj_ntypes; e += blockDim.x) ljt[e] = a.lj_tab[e];
-    for (int e = threadIdx.x; e < kErfcMaxM * (kErfcDeg + 1); e += blockDim.x) tab[e] = a.erfc_tab[e];
+    if constexpr (TYPES) {
+        for (int e = threadIdx.x; e < a.lj_ntypes; e += blockDim.x) {
+            if constexpr (MIXED) ljtf[e] = make_float2((float)a.lj_tab[e].x, (float)a.lj_tab[e].y);
+            else ljt[e] = a.lj_tab[e];
+        }
+    }
+    if constexpr (MIXED) {
+        for (int e = threadIdx.x; e < a.erfc_m_f * (kErfcDegF + 1); e += blockDim.x) tabf[e] = a.erfc_tab_f[e];
+    } else {
+        for (int e = threadIdx.x; e < kErfcMaxM * (kErfcDeg + 1); e += blockDim.x) tab[e] = a.erfc_tab[e];
+    }
     __syncthreads();
     if (threadIdx.x == 0) {
         int off = 0;
@@ -1050,8 +1069,74 @@ __global__ void __launch_bounds__(1024) k_pairs_half(DirectArgs a) {
         const int row = r0 + (active ? rr : 0);
         const int cnt = active ? a.nl_cnt[(size_t)g * a.nlr + row] : 0;
         if (cnt > a.nb_cap) { bad = true; active = false; }
-        PairAcc acc;
-        if (active) {
+        std::conditional_t<MIXED, PairAccF, PairAcc> acc;
+        if constexpr (MIXED) {
+          if (active) {
+            const double4 pi = a.pos4s[row];
+            const float2 li = make_float2((float)a.ljs[row].x, (float)a.ljs[row].y);
+            const float qi = (float)pi.w, ke = (float)kOne4PiEps0, keqi = ke * qi;
+            const float rc2 = (float)a.rc2, alpha = (float)a.alpha, escale = (float)a.erfc_scale_f;
+            const v4i* nl4 = reinterpret_cast<const v4i*>(a.nl) + (size_t)g * (a.nb_cap / kChunk) * a.nlr + row;
+            struct Cand { double4 p; float2 lj; int slot; };
+            auto gather = [&](int e, bool ok) {
+                const int t = ok ? (e & kHalfSlotMask) : 0;
+                Cand cd;
+                cd.p = a.pos4s[t];
+                if constexpr (TYPES) {
+                    cd.lj = ljtf[(unsigned)e >> kShiftBits];
+                } else {
+                    const double2 d = a.ljs[t];
+                    cd.lj = make_float2((float)d.x, (float)d.y);
+                }
+                cd.slot = wdel[ok ? (e >> kHalfSlotBits) & 31 : 0] + t;
+                return cd;
+            };
+            auto eval = [&](const Cand& cd) {
+                double dxd = pi.x - cd.p.x, dyd = pi.y - cd.p.y, dzd = pi.z - cd.p.z;
+                dxd -= a.L.x * rint(dxd * a.invL.x);
+                dyd -= a.L.y * rint(dyd * a.invL.y);
+                dzd -= a.L.z * rint(dzd * a.invL.z);
+                const float dx = (float)dxd, dy = (float)dyd, dz = (float)dzd;
+                const float r2 = fmaf(dx, dx, fmaf(dy, dy, dz * dz));
+                if (r2 <= rc2) {
+                    const float inv_r = rsqrtf(r2);
+                    const float ar = alpha * (r2 * inv_r);
+                    const float y = ar * escale;
+                    const int it = (int)y;
+                    const float u = 2.0f * (y - (float)it) - 1.0f;
+                    const float* c = tabf + it * (kErfcDegF + 1);
+                    float pc = c[kErfcDegF];
+#pragma unroll
+                    for (int j = kErfcDegF - 1; j >= 0; j--) pc = fmaf(pc, u, c[j]);
+                    const float e2 = __expf(-ar * ar);
+                    const float ec = e2 * pc;
+                    const float sig = li.x + cd.lj.x;
+                    float s2 = inv_r * sig;
+                    s2 *= s2;
+                    const float sig6 = s2 * s2 * s2;
+                    const float es6 = sig6 * li.y * cd.lj.y;
+                    const float qj = ke * (float)cd.p.w * inv_r;
+                    const float qq = qi * qj;
+                    if (a.include_forces) {
+                        const float inv_r2 = inv_r * inv_r;
+                        const float dEdR = qq * inv_r2 * fmaf(ar * e2, 1.1283791670955126f, ec) +
+                                           es6 * (12.0f * sig6 - 6.0f) * inv_r2;
+                        const float fx = dEdR * dx, fy = dEdR * dy, fz = dEdR * dz;
+                        const float dqj = keqi * inv_r * ec;
+                        acc.fx += fx; acc.fy += fy; acc.fz += fz;
+                        acc.dq = fmaf(qj, ec, acc.dq);
+                        bad |= !(fmaxf(fmaxf(fabsf(fx), fabsf(fy)), fmaxf(fabsf(fz), fabsf(dqj))) < (float)kFixMax);
+                        atomicAdd(&accw[0][cd.slot], to_fix(-(double)fx));
+                        atomicAdd(&accw[1][cd.slot], to_fix(-(double)fy));
+                        atomicAdd(&accw[2][cd.slot], to_fix(-(double)fz));
+                        atomicAdd(&accw[3][cd.slot], to_fix((double)dqj));
+                    }
+                    acc.e += (double)fmaf(qq, ec, es6 * (sig6 - 1.0f));   // the whole pair energy
+                }
+            };
+            walk_list(nl4, a.nlr, cnt, 0, 1, gather, eval);
+          }
+        } else if (active) {
             const double4 pi = a.pos4s[row];
             const double2 li = a.ljs[row];
             const double kqis = kOne4PiEps0 * pi.w * kFixScale;   // k_e q_i in fixed-point units
@@ -1061,7 +1146,8 @@ __global__ void __launch_bounds__(1024) k_pairs_half(DirectArgs a) {
                 const int t = ok ? (e & kHalfSlotMask) : 0;
                 Cand cd;
                 cd.p = a.pos4s[t];
-                cd.lj = TYPES ? ljt[(unsigned)e >> kShiftBits] : a.ljs[t];
+                if constexpr (TYPES) cd.lj = ljt[(unsigned)e >> kShiftBits];
+                else cd.lj = a.ljs[t];
                 cd.slot = wdel[ok ? (e >> kHalfSlotBits) & 31 : 0] + t;
                 return cd;
             };
@@ -1116,9 +1202,15 @@ __global__ void __launch_bounds__(1024) k_pairs_half(DirectArgs a) {
             a.e_atom[3 * i + 1] = acc.e;
             if (a.include_forces) {
                 a.dedq[i] = acc.dq;
-                a.f_part[3 * i] = acc.fx * -kFixInv;
-                a.f_part[3 * i + 1] = acc.fy * -kFixInv;
-                a.f_part[3 * i + 2] = acc.fz * -kFixInv;
+                if constexpr (MIXED) {
+                    a.f_part[3 * i] = acc.fx;
+                    a.f_part[3 * i + 1] = acc.fy;
+                    a.f_part[3 * i + 2] = acc.fz;
+                } else {   // accumulated as -F in fixed-point units
+                    a.f_part[3 * i] = acc.fx * -kFixInv;
+                    a.f_part[3 * i + 1] = acc.fy * -kFixInv;
+                    a.f_part[3 * i + 2] = acc.fz * -kFixInv;
+                }
             }
         }
     }
@@ -1159,11 +1251,6 @@ __device__ __forceinline__ void half_window_sums(const DirectArgs& a, int s, dou
 //     in fp32 per lane, the energy in fp64; lanes are combined and the exclusion correction
 //     is applied in fp64 (excl_atom).
 // ---------------------------------------------------------------------------------
-struct PairAccF {
-    float fx = 0, fy = 0, fz = 0, dq = 0;
-    double e = 0;
-};
-
 __device__ __forceinline__ void pair_term_f(PairAccF& acc, float alpha, int include_forces, const float* tab,
                                             float scale, float4 pi, float2 li, float4 pj, float2 lj2, float dx,
                                             float dy, float dz, float r2) {
@@ -1602,8 +1689,13 @@ void launch_direct(Handle& h, const double* pos, int include_forces) {
     DirectArgs a = direct_args(h, pos, include_forces);
     if (a.half) {
         const int ncell = h.nc[0] * h.nc[1] * h.nc[2];
-        if (a.typ_s) hipLaunchKernelGGL((k_pairs_half<true>), dim3(ncell), dim3(1024), 0, h.stream, a);
-        else hipLaunchKernelGGL((k_pairs_half<false>), dim3(ncell), dim3(1024), 0, h.stream, a);
+        if (h.mixed) {
+            if (a.typ_s) hipLaunchKernelGGL((k_pairs_half<true, true>), dim3(ncell), dim3(1024), 0, h.stream, a);
+            else hipLaunchKernelGGL((k_pairs_half<false, true>), dim3(ncell), dim3(1024), 0, h.stream, a);
+        } else {
+            if (a.typ_s) hipLaunchKernelGGL((k_pairs_half<true, false>), dim3(ncell), dim3(1024), 0, h.stream, a);
+            else hipLaunchKernelGGL((k_pairs_half<false, false>), dim3(ncell), dim3(1024), 0, h.stream, a);
+        }
         return;
     }
     // lanes per atom: enough threads for ~2 waves per SIMD on 256 CUs

@@ -208,9 +208,12 @@ def test_c5_mixed_four_rank_split(c5):
     system, force, pos, box = c5
     k = HipCalcCoulForceKernel(kspace_algo=GRID, precision="mixed").initialize(system, force)
     e1, f1 = k.execute_host(pos, box)
+    t1 = k.energy_terms()
     k.destroy()
     e4, f4, _, ranges = _decomposed(system, force, pos, box, 4, GRID, precision="mixed")
     assert all(hi > lo for lo, hi in ranges)
-    assert e4 == pytest.approx(e1, rel=1e-11)
-    # fp32 per-lane force sums: a rank's lanes-per-atom choice changes their rounding
+    # one rank walks the half list (each pair once), four ranks the full list: the fp32 pair
+    # terms round differently (observed |dE| 2.6e-3 kJ/mol = 2e-11 of sum|terms|)
+    assert abs(e4 - e1) <= 1e-10 * np.abs(t1).sum()
+    # fp32 per-lane force sums: the list kind and a rank's lanes-per-atom choice change their rounding
     assert np.abs(f4 - f1).max() <= 1e-6 * np.abs(f1).max()

@@ -29,11 +29,11 @@ def _need_gpu():
         pytest.skip("no HIP device")
 
 
-def _kernel(system, force, half, algo=0, skin=0.0):
+def _kernel(system, force, half, algo=0, skin=0.0, precision="double"):
     old = os.environ.get("CF_HALF")
     os.environ["CF_HALF"] = "1" if half else "0"
     try:
-        k = HipCalcCoulForceKernel(kspace_algo=algo).initialize(system, force)
+        k = HipCalcCoulForceKernel(kspace_algo=algo, precision=precision).initialize(system, force)
         if skin:
             k.set_neighbor_skin(skin)
     finally:
@@ -107,3 +107,16 @@ def test_half_list_fallback_on_fixed_point_range():
     ref = Oracle(force, box).execute(p, box)
     assert np.abs(f - ref["forces"]).max() <= 1e-8 * max(1.0, np.abs(ref["forces"]).max() / 1e3)
     assert abs(e - ref["energy"]) <= 1e-9 * np.abs(ref["terms"]).sum() + 1e-8
+
+
+def test_half_list_mixed_precision():
+    # the fp32 half-list kernel against the fp32 full list and the fp64 half list (same k-space)
+    system, force, pos, box = ts.water_box(4000, cutoff=1.0, ewald_tol=1e-4, every_bond_angle=5)
+    em, fm, dm, tm = _eval(_kernel(system, force, True, 0, precision="mixed"), pos, box)
+    ef, ff, df, tf = _eval(_kernel(system, force, False, 0, precision="mixed"), pos, box)
+    ed, fd, dd, td = _eval(_kernel(system, force, True, 0), pos, box)
+    rms = lambda a, b: np.sqrt(((a - b) ** 2).sum(1).mean() / (b ** 2).sum(1).mean())
+    assert rms(fm, ff) <= 1e-5 and np.abs(fm - ff).max() <= 0.05
+    assert rms(fm, fd) <= 1e-5 and np.abs(fm - fd).max() <= 0.05
+    assert np.abs(dm - dd).max() <= 1e-5 * np.abs(dd).max()
+    assert abs(em - ed) <= 1e-9 * np.abs(td).sum()
