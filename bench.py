@@ -118,7 +118,7 @@ def cpu_baseline(force, pos, box, k_sample):
 # rocprofv3 kernel names of the library's timing phases at C3
 # (a phase timed as one bracket may be several launches: their bytes are summed)
 PMC_KERNEL = {"kspace_force": ["cf::k_force<2>"], "kspace_sfac": ["cf::k_sfac<4, 32>"],
-              "direct_pairs": ["cf::k_pairs_half<true>"],
+              "direct_pairs": ["cf::k_pairs_half<true, false>"],
               "grid_spread": ["cf::k_g_spread_tile<3, 32>"], "grid_interp": ["cf::k_g_interp<14>"]}
 
 

@@ -143,6 +143,7 @@ def test_grid_multi_rank_decomposition_on_one_gpu(world, shuffled, precision):
     pt = torch.tensor(pos, dtype=torch.float64, device="cuda")
     single = HipCalcCoulForceKernel(stream=stream, kspace_algo=GRID, precision=precision).initialize(system, force)
     e1, f1 = single.execute_host(pos, box)
+    t1 = single.energy_terms()
     ks = [HipCalcCoulForceKernel(stream=stream, rank=r, world_size=world, kspace_algo=GRID,
                                  precision=precision).initialize(system, force)
           for r in range(world)]
@@ -160,11 +161,17 @@ def test_grid_multi_rank_decomposition_on_one_gpu(world, shuffled, precision):
             k.end(f, e)
             es.append(e)
         torch.cuda.synchronize()
-        assert sum(x.item() for x in es) == pytest.approx(e1, rel=1e-11)
+        if precision == "double":
+            assert sum(x.item() for x in es) == pytest.approx(e1, rel=1e-11)
+        else:   # one mixed rank walks the half list (each pair once), several the full list: the
+            # fp32 pair terms round differently (observed 2.4e-3 kJ/mol = 2e-9 of sum|terms|;
+            # the mixed-precision energy bar against fp64 is 1e-8 of sum|terms|)
+            assert abs(sum(x.item() for x in es) - e1) <= 1e-8 * np.abs(t1).sum()
         if precision == "double":
             assert np.abs(f.cpu().numpy() - f1).max() < 1e-8
-        else:   # fp32 per-lane force sums: the rank's lanes-per-atom choice changes their rounding
-            assert np.abs(f.cpu().numpy() - f1).max() < 1e-6 * np.abs(f1).max()
+        else:   # fp32 per-lane force sums: the list kind (half on one rank, full on several) and the
+            # rank's lanes-per-atom choice change their rounding (observed 2.5e-3 = 1.0e-6 of max|F|)
+            assert np.abs(f.cpu().numpy() - f1).max() < 1e-5 * np.abs(f1).max()
 
 
 def test_grid_c3_matches_exact_mfma_path():
