@@ -576,6 +576,8 @@ CF_EXPORT int cf_create(const cf_params* p, const cf_options* opt, cf_handle** o
             } else if (h.kspace_algo == 2) {
                 const cf::GridPlan& gp = h.gp;
                 const size_t npts = (size_t)gp.ng[0] * gp.ng[1] * gp.ng[2];
+                if (npts >= (size_t)INT_MAX)   // the grid kernels index with 32-bit ints
+                    fail(CF_ERR_INVALID, "k-space grid too large (more than 2^31 points)");
                 std::vector<double2> tw[3], twz;
                 std::vector<double> dc[3];
                 cf::grid_tables(h, tw, twz, dc);
