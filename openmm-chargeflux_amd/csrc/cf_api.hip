@@ -578,11 +578,14 @@ CF_EXPORT int cf_create(const cf_params* p, const cf_options* opt, cf_handle** o
                 const size_t npts = (size_t)gp.ng[0] * gp.ng[1] * gp.ng[2];
                 if (npts >= (size_t)INT_MAX)   // the grid kernels index with 32-bit ints
                     fail(CF_ERR_INVALID, "k-space grid too large (more than 2^31 points)");
-                std::vector<double2> tw[3], twz;
+                std::vector<double2> tw[3], tw8[3];
                 std::vector<double> dc[3];
-                cf::grid_tables(h, tw, twz, dc);
-                for (int d = 0; d < 3; d++) { h.g_tw[d] = dupload(H, tw[d]); h.g_deconv[d] = dupload(H, dc[d]); }
-                h.g_twz = dupload(H, twz);
+                cf::grid_tables(h, tw, tw8, dc);
+                for (int d = 0; d < 3; d++) {
+                    h.g_tw[d] = dupload(H, tw[d]);
+                    h.g_deconv[d] = dupload(H, dc[d]);
+                    if (!tw8[d].empty()) h.g_tw8[d] = dupload(H, tw8[d]);
+                }
                 h.g_grid = dalloc<double>(H, npts);
                 h.g_t1 = dalloc<double2>(H, (size_t)gp.ng[0] * gp.ng[1] * gp.KZ);
                 h.g_t2 = dalloc<double2>(H, (size_t)gp.ng[0] * gp.NY * gp.KZ);

@@ -72,7 +72,12 @@ struct GridPlan {
     int nbins = 0;
     int KX = 0, KY = 0, KZ = 0;
     int NX = 0, NY = 0;      // 2KX-1, 2KY-1 (mode rows nx, ny in (-K, K)); nz in [0, KZ)
-    int KZP = 0;             // KZ padded for the forward z stage
+    // pruned DFT stages by the 8 x Q factorization (ng = 8Q; k_g_dft8_*), per axis: modes
+    // per residue class k = r (mod 8) padded to mt (0: the axis uses the GEMM stages), j of the
+    // first mode of class r and the class size
+    int mt[3] = {0, 0, 0};
+    int rj[3][8] = {}, rc[3][8] = {};
+    bool dft8 = false;       // every axis qualifies and CF_DFT8 != 0
 };
 
 struct Handle {
@@ -171,7 +176,7 @@ struct Handle {
     double2* g_t2 = nullptr;    // [ngx][NY][KZ]
     double2* g_b = nullptr;     // [NX][NY][KZ] B(n) (all-reduced), then coefficients f(n)
     double2* g_tw[3] = {nullptr, nullptr, nullptr};  // [2K-1][ng] e^{i 2pi n g/ng}
-    double2* g_twz = nullptr;   // [ngz][KZP] e^{i 2pi nz z/ngz}, nz >= 0
+    double2* g_tw8[3] = {nullptr, nullptr, nullptr};  // [8 r][Q b][mt] e^{i 2pi b k/ng}, k the class-r modes
     double* g_deconv[3] = {nullptr, nullptr, nullptr};  // [K] 1/phih(n/ng)
     int* g_cnt = nullptr;       // [nbins]
     int* g_start = nullptr;     // [nbins+1]
@@ -235,7 +240,7 @@ void launch_kspace_direct_force(Handle& h, const double* pos);
 
 // grid path (kspace_algo = 2)
 void grid_plan(Handle& h, int width, double sigma);
-void grid_tables(const Handle& h, std::vector<double2> tw[3], std::vector<double2>& twz, std::vector<double> deconv[3]);
+void grid_tables(const Handle& h, std::vector<double2> tw[3], std::vector<double2> tw8[3], std::vector<double> deconv[3]);
 void launch_grid_sort(Handle& h, const double* pos);
 void launch_grid_spread(Handle& h);
 void launch_grid_dft_fwd(Handle& h);

@@ -19,6 +19,7 @@
 // fixed order (atoms are sorted by grid tile each evaluation with a deterministic counting
 // sort), so results are bitwise reproducible.  All fp64.
 #include <algorithm>
+#include <cstdlib>
 #include <cmath>
 #include <vector>
 
@@ -418,8 +419,6 @@ __global__ void __launch_bounds__(256) k_g_spread_tile(int3 ng, int3 nb, const i
 // ---------------------------------------------------------------------------------
 // 3. pruned DFT stages
 // ---------------------------------------------------------------------------------
-constexpr int kNZB = 4;   // KZ padding unit of the plan's KZP
-
 // Every pruned-DFT stage as one batched complex GEMM on the fp64 matrix cores,
 //   C(m, n) = sum_k A(m, k) B(k, n),
 //   A(m, k) = A[m sam + k sak]            (complex; real for the forward z stage's grid rows)
@@ -599,6 +598,394 @@ __global__ void __launch_bounds__(256) k_g_cgemm(CGemm g) {
                 if (CREAL) reinterpret_cast<double*>(g.C)[off] = cre[i][j][q];
                 else reinterpret_cast<double2*>(g.C)[off] = make_double2(cre[i][j][q], cim[i][j][q]);
             }
+    }
+}
+
+// ---------------------------------------------------------------------------------
+// 3b. pruned DFT stages by the 8 x Q factorization (ng = 8Q, every axis; the default).
+//     Each stage maps a batch of sequences between the length side (n < ng, grid points)
+//     and the mode side (k = k0 + j, j < J; the reference's mode box), w = e^{i 2pi/ng}:
+//       analysis   X[k] = sum_n x[n] w^{nk}        (forward z, y, x stages)
+//       synthesis  x[n] = sum_j c[j] w^{n k_j}     (inverse x, y, z stages; z keeps Re)
+//     With n = Qa + b (a < 8, b < Q), w^{nk} = e^{i 2pi a (k mod 8)/8} w^{bk}, so
+//       analysis:  Y[b][r] = sum_a x[Qa+b] e^{i 2pi a r/8}   (8-point DFT per b: ~70 flops)
+//                  X[k]    = sum_b w^{bk} Y[b][k mod 8]      (Q complex MACs per mode)
+//       synthesis: Z[b][r] = sum_{k = r mod 8} c_k w^{bk}     (same count), then the 8-point DFT
+//                  over r gives x[Qa+b] for every a.
+//     Per sequence ~Q (J + 70) complex operations instead of ng J (C5: 8x fewer than the GEMM
+//     stages for the x/y stages, 3.6x for z), which makes the stages HBM-bound instead of
+//     bound by the matrix pipe.  Layout: a 256-thread block owns 64 sequences, lane = sequence;
+//     wave w owns the residue classes r = w and w + 4 (the modes k = r mod 8 of every lane's
+//     sequence: mt accumulators per class in registers).  b is walked in chunks of 8: the
+//     chunk's 8-point DFTs (threads along whichever index is contiguous in memory) go to LDS
+//     [b][r][sequence]; each lane then reads its sequence's Y[b][r] (conflict-free).  The
+//     twiddles are factored, w^{b(k_r + 8t)} = w^{b k_r} w_Q^{bt} (k_r the first mode of class
+//     r, w_Q = w^8): a [8][Q] twist table and one [Q][mt] table shared by every class (<= 13 KB
+//     per axis: it stays in the scalar cache), read with wave-uniform scalar loads and fed to
+//     the FMAs as SGPR operands.  (Per-class [r][b][mt] tables of up to 72 KB missed the
+//     scalar cache on every b: C5 stages 2-4x slower.)  Every output is one lane's sum in b
+//     order: deterministic.  Multi-rank x-slab: blocks whose sequences all lie in x-planes
+//     outside the slab exit (z and y stages); the forward x stage reads planes outside the
+//     slab as zero (select, not multiply: they are stale).
+// ---------------------------------------------------------------------------------
+struct Dft8 {
+    int nseq, Q, sdiv;
+    long s1, s0, sn;     // length side: element (s, n) at (s / sdiv) s1 + (s % sdiv) s0 + n sn
+    long c1, c0, cj;     // mode side:   element (s, j) at (s / sdiv) c1 + (s % sdiv) c0 + j cj
+    const void* in;
+    void* out;
+    int rj[8], rc[8];    // j of the first mode of class r, class size
+    int xmode, xdiv;     // 1: sequence s lies in x-plane s / xdiv; 2: n is the x-plane (analysis)
+    const int* xr;
+    int W, ngx;
+};
+
+constexpr int kD8Seq = 64, kD8BC = 8, kD8SP = kD8Seq + 1;
+constexpr int kDft8Mt[] = {4, 8, 9, 16, 17};   // class-size paddings instantiated (CF_D8_MT)
+
+__device__ __forceinline__ v2d mul_i(v2d v) { return v2d{-v.y, v.x}; }
+
+// y[r] = sum_a x[a] e^{+i 2pi a r/8} (radix-2 in registers)
+__device__ __forceinline__ void dft8(const v2d (&x)[8], v2d (&y)[8]) {
+    const double c = 0.70710678118654752440;
+    const v2d e0 = x[0] + x[4], e1 = x[0] - x[4], e2 = x[2] + x[6], e3 = x[2] - x[6];
+    const v2d o0 = x[1] + x[5], o1 = x[1] - x[5], o2 = x[3] + x[7], o3 = x[3] - x[7];
+    const v2d E0 = e0 + e2, E2 = e0 - e2, E1 = e1 + mul_i(e3), E3 = e1 - mul_i(e3);
+    const v2d O0 = o0 + o2, O2 = o0 - o2, O1 = o1 + mul_i(o3), O3 = o1 - mul_i(o3);
+    const v2d wO1 = v2d{c * (O1.x - O1.y), c * (O1.x + O1.y)};      // e^{i pi/4} O1
+    const v2d w3O3 = v2d{-c * (O3.x + O3.y), c * (O3.x - O3.y)};    // e^{i 3pi/4} O3
+    const v2d iO2 = mul_i(O2);
+    y[0] = E0 + O0; y[4] = E0 - O0;
+    y[1] = E1 + wO1; y[5] = E1 - wO1;
+    y[2] = E2 + iO2; y[6] = E2 - iO2;
+    y[3] = E3 + w3O3; y[7] = E3 - w3O3;
+}
+
+__device__ __forceinline__ void cmac(v2d& acc, v2d y, double2 t) {
+    acc.x = fma(y.x, t.x, acc.x);
+    acc.x = fma(-y.y, t.y, acc.x);
+    acc.y = fma(y.x, t.y, acc.y);
+    acc.y = fma(y.y, t.x, acc.y);
+}
+
+__device__ __forceinline__ bool d8_block_outside(const Dft8& d, int s0) {
+    return d.xmode == 1 && d.xr &&
+           !x_range_in_slab(s0 / d.xdiv, min(s0 + kD8Seq - 1, d.nseq - 1) / d.xdiv, d.xr, d.W, d.ngx);
+}
+
+// analysis (CIN: complex input; else real input, classes r > 4 from conj Y[b][8 - r]).
+// 8 waves: wave r owns residue class r of the block's 64 sequences.  Each thread does one
+// (sequence, b) 8-point DFT per chunk; the next chunk's 8 inputs are loaded into registers
+// before the current chunk's class sums, so the global latency overlaps the FMAs.
+template <int MT, bool CIN>
+__global__ void __launch_bounds__(512) k_g_dft8_fwd(Dft8 d, const double2* __restrict__ twist,
+                                                    const double2* __restrict__ tq) {
+    constexpr int NR = CIN ? 8 : 5;
+    __shared__ v2d sY[kD8BC * NR * kD8SP];
+    const int s0 = blockIdx.x * kD8Seq;
+    if (d8_block_outside(d, s0)) return;
+    const int tid = threadIdx.x, lane = tid & 63, r = wave_id();
+    // this thread's step-1 item: real input rows are contiguous along n (8 lanes per sequence
+    // over b); complex inputs are contiguous along the sequence index (lanes over sequences)
+    const int sl = CIN ? (tid & 63) : (tid >> 3), bl = CIN ? (tid >> 6) : (tid & 7);
+    const int si = s0 + sl;
+    const bool sok = si < d.nseq;
+    const long ibase = sok ? (long)(si / d.sdiv) * d.s1 + (long)(si % d.sdiv) * d.s0 : 0;
+    v2d xn[8];
+    auto load = [&](int bc) {
+        const bool ok = sok && bc + bl < d.Q;
+#pragma unroll
+        for (int a = 0; a < 8; a++) {
+            const int n = d.Q * a + bc + bl;
+            const bool oka = ok && (d.xmode != 2 || x_in_slab(n, d.xr, d.W, d.ngx));
+            if constexpr (CIN) {
+                const v2d v = reinterpret_cast<const v2d*>(d.in)[oka ? ibase + n * d.sn : 0];
+                xn[a] = oka ? v : v2d{0.0, 0.0};
+            } else {
+                const double v = reinterpret_cast<const double*>(d.in)[oka ? ibase + n * d.sn : 0];
+                xn[a] = v2d{oka ? v : 0.0, 0.0};
+            }
+        }
+    };
+    v2d acc[MT];
+#pragma unroll
+    for (int t = 0; t < MT; t++) acc[t] = v2d{0.0, 0.0};
+    const bool cj = !CIN && r > 4;
+    const int rr = cj ? 8 - r : r;
+    load(0);
+    for (int bc = 0; bc < d.Q; bc += kD8BC) {
+        const int nb = min(kD8BC, d.Q - bc);
+        {
+            v2d y[8];
+            dft8(xn, y);
+#pragma unroll
+            for (int q = 0; q < NR; q++) sY[(bl * NR + q) * kD8SP + sl] = y[q];
+        }
+        __syncthreads();
+        if (bc + kD8BC < d.Q) load(bc + kD8BC);
+        const double2* twr = twist + (long)r * d.Q + bc;
+        const double2* tqb = tq + (long)bc * MT;
+#pragma unroll 2
+        for (int b = 0; b < nb; b++) {
+            v2d y = sY[(b * NR + rr) * kD8SP + lane];
+            if (cj) y.y = -y.y;
+            v2d yt = v2d{0.0, 0.0};
+            cmac(yt, y, twr[b]);   // w^{b k_r} Y[b][r]
+#pragma unroll
+            for (int t = 0; t < MT; t++) cmac(acc[t], yt, tqb[b * MT + t]);
+        }
+        __syncthreads();
+    }
+    const int s = s0 + lane;
+    if (s >= d.nseq) return;
+    const long base = (long)(s / d.sdiv) * d.c1 + (long)(s % d.sdiv) * d.c0;
+    const int cnt = d.rc[r], j0 = d.rj[r];
+#pragma unroll
+    for (int t = 0; t < MT; t++)
+        if (t < cnt) reinterpret_cast<v2d*>(d.out)[base + (long)(j0 + 8 * t) * d.cj] = acc[t];
+}
+
+// analysis along z of the real grid rows (contiguous along n): 8 rows per block, NB waves;
+// lane = (row, class), wave g = the g-th of NB contiguous b ranges (so the [Q][mt] twiddle rows
+// stay wave-uniform scalar loads).  The rows' 8-point DFTs are computed for every b at once from
+// loads that run along the row ((row, b) items with lane-consecutive b: each a-slice of a row is
+// one contiguous run, every element loaded once); Y[row][b][r <= 4] and the twist table live in
+// LDS (21 KB at C5: many blocks per CU).  The b loop is software-pipelined (the next b's LDS and
+// scalar loads are issued before the current b's FMAs).  The NB partial sums are added in wave
+// order into LDS output rows (deterministic), written as contiguous rows of t1.  (The
+// sequence-lane kernel read a row as 8-element pieces per b chunk: 2.9x the grid's bytes
+// fetched at C5.)
+constexpr int kZR = 8;    // rows per block of the z analysis
+constexpr int kZIR = 16;  // rows per block of the z synthesis
+
+template <int MT, int NB>
+__global__ void __launch_bounds__(64 * NB) k_g_dft8_zfwd(Dft8 d, const double2* __restrict__ twist,
+                                                         const double2* __restrict__ tq) {
+    extern __shared__ v2d sm8[];
+    constexpr int R = kZR;
+    const int Q = d.Q;
+    v2d* sY = sm8;                        // [R][Q][5]
+    v2d* stw = sm8 + R * Q * 5;           // [8][Q]
+    v2d* sO = stw + 8 * Q;                // [R][J] output rows
+    const int s0 = blockIdx.x * R;
+    if (d.xmode == 1 && d.xr &&
+        !x_range_in_slab(s0 / d.xdiv, min(s0 + R - 1, d.nseq - 1) / d.xdiv, d.xr, d.W, d.ngx))
+        return;
+    const int tid = threadIdx.x;
+    for (int e = tid; e < 8 * Q; e += 64 * NB) stw[e] = reinterpret_cast<const v2d*>(twist)[e];
+    const double* in = reinterpret_cast<const double*>(d.in);
+    for (int it = tid; it < R * Q; it += 64 * NB) {
+        const int row = it / Q, b = it - row * Q;
+        const int s = s0 + row;
+        const bool ok = s < d.nseq;
+        const long base = (long)(ok ? s : 0) * d.s1 + b;
+        v2d x[8], y[8];
+#pragma unroll
+        for (int a = 0; a < 8; a++) {
+            const double v = in[base + (long)Q * a];
+            x[a] = v2d{ok ? v : 0.0, 0.0};
+        }
+        dft8(x, y);
+#pragma unroll
+        for (int r = 0; r < 5; r++) sY[(row * Q + b) * 5 + r] = y[r];
+    }
+    __syncthreads();
+    const int lane = tid & 63, g = wave_id();
+    const int row = lane & 7, r = lane >> 3;
+    const bool cj = r > 4;
+    const int rr = cj ? 8 - r : r;
+    const int b0 = g * Q / NB, b1 = (g + 1) * Q / NB;
+    v2d acc[MT];
+#pragma unroll
+    for (int t = 0; t < MT; t++) acc[t] = v2d{0.0, 0.0};
+    if (b0 < b1) {
+        v2d yn = sY[(row * Q + b0) * 5 + rr], twn = stw[r * Q + b0];
+        double2 qn[MT];
+#pragma unroll
+        for (int t = 0; t < MT; t++) qn[t] = tq[b0 * MT + t];
+        for (int b = b0; b < b1; b++) {
+            v2d y = yn;
+            const v2d tw = twn;
+            double2 q[MT];
+#pragma unroll
+            for (int t = 0; t < MT; t++) q[t] = qn[t];
+            if (b + 1 < b1) {
+                yn = sY[(row * Q + b + 1) * 5 + rr];
+                twn = stw[r * Q + b + 1];
+#pragma unroll
+                for (int t = 0; t < MT; t++) qn[t] = tq[(b + 1) * MT + t];
+            }
+            if (cj) y.y = -y.y;
+            v2d yt = v2d{0.0, 0.0};
+            cmac(yt, y, make_double2(tw.x, tw.y));   // w^{b k_r} Y[b][r]
+#pragma unroll
+            for (int t = 0; t < MT; t++) cmac(acc[t], yt, q[t]);
+        }
+    }
+    const int J = d.rc[0] + d.rc[1] + d.rc[2] + d.rc[3] + d.rc[4] + d.rc[5] + d.rc[6] + d.rc[7];
+    const int cnt = d.rc[r], j0 = d.rj[r];
+    for (int gg = 0; gg < NB; gg++) {   // partial sums added in wave order
+        if (g == gg) {
+#pragma unroll
+            for (int t = 0; t < MT; t++)
+                if (t < cnt) {
+                    v2d& o = sO[row * J + j0 + 8 * t];
+                    o = gg == 0 ? acc[t] : o + acc[t];
+                }
+        }
+        __syncthreads();
+    }
+    const int nrow = min(R, d.nseq - s0);
+    v2d* out = reinterpret_cast<v2d*>(d.out) + (long)s0 * d.c1;   // rows of J = c1 consecutive modes
+    for (int e = tid; e < nrow * J; e += 64 * NB) out[e] = sO[e];
+}
+
+// synthesis along z into the real grid rows: 16 rows per block, NB waves; lane = (row, class
+// pair) with pairs {0, 4}, {1, 7}, {2, 6}, {3, 5}, wave g = the g-th of NB b ranges.  Only Re x is
+// kept, so a pair needs only P_r = Z_r + conj Z_{8-r} (Re(e^{it} Z_r) + Re(e^{-it} Z_{8-r}) =
+// Re(e^{it} P_r)) and (Re Z_0, Re Z_4): 4 complex values per (row, b) in LDS for every b at
+// once; then the outputs x[Qa + b] are formed per (row, b) item with lane-consecutive b, so each
+// a-slice of a row is written as one contiguous run (the sequence-lane kernel wrote 64-byte
+// pieces per b chunk: 1.55x the grid's bytes written at C5).
+template <int MT, int NB>
+__global__ void __launch_bounds__(64 * NB) k_g_dft8_zinv(Dft8 d, const double2* __restrict__ twist,
+                                                         const double2* __restrict__ tq) {
+    extern __shared__ v2d sm8[];
+    constexpr int R = kZIR;
+    const int Q = d.Q;
+    v2d* sZ = sm8;                 // [R][Q][4]
+    v2d* stw = sm8 + R * Q * 4;    // [8][Q]
+    const int s0 = blockIdx.x * R;
+    if (d.xmode == 1 && d.xr &&
+        !x_range_in_slab(s0 / d.xdiv, min(s0 + R - 1, d.nseq - 1) / d.xdiv, d.xr, d.W, d.ngx))
+        return;
+    const int tid = threadIdx.x;
+    for (int e = tid; e < 8 * Q; e += 64 * NB) stw[e] = reinterpret_cast<const v2d*>(twist)[e];
+    const int lane = tid & 63, g = wave_id();
+    const int row = lane & 15, p = lane >> 4;
+    const int r1 = p, r2 = p == 0 ? 4 : 8 - p;
+    v2d c1[MT], c2[MT];
+    {
+        const int s = s0 + row;
+        const bool ok = s < d.nseq;
+        const v2d* in = reinterpret_cast<const v2d*>(d.in) + (long)(ok ? s : 0) * d.c1;
+        const int n1 = d.rc[r1], j1 = d.rj[r1], n2 = d.rc[r2], j2 = d.rj[r2];
+#pragma unroll
+        for (int t = 0; t < MT; t++) {
+            const bool o1 = ok && t < n1, o2 = ok && t < n2;
+            const v2d a1 = in[o1 ? j1 + 8 * t : 0], a2 = in[o2 ? j2 + 8 * t : 0];
+            c1[t] = o1 ? a1 : v2d{0.0, 0.0};
+            c2[t] = o2 ? a2 : v2d{0.0, 0.0};
+        }
+    }
+    __syncthreads();
+    const int b0 = g * Q / NB, b1 = (g + 1) * Q / NB;
+    if (b0 < b1) {
+        double2 qn[MT];
+#pragma unroll
+        for (int t = 0; t < MT; t++) qn[t] = tq[b0 * MT + t];
+        for (int b = b0; b < b1; b++) {
+            double2 q[MT];
+#pragma unroll
+            for (int t = 0; t < MT; t++) q[t] = qn[t];
+            if (b + 1 < b1) {
+#pragma unroll
+                for (int t = 0; t < MT; t++) qn[t] = tq[(b + 1) * MT + t];
+            }
+            v2d z1 = v2d{0.0, 0.0}, z2 = v2d{0.0, 0.0};
+#pragma unroll
+            for (int t = 0; t < MT; t++) {
+                cmac(z1, c1[t], q[t]);
+                cmac(z2, c2[t], q[t]);
+            }
+            const v2d t1 = stw[r1 * Q + b], t2 = stw[r2 * Q + b];
+            v2d y1 = v2d{0.0, 0.0}, y2 = v2d{0.0, 0.0};
+            cmac(y1, z1, make_double2(t1.x, t1.y));
+            cmac(y2, z2, make_double2(t2.x, t2.y));
+            sZ[(row * Q + b) * 4 + p] = p == 0 ? v2d{y1.x, y2.x} : v2d{y1.x + y2.x, y1.y - y2.y};
+        }
+    }
+    __syncthreads();
+    const double c = 0.70710678118654752440;
+    double* out = reinterpret_cast<double*>(d.out);
+    for (int it = tid; it < R * Q; it += 64 * NB) {
+        const int rw = it / Q, b = it - rw * Q;
+        const int s = s0 + rw;
+        if (s >= d.nseq) break;   // rows are in order: every later item is past the end too
+        const v2d* z = sZ + (rw * Q + b) * 4;
+        const v2d z04 = z[0], P1 = z[1], P2 = z[2], P3 = z[3];
+        const double e = z04.x + z04.y, o = z04.x - z04.y;               // a even / odd: Re Z0 +- Re Z4
+        const double u1 = c * (P1.x - P1.y), v1 = c * (P1.x + P1.y);     // Re(e^{i pi/4} P1), Re(e^{-i pi/4} P1)
+        const double u3 = c * (-P3.x - P3.y), v3 = c * (-P3.x + P3.y);   // Re(e^{i 3pi/4} P3), Re(e^{-i 3pi/4} P3)
+        // angle pi a r/4 of class r at output a (mod 2pi): r = 1: a pi/4, r = 2: a pi/2, r = 3: 3a pi/4
+        double x[8];
+        x[0] = e + P1.x + P2.x + P3.x;
+        x[1] = o + u1 - P2.y + u3;
+        x[2] = e - P1.y - P2.x + P3.y;
+        x[3] = o - v1 + P2.y - v3;
+        x[4] = e - P1.x + P2.x - P3.x;
+        x[5] = o - u1 - P2.y - u3;
+        x[6] = e + P1.y - P2.x - P3.y;
+        x[7] = o + v1 + P2.y + v3;
+        const long base = (long)s * d.s1 + b;
+#pragma unroll
+        for (int a = 0; a < 8; a++) out[base + (long)Q * a] = x[a];
+    }
+}
+
+// synthesis (ROUT: keep the real part, written as doubles).  8 waves: wave r holds the modes
+// of class r of the block's 64 sequences (lane = sequence) and forms Z[b][r] for the chunk;
+// then each thread turns one (sequence, b) into the outputs n = Qa + b.  b chunks are
+// independent, so they are also dealt over gridDim.y blocks of the same sequences.
+template <int MT, bool ROUT>
+__global__ void __launch_bounds__(512) k_g_dft8_inv(Dft8 d, const double2* __restrict__ twist,
+                                                    const double2* __restrict__ tq) {
+    __shared__ v2d sZ[kD8BC * 8 * kD8SP];
+    const int s0 = blockIdx.x * kD8Seq;
+    if (d8_block_outside(d, s0)) return;
+    const int tid = threadIdx.x, lane = tid & 63, r = wave_id();
+    const int s = s0 + lane;
+    v2d cv[MT];
+    {
+        const bool ok = s < d.nseq;
+        const long base = ok ? (long)(s / d.sdiv) * d.c1 + (long)(s % d.sdiv) * d.c0 : 0;
+        const int cnt = d.rc[r], j0 = d.rj[r];
+#pragma unroll
+        for (int t = 0; t < MT; t++) {
+            const bool okt = ok && t < cnt;
+            const v2d v = reinterpret_cast<const v2d*>(d.in)[okt ? base + (long)(j0 + 8 * t) * d.cj : 0];
+            cv[t] = okt ? v : v2d{0.0, 0.0};
+        }
+    }
+    const int sl = ROUT ? (tid >> 3) : (tid & 63), bl = ROUT ? (tid & 7) : (tid >> 6);
+    const int ss = s0 + sl;
+    const long obase = ss < d.nseq ? (long)(ss / d.sdiv) * d.s1 + (long)(ss % d.sdiv) * d.s0 : 0;
+    for (int bc = kD8BC * blockIdx.y; bc < d.Q; bc += kD8BC * gridDim.y) {
+        const int nb = min(kD8BC, d.Q - bc);
+        const double2* twr = twist + (long)r * d.Q + bc;
+        const double2* tqb = tq + (long)bc * MT;
+#pragma unroll 2
+        for (int b = 0; b < nb; b++) {
+            v2d z = v2d{0.0, 0.0}, zt = v2d{0.0, 0.0};
+#pragma unroll
+            for (int t = 0; t < MT; t++) cmac(z, cv[t], tqb[b * MT + t]);
+            cmac(zt, z, twr[b]);   // w^{b k_r} sum_t c_t w_Q^{b t}
+            sZ[(b * 8 + r) * kD8SP + lane] = zt;
+        }
+        __syncthreads();
+        if (ss < d.nseq && bl < nb) {
+            v2d z[8], x[8];
+#pragma unroll
+            for (int q = 0; q < 8; q++) z[q] = sZ[(bl * 8 + q) * kD8SP + sl];
+            dft8(z, x);
+#pragma unroll
+            for (int a = 0; a < 8; a++) {
+                const long o = obase + (long)(d.Q * a + bc + bl) * d.sn;
+                if constexpr (ROUT) reinterpret_cast<double*>(d.out)[o] = x[a].x;
+                else reinterpret_cast<v2d*>(d.out)[o] = x[a];
+            }
+        }
+        __syncthreads();
     }
 }
 
@@ -843,10 +1230,26 @@ void grid_plan(Handle& h, int width, double sigma) {
     p.nbins = p.nb[0] * p.nb[1] * p.nb[2];
     p.KX = h.kmax[0]; p.KY = h.kmax[1]; p.KZ = h.kmax[2];
     p.NX = 2 * p.KX - 1; p.NY = 2 * p.KY - 1;
-    p.KZP = (p.KZ + kNZB - 1) / kNZB * kNZB;
+    // factorized stages: mode set k0 + j, j < J per axis (x, y: |n| < K; z: 0 <= nz < K)
+    const char* env = getenv("CF_DFT8");
+    p.dft8 = !(env && env[0] == '0');
+    for (int d = 0; d < 3; d++) {
+        const int K = h.kmax[d], J = d == 2 ? K : 2 * K - 1, k0 = d == 2 ? 0 : -(K - 1);
+        int mx = 0;
+        for (int r = 0; r < 8; r++) {
+            const int j0 = ((r - k0) % 8 + 8) % 8;
+            p.rj[d][r] = j0;
+            p.rc[d][r] = j0 < J ? (J - 1 - j0) / 8 + 1 : 0;
+            mx = std::max(mx, p.rc[d][r]);
+        }
+        p.mt[d] = 0;
+        for (int m : kDft8Mt)
+            if (mx <= m) { p.mt[d] = m; break; }
+        if (p.mt[d] == 0) p.dft8 = false;
+    }
 }
 
-void grid_tables(const Handle& h, std::vector<double2> tw[3], std::vector<double2>& twz, std::vector<double> deconv[3]) {
+void grid_tables(const Handle& h, std::vector<double2> tw[3], std::vector<double2> tw8[3], std::vector<double> deconv[3]) {
     const GridPlan& p = h.gp;
     std::vector<double> gx, gw;
     gauss_legendre(200, gx, gw);
@@ -873,9 +1276,24 @@ void grid_tables(const Handle& h, std::vector<double2> tw[3], std::vector<double
             deconv[d][n] = 1.0 / s;
         }
     }
-    twz.assign((size_t)p.ng[2] * p.KZP, make_double2(0, 0));
-    for (int z = 0; z < p.ng[2]; z++)
-        for (int nz = 0; nz < p.KZ; nz++) twz[(size_t)z * p.KZP + nz] = tw[2][(size_t)(nz + p.KZ - 1) * p.ng[2] + z];
+    // factorized stages: tw8[d] = twist [8 r][Q b] = w^{b k_r} (k_r = k0 + rj[r], the first mode
+    // of class r), then [Q b][mt t] = w^{8bt}; exact angles (b k mod ng) like the tables above
+    for (int d = 0; d < 3; d++) {
+        if (!p.dft8) break;
+        const int ng = p.ng[d], Q = ng / 8, K = h.kmax[d], mt = p.mt[d];
+        const int k0 = d == 2 ? 0 : -(K - 1);
+        auto w = [&](long e) {
+            long m = e % ng;
+            if (m < 0) m += ng;
+            const double th = 2.0 * kPi * (double)m / ng;
+            return make_double2(std::cos(th), std::sin(th));
+        };
+        tw8[d].resize((size_t)8 * Q + (size_t)Q * mt);
+        for (int r = 0; r < 8; r++)
+            for (int b = 0; b < Q; b++) tw8[d][(size_t)r * Q + b] = w((long)b * (k0 + p.rj[d][r]));
+        for (int b = 0; b < Q; b++)
+            for (int t = 0; t < mt; t++) tw8[d][(size_t)8 * Q + (size_t)b * mt + t] = w(8L * b * t);
+    }
 }
 
 static double3 recip_vec(const Handle& h) {
@@ -962,8 +1380,103 @@ static void cgemm(Handle& h, CGemm g, int xdim = 0, int xdiv = 1) {
     }
 }
 
+// stage geometry (the same for analysis and synthesis along an axis)
+static Dft8 d8_stage(const Handle& h, int axis) {
+    const GridPlan& p = h.gp;
+    const int ngx = p.ng[0], ngy = p.ng[1], ngz = p.ng[2], KZ = p.KZ, NY = p.NY;
+    const long NYKZ = (long)NY * KZ;
+    Dft8 d{};
+    d.Q = p.ng[axis] / 8;
+    for (int r = 0; r < 8; r++) { d.rj[r] = p.rj[axis][r]; d.rc[r] = p.rc[axis][r]; }
+    d.xr = h.g_xrange; d.W = p.W; d.ngx = ngx;
+    if (axis == 2) {          // rows (x, y): grid[row][z] <-> t1[row][nz]
+        d.nseq = ngx * ngy; d.sdiv = 1;
+        d.s1 = ngz; d.s0 = 0; d.sn = 1;
+        d.c1 = KZ; d.c0 = 0; d.cj = 1;
+        d.xmode = 1; d.xdiv = ngy;
+    } else if (axis == 1) {   // (x, nz): t1[x][y][nz] <-> t2[x][ny][nz]
+        d.nseq = ngx * KZ; d.sdiv = KZ;
+        d.s1 = (long)ngy * KZ; d.s0 = 1; d.sn = KZ;
+        d.c1 = NYKZ; d.c0 = 1; d.cj = KZ;
+        d.xmode = 1; d.xdiv = KZ;
+    } else {                  // r = (ny, nz): t2[x][r] <-> b[nx][r]
+        d.nseq = (int)NYKZ; d.sdiv = (int)NYKZ;
+        d.s1 = 0; d.s0 = 1; d.sn = NYKZ;
+        d.c1 = 0; d.c0 = 1; d.cj = NYKZ;
+        d.xmode = 2; d.xdiv = 1;
+    }
+    return d;
+}
+
+#define CF_D8_MT(MT_, CALL) \
+    switch (MT_) {          \
+        case 4: CALL(4); break;   \
+        case 8: CALL(8); break;   \
+        case 9: CALL(9); break;   \
+        case 16: CALL(16); break; \
+        default: CALL(17); break; \
+    }
+
+static void d8_fwd(Handle& h, int axis, const void* in, void* out) {
+    Dft8 d = d8_stage(h, axis);
+    d.in = in; d.out = out;
+    const int nb = nblk(d.nseq, kD8Seq);
+    const double2* twist = h.g_tw8[axis];
+    const double2* tq = twist + 8 * d.Q;
+    const int J = d.rc[0] + d.rc[1] + d.rc[2] + d.rc[3] + d.rc[4] + d.rc[5] + d.rc[6] + d.rc[7];
+    const size_t lds = (size_t)(kZR * d.Q * 5 + 8 * d.Q + kZR * J) * sizeof(double2);
+    if (axis == 2 && lds <= 64 * 1024) {   // grid rows: the row kernel (4 waves, each a quarter of b)
+        const dim3 g((unsigned)nblk(d.nseq, kZR));
+#define CF_D8Z(MT_) hipLaunchKernelGGL((k_g_dft8_zfwd<MT_, 4>), g, dim3(256), lds, h.stream, d, twist, tq)
+        CF_D8_MT(h.gp.mt[axis], CF_D8Z)
+#undef CF_D8Z
+        return;
+    }
+    const dim3 grid((unsigned)nb);
+#define CF_D8F(MT_)                                                                                       \
+    if (axis == 2) hipLaunchKernelGGL((k_g_dft8_fwd<MT_, false>), grid, dim3(512), 0, h.stream, d, twist, tq); \
+    else hipLaunchKernelGGL((k_g_dft8_fwd<MT_, true>), grid, dim3(512), 0, h.stream, d, twist, tq)
+    CF_D8_MT(h.gp.mt[axis], CF_D8F)
+#undef CF_D8F
+}
+
+static void d8_inv(Handle& h, int axis, const void* in, void* out) {
+    Dft8 d = d8_stage(h, axis);
+    d.in = in; d.out = out;
+    if (axis == 0) d.xmode = 0;   // synthesis along x: every plane is written (inputs are complete)
+    const size_t lds = (size_t)(kZIR * d.Q * 4 + 8 * d.Q) * sizeof(double2);
+    if (axis == 2 && lds <= 64 * 1024) {   // grid rows: the row kernel (2 waves, each half of b)
+        const double2* tw0 = h.g_tw8[axis];
+        const double2* tq0 = tw0 + 8 * d.Q;
+        const dim3 g((unsigned)nblk(d.nseq, kZIR));
+#define CF_D8ZI(MT_) hipLaunchKernelGGL((k_g_dft8_zinv<MT_, 2>), g, dim3(128), lds, h.stream, d, tw0, tq0)
+        CF_D8_MT(h.gp.mt[axis], CF_D8ZI)
+#undef CF_D8ZI
+        return;
+    }
+    const int nb = nblk(d.nseq, kD8Seq), nchunks = (d.Q + kD8BC - 1) / kD8BC;
+    const dim3 grid((unsigned)nb, (unsigned)std::max(1, std::min(nchunks, 1024 / nb)));
+    const double2* twist = h.g_tw8[axis];
+    const double2* tq = twist + 8 * d.Q;
+    if (axis == 2) {
+#define CF_D8I(MT_) hipLaunchKernelGGL((k_g_dft8_inv<MT_, true>), grid, dim3(512), 0, h.stream, d, twist, tq)
+        CF_D8_MT(h.gp.mt[axis], CF_D8I)
+#undef CF_D8I
+    } else {
+#define CF_D8I(MT_) hipLaunchKernelGGL((k_g_dft8_inv<MT_, false>), grid, dim3(512), 0, h.stream, d, twist, tq)
+        CF_D8_MT(h.gp.mt[axis], CF_D8I)
+#undef CF_D8I
+    }
+}
+
 void launch_grid_dft_fwd(Handle& h) {
     const GridPlan& p = h.gp;
+    if (p.dft8) {
+        d8_fwd(h, 2, h.g_grid, h.g_t1);
+        d8_fwd(h, 1, h.g_t1, h.g_t2);
+        d8_fwd(h, 0, h.g_t2, h.g_b);
+        return;
+    }
     const int ngx = p.ng[0], ngy = p.ng[1], ngz = p.ng[2], KZ = p.KZ, NY = p.NY, NX = p.NX;
     const long NYKZ = (long)NY * KZ;
     const double2* tzh = h.g_tw[2] + (size_t)(KZ - 1) * ngz;   // e^{i th nz z}, nz >= 0: tzh[nz * ngz + z]
@@ -995,6 +1508,12 @@ void launch_grid_coeffs(Handle& h, int include_energy) {
 
 void launch_grid_dft_inv(Handle& h) {
     const GridPlan& p = h.gp;
+    if (p.dft8) {
+        d8_inv(h, 0, h.g_b, h.g_t2);
+        d8_inv(h, 1, h.g_t2, h.g_t1);
+        d8_inv(h, 2, h.g_t1, h.g_grid);
+        return;
+    }
     const int ngx = p.ng[0], ngy = p.ng[1], ngz = p.ng[2], KZ = p.KZ, NY = p.NY, NX = p.NX;
     const long NYKZ = (long)NY * KZ;
     const double2* tzh = h.g_tw[2] + (size_t)(KZ - 1) * ngz;

@@ -195,3 +195,47 @@ def test_grid_options_validation():
         HipCalcCoulForceKernel(kspace_algo=GRID, grid_width=3).initialize(system, force)
     with pytest.raises(ChargeFluxError):
         HipCalcCoulForceKernel(kspace_algo=7).initialize(system, force)
+
+
+def _with_dft8(flag, system, force, **kw):
+    # CF_DFT8 is read when the handle is created (grid plan): "0" selects the GEMM stages
+    import os
+    old = os.environ.get("CF_DFT8")
+    os.environ["CF_DFT8"] = flag
+    try:
+        return HipCalcCoulForceKernel(kspace_algo=GRID, **kw).initialize(system, force)
+    finally:
+        if old is None:
+            del os.environ["CF_DFT8"]
+        else:
+            os.environ["CF_DFT8"] = old
+
+
+@pytest.mark.parametrize("case", ["C2", "noncubic", "odd_kmax_12k", "C3"])
+def test_grid_dft8_matches_gemm_stages(case):
+    # the factorized DFT stages (ng = 8Q: 8-point DFTs + Q-term sums per mode)
+    # evaluate the same pruned sums as the fp64-MFMA GEMM stages; only the summation order
+    # differs: energy, dE/dq and forces equal to <= 1e-12 relative
+    if case == "C2":
+        system, force, pos, box = ts.make("C2")
+    elif case == "C3":
+        system, force, pos, box = ts.make("C3")
+    elif case == "noncubic":
+        system, force, pos, box = ts.water_box(400, cutoff=0.7, ewald_tol=1e-4)
+        box = box.copy()
+        box[0, 0] *= 1.3
+        box[2, 2] *= 0.95
+        system.setDefaultPeriodicBoxVectors(*box)
+    else:
+        system, force, pos, box = ts.water_box(4000, cutoff=1.0, ewald_tol=1e-4)
+    out = []
+    for flag in ("0", "1"):
+        k = _with_dft8(flag, system, force)
+        e, f = k.execute_host(pos, box)
+        out.append((e, f, k.dedq(), k.energy_terms()))
+        k.destroy()
+    (e0, f0, d0, t0), (e1, f1, d1, t1) = out
+    scale = sum(abs(t) for t in t0)
+    assert abs(e1 - e0) <= 1e-12 * scale, (e0, e1)
+    assert np.abs(f1 - f0).max() <= 1e-12 * np.abs(f0).max(), np.abs(f1 - f0).max()
+    assert np.abs(d1 - d0).max() <= 1e-12 * np.abs(d0).max(), np.abs(d1 - d0).max()
