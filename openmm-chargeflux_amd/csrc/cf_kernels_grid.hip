@@ -640,7 +640,7 @@ struct Dft8 {
     int W, ngx;
 };
 
-constexpr int kD8Seq = 64, kD8BC = 8, kD8SP = kD8Seq + 1;
+constexpr int kD8Seq = 64, kD8BC = 8;
 constexpr int kDft8Mt[] = {4, 8, 9, 16, 17};   // class-size paddings instantiated (CF_D8_MT)
 
 __device__ __forceinline__ v2d mul_i(v2d v) { return v2d{-v.y, v.x}; }
@@ -668,26 +668,29 @@ __device__ __forceinline__ void cmac(v2d& acc, v2d y, double2 t) {
     acc.y = fma(y.y, t.x, acc.y);
 }
 
-__device__ __forceinline__ bool d8_block_outside(const Dft8& d, int s0) {
-    return d.xmode == 1 && d.xr &&
-           !x_range_in_slab(s0 / d.xdiv, min(s0 + kD8Seq - 1, d.nseq - 1) / d.xdiv, d.xr, d.W, d.ngx);
-}
-
 // analysis (CIN: complex input; else real input, classes r > 4 from conj Y[b][8 - r]).
-// 8 waves: wave r owns residue class r of the block's 64 sequences.  Each thread does one
-// (sequence, b) 8-point DFT per chunk; the next chunk's 8 inputs are loaded into registers
-// before the current chunk's class sums, so the global latency overlaps the FMAs.
-template <int MT, bool CIN>
-__global__ void __launch_bounds__(512) k_g_dft8_fwd(Dft8 d, const double2* __restrict__ twist,
-                                                    const double2* __restrict__ tq) {
-    constexpr int NR = CIN ? 8 : 5;
-    __shared__ v2d sY[kD8BC * NR * kD8SP];
-    const int s0 = blockIdx.x * kD8Seq;
-    if (d8_block_outside(d, s0)) return;
-    const int tid = threadIdx.x, lane = tid & 63, r = wave_id();
+// A block owns SEQ sequences (64, or 16 for the stages with few sequences, so the grid still
+// fills the chip) and 8 SEQ threads: lane = (sequence, class), 64 / SEQ classes per wave.  Each
+// thread does one (sequence, b) 8-point DFT per chunk; the next chunk's 8 inputs are loaded
+// into registers before the current chunk's class sums, so the global latency overlaps the
+// FMAs.  The twist table (class-dependent) is read from LDS, the [Q][mt] rows as scalar loads.
+template <int MT, bool CIN, int SEQ>
+__global__ void __launch_bounds__(8 * SEQ) k_g_dft8_fwd(Dft8 d, const double2* __restrict__ twist,
+                                                        const double2* __restrict__ tq) {
+    constexpr int NR = CIN ? 8 : 5, SP = SEQ + 1, NT = 8 * SEQ;
+    extern __shared__ v2d sm8[];
+    v2d* sY = sm8;                       // [kD8BC][NR][SP]
+    v2d* stw = sm8 + kD8BC * NR * SP;    // [8][Q]
+    const int s0 = blockIdx.x * SEQ;
+    if (d.xmode == 1 && d.xr &&
+        !x_range_in_slab(s0 / d.xdiv, min(s0 + SEQ - 1, d.nseq - 1) / d.xdiv, d.xr, d.W, d.ngx))
+        return;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int sq = lane % SEQ, r = wave_id() * (64 / SEQ) + lane / SEQ;
+    for (int e = tid; e < 8 * d.Q; e += NT) stw[e] = reinterpret_cast<const v2d*>(twist)[e];
     // this thread's step-1 item: real input rows are contiguous along n (8 lanes per sequence
     // over b); complex inputs are contiguous along the sequence index (lanes over sequences)
-    const int sl = CIN ? (tid & 63) : (tid >> 3), bl = CIN ? (tid >> 6) : (tid & 7);
+    const int sl = CIN ? (tid % SEQ) : (tid >> 3), bl = CIN ? (tid / SEQ) : (tid & 7);
     const int si = s0 + sl;
     const bool sok = si < d.nseq;
     const long ibase = sok ? (long)(si / d.sdiv) * d.s1 + (long)(si % d.sdiv) * d.s0 : 0;
@@ -719,24 +722,25 @@ __global__ void __launch_bounds__(512) k_g_dft8_fwd(Dft8 d, const double2* __res
             v2d y[8];
             dft8(xn, y);
 #pragma unroll
-            for (int q = 0; q < NR; q++) sY[(bl * NR + q) * kD8SP + sl] = y[q];
+            for (int q = 0; q < NR; q++) sY[(bl * NR + q) * SP + sl] = y[q];
         }
         __syncthreads();
         if (bc + kD8BC < d.Q) load(bc + kD8BC);
-        const double2* twr = twist + (long)r * d.Q + bc;
+        const v2d* twr = stw + r * d.Q + bc;
         const double2* tqb = tq + (long)bc * MT;
 #pragma unroll 2
         for (int b = 0; b < nb; b++) {
-            v2d y = sY[(b * NR + rr) * kD8SP + lane];
+            v2d y = sY[(b * NR + rr) * SP + sq];
             if (cj) y.y = -y.y;
+            const v2d tw = twr[b];
             v2d yt = v2d{0.0, 0.0};
-            cmac(yt, y, twr[b]);   // w^{b k_r} Y[b][r]
+            cmac(yt, y, make_double2(tw.x, tw.y));   // w^{b k_r} Y[b][r]
 #pragma unroll
             for (int t = 0; t < MT; t++) cmac(acc[t], yt, tqb[b * MT + t]);
         }
         __syncthreads();
     }
-    const int s = s0 + lane;
+    const int s = s0 + sq;
     if (s >= d.nseq) return;
     const long base = (long)(s / d.sdiv) * d.c1 + (long)(s % d.sdiv) * d.c0;
     const int cnt = d.rc[r], j0 = d.rj[r];
@@ -933,18 +937,26 @@ __global__ void __launch_bounds__(64 * NB) k_g_dft8_zinv(Dft8 d, const double2* 
     }
 }
 
-// synthesis (ROUT: keep the real part, written as doubles).  8 waves: wave r holds the modes
-// of class r of the block's 64 sequences (lane = sequence) and forms Z[b][r] for the chunk;
-// then each thread turns one (sequence, b) into the outputs n = Qa + b.  b chunks are
-// independent, so they are also dealt over gridDim.y blocks of the same sequences.
-template <int MT, bool ROUT>
-__global__ void __launch_bounds__(512) k_g_dft8_inv(Dft8 d, const double2* __restrict__ twist,
-                                                    const double2* __restrict__ tq) {
-    __shared__ v2d sZ[kD8BC * 8 * kD8SP];
-    const int s0 = blockIdx.x * kD8Seq;
-    if (d8_block_outside(d, s0)) return;
-    const int tid = threadIdx.x, lane = tid & 63, r = wave_id();
-    const int s = s0 + lane;
+// synthesis (ROUT: keep the real part, written as doubles).  A block owns SEQ sequences and
+// 8 SEQ threads, lane = (sequence, class) as in the analysis: each lane holds the modes of its
+// class and forms Z[b][r] for the chunk; then each thread turns one (sequence, b) into the
+// outputs n = Qa + b.  b chunks are independent, so they are also dealt over gridDim.y blocks
+// of the same sequences.
+template <int MT, bool ROUT, int SEQ>
+__global__ void __launch_bounds__(8 * SEQ) k_g_dft8_inv(Dft8 d, const double2* __restrict__ twist,
+                                                        const double2* __restrict__ tq) {
+    constexpr int SP = SEQ + 1, NT = 8 * SEQ;
+    extern __shared__ v2d sm8[];
+    v2d* sZ = sm8;                      // [kD8BC][8][SP]
+    v2d* stw = sm8 + kD8BC * 8 * SP;    // [8][Q]
+    const int s0 = blockIdx.x * SEQ;
+    if (d.xmode == 1 && d.xr &&
+        !x_range_in_slab(s0 / d.xdiv, min(s0 + SEQ - 1, d.nseq - 1) / d.xdiv, d.xr, d.W, d.ngx))
+        return;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int sq = lane % SEQ, r = wave_id() * (64 / SEQ) + lane / SEQ;
+    for (int e = tid; e < 8 * d.Q; e += NT) stw[e] = reinterpret_cast<const v2d*>(twist)[e];
+    const int s = s0 + sq;
     v2d cv[MT];
     {
         const bool ok = s < d.nseq;
@@ -957,26 +969,28 @@ __global__ void __launch_bounds__(512) k_g_dft8_inv(Dft8 d, const double2* __res
             cv[t] = okt ? v : v2d{0.0, 0.0};
         }
     }
-    const int sl = ROUT ? (tid >> 3) : (tid & 63), bl = ROUT ? (tid & 7) : (tid >> 6);
+    const int sl = ROUT ? (tid >> 3) : (tid % SEQ), bl = ROUT ? (tid & 7) : (tid / SEQ);
     const int ss = s0 + sl;
     const long obase = ss < d.nseq ? (long)(ss / d.sdiv) * d.s1 + (long)(ss % d.sdiv) * d.s0 : 0;
+    __syncthreads();
     for (int bc = kD8BC * blockIdx.y; bc < d.Q; bc += kD8BC * gridDim.y) {
         const int nb = min(kD8BC, d.Q - bc);
-        const double2* twr = twist + (long)r * d.Q + bc;
+        const v2d* twr = stw + r * d.Q + bc;
         const double2* tqb = tq + (long)bc * MT;
 #pragma unroll 2
         for (int b = 0; b < nb; b++) {
             v2d z = v2d{0.0, 0.0}, zt = v2d{0.0, 0.0};
 #pragma unroll
             for (int t = 0; t < MT; t++) cmac(z, cv[t], tqb[b * MT + t]);
-            cmac(zt, z, twr[b]);   // w^{b k_r} sum_t c_t w_Q^{b t}
-            sZ[(b * 8 + r) * kD8SP + lane] = zt;
+            const v2d tw = twr[b];
+            cmac(zt, z, make_double2(tw.x, tw.y));   // w^{b k_r} sum_t c_t w_Q^{b t}
+            sZ[(b * 8 + r) * SP + sq] = zt;
         }
         __syncthreads();
         if (ss < d.nseq && bl < nb) {
             v2d z[8], x[8];
 #pragma unroll
-            for (int q = 0; q < 8; q++) z[q] = sZ[(bl * 8 + q) * kD8SP + sl];
+            for (int q = 0; q < 8; q++) z[q] = sZ[(bl * 8 + q) * SP + sl];
             dft8(z, x);
 #pragma unroll
             for (int a = 0; a < 8; a++) {
@@ -1432,12 +1446,21 @@ static void d8_fwd(Handle& h, int axis, const void* in, void* out) {
 #undef CF_D8Z
         return;
     }
-    const dim3 grid((unsigned)nb);
-#define CF_D8F(MT_)                                                                                       \
-    if (axis == 2) hipLaunchKernelGGL((k_g_dft8_fwd<MT_, false>), grid, dim3(512), 0, h.stream, d, twist, tq); \
-    else hipLaunchKernelGGL((k_g_dft8_fwd<MT_, true>), grid, dim3(512), 0, h.stream, d, twist, tq)
+    // blocks of 16 sequences x 8 classes for the mid-sized y and x stages (C5: 44.9 -> 35.2 us
+    // per stage); at C3's sizes (< 128 blocks of 64) and for the synthesis the 64-sequence
+    // blocks measured faster (10.0 against 10.4 us, 6.8 against 7.7 us)
+    const bool small = nb >= 128 && nb < 2048;
+    const int seq = small ? 16 : 64;
+    const dim3 grid((unsigned)nblk(d.nseq, seq));
+    const size_t lds2 = (size_t)(kD8BC * (axis == 2 ? 5 : 8) * (seq + 1) + 8 * d.Q) * sizeof(double2);
+#define CF_D8F_(MT_, CIN_, SEQ_) \
+    hipLaunchKernelGGL((k_g_dft8_fwd<MT_, CIN_, SEQ_>), grid, dim3(8 * SEQ_), lds2, h.stream, d, twist, tq)
+#define CF_D8F(MT_)                                         \
+    if (axis == 2) { if (small) CF_D8F_(MT_, false, 16); else CF_D8F_(MT_, false, 64); } \
+    else { if (small) CF_D8F_(MT_, true, 16); else CF_D8F_(MT_, true, 64); }
     CF_D8_MT(h.gp.mt[axis], CF_D8F)
 #undef CF_D8F
+#undef CF_D8F_
 }
 
 static void d8_inv(Handle& h, int axis, const void* in, void* out) {
@@ -1454,19 +1477,21 @@ static void d8_inv(Handle& h, int axis, const void* in, void* out) {
 #undef CF_D8ZI
         return;
     }
-    const int nb = nblk(d.nseq, kD8Seq), nchunks = (d.Q + kD8BC - 1) / kD8BC;
-    const dim3 grid((unsigned)nb, (unsigned)std::max(1, std::min(nchunks, 1024 / nb)));
+    const bool small = false;
+    const int seq = small ? 16 : 64;
+    const int nb = nblk(d.nseq, seq), nchunks = (d.Q + kD8BC - 1) / kD8BC;
+    const dim3 grid((unsigned)nb, (unsigned)std::max(1, std::min(nchunks, 2048 / nb)));
     const double2* twist = h.g_tw8[axis];
     const double2* tq = twist + 8 * d.Q;
-    if (axis == 2) {
-#define CF_D8I(MT_) hipLaunchKernelGGL((k_g_dft8_inv<MT_, true>), grid, dim3(512), 0, h.stream, d, twist, tq)
-        CF_D8_MT(h.gp.mt[axis], CF_D8I)
+    const size_t lds2 = (size_t)(kD8BC * 8 * (seq + 1) + 8 * d.Q) * sizeof(double2);
+#define CF_D8I_(MT_, ROUT_, SEQ_) \
+    hipLaunchKernelGGL((k_g_dft8_inv<MT_, ROUT_, SEQ_>), grid, dim3(8 * SEQ_), lds2, h.stream, d, twist, tq)
+#define CF_D8I(MT_)                                        \
+    if (axis == 2) { if (small) CF_D8I_(MT_, true, 16); else CF_D8I_(MT_, true, 64); } \
+    else { if (small) CF_D8I_(MT_, false, 16); else CF_D8I_(MT_, false, 64); }
+    CF_D8_MT(h.gp.mt[axis], CF_D8I)
 #undef CF_D8I
-    } else {
-#define CF_D8I(MT_) hipLaunchKernelGGL((k_g_dft8_inv<MT_, false>), grid, dim3(512), 0, h.stream, d, twist, tq)
-        CF_D8_MT(h.gp.mt[axis], CF_D8I)
-#undef CF_D8I
-    }
+#undef CF_D8I_
 }
 
 void launch_grid_dft_fwd(Handle& h) {

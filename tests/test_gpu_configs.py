@@ -217,3 +217,16 @@ def test_c5_mixed_four_rank_split(c5):
     assert abs(e4 - e1) <= 1e-10 * np.abs(t1).sum()
     # fp32 per-lane force sums: the list kind and a rank's lanes-per-atom choice change their rounding
     assert np.abs(f4 - f1).max() <= 1e-6 * np.abs(f1).max()
+
+
+def test_c5_dft8_matches_gemm_stages(c5, monkeypatch):
+    """C5 (kmax 65, ng 264 = 8 x 33): the factorized DFT stages (default) against the fp64-MFMA
+    GEMM stages (CF_DFT8=0, read when the handle is created) on the same positions, fp64 W = 14:
+    only the summation order differs -> energy and forces equal to <= 1e-12 relative."""
+    system, force, pos, box = c5
+    monkeypatch.setenv("CF_DFT8", "0")
+    eg, fg, tg = _c5_eval(system, force, pos, box, "double", 14)
+    monkeypatch.setenv("CF_DFT8", "1")
+    e8, f8, t8 = _c5_eval(system, force, pos, box, "double", 14)
+    assert abs(e8 - eg) <= 1e-12 * np.abs(tg).sum(), (e8, eg)
+    assert np.abs(f8 - fg).max() <= 1e-12 * np.abs(fg).max(), np.abs(f8 - fg).max()
