@@ -57,6 +57,7 @@ class MDHarness:
         vp, d, i = C.c_void_p, C.c_double, C.c_int
         L.md_kick_drift.argtypes = [i, i, d, vp, vp, vp, vp, vp]
         L.md_restrain_kick.argtypes = [i, i, i, d, d, d, d, d, vp, vp, vp, vp, vp]
+        L.md_restrain_kick_drift.argtypes = [i, i, i, d, d, d, d, d, i, vp, vp, vp, vp, vp]
         self.L, self.C = L, C
         self.nw, self.lo, self.hi, self.dt = n_waters, lo, hi, dt
         self.inv_m = inv_mass
@@ -65,6 +66,13 @@ class MDHarness:
     def kick_drift(self, pos, vel, frc):   # also zeroes frc[lo:hi] (its last reader in the step)
         rc = self.L.md_kick_drift(self.lo, self.hi, self.dt, pos.data_ptr(), vel.data_ptr(), frc.data_ptr(),
                                   self.inv_m.data_ptr(), self.stream)
+        assert rc == 0
+
+    def restrain_kick_drift(self, pos, vel, frc, first):
+        # f += restraints ; v += dt/2 f/m (not on the first step) ; v += dt/2 f/m ; x += dt v ; f = 0
+        rc = self.L.md_restrain_kick_drift(self.lo, self.hi, self.nw, K_OH, R_OH0, K_HH, R_HH0, self.dt, int(first),
+                                           pos.data_ptr(), vel.data_ptr(), frc.data_ptr(), self.inv_m.data_ptr(),
+                                           self.stream)
         assert rc == 0
 
     def restrain_kick(self, pos, vel, frc, kick=True):
@@ -222,11 +230,14 @@ def main():
     md = MDHarness(n_waters, lo, hi, dt, (1.0 / masses).contiguous(), torch.cuda.current_stream(dev).cuda_stream)
     frc.zero_()
     energy = kern.execute(pos, box, frc, include_energy=True)
-    md.restrain_kick(pos, vel, frc, kick=False)
     ev = []
+    first = [True]
 
     def step(record):
-        md.kick_drift(pos, vel, frc)            # v += dt/2 f/m ; x += dt v ; f = 0  (owned atoms)
+        # the previous step's restraints and second half kick fused with this step's first half
+        # kick and drift (one harness launch per step; f = 0 afterwards for the force evaluation)
+        md.restrain_kick_drift(pos, vel, frc, first[0])
+        first[0] = False
         kern.replicate_positions(pos)
         if record:
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -235,7 +246,6 @@ def main():
         if record:
             b.record()
             ev.append((a, b))
-        md.restrain_kick(pos, vel, frc)         # f += restraints ; v += dt/2 f/m
         return e
 
     for _ in range(args.warmup):

@@ -6,6 +6,8 @@
 // Step:  md_kick_drift   v += dt/2 f/m ; x += dt v            (owned atoms)
 //        <positions replicated, forces zeroed, CoulForce adds its forces>
 //        md_restrain_kick f += restraint(x) ; v += dt/2 f/m   (owned atoms)
+// bench.py fuses the last kernel of a step with the first of the next (md_restrain_kick_drift):
+// one harness launch per step.
 // Waters are atoms 3w, 3w+1, 3w+2 (O, H, H) for w < n_waters; every atom recomputes the
 // three bonds of its own water, so there are no atomics and the result is deterministic.
 #include <hip/hip_runtime.h>
@@ -67,6 +69,50 @@ __global__ void __launch_bounds__(256) k_restrain_kick(int lo, int hi, int n_wat
     }
 }
 
+// The end of step n and the start of step n + 1 in one launch: f += restraint(x) ; v += dt/2 f/m
+// (the second half kick; skipped on the first call, where x, v are the initial state) ; v += dt/2
+// f/m ; x += dt v ; f = 0.  One thread per water (its three atoms: every restraint is evaluated
+// from positions no thread has drifted yet) or per other atom.
+__global__ void __launch_bounds__(256) k_restrain_kick_drift(int lo, int hi, int n_waters, double k_oh, double r_oh,
+                                                             double k_hh, double r_hh, double dt, int first,
+                                                             double* __restrict__ x, double* __restrict__ v,
+                                                             double* __restrict__ f,
+                                                             const double* __restrict__ inv_m) {
+    const int wend = min(hi, 3 * n_waters);                 // owned water atoms [lo, wend): whole waters
+    const int nwu = wend > lo ? (wend - lo) / 3 : 0;
+    const int u = blockIdx.x * blockDim.x + threadIdx.x;
+    int a0, na;
+    if (u < nwu) { a0 = lo + 3 * u; na = 3; }
+    else { a0 = max(lo, wend) + (u - nwu); na = 1; if (a0 >= hi) return; }
+    double fr[3][3] = {};
+    if (na == 3) {
+        double g1[3], g2[3], g3[3];
+        bond(x, a0, a0 + 1, k_oh, r_oh, g1);
+        bond(x, a0, a0 + 2, k_oh, r_oh, g2);
+        bond(x, a0 + 1, a0 + 2, k_hh, r_hh, g3);
+#pragma unroll
+        for (int d = 0; d < 3; d++) {
+            fr[0][d] = g1[d] + g2[d];
+            fr[1][d] = -g1[d] + g3[d];
+            fr[2][d] = -g2[d] - g3[d];
+        }
+    }
+    for (int q = 0; q < na; q++) {
+        const int i = a0 + q;
+        const double h = 0.5 * dt * inv_m[i];
+#pragma unroll
+        for (int d = 0; d < 3; d++) {
+            const double fi = f[3 * i + d] + fr[q][d];
+            double vv = v[3 * i + d];
+            if (!first) vv += h * fi;   // second half kick of the previous step
+            vv += h * fi;               // first half kick of this step
+            v[3 * i + d] = vv;
+            x[3 * i + d] += dt * vv;
+            f[3 * i + d] = 0.0;
+        }
+    }
+}
+
 inline int nblk(int n) { return (n + 255) / 256; }
 
 }  // namespace
@@ -84,5 +130,14 @@ MD_EXPORT int md_restrain_kick(int lo, int hi, int n_waters, double k_oh, double
     if (hi <= lo) return 0;
     hipLaunchKernelGGL(k_restrain_kick, dim3(nblk(hi - lo)), dim3(256), 0, (hipStream_t)stream, lo, hi, n_waters,
                        k_oh, r_oh, k_hh, r_hh, dt, x, v, f, inv_m);
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+MD_EXPORT int md_restrain_kick_drift(int lo, int hi, int n_waters, double k_oh, double r_oh, double k_hh, double r_hh,
+                                     double dt, int first, double* x, double* v, double* f, const double* inv_m,
+                                     void* stream) {
+    if (hi <= lo) return 0;
+    hipLaunchKernelGGL(k_restrain_kick_drift, dim3(nblk(hi - lo)), dim3(256), 0, (hipStream_t)stream, lo, hi,
+                       n_waters, k_oh, r_oh, k_hh, r_hh, dt, first, x, v, f, inv_m);
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }

@@ -64,3 +64,28 @@ def test_md_harness_matches_torch(lo, hi):
     torch.cuda.synchronize()
     assert torch.allclose(f[lo:hi], fr[lo:hi], rtol=1e-12, atol=1e-9)
     assert torch.allclose(v, vr, rtol=1e-12, atol=1e-12)
+
+
+@pytest.mark.parametrize("lo,hi,first", [(0, 905, False), (300, 609, False), (0, 905, True)])
+def test_md_fused_step_matches_two_kernels(lo, hi, first):
+    # md_restrain_kick_drift (the bench's one launch per step) = restrain_kick then kick_drift
+    # (without the restraint kick on the first step)
+    rng = np.random.default_rng(7)
+    n, nw, dt = 905, 300, 0.001
+    dev = torch.device("cuda", 0)
+    o = rng.uniform(0, 3, size=(nw, 3))
+    x0 = np.concatenate([(o[:, None, :] + rng.normal(scale=0.06, size=(nw, 3, 3))).reshape(-1, 3),
+                         rng.uniform(0, 3, size=(n - 3 * nw, 3))])
+    v0 = rng.normal(size=(n, 3))
+    f0 = rng.normal(size=(n, 3)) * 100
+    inv_m = torch.tensor(1.0 / rng.uniform(1, 16, size=(n, 1)), device=dev)
+    md = bench.MDHarness(nw, lo, hi, dt, inv_m, torch.cuda.current_stream().cuda_stream)
+    xa, va, fa = (torch.tensor(a, device=dev) for a in (x0, v0, f0))
+    md.restrain_kick(xa, va, fa, kick=not first)
+    md.kick_drift(xa, va, fa)
+    xb, vb, fb = (torch.tensor(a, device=dev) for a in (x0, v0, f0))
+    md.restrain_kick_drift(xb, vb, fb, first)
+    torch.cuda.synchronize()
+    assert torch.allclose(xb, xa, rtol=1e-14, atol=1e-15)
+    assert torch.allclose(vb, va, rtol=1e-13, atol=1e-13)
+    assert torch.equal(fb, fa)   # owned rows zeroed, the rest untouched
