@@ -143,7 +143,9 @@ CF_EXPORT int cf_get_neighbor_stats(const cf_handle* h, int64_t* builds, int64_t
  * Replaces ReferenceCalcCoulForceKernel::execute (ReferenceCoulKernels.cpp:424-636).
  * Device-resident, asynchronous on the handle's stream:
  *   pos_dev    [N*3] fp64 positions (nm), AoS x,y,z, DEVICE memory
- *   box9       host array, current periodic box vectors (rows); ignored without PBC
+ *   box9       host array, current periodic box vectors (rows) in OpenMM's reduced form
+ *              a = (ax,0,0), b = (bx,by,0), c = (cx,cy,cz), |bx|,|cx| <= ax/2, |cy| <= by/2
+ *              (triclinic boxes take the all-pairs neighbour list); ignored without PBC
  *   forces_dev [N*3] fp64 DEVICE buffer; forces are ADDED (+=) like the reference
  *              (ReferenceCoulKernels.cpp:426, 455, 585, 630).  Only owned atoms when world_size>1.
  *   energy_dev [1] fp64 DEVICE scalar, OVERWRITTEN with the (partial, per rank) energy.

@@ -129,10 +129,16 @@ double ewald_param_value(int kmax, double width, double alpha) {
     return 0.05 * std::sqrt(width * alpha) * kmax * std::exp(-t * t);
 }
 
-void check_box_orthorhombic(const double* b, const char* what) {
-    if (b[1] != 0 || b[2] != 0 || b[3] != 0 || b[5] != 0 || b[6] != 0 || b[7] != 0)
-        fail(CF_ERR_INVALID, std::string(what) + ": only orthorhombic periodic boxes are supported");
+// OpenMM's reduced box form (System::setDefaultPeriodicBoxVectors requires it): a = (ax,0,0),
+// b = (bx,by,0), c = (cx,cy,cz), |bx|, |cx| <= ax/2, |cy| <= by/2.  The reference reads the
+// diagonals for the reciprocal part (RCK:513-517) and the box vectors for the minimum image
+// (getDeltaRPeriodic, RCK:567, 601).
+void check_box_reduced(const double* b, const char* what) {
+    if (b[1] != 0 || b[2] != 0 || b[5] != 0)
+        fail(CF_ERR_INVALID, std::string(what) + ": box vectors must be in OpenMM's reduced form (a = (ax,0,0), b = (bx,by,0))");
     if (!(b[0] > 0 && b[4] > 0 && b[8] > 0)) fail(CF_ERR_INVALID, std::string(what) + ": box lengths must be > 0");
+    if (std::fabs(b[3]) > 0.5 * b[0] || std::fabs(b[6]) > 0.5 * b[0] || std::fabs(b[7]) > 0.5 * b[4])
+        fail(CF_ERR_INVALID, std::string(what) + ": box vectors must be in OpenMM's reduced form (|bx|, |cx| <= ax/2, |cy| <= by/2)");
 }
 
 int find_root(std::vector<int>& p, int x) {
@@ -146,6 +152,9 @@ void set_cells(cf_handle* H, const double L[3]) {
     for (int d = 0; d < 3; d++) {
         double v = std::floor(L[d] / (h.cutoff + h.list_skin));
         nc[d] = (int)std::max(1.0, std::min(v, 1024.0));
+        // reduced triclinic box: one cell, i.e. the all-pairs list with the box-vector minimum
+        // image (correct for any reduced box; O(N^2) per build -- the fast paths are orthorhombic)
+        if (h.tric) nc[d] = 1;
     }
     int64_t ncell = (int64_t)nc[0] * nc[1] * nc[2];
     if (ncell > h.ncell_alloc) {
@@ -184,12 +193,14 @@ void set_box(cf_handle* H, const double* box9) {
     cf::Handle& h = H->h;
     if (!h.pbc) { h.box_L[0] = h.box_L[1] = h.box_L[2] = 1.0; return; }
     if (!box9) fail(CF_ERR_INVALID, "periodic box required");
-    check_box_orthorhombic(box9, "current box");
+    check_box_reduced(box9, "current box");
     double L[3] = {box9[0], box9[4], box9[8]};
     for (int d = 0; d < 3; d++)
         if (h.cutoff > 0.5 * L[d] * (1 + 1e-12))
             fail(CF_ERR_INVALID, "cutoff exceeds half the periodic box (minimum image would be ambiguous)");
     h.box_L[0] = L[0]; h.box_L[1] = L[1]; h.box_L[2] = L[2];
+    h.box_t[0] = box9[3]; h.box_t[1] = box9[6]; h.box_t[2] = box9[7];
+    h.tric = box9[3] != 0 || box9[6] != 0 || box9[7] != 0;
 }
 
 // Atom decomposition: contiguous owned ranges [lo,hi), cut only where no molecule
@@ -475,7 +486,7 @@ CF_EXPORT int cf_create(const cf_params* p, const cf_options* opt, cf_handle** o
             h.tol = p->ewald_tol;
             if (!(h.cutoff > 0)) fail(CF_ERR_INVALID, "cutoff must be > 0");
             if (!(h.tol > 0 && h.tol < 0.5)) fail(CF_ERR_INVALID, "ewald tolerance must be in (0, 0.5)");
-            check_box_orthorhombic(p->default_box, "default box");
+            check_box_reduced(p->default_box, "default box");
             double L[3] = {p->default_box[0], p->default_box[4], p->default_box[8]};
             for (int d = 0; d < 3; d++)
                 if (h.cutoff > 0.5 * L[d] * (1 + 1e-12))
@@ -525,6 +536,7 @@ CF_EXPORT int cf_create(const cf_params* p, const cf_options* opt, cf_handle** o
         int nown = h.hi - h.lo;
         if (h.pbc) {
             const cf::KGeom& g = h.kg;
+            h.tric = p->default_box[3] != 0 || p->default_box[6] != 0 || p->default_box[7] != 0;
             set_cells(H, std::vector<double>{p->default_box[0], p->default_box[4], p->default_box[8]}.data());
             h.erfc_tab = dupload(H, cf::erfc_table(h.alpha * h.cutoff * (1.0 + 1e-9), &h.erfc_scale, &h.erfc_m));
             if (h.mixed) {
@@ -781,7 +793,8 @@ CF_EXPORT int cf_compute_begin(cf_handle* H, const double* pos_dev, const double
         const double Lmin = std::min(h.box_L[0], std::min(h.box_L[1], h.box_L[2]));
         const double s_call = h.skin > 0 ? std::max(0.0, std::min(h.skin, 0.5 * Lmin - h.cutoff)) : 0.0;
         const bool reusable = h.pbc && h.skin > 0 && h.list_valid && s_call == h.list_skin &&
-                              h.list_L[0] == h.box_L[0] && h.list_L[1] == h.box_L[1] && h.list_L[2] == h.box_L[2];
+                              h.list_L[0] == h.box_L[0] && h.list_L[1] == h.box_L[1] && h.list_L[2] == h.box_L[2] &&
+                              h.list_T[0] == h.box_t[0] && h.list_T[1] == h.box_t[1] && h.list_T[2] == h.box_t[2];
         { Timed t(H, PH_FLUX); cf::launch_flux_terms(h, pos_dev); }
         { Timed t(H, PH_PREP); cf::launch_atoms_prep(h, pos_dev, reusable); }
         if (h.pbc) {
@@ -793,6 +806,7 @@ CF_EXPORT int cf_compute_begin(cf_handle* H, const double* pos_dev, const double
                     cf::launch_force_rebuild(h);
                     h.list_valid = h.skin > 0;
                     std::copy(h.box_L, h.box_L + 3, h.list_L);
+                    std::copy(h.box_t, h.box_t + 3, h.list_T);
                 }
                 cf::launch_cell_sort(h, pos_dev);
             }

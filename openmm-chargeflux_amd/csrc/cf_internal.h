@@ -137,6 +137,7 @@ struct Handle {
     double skin = 0.0;          // requested skin (nm); 0 = rebuild on every evaluation
     double list_skin = 0.0;     // skin the current list was built with
     double list_L[3] = {0, 0, 0};
+    double list_T[3] = {0, 0, 0};
     bool list_valid = false;
     double* pos_ref = nullptr;  // [N*3] positions at the last build (skin > 0)
     int* skin_flag = nullptr;   // [1] device: rebuild this evaluation (host-forced or moved > skin/2)
@@ -207,6 +208,8 @@ struct Handle {
     int pending_flags = -1;     // flags of a begun evaluation
     bool direct_done = false;   // cf_compute_direct already ran for the begun evaluation
     double box_L[3] = {0, 0, 0};
+    double box_t[3] = {0, 0, 0};   // reduced triclinic box off-diagonals (bx, cx, cy); 0 = orthorhombic
+    bool tric = false;             // any off-diagonal nonzero: all-pairs neighbour list
 };
 
 // ---- launchers (cf_kernels_*.hip) ------------------------------------------------

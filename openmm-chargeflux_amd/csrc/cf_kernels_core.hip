@@ -10,14 +10,25 @@
 
 namespace cf {
 
-// OpenMM ReferenceForce::getDeltaR[Periodic]: d = J - I, minimum image per axis of an
-// orthorhombic box via floor(d/L + 0.5)  (used by RCK:53-55, 567, 601).
-__device__ __forceinline__ double3 delta_r(double3 pi, double3 pj, double3 L, int pbc) {
+// OpenMM ReferenceForce::getDeltaR[Periodic]: d = J - I, minimum image by the box vectors c,
+// b, a in that order via floor(d/L + 0.5) (used by RCK:53-55, 567, 601).  Boxes are in OpenMM's
+// reduced form a = (Lx,0,0), b = (bx,Ly,0), c = (cx,cy,Lz); T = (bx, cx, cy), zero for an
+// orthorhombic box (the per-axis form, the same bits).
+__device__ __forceinline__ double3 delta_r(double3 pi, double3 pj, double3 L, int pbc,
+                                           double3 T = make_double3(0.0, 0.0, 0.0)) {
     double3 d = make_double3(pj.x - pi.x, pj.y - pi.y, pj.z - pi.z);
     if (pbc) {
-        d.z -= L.z * floor(d.z / L.z + 0.5);
-        d.y -= L.y * floor(d.y / L.y + 0.5);
-        d.x -= L.x * floor(d.x / L.x + 0.5);
+        if (T.x != 0.0 || T.y != 0.0 || T.z != 0.0) {
+            const double sc = floor(d.z / L.z + 0.5);
+            d.x -= sc * T.y; d.y -= sc * T.z; d.z -= sc * L.z;
+            const double sb = floor(d.y / L.y + 0.5);
+            d.x -= sb * T.x; d.y -= sb * L.y;
+            d.x -= L.x * floor(d.x / L.x + 0.5);
+        } else {
+            d.z -= L.z * floor(d.z / L.z + 0.5);
+            d.y -= L.y * floor(d.y / L.y + 0.5);
+            d.x -= L.x * floor(d.x / L.x + 0.5);
+        }
     }
     return d;
 }
@@ -40,7 +51,7 @@ __device__ __forceinline__ long dqdx_start(int t, int nb, int na) {
 
 __global__ void __launch_bounds__(256) k_flux_terms(int nterms, int nb, int na, const int4* __restrict__ tidx,
                                                     const double* __restrict__ tpar, const double* __restrict__ pos,
-                                                    double3 L, int pbc, double* __restrict__ dq_slot,
+                                                    double3 L, double3 T, int pbc, double* __restrict__ dq_slot,
                                                     double* __restrict__ dqdx) {
     // the block's dq/dx blocks are staged in LDS and written out as one coalesced run (each
     // lane's 12 or 27 doubles written straight to memory spread every store instruction over
@@ -54,7 +65,7 @@ __global__ void __launch_bounds__(256) k_flux_terms(int nterms, int nb, int na, 
         const double* p = tpar + 5 * t;
         double* o = st + (dqdx_start(t, nb, na) - base);
         if (ti.x == 0) {  // bond p1-p2
-            double3 d = delta_r(ld3(pos, ti.y), ld3(pos, ti.z), L, pbc);
+            double3 d = delta_r(ld3(pos, ti.y), ld3(pos, ti.z), L, pbc, T);
             double r = sqrt(d.x * d.x + d.y * d.y + d.z * d.z);
             double k = p[0], dq = k * (r - p[1]);
             dq_slot[2 * t] = dq;
@@ -66,7 +77,7 @@ __global__ void __launch_bounds__(256) k_flux_terms(int nterms, int nb, int na, 
         } else if (ti.x == 1) {  // angle p1-p2-p3, p2 central
             int a = t - nb;
             double3 x1 = ld3(pos, ti.y), x2 = ld3(pos, ti.z), x3 = ld3(pos, ti.w);
-            double3 d21 = delta_r(x2, x1, L, pbc), d23 = delta_r(x2, x3, L, pbc), d13 = delta_r(x1, x3, L, pbc);
+            double3 d21 = delta_r(x2, x1, L, pbc, T), d23 = delta_r(x2, x3, L, pbc, T), d13 = delta_r(x1, x3, L, pbc, T);
             double r21_2 = d21.x * d21.x + d21.y * d21.y + d21.z * d21.z;
             double r23_2 = d23.x * d23.x + d23.y * d23.y + d23.z * d23.z;
             double r13_2 = d13.x * d13.x + d13.y * d13.y + d13.z * d13.z;
@@ -93,7 +104,7 @@ __global__ void __launch_bounds__(256) k_flux_terms(int nterms, int nb, int na, 
         } else {  // water O,H1,H2
             int w = t - nb - na;
             double3 x1 = ld3(pos, ti.y), x2 = ld3(pos, ti.z), x3 = ld3(pos, ti.w);
-            double3 d12 = delta_r(x1, x2, L, pbc), d13 = delta_r(x1, x3, L, pbc), d23 = delta_r(x2, x3, L, pbc);
+            double3 d12 = delta_r(x1, x2, L, pbc, T), d13 = delta_r(x1, x3, L, pbc, T), d23 = delta_r(x2, x3, L, pbc, T);
             double r12 = sqrt(d12.x * d12.x + d12.y * d12.y + d12.z * d12.z);
             double r13 = sqrt(d13.x * d13.x + d13.y * d13.y + d13.z * d13.z);
             double r23 = sqrt(d23.x * d23.x + d23.y * d23.y + d23.z * d23.z);
@@ -258,13 +269,14 @@ __global__ void __launch_bounds__(256) k_cell_order(int ncell, const int* __rest
 }
 
 // rebuild (flag set): commit the new order (scratch -> live), sorted wrapped (x,y,z,q) +
-// LJ, build positions.  No rebuild: the sorted order and every atom's periodic image are
+// LJ, build positions.  wrap = 0 (reduced triclinic box, all-pairs list): unwrapped coordinates,
+// since a per-axis wrap by a diagonal is not a lattice translation there.  No rebuild: the sorted order and every atom's periodic image are
 // kept from the last build (wrap offsets recomputed from the build positions, so
 // bit-identical to the commit); only coordinates and flux charges are refreshed.
 __global__ void __launch_bounds__(256) k_cell_commit(int n, const int* __restrict__ flag,
                                                      const int* __restrict__ key, const int* __restrict__ idx_new,
                                                      const double* __restrict__ pos, const double* __restrict__ q,
-                                                     const double2* __restrict__ lj, double3 L,
+                                                     const double2* __restrict__ lj, double3 L, int wrap,
                                                      int* __restrict__ key_s, int* __restrict__ idx_s,
                                                      double4* __restrict__ pos4s, double2* __restrict__ ljs,
                                                      const int* __restrict__ atype, int* __restrict__ typ_s,
@@ -277,8 +289,9 @@ __global__ void __launch_bounds__(256) k_cell_commit(int n, const int* __restric
         key_s[s] = key[i];
         idx_s[s] = i;
         double3 x = ld3(pos, i);
-        p4 = make_double4(x.x - floor(x.x / L.x) * L.x, x.y - floor(x.y / L.y) * L.y, x.z - floor(x.z / L.z) * L.z,
-                          q[i]);
+        p4 = wrap ? make_double4(x.x - floor(x.x / L.x) * L.x, x.y - floor(x.y / L.y) * L.y,
+                                 x.z - floor(x.z / L.z) * L.z, q[i])
+                  : make_double4(x.x, x.y, x.z, q[i]);
         ljs[s] = lj[i];
         if (typ_s) typ_s[s] = atype[i];
         if (pos_ref) { pos_ref[3 * i] = x.x; pos_ref[3 * i + 1] = x.y; pos_ref[3 * i + 2] = x.z; }
@@ -286,8 +299,9 @@ __global__ void __launch_bounds__(256) k_cell_commit(int n, const int* __restric
     } else {
         int i = idx_s[s];
         double3 x = ld3(pos, i), r = ld3(pos_ref, i);
-        p4 = make_double4(x.x - floor(r.x / L.x) * L.x, x.y - floor(r.y / L.y) * L.y, x.z - floor(r.z / L.z) * L.z,
-                          q[i]);
+        p4 = wrap ? make_double4(x.x - floor(r.x / L.x) * L.x, x.y - floor(r.y / L.y) * L.y,
+                                 x.z - floor(r.z / L.z) * L.z, q[i])
+                  : make_double4(x.x, x.y, x.z, q[i]);
     }
     pos4s[s] = p4;
 }
@@ -343,6 +357,7 @@ constexpr double kFixMax = 65536.0;
 struct DirectArgs {
     int n, lo, hi, include_forces;
     double3 L; double3 invL; int3 nc; int brute;
+    double3 T; int tric;        // reduced triclinic box: off-diagonals (bx, cx, cy); tric = any nonzero
     double rc2, alpha;
     const double* erfc_tab;     // [kErfcDeg+1][kErfcMaxM] erfcx(x) on intervals of width 1/erfc_scale
     const float* erfc_tab_f;    // [erfc_m_f][kErfcDegF+1] fp32 (mixed precision), width 1/erfc_scale_f
@@ -372,6 +387,23 @@ struct DirectArgs {
 };
 
 __device__ __forceinline__ int own_slot(const DirectArgs& a, int c) { return a.own_s ? a.own_s[c] : c; }
+
+// minimum image of a pair vector d = pos_i - pos_j: per axis d - L rint(d/L) (getDeltaRPeriodic's
+// floor(d/L + 0.5) up to exact half-box ties, which lie beyond the cutoff); a reduced triclinic
+// box subtracts c, b, a in that order (kernel-uniform branch)
+__device__ __forceinline__ void min_image(const DirectArgs& a, double& dx, double& dy, double& dz) {
+    if (a.tric) {
+        const double sc = rint(dz * a.invL.z);
+        dx -= sc * a.T.y; dy -= sc * a.T.z; dz -= sc * a.L.z;
+        const double sb = rint(dy * a.invL.y);
+        dx -= sb * a.T.x; dy -= sb * a.L.y;
+        dx -= a.L.x * rint(dx * a.invL.x);
+    } else {
+        dx -= a.L.x * rint(dx * a.invL.x);
+        dy -= a.L.y * rint(dy * a.invL.y);
+        dz -= a.L.z * rint(dz * a.invL.z);
+    }
+}
 
 // List layout: sub-list seg of row c holds its entries in chunks of kChunk = 4 consecutive
 // entries (16 B), chunk q of every row contiguous in row order:
@@ -441,7 +473,7 @@ __device__ __forceinline__ void scan_cells(const DirectArgs& a, int s, double4 p
         for (int t = part; t < a.n; t += nparts) {
             if (t == s) continue;
             double4 pj = a.pos4s[t];
-            double3 d = delta_r(make_double3(pj.x, pj.y, pj.z), make_double3(pi.x, pi.y, pi.z), a.L, 1);
+            double3 d = delta_r(make_double3(pj.x, pj.y, pj.z), make_double3(pi.x, pi.y, pi.z), a.L, 1, a.T);
             double r2 = d.x * d.x + d.y * d.y + d.z * d.z;
             if (r2 > r2max) continue;
             fn(t, kBruteShift, d.x, d.y, d.z, r2);
@@ -838,7 +870,7 @@ __device__ __forceinline__ void excl_atom(const DirectArgs& a, int i, double3 ad
         double qi = a.q[i];
         for (int k = 0; k < exc; k++) {
             int j = a.ex_list[ex0 + k];
-            double3 d = delta_r(ld3(a.pos, j), xi, a.L, 1);
+            double3 d = delta_r(ld3(a.pos, j), xi, a.L, 1, a.T);
             double r = sqrt(d.x * d.x + d.y * d.y + d.z * d.z);
             double inv_r = 1.0 / r, ar = a.alpha * r;
             double ef = erf(ar);
@@ -962,9 +994,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))
         // image code stored in the list is not needed.
         auto eval = [&](const Cand& cd) {
             double dx = pi.x - cd.p.x, dy = pi.y - cd.p.y, dz = pi.z - cd.p.z;
-            dx -= a.L.x * rint(dx * a.invL.x);
-            dy -= a.L.y * rint(dy * a.invL.y);
-            dz -= a.L.z * rint(dz * a.invL.z);
+            min_image(a, dx, dy, dz);
             const double r2 = dx * dx + dy * dy + dz * dz;
             if (r2 <= a.rc2) pair_term(acc, a, tab, pi, li, cd.p, cd.lj, dx, dy, dz, r2);  // exact voxel-hash test
         };
@@ -1333,9 +1363,7 @@ __global__ void __launch_bounds__(256) k_pairs_mixed(DirectArgs a) {
         // the absolute coordinates loses 2e-6 nm at C5's L = 19.7 nm)
         auto eval = [&](const Cand& cd) {
             double dxd = pid.x - cd.p.x, dyd = pid.y - cd.p.y, dzd = pid.z - cd.p.z;
-            dxd -= a.L.x * rint(dxd * a.invL.x);
-            dyd -= a.L.y * rint(dyd * a.invL.y);
-            dzd -= a.L.z * rint(dzd * a.invL.z);
+            min_image(a, dxd, dyd, dzd);
             const float dx = (float)dxd, dy = (float)dyd, dz = (float)dzd;
             const float r2 = fmaf(dx, dx, fmaf(dy, dy, dz * dz));
             const float4 pj = make_float4(0.f, 0.f, 0.f, (float)cd.p.w);
@@ -1609,7 +1637,8 @@ void launch_flux_terms(Handle& h, const double* pos) {
     if (h.nterms == 0) return;
     double3 L = make_double3(h.box_L[0], h.box_L[1], h.box_L[2]);
     hipLaunchKernelGGL(k_flux_terms, dim3(nblk(h.nterms, 256)), dim3(256), 0, h.stream, h.nterms, h.nb, h.na,
-                       h.term_idx, h.term_par, pos, L, h.pbc, h.dq_slot, h.dqdx);
+                       h.term_idx, h.term_par, pos, L, make_double3(h.box_t[0], h.box_t[1], h.box_t[2]), h.pbc,
+                       h.dq_slot, h.dqdx);
 }
 
 void launch_atoms_prep(Handle& h, const double* pos, bool skin_check) {
@@ -1637,7 +1666,8 @@ void launch_cell_sort(Handle& h, const double* pos) {
     hipLaunchKernelGGL(k_cell_order, dim3(nblk(ncell, 4)), dim3(256), 0, h.stream, ncell, f, h.cell_start,
                        h.cell_end, h.atom_tmp, h.key_tmp, h.lo, h.hi, h.own_start, oc ? h.own_s : nullptr);
     hipLaunchKernelGGL(k_cell_commit, dim3(nblk(h.n, 256)), dim3(256), 0, h.stream, h.n, f, h.cell_key, h.key_tmp,
-                       pos, h.q, h.lj, L, h.cell_key_sorted, h.atom_sorted, h.pos4s, h.ljs, h.atom_type, h.typ_s,
+                       pos, h.q, h.lj, L, h.tric ? 0 : 1, h.cell_key_sorted, h.atom_sorted, h.pos4s, h.ljs,
+                       h.atom_type, h.typ_s,
                        h.pos_ref, h.n_builds_dev);
 }
 
@@ -1649,6 +1679,8 @@ static DirectArgs direct_args(Handle& h, const double* pos, int include_forces) 
     DirectArgs a;
     a.n = h.n; a.lo = h.lo; a.hi = h.hi; a.include_forces = include_forces;
     a.L = make_double3(h.box_L[0], h.box_L[1], h.box_L[2]);
+    a.T = make_double3(h.box_t[0], h.box_t[1], h.box_t[2]);
+    a.tric = h.tric ? 1 : 0;
     a.invL = make_double3(1.0 / h.box_L[0], 1.0 / h.box_L[1], 1.0 / h.box_L[2]);
     a.nc = make_int3(h.nc[0], h.nc[1], h.nc[2]);
     a.brute = (h.nc[0] < 3 || h.nc[1] < 3 || h.nc[2] < 3) ? 1 : 0;

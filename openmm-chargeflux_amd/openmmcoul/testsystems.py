@@ -81,6 +81,36 @@ def water_box(n_waters: int, cutoff: float = 1.0, ewald_tol: float = 1e-4, seed:
     return system, force, pos, box
 
 
+def triclinic_water_box(n_waters: int, cutoff: float = 0.7, ewald_tol: float = 1e-4, seed: int = SEED,
+                        shear=(0.3, -0.25, 0.2), every_bond_angle: int = 3):
+    """Periodic water box with a reduced triclinic cell a = (L,0,0), b = (sb L, L, 0),
+    c = (sc L, scy L, L) (OpenMM's reduced form: |shears| <= 1/2).  Molecule centres sit on
+    the lattice's own fractional grid, so no two periodic images overlap.  Returns
+    (system, force, positions[N,3], box[3,3] with the box vectors as rows)."""
+    rng = np.random.default_rng(seed)
+    L = (n_waters / WATER_DENSITY) ** (1.0 / 3.0)
+    m = int(math.ceil(n_waters ** (1.0 / 3.0) - 1e-9))
+    box = np.array([[L, 0.0, 0.0], [shear[0] * L, L, 0.0], [shear[1] * L, shear[2] * L, L]])
+    idx = np.array([(i, j, k) for i in range(m) for j in range(m) for k in range(m)][:n_waters], dtype=np.float64)
+    frac = (idx + 0.5) / m + rng.uniform(-0.005, 0.005, size=(n_waters, 3))
+    centres = frac @ box
+    pos = _water_geometry(rng, centres).reshape(-1, 3)
+    force = CoulForce()
+    system = System()
+    for w in range(n_waters):
+        for q, s, e, mass in ((Q_O, SIG_O, EPS_O, 15.999), (Q_H, 0.0, 0.0, 1.008), (Q_H, 0.0, 0.0, 1.008)):
+            force.addParticle(q, s, e)
+            system.addParticle(mass)
+    for w in range(n_waters):
+        add_water(force, 3 * w, every_bond_angle > 0 and w % every_bond_angle == every_bond_angle - 1)
+    force.setUsesPeriodicBoundaryConditions(True)
+    force.setCutoffDistance(cutoff)
+    force.setEwaldErrorTolerance(ewald_tol)
+    system.setDefaultPeriodicBoxVectors(*box)
+    system.addForce(force)
+    return system, force, pos, box
+
+
 def cluster_c1(seed: int = SEED):
     """C1: 256-atom non-periodic cluster: 64 waters (32 FluxWater, 32 bond+angle) in a
     1.3 nm cube plus 64 LJ ions (+-1 e, sigma 0.3 nm, eps 0.5 kJ/mol)."""

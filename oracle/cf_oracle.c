@@ -6,8 +6,9 @@
  *   container openmmapi/src/CoulForce.cpp.  Each function cites the lines it follows.
  * It is written from the semantics, not copied; loop order of the reciprocal sum and
  * every quirk listed in SURVEY.md Appendix A.3 ("Reproduce") are kept so it can serve
- * as the serial CPU baseline.  Orthorhombic boxes only (the reference's reciprocal
- * part reads only box diagonals, RCK:513-517).
+ * as the serial CPU baseline.  Periodic boxes in OpenMM's reduced form a = (ax,0,0),
+ * b = (bx,by,0), c = (cx,cy,cz): the minimum image uses the box vectors
+ * (getDeltaRPeriodic), the reciprocal part reads only the box diagonals (RCK:513-517).
  *
  * PARITY UNPINNED: see cf_oracle.h.
  */
@@ -140,7 +141,10 @@ cfo_state* cfo_create(const cf_params* p, char* err, int errlen) {
         s->cutoff = p->cutoff;
         s->tol = p->ewald_tol;
         if (!(s->cutoff > 0) || !(s->tol > 0 && s->tol < 0.5)) { set_err(err, errlen, "invalid cutoff or ewald tolerance"); cfo_destroy(s); return NULL; }
-        if (b[1] != 0 || b[2] != 0 || b[3] != 0 || b[5] != 0 || b[6] != 0 || b[7] != 0) { set_err(err, errlen, "only orthorhombic boxes are supported"); cfo_destroy(s); return NULL; }
+        if (b[1] != 0 || b[2] != 0 || b[5] != 0 || !(b[0] > 0 && b[4] > 0 && b[8] > 0) ||
+            fabs(b[3]) > 0.5 * b[0] || fabs(b[6]) > 0.5 * b[0] || fabs(b[7]) > 0.5 * b[4]) {
+            set_err(err, errlen, "periodic box must be in OpenMM's reduced form"); cfo_destroy(s); return NULL;
+        }
         s->alpha = (1.0 / s->cutoff) * sqrt(-log(2.0 * s->tol));  /* RCK:401 */
         s->one_alpha2 = 1.0 / s->alpha / s->alpha;                /* RCK:402 */
         double L[3] = {b[0], b[4], b[8]};
@@ -168,12 +172,17 @@ int cfo_ewald(const cfo_state* s, double* alpha, int32_t kmax[3]) {
     return 0;
 }
 
-/* ReferenceForce::getDeltaR / getDeltaRPeriodic (OpenMM): d = J - I, minimum image
- * applied z, y, x for an orthorhombic box. */
+/* ReferenceForce::getDeltaR / getDeltaRPeriodic (OpenMM): d = J - I, minimum image by the
+ * box vectors c, b, a in that order.  L = {ax, by, cz, bx, cx, cy} (off-diagonals 0 for an
+ * orthorhombic box: the same bits as the per-axis form). */
 static inline void delta_r(const double* pi, const double* pj, const double* L, int pbc, double d[3]) {
     for (int k = 0; k < 3; k++) d[k] = pj[k] - pi[k];
     if (pbc) {
-        for (int k = 2; k >= 0; k--) d[k] -= L[k] * floor(d[k] / L[k] + 0.5);
+        double sc = floor(d[2] / L[2] + 0.5);
+        d[0] -= sc * L[4]; d[1] -= sc * L[5]; d[2] -= sc * L[2];
+        double sb = floor(d[1] / L[1] + 0.5);
+        d[0] -= sb * L[3]; d[1] -= sb * L[1];
+        d[0] -= L[0] * floor(d[0] / L[0] + 0.5);
     }
 }
 
@@ -277,7 +286,8 @@ static void for_each_pair(cfo_state* s, const double* pos, const double* L, pair
     double rc = s->cutoff, rc2 = rc * rc;
     int nc[3];
     for (int d = 0; d < 3; d++) { nc[d] = (int)floor(L[d] / rc); if (nc[d] < 1) nc[d] = 1; }
-    if (nc[0] < 3 || nc[1] < 3 || nc[2] < 3) {
+    const int triclinic = L[3] != 0 || L[4] != 0 || L[5] != 0;   /* all pairs (small test systems) */
+    if (triclinic || nc[0] < 3 || nc[1] < 3 || nc[2] < 3) {
         for (int i = 0; i < n; i++)
             for (int j = i + 1; j < n; j++) {
                 double d[3]; delta_r(pos + 3 * j, pos + 3 * i, L, 1, d);
@@ -410,8 +420,8 @@ static double execute_impl(cfo_state* s, const double* pos, const double* box9, 
                            int include_energy, double* forces, double terms[4], double* dedq_out,
                            int64_t kspace_limit, double* t_nonrecip, double* t_recip) {
     int n = s->n;
-    double L[3] = {1, 1, 1};
-    if (s->pbc) { L[0] = box9[0]; L[1] = box9[4]; L[2] = box9[8]; }
+    double L[6] = {1, 1, 1, 0, 0, 0};
+    if (s->pbc) { L[0] = box9[0]; L[1] = box9[4]; L[2] = box9[8]; L[3] = box9[3]; L[4] = box9[6]; L[5] = box9[7]; }
     double t0 = now_s();
     update_real_charge(s, pos, L);                                  /* RCK:429 */
     double* dedq = (double*)calloc((size_t)n, sizeof(double));

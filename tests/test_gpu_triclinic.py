@@ -1,0 +1,122 @@
+"""GPU parity for reduced triclinic boxes (OpenMM's form a = (ax,0,0), b = (bx,by,0),
+c = (cx,cy,cz)).  The reference takes the minimum image with the box vectors
+(getDeltaRPeriodic: c, b, a in turn; ReferenceCoulKernels.cpp:567, 601 and the flux terms
+RCK:53-55) and the reciprocal k-set and weights from the box diagonals only, on unwrapped
+positions (RCK:513-547).  Here the real space uses the all-pairs list with the same box-vector
+minimum image (cf_api.hip set_cells; the cell paths are orthorhombic), the k-space paths are
+unchanged (both evaluate the diagonal-only sum on per-axis wrapped coordinates, which leave
+every factor e^{i k_a x_a} unchanged).
+Tolerances as in test_gpu_parity.py (exact k-sum: forces 1e-8) and test_gpu_grid.py (grid: 1e-6).
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+from oracle import Oracle  # noqa: E402
+from openmmcoul import HipCalcCoulForceKernel  # noqa: E402
+from openmmcoul import testsystems as ts  # noqa: E402
+
+EXACT = HipCalcCoulForceKernel.KSPACE_EXACT_MFMA
+GRID = HipCalcCoulForceKernel.KSPACE_GRID
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+
+
+def _compare(k, pos, box, ref, f_tol, fl=True, en=True):
+    e, f = k.execute_host(pos, box, fl, en)
+    assert abs(e - ref["energy"]) <= 1e-9 * abs(ref["energy"]) + 1e-8, (e, ref["energy"])
+    if fl:
+        assert np.abs(f - ref["forces"]).max() <= f_tol, np.abs(f - ref["forces"]).max()
+        scale = np.abs(ref["dedq"]).max()
+        assert np.abs(k.dedq() - ref["dedq"]).max() <= 1e-9 * scale + 1e-9
+    assert np.abs(k.charges() - ref["charges"]).max() <= 1e-12
+    for a, b in zip(k.energy_terms(), ref["terms"]):
+        assert abs(a - b) <= 1e-9 * max(abs(b), 1.0) + 1e-8, (k.energy_terms(), ref["terms"])
+
+
+@pytest.mark.parametrize("algo,f_tol", [(EXACT, 1e-8), (GRID, 1e-6)])
+def test_triclinic_vs_oracle(algo, f_tol):
+    system, force, pos, box = ts.triclinic_water_box(300, cutoff=0.7)
+    k = HipCalcCoulForceKernel(kspace_algo=algo).initialize(system, force)
+    o = Oracle(force, box)
+    for fl, en in ((True, True), (True, False), (False, True)):
+        _compare(k, pos, box, o.execute(pos, box, fl, en), f_tol, fl, en)
+
+
+@pytest.mark.parametrize("algo,f_tol", [(EXACT, 1e-8), (GRID, 1e-6)])
+def test_triclinic_moved_and_lattice_shifted(algo, f_tol):
+    # atoms displaced and some moved by whole box vectors (the reference's k-sum uses the
+    # unwrapped positions, so a lattice shift changes it: both sides see the same positions)
+    system, force, pos, box = ts.triclinic_water_box(300, cutoff=0.7, shear=(-0.4, 0.35, -0.3))
+    rng = np.random.default_rng(3)
+    p2 = pos + rng.normal(scale=0.01, size=pos.shape)
+    p2[::7] += box[1]
+    p2[::11] -= box[2]
+    p2[::13] += box[0] + box[2]
+    k = HipCalcCoulForceKernel(kspace_algo=algo).initialize(system, force)
+    _compare(k, p2, box, Oracle(force, box).execute(p2, box), f_tol)
+
+
+def test_triclinic_with_skin_trajectory_and_box_switch():
+    # persistent list with skin over a short trajectory, then an orthorhombic box and back:
+    # every evaluation matches the oracle (the list is rebuilt when the box changes)
+    system, force, pos, box = ts.triclinic_water_box(300, cutoff=0.7)
+    k = HipCalcCoulForceKernel(kspace_algo=EXACT).initialize(system, force)
+    k.set_neighbor_skin(0.1)
+    o = Oracle(force, box)
+    rng = np.random.default_rng(9)
+    p = pos.copy()
+    for step in range(4):
+        p = p + rng.normal(scale=0.004, size=p.shape)
+        _compare(k, p, box, o.execute(p, box), 1e-8)
+    ortho = np.diag(np.diag(box))
+    _compare(k, p, ortho, o.execute(p, ortho), 1e-8)
+    _compare(k, p, box, o.execute(p, box), 1e-8)
+
+
+@pytest.mark.parametrize("algo", [EXACT, GRID])
+def test_triclinic_two_rank_split_on_one_gpu(algo):
+    # atom decomposition (the all-reduce of the k-space buffer done by hand) on a triclinic box
+    from openmmcoul.distributed import device_buffer_as_tensor
+    system, force, pos, box = ts.triclinic_water_box(300, cutoff=0.7)
+    stream = torch.cuda.current_stream().cuda_stream
+    pt = torch.tensor(pos, dtype=torch.float64, device="cuda")
+    e1, f1 = HipCalcCoulForceKernel(stream=stream, kspace_algo=algo).initialize(system, force).execute_host(pos, box)
+    ks = [HipCalcCoulForceKernel(stream=stream, rank=r, world_size=2, kspace_algo=algo).initialize(system, force)
+          for r in range(2)]
+    for k in ks:
+        k.begin(pt, box, True, True)
+    bufs = [device_buffer_as_tensor(*k.kspace_buffer(), "cuda") for k in ks]
+    total = bufs[0] + bufs[1]
+    for b in bufs:
+        b.copy_(total)
+    f = torch.zeros_like(pt)
+    es = []
+    for k in ks:
+        e = torch.zeros(1, dtype=torch.float64, device="cuda")
+        k.end(f, e)
+        es.append(e)
+    torch.cuda.synchronize()
+    assert (es[0] + es[1]).item() == pytest.approx(e1, rel=1e-11)
+    assert np.abs(f.cpu().numpy() - f1).max() < 1e-8
+
+
+def test_non_reduced_box_rejected():
+    from openmmcoul import ChargeFluxError
+    system, force, pos, box = ts.triclinic_water_box(300, cutoff=0.7)
+    k = HipCalcCoulForceKernel(kspace_algo=EXACT).initialize(system, force)
+    bad = box.copy()
+    bad[1, 0] = 0.7 * box[0, 0]
+    with pytest.raises(ChargeFluxError):
+        k.execute_host(pos, bad)
+    bad = box.copy()
+    bad[0, 2] = 0.1
+    with pytest.raises(ChargeFluxError):
+        k.execute_host(pos, bad)

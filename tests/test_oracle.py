@@ -148,3 +148,35 @@ def test_energy_flag_quirk():
     # non-periodic: nothing without includeEnergy
     system, force, pos, _ = ts.cluster_c1()
     assert Oracle(force).execute(pos, None, True, False)["energy"] == 0.0
+
+
+def test_triclinic_reduced_box_accepted_and_validated():
+    # OpenMM's reduced form a = (ax,0,0), b = (bx,by,0), c = (cx,cy,cz), |bx|,|cx| <= ax/2, |cy| <= by/2
+    system, force, pos, box = ts.triclinic_water_box(60, cutoff=0.5)
+    o = Oracle(force, box)
+    r = o.execute(pos, box)
+    assert np.isfinite(r["energy"]) and np.isfinite(r["forces"]).all()
+    bad = box.copy()
+    bad[0, 1] = 0.1            # a must lie along x
+    with pytest.raises(Exception):
+        Oracle(force, bad)
+    bad = box.copy()
+    bad[1, 0] = 0.6 * box[0, 0]   # |bx| > ax/2
+    with pytest.raises(Exception):
+        Oracle(force, bad)
+
+
+def test_finite_difference_triclinic_box():
+    # the box-vector minimum image (getDeltaRPeriodic) in the pair and flux terms and the
+    # reference's diagonal-only k-sum on unwrapped positions (RCK:513-567) are FD-consistent
+    system, force, pos, box = ts.triclinic_water_box(60, cutoff=0.5, ewald_tol=1e-6)
+    o = Oracle(force, box)
+    _fd_check(o, pos, box, atoms=[0, 1, 2, 6, 7, 8, 30, 61, 120, 179])
+
+
+def test_triclinic_zero_shear_equals_orthorhombic():
+    system, force, pos, box = ts.triclinic_water_box(60, cutoff=0.5, shear=(0.0, 0.0, 0.0))
+    o = Oracle(force, box)
+    r1 = o.execute(pos, box)
+    r2 = o.execute(pos, np.diag(np.diag(box)))
+    assert r1["energy"] == r2["energy"] and np.array_equal(r1["forces"], r2["forces"])
