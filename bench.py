@@ -190,7 +190,7 @@ def main():
     ap.add_argument("--no-kernel-timing", action="store_true",
                     help="no per-kernel HIP events in the timed steps (measures their overhead; no roofline)")
     ap.add_argument("--dt", type=float, default=0.001, help="ps")
-    ap.add_argument("--neighbor-skin", type=float, default=0.1,
+    ap.add_argument("--neighbor-skin", type=float, default=0.15,
                     help="nm; persistent list rebuilt when an atom moved > skin/2 (0 = every step)")
     args = ap.parse_args()
 
