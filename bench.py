@@ -190,9 +190,12 @@ def main():
     ap.add_argument("--no-kernel-timing", action="store_true",
                     help="no per-kernel HIP events in the timed steps (measures their overhead; no roofline)")
     ap.add_argument("--dt", type=float, default=0.001, help="ps")
-    ap.add_argument("--neighbor-skin", type=float, default=0.15,
-                    help="nm; persistent list rebuilt when an atom moved > skin/2 (0 = every step)")
+    ap.add_argument("--neighbor-skin", type=float, default=None,
+                    help="nm; persistent list rebuilt when an atom moved > skin/2 (0 = every step); default "
+                         "0.15 (C2, C3) or 0.2 (C5), the optima of profiles/r02_skin_sweep_m.txt")
     args = ap.parse_args()
+    if args.neighbor_skin is None:
+        args.neighbor_skin = 0.2 if args.config == "C5" else 0.15
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
