@@ -120,3 +120,18 @@ def test_non_reduced_box_rejected():
     bad[0, 2] = 0.1
     with pytest.raises(ChargeFluxError):
         k.execute_host(pos, bad)
+
+
+@pytest.mark.parametrize("algo", [EXACT, GRID])
+def test_triclinic_mixed_precision(algo):
+    # the fp32 full-list pair kernel (k_pairs_mixed) with the box-vector minimum image formed in
+    # fp64; bars of tests/test_gpu_mixed.py (RMS-relative force error 1e-4, energy 1e-7 of
+    # sum |terms|; the pair kernel alone, exact k-sum: 1e-5)
+    system, force, pos, box = ts.triclinic_water_box(300, cutoff=0.7)
+    k = HipCalcCoulForceKernel(kspace_algo=algo, precision="mixed").initialize(system, force)
+    ref = Oracle(force, box).execute(pos, box)
+    e, f = k.execute_host(pos, box)
+    d = f - ref["forces"]
+    err = np.sqrt((d ** 2).sum(1).mean() / (ref["forces"] ** 2).sum(1).mean())
+    assert err <= (1e-5 if algo == EXACT else 1e-4), err
+    assert abs(e - ref["energy"]) <= 1e-7 * np.abs(ref["terms"]).sum()
