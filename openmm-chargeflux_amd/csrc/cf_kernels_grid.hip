@@ -175,61 +175,121 @@ __global__ void __launch_bounds__(256) k_g_scatter(int nown, const int4* __restr
 // window p = 8*db + i, so no per-atom offset is needed to address the taps.
 constexpr int kRow = 24;
 constexpr int kTapStride = 3 * kRow;
-constexpr int kOrderLdsG = 512;   // bin members staged in LDS (denser bins read global memory)
+constexpr int kOtWaves = 4;     // bins per 256-thread block: one wave per bin, no block barriers
+constexpr int kOtLds = 128;     // members per bin staged in LDS (denser bins read global memory)
+constexpr int kOtChunk = 8;     // atoms whose tap rows are assembled in LDS at a time
 
-// one 256-thread block per bin: slot of each member = bin start + number of members with a
-// smaller atom index (the order of a stable sort), then the block writes the members' tap
-// rows, one thread per 16-byte pair of a row, so consecutive threads store consecutive 16 B
-// of the bin's contiguous slot range (one launch for the order and the taps)
+// LDS written by some lanes of a wave, then read by others of the same wave
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// one wave per bin (a bin holds ~23 atoms at C3: a 256-thread block per bin left most of its
+// lanes idle and serialised two block barriers per bin).  Slot of each member = bin start +
+// number of members with a smaller atom index (the order of a stable sort).  The tap rows of
+// kOtChunk members at a time: one lane per nonzero tap (atom, axis, tap m) -- exactly W
+// evaluations per row, where a lane per 16-B pair of the 24-point row evaluated both points
+// whenever either was nonzero -- written into a zeroed LDS copy of the rows, which the wave
+// then stores to the bin's contiguous slot range in consecutive 16 B per lane.
+// WT > 0: the kernel width as a compile-time constant (the tap index divisions become
+// multiplies); WT = 0: W at run time
+template <int WT>
 __global__ void __launch_bounds__(256) k_g_order_taps(int nbins, const int* __restrict__ start,
-                                                      const int* __restrict__ tmp, int* __restrict__ order, int W,
+                                                      const int* __restrict__ tmp, int* __restrict__ order, int Wr,
                                                       double beta, int3 ng, const double4* __restrict__ srec,
                                                       const int4* __restrict__ g0u, double* __restrict__ taps,
                                                       int4* __restrict__ g0s) {
-    __shared__ int mem[kOrderLdsG];
-    __shared__ int srt[kOrderLdsG];
+    __shared__ int mem[kOtWaves][kOtLds];
+    __shared__ int srt[kOtWaves][kOtLds];
+    __shared__ double4 srl[kOtWaves][64];   // sorted members' srec / g0u (bins of <= 64 members)
+    __shared__ int4 gl[kOtWaves][64];
+    __shared__ __attribute__((aligned(16))) double rows[kOtWaves][kOtChunk * kTapStride];
     constexpr int kPairs = kTapStride / 2;   // 36
-    const int b = blockIdx.x;
+    const int W = WT > 0 ? WT : Wr;
+    const int w = wave_id(), lane = threadIdx.x & 63;
+    const int b = blockIdx.x * kOtWaves + w;
+    if (b >= nbins) return;   // wave-uniform
     const int b0 = start[b], m = start[b + 1] - b0;
-    if (m == 0) return;   // block-uniform
+    if (m == 0) return;
     const int* src = tmp + b0;
-    const bool in_lds = m <= kOrderLdsG;
-    if (in_lds) {
-        for (int e = threadIdx.x; e < m; e += 256) mem[e] = src[e];
-        __syncthreads();
-        src = mem;
-    }
-    for (int e = threadIdx.x; e < m; e += 256) {
-        const int v = src[e];
-        int r = 0;
-        for (int j = 0; j < m; j++) r += src[j] < v;
-        order[b0 + r] = v;
-        if (in_lds) srt[r] = v;
-    }
-    if (in_lds) __syncthreads();
-    else __threadfence_block();   // order[] stores of this block, read back below
-    if (!in_lds) __syncthreads();
-    const int* so = in_lds ? srt : order + b0;
-    for (int e = threadIdx.x; e < m * kPairs; e += 256) {
-        const int u = e / kPairs, pp = e - kPairs * u;
-        const int d = pp / (kRow / 2), p0 = 2 * (pp - d * (kRow / 2));   // axis, first point of the pair
-        const int io = so[u];
-        const double4 sr = srec[io];
-        const int4 g = g0u[io];
-        const double sd = d == 0 ? sr.x : (d == 1 ? sr.y : sr.z);
-        const int g0 = d == 0 ? g.x : (d == 1 ? g.y : g.z);
-        const int r = g0 & 7;   // == wrapped g0 mod 8 (ng is a multiple of 8)
-        const double scale = d == 0 ? sr.w : 1.0;
-        double v[2];
-#pragma unroll
-        for (int k = 0; k < 2; k++) {
-            const int mm = p0 + k - r;   // tap index of bin-aligned point p0 + k
-            v[k] = (mm >= 0 && mm < W) ? scale * es_val((double)(g0 + mm) - sd, 2.0 / W, beta) : 0.0;
+    const bool fast = m <= 64, in_lds = m <= kOtLds;
+    if (fast) {   // members in registers: rank by wave-uniform lane reads, their srec / g0u
+                  // loads in flight meanwhile, then kept in LDS in slot order
+        const int v = lane < m ? src[lane] : INT_MAX;
+        double4 sr = make_double4(0.0, 0.0, 0.0, 0.0);
+        int4 g = make_int4(0, 0, 0, 0);
+        if (lane < m) {
+            sr = srec[v];
+            g = g0u[v];
         }
-        const size_t slot = (size_t)b0 + u;
-        reinterpret_cast<v2d*>(taps)[slot * kPairs + pp] = v2d{v[0], v[1]};
-        if (pp == 0)
-            g0s[slot] = make_int4(g.x < 0 ? g.x + ng.x : g.x, g.y < 0 ? g.y + ng.y : g.y, g.z < 0 ? g.z + ng.z : g.z, io);
+        int r = 0;
+        for (int j = 0; j < m; j++) r += __builtin_amdgcn_readlane(v, j) < v;
+        if (lane < m) {
+            order[b0 + r] = v;
+            srl[w][r] = sr;
+            gl[w][r] = g;
+            g0s[b0 + r] = make_int4(g.x < 0 ? g.x + ng.x : g.x, g.y < 0 ? g.y + ng.y : g.y,
+                                    g.z < 0 ? g.z + ng.z : g.z, v);
+        }
+    } else {
+        if (in_lds) {
+            for (int e = lane; e < m; e += 64) mem[w][e] = src[e];
+            wave_sync();
+            src = mem[w];
+        }
+        for (int e = lane; e < m; e += 64) {
+            const int v = src[e];
+            int r = 0;
+            for (int j = 0; j < m; j++) r += src[j] < v;
+            order[b0 + r] = v;
+            if (in_lds) srt[w][r] = v;
+        }
+        if (!in_lds) __threadfence();   // order[] stores of other lanes, read back below
+    }
+    wave_sync();
+    const int* so = in_lds ? srt[w] : order + b0;
+    double* rw = rows[w];
+    const int per = 3 * W;
+    const double hw_inv = 2.0 / W;
+    for (int c0 = 0; c0 < m; c0 += kOtChunk) {
+        const int mc = min(kOtChunk, m - c0);
+        for (int e = lane; e < mc * kPairs; e += 64) reinterpret_cast<v2d*>(rw)[e] = v2d{0.0, 0.0};
+        wave_sync();
+        for (int e = lane; e < mc * per; e += 64) {
+            const int u = e / per, rem = e - u * per, d = rem / W, mm = rem - d * W;
+            double sd, scale;
+            int g0;
+            if (fast) {
+                const double* sp = reinterpret_cast<const double*>(&srl[w][c0 + u]);
+                const int* gp = reinterpret_cast<const int*>(&gl[w][c0 + u]);
+                sd = sp[d];
+                scale = d == 0 ? sp[3] : 1.0;
+                g0 = gp[d];
+            } else {
+                const int io = so[c0 + u];
+                const double* sp = reinterpret_cast<const double*>(srec + io);
+                const int* gp = reinterpret_cast<const int*>(g0u + io);
+                sd = sp[d];
+                scale = d == 0 ? sp[3] : 1.0;
+                g0 = gp[d];
+            }
+            // q folded into the x row; bin-aligned point (g0 mod 8) + m, g0 mod 8 == wrapped
+            // g0 mod 8 (ng is a multiple of 8)
+            rw[u * kTapStride + d * kRow + (g0 & 7) + mm] = scale * es_val((double)(g0 + mm) - sd, hw_inv, beta);
+        }
+        wave_sync();
+        const size_t s0 = (size_t)b0 + c0;
+        for (int e = lane; e < mc * kPairs; e += 64)
+            reinterpret_cast<v2d*>(taps)[s0 * kPairs + e] = reinterpret_cast<const v2d*>(rw)[e];
+        if (!fast && lane < mc) {
+            const int io = so[c0 + lane];
+            const int4 g = g0u[io];
+            g0s[s0 + lane] = make_int4(g.x < 0 ? g.x + ng.x : g.x, g.y < 0 ? g.y + ng.y : g.y,
+                                       g.z < 0 ? g.z + ng.z : g.z, io);
+        }
+        wave_sync();   // the rows are re-zeroed for the next chunk
     }
 }
 
@@ -1324,7 +1384,9 @@ void launch_grid_sort(Handle& h, const double* pos) {
                        nb, h.g_srec, h.g_g0u, h.g_rank, h.g_cnt, h.g_xrange, h.e_ticket + kTicketGrid, h.g_start);
     hipLaunchKernelGGL(k_g_scatter, dim3(nblk(nown, 256)), dim3(256), 0, h.stream, nown, h.g_g0u, h.g_rank, h.g_start,
                        h.g_tmp, p.nbins, h.g_cnt);
-    hipLaunchKernelGGL(k_g_order_taps, dim3(p.nbins), dim3(256), 0, h.stream, p.nbins, h.g_start, h.g_tmp,
+    if (p.W == 14) hipLaunchKernelGGL(k_g_order_taps<14>, dim3(nblk(p.nbins, kOtWaves)), dim3(256), 0, h.stream, p.nbins, h.g_start, h.g_tmp,
+                       h.g_order, p.W, p.beta, ng, h.g_srec, h.g_g0u, h.g_taps, h.g_g0s);
+    else hipLaunchKernelGGL(k_g_order_taps<0>, dim3(nblk(p.nbins, kOtWaves)), dim3(256), 0, h.stream, p.nbins, h.g_start, h.g_tmp,
                        h.g_order, p.W, p.beta, ng, h.g_srec, h.g_g0u, h.g_taps, h.g_g0s);
 }
 

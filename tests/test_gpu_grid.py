@@ -106,6 +106,19 @@ def test_grid_noncubic_box():
     _compare(_run(k, pos, box2), o.execute(pos, box2))
 
 
+@pytest.mark.parametrize("nw,rc,tol,min_per_bin", [(1500, 1.5, 1e-3, 128), (800, 1.3, 1e-3, 64)])
+def test_grid_dense_bins(nw, rc, tol, min_per_bin):
+    # few, crowded 8^3 bins (a short k-sum on a small grid): bins of more than 64 and more
+    # than 128 members take k_g_order_taps' LDS and global-memory ranking paths
+    system, force, pos, box = ts.water_box(nw, cutoff=rc, ewald_tol=tol, every_bond_angle=3)
+    k = HipCalcCoulForceKernel(kspace_algo=GRID).initialize(system, force)
+    ng = k.grid_shape()
+    per_bin = len(pos) / np.prod([n // 8 for n in ng])
+    print("grid", ng, "mean atoms per bin", per_bin)
+    assert per_bin > min_per_bin
+    _compare(_run(k, pos, box), Oracle(force, box).execute(pos, box))
+
+
 def test_grid_device_api_deterministic():
     system, force, pos, box = ts.water_box(1500, cutoff=1.0, ewald_tol=1e-4)
     stream = torch.cuda.current_stream().cuda_stream
