@@ -376,6 +376,24 @@ def main():
                  "denergy_grid_vs_exact": float(eg.item() - ee.item())}
         del ke
 
+    host = None
+    if world == 1 and not args.no_exact_compare:
+        # the host-buffer boundary (cf_compute_host: what a Reference/CPU-platform adapter
+        # calls): positions H2D, forces D2H and a stream sync inside every call -- the
+        # PCIe-inclusive rate, never `value`
+        pos_h = pos.cpu().numpy()
+        f_h = np.zeros_like(pos_h)
+        for _ in range(3):
+            kern.kernel.execute_host(pos_h, box, forces=f_h)
+        reps = 20
+        t_h = time.perf_counter()
+        for _ in range(reps):
+            kern.kernel.execute_host(pos_h, box, forces=f_h)
+        ms_h = (time.perf_counter() - t_h) / reps * 1e3
+        host = {"ms_per_force_eval": round(ms_h, 4), "bytes_h2d": int(pos_h.nbytes), "bytes_d2h": int(f_h.nbytes),
+                "note": "cf_compute_host with host positions/forces, wall clock over 20 calls (each syncs); "
+                        "compare ms_per_force_eval (device-resident)"}
+
     if rank == 0:
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
@@ -405,6 +423,7 @@ def main():
             "roofline": roofline,
             "kernels_roofline": others,
             "exact_kspace": exact,
+            "host_boundary": host,
             "cpu_baseline": cpu,
         }
         if cpu:
