@@ -194,7 +194,7 @@ __device__ __forceinline__ void wave_sync() {
 // whenever either was nonzero -- written into a zeroed LDS copy of the rows, which the wave
 // then stores to the bin's contiguous slot range in consecutive 16 B per lane.
 // WT > 0: the kernel width as a compile-time constant (the tap index divisions become
-// multiplies); WT = 0: W at run time
+// multiplies; 14 = the fp64 default, 8 = mixed precision); WT = 0: W at run time
 template <int WT>
 __global__ void __launch_bounds__(256) k_g_order_taps(int nbins, const int* __restrict__ start,
                                                       const int* __restrict__ tmp, int* __restrict__ order, int Wr,
@@ -1385,6 +1385,8 @@ void launch_grid_sort(Handle& h, const double* pos) {
     hipLaunchKernelGGL(k_g_scatter, dim3(nblk(nown, 256)), dim3(256), 0, h.stream, nown, h.g_g0u, h.g_rank, h.g_start,
                        h.g_tmp, p.nbins, h.g_cnt);
     if (p.W == 14) hipLaunchKernelGGL(k_g_order_taps<14>, dim3(nblk(p.nbins, kOtWaves)), dim3(256), 0, h.stream, p.nbins, h.g_start, h.g_tmp,
+                       h.g_order, p.W, p.beta, ng, h.g_srec, h.g_g0u, h.g_taps, h.g_g0s);
+    else if (p.W == 8) hipLaunchKernelGGL(k_g_order_taps<8>, dim3(nblk(p.nbins, kOtWaves)), dim3(256), 0, h.stream, p.nbins, h.g_start, h.g_tmp,
                        h.g_order, p.W, p.beta, ng, h.g_srec, h.g_g0u, h.g_taps, h.g_g0s);
     else hipLaunchKernelGGL(k_g_order_taps<0>, dim3(nblk(p.nbins, kOtWaves)), dim3(256), 0, h.stream, p.nbins, h.g_start, h.g_tmp,
                        h.g_order, p.W, p.beta, ng, h.g_srec, h.g_g0u, h.g_taps, h.g_g0s);
