@@ -392,39 +392,49 @@ __device__ __forceinline__ int block_exclusive_scan_t(int v, int* sh) {
 
 // counts cnt[0..m) (device-scope atomics of other blocks: read with ld_agent) -> start[c]
 // (and end[c] = start[c + 1] when end != null; start[m] = total when total_at_end), by the NT
-// threads of one block, in tiles of 8 NT counts: each thread issues its 8 coalesced loads of
-// a tile at once (one memory latency per tile, not one per count)
+// threads of one block, in tiles of 8 NT counts: each thread issues the loads of kBoundsU
+// tiles at once (one memory latency per kBoundsU tiles, not one per count or per tile: the
+// C5 grid's 32k bins are 16 tiles at NT = 256)
+constexpr int kBoundsU = 4;
 template <int NT>
 __device__ __forceinline__ void block_counts_to_bounds(int m, int* cnt, int* start, int* end, bool total_at_end,
                                                        int* sh) {
     __shared__ int tile[8 * NT];
     const int t = threadIdx.x;
     int carry = 0;
-    for (int base = 0; base < m; base += 8 * NT) {
-        int v[8];
+    for (int sbase = 0; sbase < m; sbase += kBoundsU * 8 * NT) {
+        int vu[kBoundsU][8];
 #pragma unroll
-        for (int k = 0; k < 8; k++) {
-            const int c = base + k * NT + t;
-            v[k] = c < m ? ld_agent(cnt + c) : 0;
-        }
+        for (int u = 0; u < kBoundsU; u++)
 #pragma unroll
-        for (int k = 0; k < 8; k++) tile[k * NT + t] = v[k];
-        __syncthreads();
-        int sum = 0;
-#pragma unroll
-        for (int k = 0; k < 8; k++) { v[k] = tile[8 * t + k]; sum += v[k]; }
-        int run = carry + block_exclusive_scan_t<NT>(sum, sh);
-        carry += sh[NT - 1];   // inclusive total of the tile
-#pragma unroll
-        for (int k = 0; k < 8; k++) {
-            const int c = base + 8 * t + k;
-            if (c < m) {
-                start[c] = run;
-                run += v[k];
-                if (end) end[c] = run;
+            for (int k = 0; k < 8; k++) {
+                const int c = sbase + u * 8 * NT + k * NT + t;
+                vu[u][k] = c < m ? ld_agent(cnt + c) : 0;
             }
+#pragma unroll
+        for (int u = 0; u < kBoundsU; u++) {
+            const int base = sbase + u * 8 * NT;
+            if (base >= m) break;   // block-uniform
+#pragma unroll
+            for (int k = 0; k < 8; k++) tile[k * NT + t] = vu[u][k];
+            __syncthreads();
+            int v[8];
+            int sum = 0;
+#pragma unroll
+            for (int k = 0; k < 8; k++) { v[k] = tile[8 * t + k]; sum += v[k]; }
+            int run = carry + block_exclusive_scan_t<NT>(sum, sh);
+            carry += sh[NT - 1];   // inclusive total of the tile
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+                const int c = base + 8 * t + k;
+                if (c < m) {
+                    start[c] = run;
+                    run += v[k];
+                    if (end) end[c] = run;
+                }
+            }
+            __syncthreads();
         }
-        __syncthreads();
     }
     if (total_at_end && t == 0) start[m] = carry;
 }
