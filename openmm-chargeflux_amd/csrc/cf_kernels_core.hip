@@ -1257,12 +1257,27 @@ __device__ __forceinline__ void half_window_sums(const DirectArgs& a, int s, dou
     const int cz = key % nc.z, cy = (key / nc.z) % nc.y, cx = key / (nc.y * nc.z);
     const int jj = s - a.cstart[key];
     long long sx = 0, sy = 0, sz = 0, sq = 0;
-    for (int k = 0; k < kHalfWin; k++) {
-        const int3 o = half_offset(k);
-        const int b = (wrap_cell(cx - o.x, nc.x) * nc.y + wrap_cell(cy - o.y, nc.y)) * nc.z + wrap_cell(cz - o.z, nc.z);
-        const int slot = a.win_woff[b * kHalfWin + k] + jj;
-        const ulonglong4 v = reinterpret_cast<const ulonglong4*>(a.win_out)[(size_t)b * kHalfMaxWin + slot];
-        sx += (long long)v.x; sy += (long long)v.y; sz += (long long)v.z; sq += (long long)v.w;
+    // batches of kBatch windows: every offset load of a batch in flight, then every window
+    // load (two memory latencies per batch instead of two per window; integer sums, so the
+    // order does not change the result)
+    constexpr int kBatch = 6;
+    static_assert(kHalfWin % kBatch == 0, "window batches");
+#pragma unroll
+    for (int k0 = 0; k0 < kHalfWin; k0 += kBatch) {
+        int b[kBatch], slot[kBatch];
+#pragma unroll
+        for (int u = 0; u < kBatch; u++) {
+            const int3 o = half_offset(k0 + u);
+            b[u] = (wrap_cell(cx - o.x, nc.x) * nc.y + wrap_cell(cy - o.y, nc.y)) * nc.z + wrap_cell(cz - o.z, nc.z);
+            slot[u] = a.win_woff[b[u] * kHalfWin + k0 + u] + jj;
+        }
+        ulonglong4 v[kBatch];
+#pragma unroll
+        for (int u = 0; u < kBatch; u++) v[u] = reinterpret_cast<const ulonglong4*>(a.win_out)[(size_t)b[u] * kHalfMaxWin + slot[u]];
+#pragma unroll
+        for (int u = 0; u < kBatch; u++) {
+            sx += (long long)v[u].x; sy += (long long)v[u].y; sz += (long long)v[u].z; sq += (long long)v[u].w;
+        }
     }
     f = make_double3((double)sx * kFixInv, (double)sy * kFixInv, (double)sz * kFixInv);
     dq = (double)sq * kFixInv;
