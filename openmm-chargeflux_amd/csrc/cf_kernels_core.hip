@@ -1544,12 +1544,28 @@ __global__ void __launch_bounds__(kEChunk) k_assemble_energy(int lo, int hi, con
     if (b < hi) {
         if (out) {
             double fx = f_part[3 * b], fy = f_part[3 * b + 1], fz = f_part[3 * b + 2];
-            for (int k = cs[b]; k < cs[b + 1]; k++) {
-                int2 en = ce[k];
-                double g = dedq[en.y];
-                fx -= g * dqdx[3 * en.x];
-                fy -= g * dqdx[3 * en.x + 1];
-                fz -= g * dqdx[3 * en.x + 2];
+            // entries in batches of 4: the entry loads, then their dE/dq and dq/dx gathers, all
+            // in flight together (two memory latencies per batch, not per entry); the sums keep
+            // the entry order
+            const int k1 = cs[b + 1];
+            for (int k0 = cs[b]; k0 < k1; k0 += 4) {
+                int2 en[4];
+#pragma unroll
+                for (int u = 0; u < 4; u++) en[u] = ce[min(k0 + u, k1 - 1)];
+                double g[4], d[4][3];
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    g[u] = dedq[en[u].y];
+                    d[u][0] = dqdx[3 * en[u].x]; d[u][1] = dqdx[3 * en[u].x + 1]; d[u][2] = dqdx[3 * en[u].x + 2];
+                }
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    if (k0 + u < k1) {
+                        fx -= g[u] * d[u][0];
+                        fy -= g[u] * d[u][1];
+                        fz -= g[u] * d[u][2];
+                    }
+                }
             }
             out[3 * b] += fx;
             out[3 * b + 1] += fy;
