@@ -27,7 +27,7 @@ extern "C" {
 #define CF_EXPORT __attribute__((visibility("default")))
 #endif
 
-#define CF_API_VERSION 1
+#define CF_API_VERSION 2   /* 2: cf_params.one_4pi_eps0 */
 
 /* Error codes (negative).  cf_last_error() returns the message of the last failure
  * on the calling thread.  Mirrors the reference's OpenMMException paths. */
@@ -37,9 +37,14 @@ extern "C" {
 #define CF_ERR_STATE -3    /* call sequence error (e.g. end without begin)    */
 #define CF_ERR_NOMEM -4    /* device allocation failed                        */
 
-/* Coulomb constant ONE_4PI_EPS0 (kJ mol^-1 nm e^-2), OpenMM 7.x value used by the
- * reference via openmm/reference/SimTKOpenMMRealType.h (ReferenceCoulKernels.cpp:7). */
+/* Coulomb constant ONE_4PI_EPS0 (kJ mol^-1 nm e^-2).  The reference takes it from the
+ * OpenMM it is compiled against (openmm/reference/SimTKOpenMMRealType.h, included at
+ * ReferenceCoulKernels.cpp:7; used at :508, :517, :580-589, :608-619), so its value depends on
+ * the OpenMM version: 138.935456 in OpenMM 7.x headers, 138.93545764438198 (CODATA 2018) in
+ * OpenMM 8.x.  cf_params.one_4pi_eps0 carries the loading OpenMM's value; 0 selects the
+ * default below (OpenMM 7.x). */
 #define CF_ONE_4PI_EPS0 138.935456
+#define CF_ONE_4PI_EPS0_CODATA2018 138.93545764438198
 
 /*
  * Force parameters: the flat storage of CoulPlugin::CoulForce
@@ -70,6 +75,8 @@ typedef struct cf_params {
     double ewald_tol;         /* setEwaldErrorTolerance                                    */
     double default_box[9];    /* System::getDefaultPeriodicBoxVectors, rows a,b,c (nm);
                                  kmax is derived from THIS box (ReferenceCoulKernels.cpp:399-420) */
+    double one_4pi_eps0;      /* Coulomb constant of the OpenMM the force is evaluated for
+                                 (its ONE_4PI_EPS0); 0 = CF_ONE_4PI_EPS0.  Must be >= 0, finite */
 } cf_params;
 
 /* Execution options (all-zero = single GPU, device 0, default stream). */

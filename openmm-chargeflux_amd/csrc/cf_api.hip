@@ -141,6 +141,13 @@ void check_box_reduced(const double* b, const char* what) {
         fail(CF_ERR_INVALID, std::string(what) + ": box vectors must be in OpenMM's reduced form (|bx|, |cx| <= ax/2, |cy| <= by/2)");
 }
 
+// ONE_4PI_EPS0 of the OpenMM the force is evaluated for (cf_params.one_4pi_eps0; 0 = CF_ONE_4PI_EPS0)
+double coulomb_constant(const cf_params* p) {
+    const double ke = p->one_4pi_eps0;
+    if (!(ke >= 0) || !std::isfinite(ke)) fail(CF_ERR_INVALID, "one_4pi_eps0 must be finite and >= 0 (0 = default)");
+    return ke == 0 ? CF_ONE_4PI_EPS0 : ke;
+}
+
 int find_root(std::vector<int>& p, int x) {
     while (p[x] != x) { p[x] = p[p[x]]; x = p[x]; }
     return x;
@@ -479,6 +486,9 @@ CF_EXPORT int cf_create(const cf_params* p, const cf_options* opt, cf_handle** o
         // ---- ownership for atom decomposition (see partition())
         partition(p, world, o.rank, &h.lo, &h.hi);
 
+        // ---- Coulomb constant of the loading OpenMM (ONE_4PI_EPS0, RCK:7; 0 = the 7.x value)
+        h.ke = coulomb_constant(p);
+
         // ---- periodic / Ewald parameters  RCK:394-421
         h.pbc = p->use_pbc ? 1 : 0;
         if (h.pbc) {
@@ -697,6 +707,8 @@ CF_EXPORT int cf_update_parameters(cf_handle* H, const cf_params* p) {
         if ((p->use_pbc ? 1 : 0) != h.pbc) fail(CF_ERR_INVALID, "periodicity cannot be changed by an update");
         if (h.pbc && (p->cutoff != h.cutoff || p->ewald_tol != h.tol))
             fail(CF_ERR_INVALID, "the cutoff and Ewald tolerance cannot be changed by an update");
+        if (coulomb_constant(p) != h.ke)
+            fail(CF_ERR_INVALID, "the Coulomb constant (one_4pi_eps0) cannot be changed by an update");
         std::vector<double> q0;
         std::vector<double2> lj;
         parse_particles(p, q0, lj);

@@ -13,7 +13,7 @@
 
 namespace cf {
 
-constexpr double kOne4PiEps0 = CF_ONE_4PI_EPS0;
+// (the Coulomb constant is a run-time value, Handle::ke: cf_params.one_4pi_eps0)
 constexpr double kPi = 3.14159265358979323846;
 
 // ---------------------------------------------------------------------------------
@@ -85,6 +85,7 @@ struct Handle {
     int n = 0;
     int pbc = 0;
     double cutoff = 1.0, tol = 1e-4, alpha = 0.0;
+    double ke = CF_ONE_4PI_EPS0;   // ONE_4PI_EPS0 of the loading OpenMM (cf_params.one_4pi_eps0)
     int kmax[3] = {0, 0, 0};
     int device = 0;
     hipStream_t stream = nullptr;

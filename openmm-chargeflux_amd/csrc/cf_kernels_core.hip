@@ -136,7 +136,7 @@ __global__ void __launch_bounds__(256) k_flux_terms(int nterms, int nb, int na, 
 }
 __global__ void __launch_bounds__(256) k_atoms_prep(int n, const double* __restrict__ q0,
                                                     const int* __restrict__ qs, const int* __restrict__ qslot,
-                                                    const double* __restrict__ dq_slot, int pbc, double alpha,
+                                                    const double* __restrict__ dq_slot, int pbc, double alpha, double ke,
                                                     double* __restrict__ q, double* __restrict__ dedq_self,
                                                     double* __restrict__ e_atom, const double* __restrict__ pos,
                                                     const double* __restrict__ pos_ref, double lim2,
@@ -156,7 +156,7 @@ __global__ void __launch_bounds__(256) k_atoms_prep(int n, const double* __restr
     for (int s = qs[i]; s < qs[i + 1]; s++) qi += dq_slot[qslot[s]];
     q[i] = qi;
     if (pbc) {
-        const double c = kOne4PiEps0 * alpha / sqrt(kPi);
+        const double c = ke * alpha / sqrt(kPi);
         dedq_self[i] = -2 * c * qi;
         e_atom[3 * i] = -c * qi * qi;
     } else {
@@ -359,6 +359,7 @@ struct DirectArgs {
     double3 L; double3 invL; int3 nc; int brute;
     double3 T; int tric;        // reduced triclinic box: off-diagonals (bx, cx, cy); tric = any nonzero
     double rc2, alpha;
+    double ke;                  // Coulomb constant ONE_4PI_EPS0 (Handle::ke)
     const double* erfc_tab;     // [kErfcDeg+1][kErfcMaxM] erfcx(x) on intervals of width 1/erfc_scale
     const float* erfc_tab_f;    // [erfc_m_f][kErfcDegF+1] fp32 (mixed precision), width 1/erfc_scale_f
     double erfc_scale; int erfc_m;
@@ -578,9 +579,12 @@ __global__ void __launch_bounds__(kWaveNL * kSeg) k_nlist_wave(DirectArgs a) {
     // high bits of a list entry: the partner's LJ type when types are used, else the image code
     auto emit = [&](int t, int j, int hb) { put_entry(t | (hb << kShiftBits), j); };
     if (!fits) {  // wave-uniform (and block-uniform: every wave sees the same 64 atoms)
-        if (a.half) {   // half lists need the block frame: hand the evaluation to the fp64 rescan
-            if (active) a.nl_cnt[(size_t)seg * a.nlr + c] = 0;
-            if (lane == 0) atomicOr(a.half_flag, 1);
+        if (a.half) {
+            // half lists need the block frame: these rows get no entries and an overflowed
+            // count, so k_pairs_half raises half_flag on EVERY evaluation that uses this list
+            // (also the later ones that keep it under a skin, when this kernel does not run)
+            // and k_excl rescans with the fp64 cell scan
+            if (active) a.nl_cnt[(size_t)seg * a.nlr + c] = a.nb_cap + 1;
             return;
         }
         if (active)
@@ -804,7 +808,7 @@ __device__ __forceinline__ double erfc_exp(double x, const double* __restrict__ 
 __device__ __forceinline__ void pair_term(PairAcc& acc, const DirectArgs& a, const double* __restrict__ tab,
                                           double4 pi, double2 li, double4 pj, double2 lj2, double dx, double dy,
                                           double dz, double r2) {
-    const double ke = kOne4PiEps0;
+    const double ke = a.ke;
     const double two_over_sqrtpi = 1.1283791670955126;
     double inv_r = rsqrt_fp64(r2);
     double r = r2 * inv_r;
@@ -854,7 +858,7 @@ __device__ __forceinline__ void store_pairs(const PairAcc& acc, const DirectArgs
 // (add_f, add_dq: the half list's partner-side sums of the atom, added to the stored pair sums)
 __device__ __forceinline__ void excl_atom(const DirectArgs& a, int i, double3 add_f = make_double3(0.0, 0.0, 0.0),
                                           double add_dq = 0.0) {
-    const double ke = kOne4PiEps0;
+    const double ke = a.ke;
     const double two_over_sqrtpi = 1.1283791670955126;
     const int ex0 = a.ex_start[i], exc = a.ex_start[i + 1] - ex0;
     double fx = 0, fy = 0, fz = 0, dq = 0, ex_e = 0;
@@ -1101,7 +1105,7 @@ __global__ void __launch_bounds__(1024) k_pairs_half(DirectArgs a) {
           if (active) {
             const double4 pi = a.pos4s[row];
             const float2 li = make_float2((float)a.ljs[row].x, (float)a.ljs[row].y);
-            const float qi = (float)pi.w, ke = (float)kOne4PiEps0, keqi = ke * qi;
+            const float qi = (float)pi.w, ke = (float)a.ke, keqi = ke * qi;
             const float rc2 = (float)a.rc2, alpha = (float)a.alpha, escale = (float)a.erfc_scale_f;
             const v4i* nl4 = reinterpret_cast<const v4i*>(a.nl) + (size_t)g * (a.nb_cap / kChunk) * a.nlr + row;
             struct Cand { double4 p; float2 lj; int slot; };
@@ -1166,7 +1170,7 @@ __global__ void __launch_bounds__(1024) k_pairs_half(DirectArgs a) {
         } else if (active) {
             const double4 pi = a.pos4s[row];
             const double2 li = a.ljs[row];
-            const double kqis = kOne4PiEps0 * pi.w * kFixScale;   // k_e q_i in fixed-point units
+            const double kqis = a.ke * pi.w * kFixScale;   // k_e q_i in fixed-point units
             const v4i* nl4 = reinterpret_cast<const v4i*>(a.nl) + (size_t)g * (a.nb_cap / kChunk) * a.nlr + row;
             struct Cand { double4 p; double2 lj; int slot; };
             auto gather = [&](int e, bool ok) {
@@ -1185,7 +1189,7 @@ __global__ void __launch_bounds__(1024) k_pairs_half(DirectArgs a) {
                 dz -= a.L.z * rint(dz * a.invL.z);
                 const double r2 = dx * dx + dy * dy + dz * dz;
                 if (r2 <= a.rc2) {   // exact voxel-hash test
-                    const double ke = kOne4PiEps0;
+                    const double ke = a.ke;
                     const double two_over_sqrtpi = 1.1283791670955126;
                     const double inv_r = rsqrt_fp64(r2);
                     const double ar = a.alpha * (r2 * inv_r);
@@ -1293,10 +1297,9 @@ __device__ __forceinline__ void half_window_sums(const DirectArgs& a, int s, dou
 //     in fp32 per lane, the energy in fp64; lanes are combined and the exclusion correction
 //     is applied in fp64 (excl_atom).
 // ---------------------------------------------------------------------------------
-__device__ __forceinline__ void pair_term_f(PairAccF& acc, float alpha, int include_forces, const float* tab,
+__device__ __forceinline__ void pair_term_f(PairAccF& acc, float ke, float alpha, int include_forces, const float* tab,
                                             float scale, float4 pi, float2 li, float4 pj, float2 lj2, float dx,
                                             float dy, float dz, float r2) {
-    const float ke = (float)kOne4PiEps0;
     const float inv_r = rsqrtf(r2);
     const float r = r2 * inv_r;
     const float ar = alpha * r;
@@ -1379,7 +1382,7 @@ __global__ void __launch_bounds__(256) k_pairs_mixed(DirectArgs a) {
             const float dx = (float)dxd, dy = (float)dyd, dz = (float)dzd;
             const float r2 = fmaf(dx, dx, fmaf(dy, dy, dz * dz));
             const float4 pj = make_float4(0.f, 0.f, 0.f, (float)cd.p.w);
-            if (r2 <= rc2) pair_term_f(acc, alpha, a.include_forces, tabf, escale, pi, li, pj, cd.lj, dx, dy, dz, r2);
+            if (r2 <= rc2) pair_term_f(acc, (float)a.ke, alpha, a.include_forces, tabf, escale, pi, li, pj, cd.lj, dx, dy, dz, r2);
         };
         walk_list(nl4, a.nlr, cnt, part, LPA / kSeg, gather, eval);
     }
@@ -1442,7 +1445,7 @@ __global__ void __launch_bounds__(256) k_excl(DirectArgs a) {
 // ---------------------------------------------------------------------------------
 constexpr int kNopbcTile = 256;
 
-__global__ void __launch_bounds__(kNopbcTile) k_nopbc(int n, int lo, int hi, int include_forces, int include_energy,
+__global__ void __launch_bounds__(kNopbcTile) k_nopbc(int n, int lo, int hi, int include_forces, int include_energy, double ke,
                                                       const double* __restrict__ pos, const double* __restrict__ q,
                                                       const double2* __restrict__ lj, const int* __restrict__ ex_start,
                                                       const int* __restrict__ ex_list, double* __restrict__ dedq,
@@ -1462,7 +1465,6 @@ __global__ void __launch_bounds__(kNopbcTile) k_nopbc(int n, int lo, int hi, int
     }
 #pragma unroll
     for (int k = 0; k < kMaxRegExcl; k++) reg[k] = k < exc ? ex_list[ex0 + k] : -1;
-    const double ke = kOne4PiEps0;
     double fx = 0, fy = 0, fz = 0, dq = 0, e = 0;
     for (int base = 0; base < n; base += kNopbcTile) {
         int j = base + threadIdx.x;
@@ -1673,7 +1675,7 @@ void launch_atoms_prep(Handle& h, const double* pos, bool skin_check) {
     // the flag is 0 here: cleared at cf_create and by k_energy at the end of every evaluation
     const double lim = 0.5 * h.list_skin;
     hipLaunchKernelGGL(k_atoms_prep, dim3(nblk(h.n, 256)), dim3(256), 0, h.stream, h.n, h.q0, h.qcsr_start,
-                       h.qcsr_slot, h.dq_slot, h.pbc, h.alpha, h.q, h.dedq_self, h.e_atom, pos, h.pos_ref, lim * lim,
+                       h.qcsr_slot, h.dq_slot, h.pbc, h.alpha, h.ke, h.q, h.dedq_self, h.e_atom, pos, h.pos_ref, lim * lim,
                        skin_check ? h.skin_flag : nullptr);
 }
 
@@ -1712,7 +1714,7 @@ static DirectArgs direct_args(Handle& h, const double* pos, int include_forces) 
     a.invL = make_double3(1.0 / h.box_L[0], 1.0 / h.box_L[1], 1.0 / h.box_L[2]);
     a.nc = make_int3(h.nc[0], h.nc[1], h.nc[2]);
     a.brute = (h.nc[0] < 3 || h.nc[1] < 3 || h.nc[2] < 3) ? 1 : 0;
-    a.rc2 = h.cutoff * h.cutoff; a.alpha = h.alpha;
+    a.rc2 = h.cutoff * h.cutoff; a.alpha = h.alpha; a.ke = h.ke;
     a.erfc_tab = h.erfc_tab; a.erfc_scale = h.erfc_scale; a.erfc_m = h.erfc_m;
     a.erfc_tab_f = h.erfc_tab_f; a.erfc_scale_f = h.erfc_scale_f; a.erfc_m_f = h.erfc_m_f;
     a.rl2 = (h.cutoff + h.list_skin) * (h.cutoff + h.list_skin);
@@ -1799,7 +1801,7 @@ void launch_recip_add(Handle& h) {
 void launch_nopbc(Handle& h, const double* pos, int include_forces, int include_energy) {
     int nown = h.hi - h.lo;
     hipLaunchKernelGGL(k_nopbc, dim3(nblk(nown, kNopbcTile)), dim3(kNopbcTile), 0, h.stream, h.n, h.lo, h.hi,
-                       include_forces, include_energy, pos, h.q, h.lj, h.ex_start, h.ex_list, h.dedq, h.f_part,
+                       include_forces, include_energy, h.ke, pos, h.q, h.lj, h.ex_start, h.ex_list, h.dedq, h.f_part,
                        h.e_atom);
 }
 

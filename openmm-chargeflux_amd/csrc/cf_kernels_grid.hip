@@ -1584,7 +1584,7 @@ double* grid_reduce_buffer(Handle& h, int64_t* count) {
 void launch_grid_coeffs(Handle& h, int include_energy) {
     const GridPlan& p = h.gp;
     const double V = h.box_L[0] * h.box_L[1] * h.box_L[2];
-    const double cst = 4.0 / V * kPi * kOne4PiEps0;   // RCK:517
+    const double cst = 4.0 / V * kPi * h.ke;   // RCK:517
     const int total = p.NX * p.NY * p.KZ;
     h.e_rec_nblk = nblk(total, 256);
     hipLaunchKernelGGL(k_g_coeffs, dim3(h.e_rec_nblk), dim3(256), 0, h.stream, p.KX, p.KY, p.KZ, recip_vec(h), cst,

@@ -677,7 +677,7 @@ double* kspace_reduce_buffer(Handle& h, int64_t* count) {
 void launch_kspace_coeffs(Handle& h, int include_energy) {
     const KGeom& g = h.kg;
     double V = h.box_L[0] * h.box_L[1] * h.box_L[2];
-    double cst = 4.0 / V * kPi * kOne4PiEps0;   // RCK:517
+    double cst = 4.0 / V * kPi * h.ke;   // RCK:517
     int total = g.KX * g.NY * g.KZ;
     h.e_rec_nblk = nblk(total, 256);
     hipLaunchKernelGGL(k_coeffs, dim3(h.e_rec_nblk), dim3(256), 0, h.stream, g, recip_vec(h), cst,
@@ -800,7 +800,7 @@ __global__ void __launch_bounds__(256) k_dforce(int64_t K, int lo, int nown, con
 
 void launch_kspace_kvec(Handle& h) {
     double V = h.box_L[0] * h.box_L[1] * h.box_L[2];
-    double cst = 4.0 / V * kPi * kOne4PiEps0;
+    double cst = 4.0 / V * kPi * h.ke;
     hipLaunchKernelGGL(k_kvec, dim3(nblk(h.khalf, 256)), dim3(256), 0, h.stream, h.khalf, h.kg, recip_vec(h), cst,
                        1.0 / (h.alpha * h.alpha), h.kvec);
 }

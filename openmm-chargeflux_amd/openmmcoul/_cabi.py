@@ -23,7 +23,8 @@ CF_PRECISION_DOUBLE = 0
 CF_PRECISION_MIXED = 1
 CF_INCLUDE_FORCES = 1
 CF_INCLUDE_ENERGY = 2
-ONE_4PI_EPS0 = 138.935456
+ONE_4PI_EPS0 = 138.935456                    # OpenMM 7.x headers: cf_params.one_4pi_eps0 = 0
+ONE_4PI_EPS0_CODATA2018 = 138.93545764438198  # OpenMM 8.x headers (CODATA 2018)
 
 
 class cf_params(C.Structure):
@@ -47,6 +48,7 @@ class cf_params(C.Structure):
         ("cutoff", C.c_double),
         ("ewald_tol", C.c_double),
         ("default_box", C.c_double * 9),
+        ("one_4pi_eps0", C.c_double),
     ]
 
 

@@ -165,9 +165,10 @@ class CoulForce:
             "fwater_par": np.asarray(self._fwater_par, f64).reshape(-1, 5),
         }
 
-    def to_cparams(self, default_box=None):
+    def to_cparams(self, default_box=None, one_4pi_eps0=0.0):
         """Build the C-ABI cf_params.  Returns (params, keepalive) — keep the second
-        object alive while the struct is in use."""
+        object alive while the struct is in use.  one_4pi_eps0: the Coulomb constant of the
+        OpenMM the force is evaluated for (0 = 138.935456, the OpenMM 7.x value; include/chargeflux.h)."""
         a = {k: np.ascontiguousarray(v) for k, v in self.arrays().items()}
         p = _cabi.cf_params()
         dp = lambda x: x.ctypes.data_as(C.POINTER(C.c_double))
@@ -188,6 +189,7 @@ class CoulForce:
         box = np.zeros(9) if default_box is None else np.asarray(default_box, np.float64).reshape(9)
         for k in range(9):
             p.default_box[k] = float(box[k])
+        p.one_4pi_eps0 = float(one_4pi_eps0)
         return p, a
 
     @staticmethod

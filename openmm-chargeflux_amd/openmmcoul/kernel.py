@@ -76,8 +76,12 @@ class HipCalcCoulForceKernel:
     KSPACE_GRID = 2         # same k-sum via ES-kernel grid (spread, pruned DFT, interpolate)
 
     def __init__(self, device: int = 0, stream=None, rank: int = 0, world_size: int = 1, kspace_algo: int = 0,
-                 grid_width: int = 0, precision: str = "double"):
+                 grid_width: int = 0, precision: str = "double", one_4pi_eps0: float = 0.0):
+        """one_4pi_eps0: ONE_4PI_EPS0 of the OpenMM the force is evaluated for (the reference
+        takes it from openmm/reference/SimTKOpenMMRealType.h, ReferenceCoulKernels.cpp:7);
+        0 = 138.935456 (OpenMM 7.x), _cabi.ONE_4PI_EPS0_CODATA2018 for OpenMM 8.x."""
         self._lib = _cabi.load_library()
+        self._ke = float(one_4pi_eps0)
         self._grid_width = grid_width
         if precision not in ("double", "mixed"):
             raise ValueError("precision must be 'double' or 'mixed'")
@@ -97,7 +101,7 @@ class HipCalcCoulForceKernel:
                                         "System and CoulForce have different numbers of particles")
         a, b, c = system.getDefaultPeriodicBoxVectors()
         box = np.array([a, b, c], dtype=np.float64).reshape(9)
-        params, keep = force.to_cparams(box)
+        params, keep = force.to_cparams(box, self._ke)
         opt = _cabi.cf_options()
         opt.device = self._device
         opt.stream = C.c_void_p(self._stream) if self._stream else None
@@ -116,7 +120,7 @@ class HipCalcCoulForceKernel:
         reference has no updateParametersInContext, SURVEY §8(f) #4)."""
         if force.getNumParticles() != self._n:
             raise _cabi.ChargeFluxError(_cabi.CF_ERR_INVALID, "the number of particles has changed")
-        params, keep = force.to_cparams()
+        params, keep = force.to_cparams(None, self._ke)
         _cabi.check(self._lib.cf_update_parameters(self._h, C.byref(params)), self._lib)
         del keep
 
@@ -289,7 +293,7 @@ class Context:
     force-group test of CoulForceImpl::calcForcesAndEnergy (CoulForceImpl.cpp:23-27)."""
 
     def __init__(self, system: System, device: int = 0, kspace_algo: int = 0, grid_width: int = 0,
-                 precision: str = "double"):
+                 precision: str = "double", one_4pi_eps0: float = 0.0):
         self._system = system
         self._n = system.getNumParticles()
         self._pos = np.zeros((self._n, 3))
@@ -298,8 +302,8 @@ class Context:
         self._impls = []
         for f in system.getForces():
             if isinstance(f, CoulForce):
-                k = HipCalcCoulForceKernel(device=device, kspace_algo=kspace_algo,
-                                           grid_width=grid_width, precision=precision).initialize(system, f)
+                k = HipCalcCoulForceKernel(device=device, kspace_algo=kspace_algo, grid_width=grid_width,
+                                           precision=precision, one_4pi_eps0=one_4pi_eps0).initialize(system, f)
                 self._impls.append((f, k))
 
     def setPositions(self, positions):

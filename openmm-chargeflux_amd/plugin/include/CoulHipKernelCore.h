@@ -38,6 +38,10 @@ struct Options {
     int precision = CF_PRECISION_DOUBLE;   // OpenMM platform property "Precision": "double" / "mixed"
     int rank = 0, world_size = 1;
     double neighbor_skin = 0.0;            // nm; 0 = rebuild every call like the reference
+    // ONE_4PI_EPS0 of the OpenMM this kernel is loaded into (the reference compiles it in from
+    // openmm/reference/SimTKOpenMMRealType.h, ReferenceCoulKernels.cpp:7; the plugin's OpenMM layer
+    // sets it the same way, src/HipCoulKernels.cpp).  0 = CF_ONE_4PI_EPS0 (OpenMM 7.x).
+    double one_4pi_eps0 = 0.0;
 };
 
 class KernelCore {
@@ -51,6 +55,7 @@ public:
     template <class ForceT>
     void initialize(const ForceT& force, int num_particles, const double default_box[9], const Options& o) {
         ForceArrays a = marshal(force, num_particles, default_box);
+        a.one_4pi_eps0 = o.one_4pi_eps0;
         cf_params p = a.params();
         cf_options opt;
         std::memset(&opt, 0, sizeof(opt));
@@ -66,6 +71,7 @@ public:
         if (o.neighbor_skin > 0) check(cf_set_neighbor_skin(h_, o.neighbor_skin), "cf_set_neighbor_skin");
         n_ = num_particles;
         pbc_ = a.use_pbc != 0;
+        ke_ = o.one_4pi_eps0;
     }
 
     // updateParametersInContext -> copyParametersToContext (the reference has none):
@@ -74,6 +80,7 @@ public:
     void copy_parameters(const ForceT& force) {
         require();
         ForceArrays a = marshal(force, n_, nullptr);
+        a.one_4pi_eps0 = ke_;
         cf_params p = a.params();
         check(cf_update_parameters(h_, &p), "cf_update_parameters");
     }
@@ -113,6 +120,7 @@ private:
     cf_handle* h_ = nullptr;
     int n_ = 0;
     bool pbc_ = false;
+    double ke_ = 0.0;
 };
 
 }  // namespace coulhip

@@ -32,6 +32,7 @@ struct ForceArrays {
     int32_t use_pbc = 0;
     double cutoff = 1.0, ewald_tol = 1e-4;
     double default_box[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    double one_4pi_eps0 = 0.0;   // the loading OpenMM's ONE_4PI_EPS0 (0 = CF_ONE_4PI_EPS0)
 
     // cf_params pointing into this object's vectors (valid while it lives, unmodified)
     cf_params params() const {
@@ -56,6 +57,7 @@ struct ForceArrays {
         p.cutoff = cutoff;
         p.ewald_tol = ewald_tol;
         std::memcpy(p.default_box, default_box, sizeof(default_box));
+        p.one_4pi_eps0 = one_4pi_eps0;
         return p;
     }
 };

@@ -38,6 +38,7 @@ struct cfo_state {
     int* ex_start; int* ex_list; /* per-atom sorted unique exclusion sets RCK:385-391 */
     int pbc;
     double cutoff, tol, alpha, one_alpha2;
+    double ke;         /* ONE_4PI_EPS0 of the OpenMM evaluated for (RCK:7; cf_params.one_4pi_eps0) */
     int kmax[3];
 };
 
@@ -135,6 +136,8 @@ cfo_state* cfo_create(const cf_params* p, char* err, int errlen) {
     free(s->ex_start); s->ex_start = newstart;
     free(tmp); free(fill); free(cnt);
 
+    if (!(p->one_4pi_eps0 >= 0) || !isfinite(p->one_4pi_eps0)) { set_err(err, errlen, "one_4pi_eps0 must be finite and >= 0"); cfo_destroy(s); return NULL; }
+    s->ke = p->one_4pi_eps0 == 0 ? CF_ONE_4PI_EPS0 : p->one_4pi_eps0;
     s->pbc = p->use_pbc ? 1 : 0;
     if (s->pbc) {
         const double* b = p->default_box;
@@ -345,17 +348,17 @@ static void real_pair(cfo_state* s, int ii, int jj, const double* pos, const dou
     double qi = s->realq[ii], qj = s->realq[jj];
     double erfc_ar = erfc(ar);
     if (c->include_forces) {
-        double dEdR = CF_ONE_4PI_EPS0 * qi * qj * inv_r * inv_r * inv_r;
+        double dEdR = s->ke * qi * qj * inv_r * inv_r * inv_r;
         dEdR *= erfc_ar + ar * exp(-ar * ar) * 2.0 / sqrt(M_PI);
         dEdR += es6 * (12 * sig6 - 6) * inv_r * inv_r;
         for (int k = 0; k < 3; k++) {
             double f = dEdR * d[k];
             c->forces[3 * ii + k] += f; c->forces[3 * jj + k] -= f;
         }
-        c->dedq[ii] += CF_ONE_4PI_EPS0 * qj * inv_r * erfc_ar;
-        c->dedq[jj] += CF_ONE_4PI_EPS0 * qi * inv_r * erfc_ar;
+        c->dedq[ii] += s->ke * qj * inv_r * erfc_ar;
+        c->dedq[jj] += s->ke * qi * inv_r * erfc_ar;
     }
-    c->energy += CF_ONE_4PI_EPS0 * qi * qj * inv_r * erfc_ar + es6 * (sig6 - 1);
+    c->energy += s->ke * qi * qj * inv_r * erfc_ar + es6 * (sig6 - 1);
 }
 
 /* reciprocal half-space loop, RCK:513-556.  Visits k-vectors [k_lo, k_hi) of the
@@ -365,7 +368,7 @@ static int64_t recip_sum(cfo_state* s, const double* pos, const double* L, int i
                          int64_t k_hi) {
     int n = s->n;
     double rx = 2 * M_PI / L[0], ry = 2 * M_PI / L[1], rz = 2 * M_PI / L[2];
-    double constant = 4.0 / L[0] / L[1] / L[2] * M_PI * CF_ONE_4PI_EPS0;   /* RCK:517 */
+    double constant = 4.0 / L[0] / L[1] / L[2] * M_PI * s->ke;   /* RCK:517 */
     double energy = 0;
     int64_t visited = 0;
     int minky = 0, minkz = 1;
@@ -434,13 +437,13 @@ static double execute_impl(cfo_state* s, const double* pos, const double* box9, 
                 double d[3]; delta_r(pos + 3 * ii, pos + 3 * jj, L, 0, d);   /* pos[jj]-pos[ii] */
                 double inv_r = 1.0 / sqrt(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]);
                 double sig6, es6; lj_terms(s, ii, jj, inv_r, &sig6, &es6);
-                double qq = CF_ONE_4PI_EPS0 * s->realq[ii] * s->realq[jj] * inv_r;
+                double qq = s->ke * s->realq[ii] * s->realq[jj] * inv_r;
                 if (include_energy) { energy += qq; energy += es6 * (sig6 - 1); }
                 if (include_forces) {
                     double dEdR = (es6 * (12 * sig6 - 6) + qq) * inv_r * inv_r;
                     for (int k = 0; k < 3; k++) { forces[3 * ii + k] -= dEdR * d[k]; forces[3 * jj + k] += dEdR * d[k]; }
-                    dedq[ii] += CF_ONE_4PI_EPS0 * s->realq[jj] * inv_r;
-                    dedq[jj] += CF_ONE_4PI_EPS0 * s->realq[ii] * inv_r;
+                    dedq[ii] += s->ke * s->realq[jj] * inv_r;
+                    dedq[jj] += s->ke * s->realq[ii] * inv_r;
                 }
             }
         for (int p1 = 0; p1 < n; p1++)
@@ -450,21 +453,21 @@ static double execute_impl(cfo_state* s, const double* pos, const double* box9, 
                 double d[3]; delta_r(pos + 3 * p1, pos + 3 * p2, L, 0, d);
                 double inv_r = 1.0 / sqrt(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]);
                 double sig6, es6; lj_terms(s, p1, p2, inv_r, &sig6, &es6);
-                double qq = CF_ONE_4PI_EPS0 * s->realq[p1] * s->realq[p2] * inv_r;
+                double qq = s->ke * s->realq[p1] * s->realq[p2] * inv_r;
                 if (include_energy) { energy -= qq; energy -= es6 * (sig6 - 1); }
                 if (include_forces) {
                     double dEdR = (es6 * (12 * sig6 - 6) + qq) * inv_r * inv_r;
                     for (int c = 0; c < 3; c++) { forces[3 * p1 + c] += dEdR * d[c]; forces[3 * p2 + c] -= dEdR * d[c]; }
-                    dedq[p1] -= CF_ONE_4PI_EPS0 * s->realq[p2] * inv_r;
-                    dedq[p2] -= CF_ONE_4PI_EPS0 * s->realq[p1] * inv_r;
+                    dedq[p1] -= s->ke * s->realq[p2] * inv_r;
+                    dedq[p2] -= s->ke * s->realq[p1] * inv_r;
                 }
             }
         if (terms) terms[2] = energy;
     } else {
         double e_self = 0, e_recip = 0, e_real = 0, e_excl = 0;
         for (int i = 0; i < n; i++) {                                   /* RCK:507-510 */
-            e_self -= CF_ONE_4PI_EPS0 * s->realq[i] * s->realq[i] * s->alpha / sqrt(M_PI);
-            dedq[i] += -2 * CF_ONE_4PI_EPS0 * s->alpha / sqrt(M_PI) * s->realq[i];
+            e_self -= s->ke * s->realq[i] * s->realq[i] * s->alpha / sqrt(M_PI);
+            dedq[i] += -2 * s->ke * s->alpha / sqrt(M_PI) * s->realq[i];
         }
         double t1 = now_s();
         recip_sum(s, pos, L, include_forces, include_energy, forces, dedq, &e_recip, kspace_limit);
@@ -482,13 +485,13 @@ static double execute_impl(cfo_state* s, const double* pos, const double* box9, 
                 double inv_r = 1.0 / r, ar = s->alpha * r;
                 double erf_ar = erf(ar);
                 if (include_forces) {
-                    double dEdR = CF_ONE_4PI_EPS0 * s->realq[p1] * s->realq[p2] * inv_r * inv_r * inv_r;
+                    double dEdR = s->ke * s->realq[p1] * s->realq[p2] * inv_r * inv_r * inv_r;
                     dEdR *= erf_ar - ar * exp(-ar * ar) * 2.0 / sqrt(M_PI);
                     for (int c = 0; c < 3; c++) { forces[3 * p1 + c] -= dEdR * d[c]; forces[3 * p2 + c] += dEdR * d[c]; }
-                    dedq[p1] -= CF_ONE_4PI_EPS0 * s->realq[p2] * inv_r * erf_ar;
-                    dedq[p2] -= CF_ONE_4PI_EPS0 * s->realq[p1] * inv_r * erf_ar;
+                    dedq[p1] -= s->ke * s->realq[p2] * inv_r * erf_ar;
+                    dedq[p2] -= s->ke * s->realq[p1] * inv_r * erf_ar;
                 }
-                e_excl -= CF_ONE_4PI_EPS0 * s->realq[p1] * s->realq[p2] * inv_r * erf_ar;
+                e_excl -= s->ke * s->realq[p1] * s->realq[p2] * inv_r * erf_ar;
             }
         energy = e_self + e_recip + e_real + e_excl;                    /* RCK:633 */
         if (terms) { terms[0] = e_self; terms[1] = e_recip; terms[2] = e_real; terms[3] = e_excl; }

@@ -54,11 +54,11 @@ def _dp(a):
 class Oracle:
     """Reference-semantics evaluator of a CoulForce (ReferenceCoulKernels.cpp:230-636)."""
 
-    def __init__(self, force, default_box=None):
+    def __init__(self, force, default_box=None, one_4pi_eps0=0.0):
         # build the same cf_params the product consumes (layout from include/chargeflux.h)
         import sys
         sys.path.insert(0, os.path.join(os.path.dirname(HERE), "openmm-chargeflux_amd"))
-        params, self._keep = force.to_cparams(default_box)
+        params, self._keep = force.to_cparams(default_box, one_4pi_eps0)   # 0: 138.935456 (OpenMM 7.x)
         err = C.create_string_buffer(256)
         self._h = lib().cfo_create(C.byref(params), err, 256)
         if not self._h:

@@ -1,0 +1,109 @@
+"""The Coulomb constant is the loading OpenMM's ONE_4PI_EPS0, not a compiled-in number.
+
+The reference takes k_e from the OpenMM it is compiled against
+(openmm/reference/SimTKOpenMMRealType.h, included at ReferenceCoulKernels.cpp:7 and used at
+:508, :517, :580-589, :608-619): 138.935456 in OpenMM 7.x headers and 138.93545764438198
+(CODATA 2018) in OpenMM 8.x.  The two differ by 1.18e-8 relative, i.e. ~2e-5 kJ/mol/nm at C3's
+largest forces: above the north star's 1e-5 bar.  cf_params.one_4pi_eps0 carries the value
+(0 = 138.935456); the oracle takes the same field.
+
+Tolerances (written here): exact k-sum vs oracle at the same k_e, forces <= 1e-8 kJ/mol/nm,
+energy <= 1e-9 |E| + 1e-8 (C2) or 1e-12 of sum |terms| (C3); the grid k-sum, forces <= 1e-6.
+Passing k_e = 138.935456 explicitly gives the same bits as the default (0).
+"""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+from oracle import Oracle  # noqa: E402
+from openmmcoul import HipCalcCoulForceKernel, _cabi  # noqa: E402
+from openmmcoul import testsystems as ts  # noqa: E402
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+KE8 = _cabi.ONE_4PI_EPS0_CODATA2018
+EXACT, GRID = HipCalcCoulForceKernel.KSPACE_EXACT_MFMA, HipCalcCoulForceKernel.KSPACE_GRID
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+
+
+@pytest.mark.parametrize("algo,f_tol", [(EXACT, 1e-8), (GRID, 1e-6)])
+def test_c2_at_openmm8_constant_matches_oracle(algo, f_tol):
+    system, force, pos, box = ts.make("C2")
+    k = HipCalcCoulForceKernel(kspace_algo=algo, one_4pi_eps0=KE8).initialize(system, force)
+    e, f = k.execute_host(pos, box)
+    ref = Oracle(force, box, one_4pi_eps0=KE8).execute(pos, box)
+    assert np.abs(f - ref["forces"]).max() <= f_tol
+    assert abs(e - ref["energy"]) <= 1e-9 * abs(ref["energy"]) + 1e-8
+    assert np.abs(k.dedq() - ref["dedq"]).max() <= 1e-10 * np.abs(ref["dedq"]).max()
+    # and the constant matters: the 7.x-constant answer is farther from this one than the bar
+    ref7 = Oracle(force, box).execute(pos, box)
+    assert np.abs(ref7["forces"] - ref["forces"]).max() > 10 * f_tol or algo == GRID
+
+
+def test_c1_no_pbc_at_openmm8_constant():
+    system, force, pos, box = ts.cluster_c1()
+    e, f = HipCalcCoulForceKernel(one_4pi_eps0=KE8).initialize(system, force).execute_host(pos, None)
+    ref = Oracle(force, None, one_4pi_eps0=KE8).execute(pos, None)
+    assert np.abs(f - ref["forces"]).max() <= 1e-8
+    assert abs(e - ref["energy"]) <= 1e-9 * abs(ref["energy"]) + 1e-8
+
+
+@pytest.mark.parametrize("precision", ["double", "mixed"])
+def test_explicit_default_constant_is_bitwise_the_default(precision):
+    system, force, pos, box = ts.water_box(4000, cutoff=1.0, ewald_tol=1e-4, every_bond_angle=5)
+    outs = []
+    for ke in (0.0, _cabi.ONE_4PI_EPS0):
+        k = HipCalcCoulForceKernel(kspace_algo=GRID, precision=precision, one_4pi_eps0=ke).initialize(system, force)
+        outs.append(k.execute_host(pos, box))
+        k.destroy()
+    assert outs[0][0] == outs[1][0] and np.array_equal(outs[0][1], outs[1][1])
+
+
+def test_invalid_constant_and_update_keep_it():
+    system, force, pos, box = ts.make("C2")
+    with pytest.raises(_cabi.ChargeFluxError, match="one_4pi_eps0"):
+        HipCalcCoulForceKernel(one_4pi_eps0=-1.0).initialize(system, force)
+    with pytest.raises(_cabi.ChargeFluxError, match="one_4pi_eps0"):
+        HipCalcCoulForceKernel(one_4pi_eps0=float("nan")).initialize(system, force)
+    # a parameter update through the same kernel keeps its constant
+    k = HipCalcCoulForceKernel(one_4pi_eps0=KE8).initialize(system, force)
+    k.copyParametersToContext(force)
+    e, f = k.execute_host(pos, box)
+    ref = Oracle(force, box, one_4pi_eps0=KE8).execute(pos, box)
+    assert np.abs(f - ref["forces"]).max() <= 1e-8
+
+
+@pytest.mark.parametrize("algo,f_tol", [(EXACT, 1e-8), (GRID, 1e-6)])
+def test_c3_at_openmm8_constant_matches_oracle_fixture(algo, f_tol):
+    """Full-size C3 at k_e = 138.93545764438198 against the oracle's full-size run at the same
+    constant (tests/golden/c3_codata2018.npz, make_golden.py --c3-codata2018): a seeded
+    2 000-atom subset of forces / dE/dq / charges, the energy terms, force sum and sum of squares."""
+    import hashlib
+    d = np.load(os.path.join(GOLDEN, "c3_codata2018.npz"))
+    assert float(d["one_4pi_eps0"]) == KE8
+    system, force, pos, box = ts.make("C3")
+    assert hashlib.sha256(pos.tobytes()).hexdigest() == str(d["pos_sha256"])
+    k = HipCalcCoulForceKernel(kspace_algo=algo, one_4pi_eps0=KE8).initialize(system, force)
+    e, f = k.execute_host(pos, box)
+    sub = d["subset"]
+    scale = np.abs(d["terms"]).sum()
+    assert abs(e - float(d["energy"])) <= 1e-12 * scale + 1e-8
+    assert np.abs(f[sub] - d["forces"]).max() <= f_tol
+    assert np.abs(f.sum(0) - d["force_sum"]).max() <= f_tol * np.sqrt(len(f))
+    assert abs((f ** 2).sum() - float(d["force_sq"])) <= 1e-9 * float(d["force_sq"])
+    dq = k.dedq()
+    assert np.abs(dq[sub] - d["dedq"]).max() <= (1e-10 if algo == EXACT else 1e-9) * np.abs(d["dedq"]).max() + 1e-9
+    for a, b in zip(k.energy_terms(), d["terms"]):
+        assert abs(a - b) <= 1e-10 * max(abs(b), 1.0)
+    # the two OpenMM constants give C3 forces that differ by more than the 1e-5 bar
+    d7 = np.load(os.path.join(GOLDEN, "c3.npz"))
+    assert np.abs(d7["forces"] - d["forces"]).max() > 1e-5

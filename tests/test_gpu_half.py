@@ -109,6 +109,54 @@ def test_half_list_fallback_on_fixed_point_range():
     assert abs(e - ref["energy"]) <= 1e-9 * np.abs(ref["terms"]).sum() + 1e-8
 
 
+def _sparse_gas():
+    # 300 waters at 1/8 of water density, rc 0.7 + skin 0.1: 5 cells per axis with ~7 atoms per
+    # cell, so 64 consecutive cell-sorted atoms span more cells than the box has along z -- the
+    # wave builder's block frame does not fit and those rows cannot use the half list
+    return ts.water_box(300, cutoff=0.7, ewald_tol=1e-4, density=ts.WATER_DENSITY / 8, every_bond_angle=3)
+
+
+def _dense_overflow():
+    # list capacity sized for a 16x lower density (as test_half_list_fallback_on_list_overflow)
+    system, force, pos, box = ts.water_box(4000, cutoff=1.0, ewald_tol=1e-4)
+    system.setDefaultPeriodicBoxVectors(*[[2.5 * box[i][j] for j in range(3)] for i in range(3)])
+    return system, force, pos, box
+
+
+@pytest.mark.parametrize("make", [_sparse_gas, _dense_overflow], ids=["block_frame_misfit", "list_overflow"])
+def test_half_list_fallbacks_persist_over_kept_lists(make):
+    """A fallback raised when the list is BUILT (rows the builder could not encode, overflowed
+    rows) must hold on every later evaluation that keeps that list under a skin: each step is
+    compared with the full list rebuilt from scratch (CF_HALF=0, skin 0) on the same positions."""
+    system, force, pos, box = make()
+    k = _kernel(system, force, True, skin=0.1)
+    ref = _kernel(system, force, False)
+    rng = np.random.default_rng(11)
+    x = pos.copy()
+    for step in range(5):
+        e, f = k.execute_host(x, box)
+        ef, ff = ref.execute_host(x, box)
+        assert np.abs(f - ff).max() <= 1e-9, (step, np.abs(f - ff).max())
+        assert abs(e - ef) <= 1e-12 * abs(ef) + 1e-9, (step, e, ef)
+        x = x + rng.normal(scale=0.002, size=x.shape)
+    builds, evals = k.neighbor_stats()
+    assert evals == 5 and builds < evals   # the later steps did keep the list
+
+
+def test_half_list_sparse_gas_matches_oracle_with_skin():
+    system, force, pos, box = _sparse_gas()
+    k = _kernel(system, force, True, skin=0.1)
+    orc = Oracle(force, box)
+    x = pos.copy()
+    rng = np.random.default_rng(3)
+    for _ in range(3):
+        e, f = k.execute_host(x, box)
+        r = orc.execute(x, box)
+        assert np.abs(f - r["forces"]).max() <= 1e-8
+        assert abs(e - r["energy"]) <= 1e-9 * np.abs(r["terms"]).sum() + 1e-8
+        x = x + rng.normal(scale=0.002, size=x.shape)
+
+
 def test_half_list_mixed_precision():
     # the fp32 half-list kernel against the fp32 full list and the fp64 half list (same k-space)
     system, force, pos, box = ts.water_box(4000, cutoff=1.0, ewald_tol=1e-4, every_bond_angle=5)

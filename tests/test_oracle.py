@@ -180,3 +180,24 @@ def test_triclinic_zero_shear_equals_orthorhombic():
     r1 = o.execute(pos, box)
     r2 = o.execute(pos, np.diag(np.diag(box)))
     assert r1["energy"] == r2["energy"] and np.array_equal(r1["forces"], r2["forces"])
+
+
+def test_coulomb_constant_is_a_parameter():
+    """k_e (ONE_4PI_EPS0 of the loading OpenMM, ReferenceCoulKernels.cpp:7) enters every
+    electrostatic term linearly and nothing else: E(k_e) = k_e E_c + E_LJ, likewise F and dE/dq
+    (charges and dq/dx do not depend on it).  0 selects 138.935456 with identical bits; the C2
+    golden fixture (made at 138.935456) is reproduced bit-for-bit by the explicit value."""
+    system, force, pos, box = ts.water_box(200, cutoff=0.8, ewald_tol=1e-4, every_bond_angle=3)
+    r0 = Oracle(force, box).execute(pos, box)
+    rd = Oracle(force, box, one_4pi_eps0=ONE_4PI_EPS0).execute(pos, box)
+    assert r0["energy"] == rd["energy"] and np.array_equal(r0["forces"], rd["forces"])
+    ks = [100.0, 138.93545764438198, 200.0]
+    rs = [Oracle(force, box, one_4pi_eps0=k).execute(pos, box) for k in ks]
+    for key in ("energy", "forces", "dedq"):
+        a, b, c = (np.asarray(r[key], np.float64) for r in rs)
+        slope = (c - a) / (ks[2] - ks[0])
+        pred = a + slope * (ks[1] - ks[0])
+        assert np.abs(pred - b).max() <= 1e-9 * max(1.0, np.abs(b).max()), key
+    assert np.array_equal(rs[0]["charges"], rs[2]["charges"])
+    with pytest.raises(ValueError, match="one_4pi_eps0"):
+        Oracle(force, box, one_4pi_eps0=-1.0)
