@@ -289,6 +289,14 @@ def main():
     timing = kern.kernel.timing()
     builds1, evals1 = kern.kernel.neighbor_stats()
     kern.kernel.set_timing(False)
+    # force-evaluation pass (after the timed region, not part of it): K more MD steps with two
+    # torch events around each execute (the library's stream is torch's current stream) and no
+    # library timing at all -> ms_per_force_eval without instrumentation
+    ev.clear()
+    for _ in range(args.steps):
+        energy = step(True)
+    torch.cuda.synchronize()
+    ms_eval_clean = float(np.mean([a.elapsed_time(b) for a, b in ev])) if ev else float("nan")
     kern.synchronize()   # energy all-reduce still in flight (multi-rank)
     e_final = energy.item()
     ms_step = elapsed / args.steps * 1e3
@@ -415,11 +423,14 @@ def main():
                                   2: f"grid (ES kernel W={w_grid}, pruned DFT), same k-set"}[args.kspace_algo],
                        "nlist_builds_in_timed_steps": f"{builds1 - builds0}/{evals1 - evals0}",
                        "parallelism": f"atom-decomposition x{world}" + (" (RCCL all-reduce of S(k))" if world > 1 else "")},
-            "ms_per_force_eval": round(ms_eval, 4),
+            "ms_per_force_eval": round(ms_eval_clean, 4),
+            "ms_per_force_eval_instrumented": round(ms_eval, 4),
             "energy_kj_mol": e_final,
             "kernels_ms_per_step": {k: round(v, 4) for k, v in per_step.items()},
-            "timing_note": (f"value: K steps with HIP events around {dom} launches only; kernels_ms_per_step and "
-                            f"ms_per_force_eval: a separate K-step pass with every phase bracketed by events"),
+            "timing_note": (f"value: K steps with HIP events around {dom} launches only; ms_per_force_eval: a "
+                            f"separate K-step pass with two events around each execute and no library timing; "
+                            f"kernels_ms_per_step and ms_per_force_eval_instrumented: a K-step pass with every "
+                            f"phase bracketed by events"),
             "roofline": roofline,
             "kernels_roofline": others,
             "exact_kspace": exact,
@@ -427,7 +438,7 @@ def main():
             "cpu_baseline": cpu,
         }
         if cpu:
-            out["speedup_vs_cpu_force_eval"] = round(cpu["ms_per_force_eval"] / ms_eval, 1)
+            out["speedup_vs_cpu_force_eval"] = round(cpu["ms_per_force_eval"] / ms_eval_clean, 1)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

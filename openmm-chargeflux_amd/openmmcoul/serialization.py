@@ -1,20 +1,22 @@
 """XML serialization of CoulForce (the reference registers no
 SerializationProxy, so a System holding this force cannot be saved or reloaded).
 
-The format follows OpenMM's proxy conventions (one element named after the force with a
-``version`` attribute, parameters as attributes, one child list per kind of entry), so a C++
-``CoulForceProxy`` for OpenMM's ``XmlSerializer`` would read and write the same document:
+The document is the one OpenMM's ``XmlSerializer`` writes for a force with the plugin's C++
+``CoulForceProxy`` (openmm-chargeflux_amd/plugin/src/CoulForceProxy.cpp): root element ``Force``
+with ``type="CoulForce"`` and a ``version``, parameters as attributes, one child list per kind
+of entry (tests/test_plugin_openmm.py reads each side's output with the other):
 
-    <CoulForce version="1" forceGroup="0" cutoff="1.0" ewaldTolerance="0.0001" usesPeriodic="1">
+    <Force type="CoulForce" version="1" forceGroup="0" cutoff="1.0" ewaldTolerance="0.0001" usesPeriodic="1">
       <Particles>   <Particle q=".." sig=".." eps=".."/> ...           CoulForce.cpp:18-38
       <Exceptions>  <Exception p1=".." p2=".."/> ...                   CoulForce.cpp:56-68
       <FluxBonds>   <FluxBond p1 p2 k b/> ...                          CoulForce.cpp:78-94
       <FluxAngles>  <FluxAngle p1 p2 p3 k theta/> ...                  CoulForce.cpp:96-114
       <FluxWaters>  <FluxWater po ph1 ph2 k1 k2 kub b0 ub0/> ...       CoulForce.cpp:116-140
-    </CoulForce>
+    </Force>
 
-Floats are written with ``repr`` (shortest round-trip form), so deserialize(serialize(f))
-reproduces every parameter bit for bit.
+Floats are written with ``repr`` (shortest round-trip form; the C++ proxy writes 17 significant
+digits), so either reader reproduces every parameter bit for bit.  The round-2 form of this
+file, root element ``<CoulForce ...>`` without ``type``, is still read.
 """
 from __future__ import annotations
 
@@ -37,7 +39,8 @@ class XmlSerializer:
     def serialize(force: CoulForce) -> str:
         if not isinstance(force, CoulForce):
             raise TypeError("XmlSerializer.serialize expects a CoulForce")
-        root = ET.Element("CoulForce", {
+        root = ET.Element("Force", {
+            "type": "CoulForce",
             "version": str(VERSION),
             "forceGroup": str(force.getForceGroup()),
             "cutoff": _f(force.getCutoffDistance()),
@@ -72,8 +75,8 @@ class XmlSerializer:
     @staticmethod
     def deserialize(text: str) -> CoulForce:
         root = ET.fromstring(text)
-        if root.tag != "CoulForce":
-            raise ValueError(f"not a CoulForce document (root element <{root.tag}>)")
+        if not (root.tag == "CoulForce" or root.get("type") == "CoulForce"):
+            raise ValueError(f"not a CoulForce document (root element <{root.tag}>, type {root.get('type')!r})")
         version = int(root.get("version", "0"))
         if version < 1 or version > VERSION:
             raise ValueError(f"unsupported CoulForce serialization version {version}")

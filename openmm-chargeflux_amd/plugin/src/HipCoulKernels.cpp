@@ -3,7 +3,10 @@
 // Positions, forces and box come from the host platform's data the same way the Reference
 // kernel reads them (ReferenceCoulKernels.cpp:14-27): a ReferencePlatform::PlatformData whose
 // vector<Vec3> buffers are three contiguous doubles per particle, so they cross the C-ABI as
-// [N*3] arrays; forces are ADDED (cf_compute_host), the energy is returned.
+// [N*3] arrays; forces are ADDED (cf_compute_host), the energy is returned.  The Coulomb
+// constant is the ONE_4PI_EPS0 of the OpenMM this file is compiled against -- the header the
+// reference itself takes it from (ReferenceCoulKernels.cpp:7) -- so the two agree whatever the
+// OpenMM version (138.935456 in 7.x, 138.93545764438198 in 8.x).
 #include "HipCoulKernels.h"
 
 #include <vector>
@@ -13,6 +16,7 @@
 #include "openmm/Vec3.h"
 #include "openmm/internal/ContextImpl.h"
 #include "openmm/reference/ReferencePlatform.h"
+#include "openmm/reference/SimTKOpenMMRealType.h"
 
 using namespace CoulPlugin;
 using namespace OpenMM;
@@ -37,6 +41,12 @@ auto rethrow(F&& f) -> decltype(f()) {
 }
 
 }  // namespace
+
+HipCalcCoulForceKernel::HipCalcCoulForceKernel(std::string name, const Platform& platform,
+                                               const coulhip::Options& options)
+    : CalcCoulForceKernel(name, platform), options_(options) {
+    options_.one_4pi_eps0 = ONE_4PI_EPS0;
+}
 
 void HipCalcCoulForceKernel::initialize(const System& system, const CoulForce& force) {
     Vec3 a, b, c;

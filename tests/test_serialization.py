@@ -31,7 +31,7 @@ def test_round_trip_exact(which):
     f.setParticleParameters(0, 0.1 + 0.2, 1.0 / 3.0, 2.0 ** -40)
     f.setForceGroup(5)
     text = XmlSerializer.serialize(f)
-    assert text.startswith("<CoulForce") and 'version="1"' in text
+    assert text.startswith('<Force type="CoulForce"') and 'version="1"' in text
     g = XmlSerializer.deserialize(text)
     _same(f, g)
     assert XmlSerializer.serialize(g) == text
@@ -43,6 +43,11 @@ def test_empty_force_and_errors():
     _same(f, g)
     with pytest.raises(ValueError):
         XmlSerializer.deserialize("<NonbondedForce version='1'/>")
+    with pytest.raises(ValueError):
+        XmlSerializer.deserialize("<Force type='NonbondedForce' version='1'/>")
+    # the round-2 root element is still read
+    legacy = XmlSerializer.serialize(f).replace('<Force type="CoulForce"', "<CoulForce").replace("</Force>", "</CoulForce>")
+    _same(f, XmlSerializer.deserialize(legacy))
     with pytest.raises(ValueError):
         XmlSerializer.deserialize("<CoulForce version='99' cutoff='1' ewaldTolerance='1e-4' usesPeriodic='0'/>")
     with pytest.raises(TypeError):
