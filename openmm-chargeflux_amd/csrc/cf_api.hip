@@ -155,13 +155,20 @@ int find_root(std::vector<int>& p, int x) {
 
 void set_cells(cf_handle* H, const double L[3]) {
     cf::Handle& h = H->h;
+    // cells per lattice direction from the box's perpendicular widths (V / |b x c|, V / |c x a|,
+    // V / |a x b| for the reduced box a = (ax,0,0), b = (bx,by,0), c = (cx,cy,cz); the diagonal
+    // for an orthorhombic box): a cell at least rc + skin wide in every direction puts every
+    // partner of an atom in the 27 cells around its own, also for a sheared (triclinic) box,
+    // whose cells are parallelepipeds in fractional coordinates (cf_kernels_core.hip k_cell_hist)
+    const double bx = h.box_t[0], cx = h.box_t[1], cy = h.box_t[2];
+    const double V = L[0] * L[1] * L[2];
+    const double width[3] = {V / std::sqrt((L[1] * L[2]) * (L[1] * L[2]) + (bx * L[2]) * (bx * L[2]) +
+                                           (bx * cy - L[1] * cx) * (bx * cy - L[1] * cx)),
+                             L[1] * L[2] / std::sqrt(L[2] * L[2] + cy * cy), L[2]};
     int nc[3];
     for (int d = 0; d < 3; d++) {
-        double v = std::floor(L[d] / (h.cutoff + h.list_skin));
+        double v = std::floor((h.tric ? width[d] : L[d]) / (h.cutoff + h.list_skin));
         nc[d] = (int)std::max(1.0, std::min(v, 1024.0));
-        // reduced triclinic box: one cell, i.e. the all-pairs list with the box-vector minimum
-        // image (correct for any reduced box; O(N^2) per build -- the fast paths are orthorhombic)
-        if (h.tric) nc[d] = 1;
     }
     int64_t ncell = (int64_t)nc[0] * nc[1] * nc[2];
     if (ncell > h.ncell_alloc) {
@@ -547,6 +554,7 @@ CF_EXPORT int cf_create(const cf_params* p, const cf_options* opt, cf_handle** o
         if (h.pbc) {
             const cf::KGeom& g = h.kg;
             h.tric = p->default_box[3] != 0 || p->default_box[6] != 0 || p->default_box[7] != 0;
+            h.box_t[0] = p->default_box[3]; h.box_t[1] = p->default_box[6]; h.box_t[2] = p->default_box[7];
             set_cells(H, std::vector<double>{p->default_box[0], p->default_box[4], p->default_box[8]}.data());
             h.erfc_tab = dupload(H, cf::erfc_table(h.alpha * h.cutoff * (1.0 + 1e-9), &h.erfc_scale, &h.erfc_m));
             if (h.mixed) {

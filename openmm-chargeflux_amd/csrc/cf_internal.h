@@ -210,7 +210,7 @@ struct Handle {
     bool direct_done = false;   // cf_compute_direct already ran for the begun evaluation
     double box_L[3] = {0, 0, 0};
     double box_t[3] = {0, 0, 0};   // reduced triclinic box off-diagonals (bx, cx, cy); 0 = orthorhombic
-    bool tric = false;             // any off-diagonal nonzero: all-pairs neighbour list
+    bool tric = false;             // any off-diagonal nonzero: cells in fractional coordinates, box-vector minimum image
 };
 
 // ---- launchers (cf_kernels_*.hip) ------------------------------------------------

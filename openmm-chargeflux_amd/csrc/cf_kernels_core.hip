@@ -37,6 +37,27 @@ __device__ __forceinline__ double3 ld3(const double* p, int i) {
     return make_double3(p[3 * i], p[3 * i + 1], p[3 * i + 2]);
 }
 
+// The periodic lattice of OpenMM's reduced box: a = (L.x,0,0), b = (T.x,L.y,0), c = (T.y,T.z,L.z)
+// (T = (bx, cx, cy); all zero for an orthorhombic box, where every helper below reduces to the
+// per-axis form with the same bits: the T terms subtract exact zeros).
+// ka a + kb b + kc c
+__device__ __forceinline__ double3 lattice(double3 L, double3 T, double ka, double kb, double kc) {
+    return make_double3(ka * L.x + kb * T.x + kc * T.y, kb * L.y + kc * T.z, kc * L.z);
+}
+// fractional coordinates: x = s_a a + s_b b + s_c c
+__device__ __forceinline__ double3 fractional(double3 x, double3 L, double3 T) {
+    const double sc = x.z / L.z;
+    const double sb = (x.y - sc * T.z) / L.y;
+    const double sa = (x.x - sb * T.x - sc * T.y) / L.x;
+    return make_double3(sa, sb, sc);
+}
+// x moved by the lattice translation -(fl.x a + fl.y b + fl.z c); with fl = floor(fractional(x))
+// the result lies in the unit cell (fractional coordinates in [0, 1))
+__device__ __forceinline__ double3 wrap_by(double3 x, double3 fl, double3 L, double3 T) {
+    return make_double3(x.x - fl.x * L.x - fl.y * T.x - fl.z * T.y, x.y - fl.y * L.y - fl.z * T.z, x.z - fl.z * L.z);
+}
+__device__ __forceinline__ double3 floor3(double3 v) { return make_double3(floor(v.x), floor(v.y), floor(v.z)); }
+
 // ---------------------------------------------------------------------------------
 // 1. flux terms: one lane per term writes its charge deltas (slots) and its dq/dx
 //    block in the reference's entry order.  Bonds RCK:42-80, angles RCK:81-162,
@@ -179,7 +200,7 @@ __global__ void __launch_bounds__(256) k_atoms_prep(int n, const double* __restr
 // (own_cnt != null): also the owned atoms per cell and their scan, the first list row of each
 // cell, from which k_cell_order writes the owned rows in cell-sorted order.
 __global__ void __launch_bounds__(256) k_cell_hist(int n, const int* __restrict__ flag, const double* __restrict__ pos,
-                                                   double3 L, int3 nc, int* __restrict__ key, int* __restrict__ rank,
+                                                   double3 L, double3 T, int3 nc, int* __restrict__ key, int* __restrict__ rank,
                                                    int* __restrict__ cnt, int* __restrict__ ticket,
                                                    int* __restrict__ cstart, int* __restrict__ cend, int lo, int hi,
                                                    int* __restrict__ own_cnt, int* __restrict__ own_start) {
@@ -189,14 +210,17 @@ __global__ void __launch_bounds__(256) k_cell_hist(int n, const int* __restrict_
     const bool valid = i < n;
     int k = 0;
     if (valid) {
-        double3 x = ld3(pos, i);
-        double w[3] = {x.x - floor(x.x / L.x) * L.x, x.y - floor(x.y / L.y) * L.y, x.z - floor(x.z / L.z) * L.z};
-        double Ls[3] = {L.x, L.y, L.z};
+        // cells in fractional coordinates of the lattice-wrapped position (a sheared box's cells
+        // are parallelepipeds; nc per direction from the perpendicular widths, cf_api.hip set_cells)
+        const double3 x = ld3(pos, i);
+        const double3 wp = wrap_by(x, floor3(fractional(x, L, T)), L, T);
+        const double3 f = fractional(wp, L, T);
+        const double fs[3] = {f.x, f.y, f.z};
         int ncs[3] = {nc.x, nc.y, nc.z};
         int c[3];
 #pragma unroll
         for (int d = 0; d < 3; d++) {
-            int ci = (int)(w[d] / Ls[d] * ncs[d]);
+            int ci = (int)(fs[d] * ncs[d]);
             c[d] = ci < 0 ? 0 : (ci >= ncs[d] ? ncs[d] - 1 : ci);
         }
         k = (c[0] * nc.y + c[1]) * nc.z + c[2];
@@ -269,14 +293,15 @@ __global__ void __launch_bounds__(256) k_cell_order(int ncell, const int* __rest
 }
 
 // rebuild (flag set): commit the new order (scratch -> live), sorted wrapped (x,y,z,q) +
-// LJ, build positions.  wrap = 0 (reduced triclinic box, all-pairs list): unwrapped coordinates,
-// since a per-axis wrap by a diagonal is not a lattice translation there.  No rebuild: the sorted order and every atom's periodic image are
-// kept from the last build (wrap offsets recomputed from the build positions, so
-// bit-identical to the commit); only coordinates and flux charges are refreshed.
+// LJ, build positions.  Wrapped = moved into the unit cell by a lattice translation (for a
+// reduced triclinic box a per-axis wrap by the diagonal would not be one).  No rebuild: the
+// sorted order and every atom's periodic image are kept from the last build (the lattice
+// translation recomputed from the build positions, so bit-identical to the commit); only
+// coordinates and flux charges are refreshed.
 __global__ void __launch_bounds__(256) k_cell_commit(int n, const int* __restrict__ flag,
                                                      const int* __restrict__ key, const int* __restrict__ idx_new,
                                                      const double* __restrict__ pos, const double* __restrict__ q,
-                                                     const double2* __restrict__ lj, double3 L, int wrap,
+                                                     const double2* __restrict__ lj, double3 L, double3 T,
                                                      int* __restrict__ key_s, int* __restrict__ idx_s,
                                                      double4* __restrict__ pos4s, double2* __restrict__ ljs,
                                                      const int* __restrict__ atype, int* __restrict__ typ_s,
@@ -289,9 +314,8 @@ __global__ void __launch_bounds__(256) k_cell_commit(int n, const int* __restric
         key_s[s] = key[i];
         idx_s[s] = i;
         double3 x = ld3(pos, i);
-        p4 = wrap ? make_double4(x.x - floor(x.x / L.x) * L.x, x.y - floor(x.y / L.y) * L.y,
-                                 x.z - floor(x.z / L.z) * L.z, q[i])
-                  : make_double4(x.x, x.y, x.z, q[i]);
+        const double3 w = wrap_by(x, floor3(fractional(x, L, T)), L, T);
+        p4 = make_double4(w.x, w.y, w.z, q[i]);
         ljs[s] = lj[i];
         if (typ_s) typ_s[s] = atype[i];
         if (pos_ref) { pos_ref[3 * i] = x.x; pos_ref[3 * i + 1] = x.y; pos_ref[3 * i + 2] = x.z; }
@@ -299,9 +323,8 @@ __global__ void __launch_bounds__(256) k_cell_commit(int n, const int* __restric
     } else {
         int i = idx_s[s];
         double3 x = ld3(pos, i), r = ld3(pos_ref, i);
-        p4 = wrap ? make_double4(x.x - floor(r.x / L.x) * L.x, x.y - floor(r.y / L.y) * L.y,
-                                 x.z - floor(r.z / L.z) * L.z, q[i])
-                  : make_double4(x.x, x.y, x.z, q[i]);
+        const double3 w = wrap_by(x, floor3(fractional(r, L, T)), L, T);
+        p4 = make_double4(w.x, w.y, w.z, q[i]);
     }
     pos4s[s] = p4;
 }
@@ -445,21 +468,23 @@ __device__ __forceinline__ void scan_cells(const DirectArgs& a, int s, double4 p
         int key = a.key_sorted[s];
         int cz = key % a.nc.z, cy = (key / a.nc.z) % a.nc.y, cx = key / (a.nc.y * a.nc.z);
         for (int ox = -1; ox <= 1; ox++) {
-            int x = cx + ox; double sx = 0; int kx = ox + 1;
-            if (x < 0) { x += a.nc.x; sx = -a.L.x; kx = 0; } else if (x >= a.nc.x) { x -= a.nc.x; sx = a.L.x; kx = 2; } else kx = 1;
+            int x = cx + ox; int kx;
+            if (x < 0) { x += a.nc.x; kx = 0; } else if (x >= a.nc.x) { x -= a.nc.x; kx = 2; } else kx = 1;
             for (int oy = -1; oy <= 1; oy++) {
-                int y = cy + oy; double sy = 0; int ky;
-                if (y < 0) { y += a.nc.y; sy = -a.L.y; ky = 0; } else if (y >= a.nc.y) { y -= a.nc.y; sy = a.L.y; ky = 2; } else ky = 1;
+                int y = cy + oy; int ky;
+                if (y < 0) { y += a.nc.y; ky = 0; } else if (y >= a.nc.y) { y -= a.nc.y; ky = 2; } else ky = 1;
                 for (int oz = -1; oz <= 1; oz++) {
-                    int z = cz + oz; double sz = 0; int kz;
-                    if (z < 0) { z += a.nc.z; sz = -a.L.z; kz = 0; } else if (z >= a.nc.z) { z -= a.nc.z; sz = a.L.z; kz = 2; } else kz = 1;
+                    int z = cz + oz; int kz;
+                    if (z < 0) { z += a.nc.z; kz = 0; } else if (z >= a.nc.z) { z -= a.nc.z; kz = 2; } else kz = 1;
                     int code = kx * 9 + ky * 3 + kz;
                     int c = (x * a.nc.y + y) * a.nc.z + z;
                     if (ord++ % nparts != part) continue;
+                    // the image of the wrapped neighbour cell adjacent to this one (a lattice translate)
+                    const double3 sh = lattice(a.L, a.T, kx - 1, ky - 1, kz - 1);
                     int t1 = a.cend[c];
                     for (int t = a.cstart[c]; t < t1; t++) {
                         double4 pj = a.pos4s[t];
-                        double dx = pi.x - (pj.x + sx), dy = pi.y - (pj.y + sy), dz = pi.z - (pj.z + sz);
+                        double dx = pi.x - (pj.x + sh.x), dy = pi.y - (pj.y + sh.y), dz = pi.z - (pj.z + sh.z);
                         double r2 = dx * dx + dy * dy + dz * dz;
                         if (r2 > r2max || t == s) continue;
                         fn(t, code, dx, dy, dz, r2);
@@ -540,7 +565,6 @@ __global__ void __launch_bounds__(kWaveNL * kSeg) k_nlist_wave(DirectArgs a) {
     const int key0 = a.key_sorted[__shfl(s, 0)];
     const int c0[3] = {key0 / (a.nc.y * a.nc.z), (key0 / a.nc.z) % a.nc.y, key0 % a.nc.z};
     const int ncs[3] = {a.nc.x, a.nc.y, a.nc.z};
-    const double Ls[3] = {a.L.x, a.L.y, a.L.z};
     int lo3[3], hi3[3], lsh[3], ucell[3];
     bool fits = true;
 #pragma unroll
@@ -597,7 +621,8 @@ __global__ void __launch_bounds__(kWaveNL * kSeg) k_nlist_wave(DirectArgs a) {
 
     // block frame: every lane's position moved to the image of its unwrapped cell; origin =
     // lane 0 (lsh = 0 there), so frame coordinates stay within a few cells of 0
-    const double3 pu = make_double3(pi.x + lsh[0] * Ls[0], pi.y + lsh[1] * Ls[1], pi.z + lsh[2] * Ls[2]);
+    const double3 lu = lattice(a.L, a.T, lsh[0], lsh[1], lsh[2]);
+    const double3 pu = make_double3(pi.x + lu.x, pi.y + lu.y, pi.z + lu.z);
     const double3 org = make_double3(__shfl(pu.x, 0), __shfl(pu.y, 0), __shfl(pu.z, 0));
     const float3 pf = make_float3((float)(pu.x - org.x), (float)(pu.y - org.y), (float)(pu.z - org.z));
     const float rc2f = (float)(a.rl2 * (1.0 + 1e-5)) + 1e-6f;
@@ -622,7 +647,8 @@ __global__ void __launch_bounds__(kWaveNL * kSeg) k_nlist_wave(DirectArgs a) {
             w[d] -= (k[d] - 1) * ncs[d];
         }
         code = (k[0] - lsh[0]) * 9 + (k[1] - lsh[1]) * 3 + (k[2] - lsh[2]);  // relative to this lane's image
-        off = make_double3((k[0] - 1) * Ls[0] - org.x, (k[1] - 1) * Ls[1] - org.y, (k[2] - 1) * Ls[2] - org.z);
+        const double3 sh = lattice(a.L, a.T, k[0] - 1, k[1] - 1, k[2] - 1);
+        off = make_double3(sh.x - org.x, sh.y - org.y, sh.z - org.z);
         return (w[0] * a.nc.y + w[1]) * a.nc.z + w[2];
     };
     // This wave's candidates of a cell are the atoms whose index in the cell, in groups of 4
@@ -1041,7 +1067,8 @@ __device__ __forceinline__ int wrap_cell(int v, int n) { return v < 0 ? v + n : 
 // MIXED: the pair term in fp32 as in k_pairs_mixed (pair vector minimum-imaged in fp64, then
 // rounded; fp32 forces and dE/dq per lane, fp64 energy), the partner side in the same fixed
 // point (an fp32 value times 2^34 is exact in fp64)
-template <bool TYPES, bool MIXED>
+// TRIC: reduced triclinic box (the box-vector minimum image, min_image); else the per-axis form
+template <bool TYPES, bool MIXED, bool TRIC>
 __global__ void __launch_bounds__(1024) k_pairs_half(DirectArgs a) {
     __shared__ double tab[MIXED ? 1 : kErfcMaxM * (kErfcDeg + 1)];
     __shared__ float tabf[MIXED ? kErfcMaxMF * (kErfcDegF + 1) : 1];
@@ -1124,9 +1151,13 @@ __global__ void __launch_bounds__(1024) k_pairs_half(DirectArgs a) {
             };
             auto eval = [&](const Cand& cd) {
                 double dxd = pi.x - cd.p.x, dyd = pi.y - cd.p.y, dzd = pi.z - cd.p.z;
-                dxd -= a.L.x * rint(dxd * a.invL.x);
-                dyd -= a.L.y * rint(dyd * a.invL.y);
-                dzd -= a.L.z * rint(dzd * a.invL.z);
+                if constexpr (TRIC) {
+                    min_image(a, dxd, dyd, dzd);
+                } else {
+                    dxd -= a.L.x * rint(dxd * a.invL.x);
+                    dyd -= a.L.y * rint(dyd * a.invL.y);
+                    dzd -= a.L.z * rint(dzd * a.invL.z);
+                }
                 const float dx = (float)dxd, dy = (float)dyd, dz = (float)dzd;
                 const float r2 = fmaf(dx, dx, fmaf(dy, dy, dz * dz));
                 if (r2 <= rc2) {
@@ -1184,9 +1215,13 @@ __global__ void __launch_bounds__(1024) k_pairs_half(DirectArgs a) {
             };
             auto eval = [&](const Cand& cd) {
                 double dx = pi.x - cd.p.x, dy = pi.y - cd.p.y, dz = pi.z - cd.p.z;
-                dx -= a.L.x * rint(dx * a.invL.x);
-                dy -= a.L.y * rint(dy * a.invL.y);
-                dz -= a.L.z * rint(dz * a.invL.z);
+                if constexpr (TRIC) {
+                    min_image(a, dx, dy, dz);
+                } else {
+                    dx -= a.L.x * rint(dx * a.invL.x);
+                    dy -= a.L.y * rint(dy * a.invL.y);
+                    dz -= a.L.z * rint(dz * a.invL.z);
+                }
                 const double r2 = dx * dx + dy * dy + dz * dz;
                 if (r2 <= a.rc2) {   // exact voxel-hash test
                     const double ke = a.ke;
@@ -1688,7 +1723,8 @@ void launch_cell_sort(Handle& h, const double* pos) {
     // counts, atom_tmp = scattered order, cell_key_sorted's partner atom_new = final order
     // multi-rank: the owned rows in cell-sorted order come out of the same three launches
     int* oc = h.own_s ? h.own_cnt : nullptr;
-    hipLaunchKernelGGL(k_cell_hist, dim3(nblk(h.n, 256)), dim3(256), 0, h.stream, h.n, f, pos, L, nc, h.cell_key,
+    const double3 T = make_double3(h.box_t[0], h.box_t[1], h.box_t[2]);
+    hipLaunchKernelGGL(k_cell_hist, dim3(nblk(h.n, 256)), dim3(256), 0, h.stream, h.n, f, pos, L, T, nc, h.cell_key,
                        h.atom_val, h.cell_cnt, h.e_ticket + kTicketCells, h.cell_start, h.cell_end, h.lo, h.hi, oc,
                        h.own_start);
     hipLaunchKernelGGL(k_cell_scatter, dim3(nblk(h.n, 256)), dim3(256), 0, h.stream, h.n, f, h.cell_key, h.atom_val,
@@ -1696,7 +1732,7 @@ void launch_cell_sort(Handle& h, const double* pos) {
     hipLaunchKernelGGL(k_cell_order, dim3(nblk(ncell, 4)), dim3(256), 0, h.stream, ncell, f, h.cell_start,
                        h.cell_end, h.atom_tmp, h.key_tmp, h.lo, h.hi, h.own_start, oc ? h.own_s : nullptr);
     hipLaunchKernelGGL(k_cell_commit, dim3(nblk(h.n, 256)), dim3(256), 0, h.stream, h.n, f, h.cell_key, h.key_tmp,
-                       pos, h.q, h.lj, L, h.tric ? 0 : 1, h.cell_key_sorted, h.atom_sorted, h.pos4s, h.ljs,
+                       pos, h.q, h.lj, L, T, h.cell_key_sorted, h.atom_sorted, h.pos4s, h.ljs,
                        h.atom_type, h.typ_s,
                        h.pos_ref, h.n_builds_dev);
 }
@@ -1751,13 +1787,15 @@ void launch_direct(Handle& h, const double* pos, int include_forces) {
     DirectArgs a = direct_args(h, pos, include_forces);
     if (a.half) {
         const int ncell = h.nc[0] * h.nc[1] * h.nc[2];
+#define CF_PAIRS_HALF(TY_, MX_)                                                                              \
+    if (a.tric) hipLaunchKernelGGL((k_pairs_half<TY_, MX_, true>), dim3(ncell), dim3(1024), 0, h.stream, a); \
+    else hipLaunchKernelGGL((k_pairs_half<TY_, MX_, false>), dim3(ncell), dim3(1024), 0, h.stream, a)
         if (h.mixed) {
-            if (a.typ_s) hipLaunchKernelGGL((k_pairs_half<true, true>), dim3(ncell), dim3(1024), 0, h.stream, a);
-            else hipLaunchKernelGGL((k_pairs_half<false, true>), dim3(ncell), dim3(1024), 0, h.stream, a);
+            if (a.typ_s) { CF_PAIRS_HALF(true, true); } else { CF_PAIRS_HALF(false, true); }
         } else {
-            if (a.typ_s) hipLaunchKernelGGL((k_pairs_half<true, false>), dim3(ncell), dim3(1024), 0, h.stream, a);
-            else hipLaunchKernelGGL((k_pairs_half<false, false>), dim3(ncell), dim3(1024), 0, h.stream, a);
+            if (a.typ_s) { CF_PAIRS_HALF(true, false); } else { CF_PAIRS_HALF(false, false); }
         }
+#undef CF_PAIRS_HALF
         return;
     }
     // lanes per atom: enough threads for ~2 waves per SIMD on 256 CUs

@@ -2,8 +2,9 @@
 c = (cx,cy,cz)).  The reference takes the minimum image with the box vectors
 (getDeltaRPeriodic: c, b, a in turn; ReferenceCoulKernels.cpp:567, 601 and the flux terms
 RCK:53-55) and the reciprocal k-set and weights from the box diagonals only, on unwrapped
-positions (RCK:513-547).  Here the real space uses the all-pairs list with the same box-vector
-minimum image (cf_api.hip set_cells; the cell paths are orthorhombic), the k-space paths are
+positions (RCK:513-547).  Here the real space uses the same box-vector minimum image, with cells
+that are parallelepipeds in fractional coordinates (O(N): cf_api.hip set_cells,
+cf_kernels_core.hip k_cell_hist; boxes under 3 cells per direction use all pairs), the k-space paths are
 unchanged (both evaluate the diagonal-only sum on per-axis wrapped coordinates, which leave
 every factor e^{i k_a x_a} unchanged).
 Tolerances as in test_gpu_parity.py (exact k-sum: forces 1e-8) and test_gpu_grid.py (grid: 1e-6).
@@ -135,3 +136,95 @@ def test_triclinic_mixed_precision(algo):
     err = np.sqrt((d ** 2).sum(1).mean() / (ref["forces"] ** 2).sum(1).mean())
     assert err <= (1e-5 if algo == EXACT else 1e-4), err
     assert abs(e - ref["energy"]) <= 1e-7 * np.abs(ref["terms"]).sum()
+
+
+# ---- the O(N) cell path at sizes where it runs (>= 4 cells per lattice direction) ----------------
+# 4000 waters (12 000 atoms), rc 0.7 nm: 6 cells per direction in fractional coordinates, the
+# wave builder and the half list (one rank).  The oracle's triclinic pair search is all pairs.
+def _big(shear=(0.3, -0.25, 0.2), n=4000):
+    return ts.triclinic_water_box(n, cutoff=0.7, ewald_tol=1e-4, shear=shear)
+
+
+def _kernel(system, force, algo, half=True, skin=0.0, precision="double"):
+    import os
+    old = os.environ.get("CF_HALF")
+    os.environ["CF_HALF"] = "1" if half else "0"
+    try:
+        k = HipCalcCoulForceKernel(kspace_algo=algo, precision=precision).initialize(system, force)
+        if skin:
+            k.set_neighbor_skin(skin)
+    finally:
+        if old is None:
+            del os.environ["CF_HALF"]
+        else:
+            os.environ["CF_HALF"] = old
+    return k
+
+
+@pytest.mark.parametrize("shear", [(0.3, -0.25, 0.2), (-0.5, 0.5, -0.5), (0.45, 0.0, 0.0)])
+def test_triclinic_cell_path_vs_oracle_12k(shear):
+    system, force, pos, box = _big(shear)
+    ref = Oracle(force, box).execute(pos, box)
+    for half in (True, False):
+        _compare(_kernel(system, force, EXACT, half), pos, box, ref, 1e-8)
+
+
+def test_triclinic_cell_path_lattice_shifted_atoms_and_grid():
+    system, force, pos, box = _big((-0.4, 0.35, -0.3))
+    rng = np.random.default_rng(5)
+    p2 = pos + rng.normal(scale=0.01, size=pos.shape)
+    p2[::7] += box[1]
+    p2[::11] -= box[2]
+    p2[::13] += box[0] - box[1] + box[2]
+    ref = Oracle(force, box).execute(p2, box)
+    _compare(_kernel(system, force, GRID), p2, box, ref, 1e-6)
+
+
+def test_triclinic_cell_path_skin_trajectory_half_and_full():
+    # a kept list (skin) over moved steps, the half list and the full list, each step vs the oracle
+    system, force, pos, box = _big()
+    o = Oracle(force, box)
+    ks = [_kernel(system, force, EXACT, half, skin=0.1) for half in (True, False)]
+    rng = np.random.default_rng(2)
+    p = pos.copy()
+    for step in range(3):
+        ref = o.execute(p, box)
+        for k in ks:
+            _compare(k, p, box, ref, 1e-8)
+        p = p + rng.normal(scale=0.004, size=p.shape)
+    builds, evals = ks[0].neighbor_stats()
+    assert evals == 3 and builds < 3
+
+
+def test_triclinic_cell_path_mixed_precision():
+    system, force, pos, box = _big()
+    ref = Oracle(force, box).execute(pos, box)
+    e, f = _kernel(system, force, EXACT, precision="mixed").execute_host(pos, box)
+    d = f - ref["forces"]
+    assert np.sqrt((d ** 2).sum(1).mean() / (ref["forces"] ** 2).sum(1).mean()) <= 1e-5
+    assert abs(e - ref["energy"]) <= 1e-7 * np.abs(ref["terms"]).sum()
+
+
+def test_triclinic_cell_path_two_ranks():
+    from openmmcoul.distributed import device_buffer_as_tensor
+    system, force, pos, box = _big()
+    stream = torch.cuda.current_stream().cuda_stream
+    pt = torch.tensor(pos, dtype=torch.float64, device="cuda")
+    e1, f1 = HipCalcCoulForceKernel(stream=stream, kspace_algo=GRID).initialize(system, force).execute_host(pos, box)
+    ks = [HipCalcCoulForceKernel(stream=stream, rank=r, world_size=2, kspace_algo=GRID).initialize(system, force)
+          for r in range(2)]
+    for k in ks:
+        k.begin(pt, box, True, True)
+    bufs = [device_buffer_as_tensor(*k.kspace_buffer(), "cuda") for k in ks]
+    total = bufs[0] + bufs[1]
+    for b in bufs:
+        b.copy_(total)
+    f = torch.zeros_like(pt)
+    es = []
+    for k in ks:
+        e = torch.zeros(1, dtype=torch.float64, device="cuda")
+        k.end(f, e)
+        es.append(e)
+    torch.cuda.synchronize()
+    assert (es[0] + es[1]).item() == pytest.approx(e1, rel=1e-11)
+    assert np.abs(f.cpu().numpy() - f1).max() < 1e-8

@@ -15,6 +15,12 @@ if [ -n "$old" ]; then
     python tools/ab_bits.py cmp "$out/ab_old.npz" "$out/ab_new.npz" >> "$out/ab.log" 2>&1; echo "ab rc=$?"; tail -3 "$out/ab.log"
     rm -f "$out/ab_old.npz" "$out/ab_new.npz"
 fi
+if [ -n "$PROBES" ]; then
+    for pr in $PROBES; do
+        timeout -k 10 600 python -u "$pr" > "$out/$(basename "$pr" .py).json" 2> "$out/$(basename "$pr" .py).err"
+        rc=$?; echo "$pr rc=$rc"; tail -c 800 "$out/$(basename "$pr" .py).json"; [ $rc -eq 0 ] || exit $rc
+    done
+fi
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$out/smoke.log" 2>&1
 rc=$?; echo "smoke rc=$rc"; tail -3 "$out/smoke.log"; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 600 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline > "$out/bench.json" 2> "$out/bench.err"
