@@ -189,6 +189,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true",
                     help="no per-kernel HIP events in the timed steps (measures their overhead; no roofline)")
+    ap.add_argument("--graph", type=int, default=0,
+                    help="1: replay each step's CoulForce launches as a captured hipGraph (cf_set_graph) in the "
+                         "timed region")
     ap.add_argument("--dt", type=float, default=0.001, help="ps")
     ap.add_argument("--neighbor-skin", type=float, default=None,
                     help="nm; persistent list rebuilt when an atom moved > skin/2 (0 = every step); default "
@@ -269,7 +272,9 @@ def main():
     dom = max((k for k in HOT if per_step.get(k, 0.0) > 0), key=lambda k: per_step[k], default=None)
 
     # timed region: K steps, barrier + synchronize on both sides, max over ranks
-    if dom is not None and not args.no_kernel_timing:
+    if args.graph and world == 1:
+        kern.kernel.set_graph(True)   # replayed graphs cannot carry the per-launch events
+    elif dom is not None and not args.no_kernel_timing:
         kern.kernel.set_timing(True, phases=[dom])
     builds0, evals0 = kern.kernel.neighbor_stats()
     if world > 1:
@@ -297,6 +302,21 @@ def main():
         energy = step(True)
     torch.cuda.synchronize()
     ms_eval_clean = float(np.mean([a.elapsed_time(b) for a, b in ev])) if ev else float("nan")
+    # graph pass (after the timed region, not part of it): K steps with the CoulForce launches
+    # replayed as a captured hipGraph, wall clock; measures what graph replay would give `value`
+    graph_ms = None
+    if world == 1 and not args.graph:
+        kern.kernel.set_graph(True)
+        for _ in range(3):
+            energy = step(False)
+        torch.cuda.synchronize()
+        tg = time.perf_counter()
+        for _ in range(args.steps):
+            energy = step(False)
+        torch.cuda.synchronize()
+        graph_ms = (time.perf_counter() - tg) / args.steps * 1e3
+        gstats = kern.kernel.graph_stats()
+        kern.kernel.set_graph(False)
     kern.synchronize()   # energy all-reduce still in flight (multi-rank)
     e_final = energy.item()
     ms_step = elapsed / args.steps * 1e3
@@ -425,6 +445,8 @@ def main():
                        "parallelism": f"atom-decomposition x{world}" + (" (RCCL all-reduce of S(k))" if world > 1 else "")},
             "ms_per_force_eval": round(ms_eval_clean, 4),
             "ms_per_force_eval_instrumented": round(ms_eval, 4),
+            "graph_replay_ms_per_step": None if graph_ms is None else round(graph_ms, 4),
+            "graph_stats": None if graph_ms is None else list(gstats),
             "energy_kj_mol": e_final,
             "kernels_ms_per_step": {k: round(v, 4) for k, v in per_step.items()},
             "timing_note": (f"value: K steps with HIP events around {dom} launches only; ms_per_force_eval: a "

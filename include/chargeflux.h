@@ -145,6 +145,13 @@ CF_EXPORT int cf_set_neighbor_skin(cf_handle* h, double skin);
 CF_EXPORT int cf_update_parameters(cf_handle* h, const cf_params* params);
 /* Number of neighbour-list builds and evaluations since cf_create. */
 CF_EXPORT int cf_get_neighbor_stats(const cf_handle* h, int64_t* builds, int64_t* evaluations);
+/* Slow-path diagnostics since cf_create (synchronises the stream): evaluations whose half-list
+ * partner sums could not be used -- a window over 4096 atoms, an overflowed list, a term beyond
+ * the fixed-point range, rows the list builder could not place -- so that every atom's pair
+ * sums were recomputed by the fp64 cell rescan (same results, several times slower); and list
+ * rows rescanned after a full-list overflow.  Nonzero values on a production system mean the
+ * neighbour-list capacity or the cell geometry does not suit it. */
+CF_EXPORT int cf_get_fallback_stats(const cf_handle* h, int64_t* half_list_fallbacks, int64_t* rows_rescanned);
 
 /*
  * Replaces ReferenceCalcCoulForceKernel::execute (ReferenceCoulKernels.cpp:424-636).
@@ -174,6 +181,16 @@ CF_EXPORT int cf_kspace_buffer(cf_handle* h, double** buf_dev, int64_t* count);
  * two overlap).  cf_compute_end runs them itself if this was not called. */
 CF_EXPORT int cf_compute_direct(cf_handle* h);
 CF_EXPORT int cf_compute_end(cf_handle* h, double* forces_dev, double* energy_dev);
+
+/* Graph replay (single-rank cf_compute / cf_compute_host): enable = 1 captures the launches of an
+ * evaluation into a hipGraph (on a private stream) and replays it on the handle's stream while
+ * the calls look the same to the host: same device buffers, flags, box and neighbour-list
+ * decision (a rebuild under a kept skin is decided on the device, inside the graph).  A change
+ * re-captures.  Evaluations with timing on, the split-phase calls and multi-rank handles run
+ * eagerly.  Results are identical either way (the same kernels in the same order). */
+CF_EXPORT int cf_set_graph(cf_handle* h, int enable);
+/* Number of graph captures and replays since cf_set_graph(h, 1). */
+CF_EXPORT int cf_get_graph_stats(const cf_handle* h, int64_t* captures, int64_t* replays);
 
 /* Synchronous host-memory convenience (H2D positions, D2H forces/energy): what an
  * OpenMM Reference/CPU-platform adapter calls.  forces_host is ADDED to. */

@@ -30,6 +30,8 @@ static const char* kPhaseNames[PH_COUNT] = {"flux_terms", "atoms_prep", "cell_so
                                             "grid_dft_fwd", "grid_dft_inv", "grid_interp", "direct_excl"};
 constexpr int kMaxTimed = 8192;
 
+static void graph_forget(cf_handle* H);   // hipGraph replay cache (cf_set_graph), below
+
 struct cf_handle {
     cf::Handle h;
     bool timing = false;
@@ -585,6 +587,8 @@ CF_EXPORT int cf_create(const cf_params* p, const cf_options* opt, cf_handle** o
             check_hip(hipMemset(h.half_flag, 0, sizeof(int)), "memset");
             h.n_builds_dev = dalloc<long long>(H, 1);
             check_hip(hipMemset(h.n_builds_dev, 0, sizeof(long long)), "memset");
+            h.n_fallback_dev = dalloc<long long>(H, 2);
+            check_hip(hipMemset(h.n_fallback_dev, 0, 2 * sizeof(long long)), "memset");
             if (h.world > 1) h.own_s = dalloc<int>(H, std::max(nown, 1));  // owned atoms, cell-sorted
             std::copy(p->default_box, p->default_box + 9, H->default_box);
             alloc_nlist(H, 0.0);
@@ -663,6 +667,7 @@ CF_EXPORT int cf_destroy(cf_handle* H) {
     return guarded([&] {
         (void)hipSetDevice(H->h.device);
         (void)hipStreamSynchronize(H->h.stream);
+        graph_forget(H);
         for (void* p : H->allocs) (void)hipFree(p);
         for (auto& v : H->ev)
             for (hipEvent_t e : v) (void)hipEventDestroy(e);
@@ -774,6 +779,22 @@ CF_EXPORT int cf_get_neighbor_stats(const cf_handle* H, int64_t* builds, int64_t
     return CF_OK;
 }
 
+CF_EXPORT int cf_get_fallback_stats(const cf_handle* H, int64_t* half_list_fallbacks, int64_t* rows_rescanned) {
+    if (!H) { g_err = "null handle"; return CF_ERR_INVALID; }
+    long long v[2] = {0, 0};
+    if (H->h.n_fallback_dev) {
+        (void)hipSetDevice(H->h.device);
+        if (hipStreamSynchronize(H->h.stream) != hipSuccess ||
+            hipMemcpy(v, H->h.n_fallback_dev, sizeof(v), hipMemcpyDeviceToHost) != hipSuccess) {
+            g_err = "hipMemcpy failed";
+            return CF_ERR_HIP;
+        }
+    }
+    if (half_list_fallbacks) *half_list_fallbacks = v[0];
+    if (rows_rescanned) *rows_rescanned = v[1];
+    return CF_OK;
+}
+
 CF_EXPORT int cf_get_ewald_params(const cf_handle* H, double* alpha, int32_t kmax[3]) {
     if (!H) { g_err = "null handle"; return CF_ERR_INVALID; }
     if (alpha) *alpha = H->h.alpha;
@@ -797,60 +818,73 @@ CF_EXPORT int cf_get_owned_range(const cf_handle* H, int32_t* lo, int32_t* hi) {
     return CF_OK;
 }
 
+// Host side of one evaluation (no launches): the box, the neighbour-list decision and the
+// cell geometry (set_cells may allocate), bookkeeping.  Neighbour list: rebuilt on every call
+// (skin 0, the reference's behaviour, RCK:559), or kept while no atom has moved more than half
+// the skin.  The host forces a rebuild (first call, new box, skin change); otherwise
+// k_atoms_prep checks the displacements on the device and the cell commit / list kernels follow
+// its flag, so nothing waits on the host and the launches are graph-capturable.
+static bool host_prologue(cf_handle* H, const double* box9) {
+    cf::Handle& h = H->h;
+    set_box(H, box9);
+    const double Lmin = std::min(h.box_L[0], std::min(h.box_L[1], h.box_L[2]));
+    const double s_call = h.skin > 0 ? std::max(0.0, std::min(h.skin, 0.5 * Lmin - h.cutoff)) : 0.0;
+    const bool reusable = h.pbc && h.skin > 0 && h.list_valid && s_call == h.list_skin &&
+                          h.list_L[0] == h.box_L[0] && h.list_L[1] == h.box_L[1] && h.list_L[2] == h.box_L[2] &&
+                          h.list_T[0] == h.box_t[0] && h.list_T[1] == h.box_t[1] && h.list_T[2] == h.box_t[2];
+    if (h.pbc && !reusable) {
+        h.list_skin = s_call;
+        set_cells(H, h.box_L);
+        h.list_valid = h.skin > 0;
+        std::copy(h.box_L, h.box_L + 3, h.list_L);
+        std::copy(h.box_t, h.box_t + 3, h.list_T);
+    }
+    h.n_evals++;
+    return reusable;
+}
+
+// launches of cf_compute_begin: flux charges, cell sort + list, this rank's k-space partials
+static void launch_begin(cf_handle* H, const double* pos_dev, int flags, bool reusable) {
+    cf::Handle& h = H->h;
+    const int forces = flags & CF_INCLUDE_FORCES, energy = flags & CF_INCLUDE_ENERGY;
+    { Timed t(H, PH_FLUX); cf::launch_flux_terms(h, pos_dev); }
+    { Timed t(H, PH_PREP); cf::launch_atoms_prep(h, pos_dev, reusable); }
+    if (h.pbc) {
+        {
+            Timed t(H, PH_CELLS);
+            if (!reusable) cf::launch_force_rebuild(h);
+            cf::launch_cell_sort(h, pos_dev);
+        }
+        if (h.hi > h.lo) { Timed t(H, PH_NLIST); cf::launch_nlist(h, pos_dev); }
+        if ((forces || energy) && h.hi > h.lo) {
+            if (h.kspace_algo == 0) {
+                { Timed t(H, PH_TABLES); cf::launch_kspace_tables(h, pos_dev); }
+                { Timed t(H, PH_SFAC); cf::launch_kspace_sfac(h); }
+            } else if (h.kspace_algo == 2) {
+                { Timed t(H, PH_GSORT); cf::launch_grid_sort(h, pos_dev); }
+                { Timed t(H, PH_GSPREAD); cf::launch_grid_spread(h); }
+                { Timed t(H, PH_GDFTF); cf::launch_grid_dft_fwd(h); }
+            } else {
+                Timed t(H, PH_SFAC);
+                cf::launch_kspace_direct_sfac(h, pos_dev);
+            }
+        } else if (forces || energy) {   // no owned atoms: a zero partial S(k) (all-reduced by the caller)
+            int64_t cnt = 0;
+            double* buf = cf::kspace_reduce_buffer(h, &cnt);
+            check_hip(hipMemsetAsync(buf, 0, sizeof(double) * cnt, h.stream), "memset S");
+            if (h.kspace_algo == 1) cf::launch_kspace_kvec(h);   // read by the coefficient pass
+        }
+    }
+}
+
 CF_EXPORT int cf_compute_begin(cf_handle* H, const double* pos_dev, const double* box9, int flags) {
     return guarded([&] {
         if (!H || !pos_dev) fail(CF_ERR_INVALID, "null argument");
         cf::Handle& h = H->h;
         if (h.pending_flags >= 0) fail(CF_ERR_STATE, "cf_compute_begin called twice without cf_compute_end");
         check_hip(hipSetDevice(h.device), "hipSetDevice");
-        set_box(H, box9);
-        const int forces = flags & CF_INCLUDE_FORCES, energy = flags & CF_INCLUDE_ENERGY;
-        // neighbour list: rebuilt on every call (skin 0, the reference's behaviour, RCK:559),
-        // or kept while no atom has moved more than half the skin.  The host forces a rebuild
-        // (first call, new box, skin change); otherwise k_atoms_prep checks the displacements
-        // on the device and the cell commit / list kernels follow its flag, so nothing waits
-        // on the host and the sequence is graph-capturable.
-        const double Lmin = std::min(h.box_L[0], std::min(h.box_L[1], h.box_L[2]));
-        const double s_call = h.skin > 0 ? std::max(0.0, std::min(h.skin, 0.5 * Lmin - h.cutoff)) : 0.0;
-        const bool reusable = h.pbc && h.skin > 0 && h.list_valid && s_call == h.list_skin &&
-                              h.list_L[0] == h.box_L[0] && h.list_L[1] == h.box_L[1] && h.list_L[2] == h.box_L[2] &&
-                              h.list_T[0] == h.box_t[0] && h.list_T[1] == h.box_t[1] && h.list_T[2] == h.box_t[2];
-        { Timed t(H, PH_FLUX); cf::launch_flux_terms(h, pos_dev); }
-        { Timed t(H, PH_PREP); cf::launch_atoms_prep(h, pos_dev, reusable); }
-        if (h.pbc) {
-            {
-                Timed t(H, PH_CELLS);
-                if (!reusable) {
-                    h.list_skin = s_call;
-                    set_cells(H, h.box_L);
-                    cf::launch_force_rebuild(h);
-                    h.list_valid = h.skin > 0;
-                    std::copy(h.box_L, h.box_L + 3, h.list_L);
-                    std::copy(h.box_t, h.box_t + 3, h.list_T);
-                }
-                cf::launch_cell_sort(h, pos_dev);
-            }
-            if (h.hi > h.lo) { Timed t(H, PH_NLIST); cf::launch_nlist(h, pos_dev); }
-            if ((forces || energy) && h.hi > h.lo) {
-                if (h.kspace_algo == 0) {
-                    { Timed t(H, PH_TABLES); cf::launch_kspace_tables(h, pos_dev); }
-                    { Timed t(H, PH_SFAC); cf::launch_kspace_sfac(h); }
-                } else if (h.kspace_algo == 2) {
-                    { Timed t(H, PH_GSORT); cf::launch_grid_sort(h, pos_dev); }
-                    { Timed t(H, PH_GSPREAD); cf::launch_grid_spread(h); }
-                    { Timed t(H, PH_GDFTF); cf::launch_grid_dft_fwd(h); }
-                } else {
-                    Timed t(H, PH_SFAC);
-                    cf::launch_kspace_direct_sfac(h, pos_dev);
-                }
-            } else if (forces || energy) {   // no owned atoms: a zero partial S(k) (all-reduced by the caller)
-                int64_t cnt = 0;
-                double* buf = cf::kspace_reduce_buffer(h, &cnt);
-                check_hip(hipMemsetAsync(buf, 0, sizeof(double) * cnt, h.stream), "memset S");
-                if (h.kspace_algo == 1) cf::launch_kspace_kvec(h);   // read by the coefficient pass
-            }
-        }
-        h.n_evals++;
+        const bool reusable = host_prologue(H, box9);
+        launch_begin(H, pos_dev, flags, reusable);
         launch_check("compute_begin");
         h.pending_flags = flags;
         h.direct_done = false;
@@ -894,6 +928,41 @@ CF_EXPORT int cf_compute_direct(cf_handle* H) {
     });
 }
 
+// launches of cf_compute_end (after run_direct): k-space coefficients, reciprocal forces, chain
+// rule + energy
+static void launch_end(cf_handle* H, int flags, double* forces_dev, double* energy_dev) {
+    cf::Handle& h = H->h;
+    const int forces = flags & CF_INCLUDE_FORCES, energy = flags & CF_INCLUDE_ENERGY;
+    const double* pos = H->pos_pending;
+    // the reciprocal energy is added by rank 0 (launch_assemble_energy) from the all-reduced
+    // buffer, so rank 0 runs the coefficient pass even when it owns no atoms (its begin
+    // zeroed its partial buffer, which the caller's all-reduce then filled)
+    if (h.pbc && (forces || energy) && (h.hi > h.lo || h.rank == 0)) {
+        Timed t(H, PH_COEFFS);
+        if (h.kspace_algo == 0) cf::launch_kspace_coeffs(h, energy);
+        else if (h.kspace_algo == 2) cf::launch_grid_coeffs(h, energy);
+        else cf::launch_kspace_direct_coeffs(h, energy);
+    }
+    if (h.hi > h.lo) {
+        if (h.pbc) {
+            if (forces && h.kspace_algo == 2) {
+                { Timed t(H, PH_GDFTI); cf::launch_grid_dft_inv(h); }
+                { Timed t(H, PH_GINTERP); cf::launch_grid_interp(h); }   // adds into dE/dq and forces
+            } else if (forces) {
+                Timed t(H, PH_FORCE);
+                if (h.kspace_algo == 0) cf::launch_kspace_force(h, pos);
+                else cf::launch_kspace_direct_force(h, pos);
+                cf::launch_recip_add(h);
+            }
+        }
+    }
+    {   // chain rule (when forces are requested) and the energy reduction in one launch
+        Timed t(H, PH_ENERGY);
+        cf::launch_assemble_energy(h, (forces && forces_dev && h.hi > h.lo) ? forces_dev : nullptr, energy,
+                                   energy_dev);
+    }
+}
+
 CF_EXPORT int cf_compute_end(cf_handle* H, double* forces_dev, double* energy_dev) {
     return guarded([&] {
         if (!H) fail(CF_ERR_INVALID, "null handle");
@@ -903,44 +972,132 @@ CF_EXPORT int cf_compute_end(cf_handle* H, double* forces_dev, double* energy_de
         run_direct(H);
         const int flags = h.pending_flags;
         h.pending_flags = -1;
-        const int forces = flags & CF_INCLUDE_FORCES, energy = flags & CF_INCLUDE_ENERGY;
-        const double* pos = H->pos_pending;
-        // the reciprocal energy is added by rank 0 (launch_assemble_energy) from the all-reduced
-        // buffer, so rank 0 runs the coefficient pass even when it owns no atoms (its begin
-        // zeroed its partial buffer, which the caller's all-reduce then filled)
-        if (h.pbc && (forces || energy) && (h.hi > h.lo || h.rank == 0)) {
-            Timed t(H, PH_COEFFS);
-            if (h.kspace_algo == 0) cf::launch_kspace_coeffs(h, energy);
-            else if (h.kspace_algo == 2) cf::launch_grid_coeffs(h, energy);
-            else cf::launch_kspace_direct_coeffs(h, energy);
-        }
-        if (h.hi > h.lo) {
-            if (h.pbc) {
-                if (forces && h.kspace_algo == 2) {
-                    { Timed t(H, PH_GDFTI); cf::launch_grid_dft_inv(h); }
-                    { Timed t(H, PH_GINTERP); cf::launch_grid_interp(h); }   // adds into dE/dq and forces
-                } else if (forces) {
-                    Timed t(H, PH_FORCE);
-                    if (h.kspace_algo == 0) cf::launch_kspace_force(h, pos);
-                    else cf::launch_kspace_direct_force(h, pos);
-                    cf::launch_recip_add(h);
-                }
-            }
-        }
-        {   // chain rule (when forces are requested) and the energy reduction in one launch
-            Timed t(H, PH_ENERGY);
-            cf::launch_assemble_energy(h, (forces && forces_dev && h.hi > h.lo) ? forces_dev : nullptr, energy,
-                                       energy_dev);
-        }
+        launch_end(H, flags, forces_dev, energy_dev);
         launch_check("compute_end");
     });
 }
 
+// Graph replay of single-call evaluations (cf_set_graph): everything a call would launch is
+// captured once into a hipGraph on a private stream and replayed on the handle's stream as
+// long as the call looks the same to the host -- the same position / force / energy buffers and
+// flags, the same box and list decision (the rebuild itself is decided on the device, inside the
+// graph).  Anything else (a new box, other buffers, timing on) re-captures or runs eagerly.
+struct GraphKey {
+    const void* pos = nullptr; void* frc = nullptr; void* ene = nullptr;
+    int flags = -1; bool reusable = false;
+    double box[9] = {};
+    bool operator==(const GraphKey& o) const {
+        return pos == o.pos && frc == o.frc && ene == o.ene && flags == o.flags && reusable == o.reusable &&
+               std::memcmp(box, o.box, sizeof(box)) == 0;
+    }
+};
+
+struct GraphCache {
+    bool enabled = false;
+    hipStream_t cap = nullptr;
+    hipGraphExec_t exec = nullptr;
+    GraphKey key;
+    int64_t captures = 0, replays = 0;
+    void drop() {
+        if (exec) (void)hipGraphExecDestroy(exec);
+        exec = nullptr;
+    }
+};
+
+static std::vector<std::pair<cf_handle*, GraphCache>>& graph_caches() {
+    static std::vector<std::pair<cf_handle*, GraphCache>> v;
+    return v;
+}
+static GraphCache* graph_of(cf_handle* H, bool create) {
+    for (auto& e : graph_caches())
+        if (e.first == H) return &e.second;
+    if (!create) return nullptr;
+    graph_caches().emplace_back(H, GraphCache());
+    return &graph_caches().back().second;
+}
+static void graph_forget(cf_handle* H) {
+    auto& v = graph_caches();
+    for (size_t i = 0; i < v.size(); i++)
+        if (v[i].first == H) {
+            v[i].second.drop();
+            if (v[i].second.cap) (void)hipStreamDestroy(v[i].second.cap);
+            v.erase(v.begin() + i);
+            return;
+        }
+}
+
+CF_EXPORT int cf_set_graph(cf_handle* H, int enable) {
+    return guarded([&] {
+        if (!H) fail(CF_ERR_INVALID, "null handle");
+        if (H->h.pending_flags >= 0) fail(CF_ERR_STATE, "cf_set_graph during a begun evaluation");
+        check_hip(hipSetDevice(H->h.device), "hipSetDevice");
+        if (!enable) { graph_forget(H); return; }
+        GraphCache* g = graph_of(H, true);
+        g->enabled = true;
+        if (!g->cap) check_hip(hipStreamCreateWithFlags(&g->cap, hipStreamNonBlocking), "hipStreamCreate (graph capture)");
+    });
+}
+
+CF_EXPORT int cf_get_graph_stats(const cf_handle* H, int64_t* captures, int64_t* replays) {
+    GraphCache* g = graph_of(const_cast<cf_handle*>(H), false);
+    if (captures) *captures = g ? g->captures : 0;
+    if (replays) *replays = g ? g->replays : 0;
+    return CF_OK;
+}
+
 CF_EXPORT int cf_compute(cf_handle* H, const double* pos_dev, const double* box9, int flags, double* forces_dev,
                          double* energy_dev) {
-    int rc = cf_compute_begin(H, pos_dev, box9, flags);
-    if (rc != CF_OK) return rc;
-    return cf_compute_end(H, forces_dev, energy_dev);
+    GraphCache* g = H ? graph_of(H, false) : nullptr;
+    if (!g || !g->enabled || H->timing || H->h.world > 1) {
+        int rc = cf_compute_begin(H, pos_dev, box9, flags);
+        if (rc != CF_OK) return rc;
+        return cf_compute_end(H, forces_dev, energy_dev);
+    }
+    return guarded([&] {
+        if (!pos_dev) fail(CF_ERR_INVALID, "null argument");
+        cf::Handle& h = H->h;
+        if (h.pending_flags >= 0) fail(CF_ERR_STATE, "cf_compute during a begun evaluation");
+        check_hip(hipSetDevice(h.device), "hipSetDevice");
+        const bool reusable = host_prologue(H, box9);
+        GraphKey k;
+        k.pos = pos_dev; k.frc = forces_dev; k.ene = energy_dev; k.flags = flags; k.reusable = reusable;
+        if (h.pbc && box9) std::memcpy(k.box, box9, sizeof(k.box));
+        if (!g->exec || !(k == g->key)) {
+            g->drop();
+            hipStream_t user = h.stream;
+            h.stream = g->cap;
+            hipGraph_t graph = nullptr;
+            hipError_t e = hipStreamBeginCapture(g->cap, hipStreamCaptureModeThreadLocal);
+            if (e == hipSuccess) {
+                try {
+                    H->pos_pending = pos_dev;
+                    h.pending_flags = flags;
+                    h.direct_done = false;
+                    launch_begin(H, pos_dev, flags, reusable);
+                    run_direct(H);
+                    h.pending_flags = -1;
+                    launch_end(H, flags, forces_dev, energy_dev);
+                } catch (...) {
+                    (void)hipStreamEndCapture(g->cap, &graph);
+                    if (graph) (void)hipGraphDestroy(graph);
+                    h.stream = user;
+                    h.pending_flags = -1;
+                    throw;
+                }
+                e = hipStreamEndCapture(g->cap, &graph);
+            }
+            h.stream = user;
+            check_hip(e, "hipStreamBeginCapture / EndCapture");
+            e = hipGraphInstantiate(&g->exec, graph, nullptr, nullptr, 0);
+            (void)hipGraphDestroy(graph);
+            check_hip(e, "hipGraphInstantiate");
+            g->key = k;
+            g->captures++;
+        } else {
+            g->replays++;
+        }
+        check_hip(hipGraphLaunch(g->exec, h.stream), "hipGraphLaunch");
+    });
 }
 
 CF_EXPORT int cf_compute_host(cf_handle* H, const double* pos_host, const double* box9, int flags,

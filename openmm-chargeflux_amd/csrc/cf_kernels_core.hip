@@ -408,6 +408,7 @@ struct DirectArgs {
     unsigned long long* win_out;// [ncell][kHalfMaxWin][4] per-cell window partials (fixed point)
     int* win_woff;              // [ncell][kHalfWin] window offsets of the 18 window cells
     const int* key_s;           // cell key per sorted slot
+    long long* fallback;        // [2] diagnostics (Handle::n_fallback_dev)
 };
 
 __device__ __forceinline__ int own_slot(const DirectArgs& a, int c) { return a.own_s ? a.own_s[c] : c; }
@@ -1462,7 +1463,10 @@ __global__ void __launch_bounds__(256) k_excl(DirectArgs a) {
 #pragma unroll
         for (int g = 0; g < kSeg; g++) over = over || a.nl_cnt[(size_t)g * a.nlr + c] > a.nb_cap;
     }
-    if (over) pair_rescan(a, a.erfc_tab, s, i);   // rare: erfcx table read from global memory
+    if (over) {   // rare: erfcx table read from global memory
+        pair_rescan(a, a.erfc_tab, s, i);
+        if (!a.half && a.fallback) atomicAdd((unsigned long long*)&a.fallback[1], 1ull);
+    }
     if (a.half && !over && a.include_forces) {    // the partner-side sums of the half list
         double3 f;
         double dq;
@@ -1574,7 +1578,8 @@ __global__ void __launch_bounds__(kEChunk) k_assemble_energy(int lo, int hi, con
                                                              double* __restrict__ terms, double* __restrict__ energy_out,
                                                              double* __restrict__ energy_int, int* __restrict__ ticket,
                                                              int* __restrict__ flag, int* __restrict__ xrange,
-                                                             int* __restrict__ half_flag) {
+                                                             int* __restrict__ half_flag,
+                                                             long long* __restrict__ fallback) {
     __shared__ double red[3][256];
     const int b = lo + blockIdx.x * kEChunk + threadIdx.x;
     double a0 = 0, a1 = 0, a2 = 0;
@@ -1634,7 +1639,10 @@ __global__ void __launch_bounds__(kEChunk) k_assemble_energy(int lo, int hi, con
         *energy_int = e;
         if (energy_out) *energy_out = e;
         if (flag) *flag = 0;
-        if (half_flag) *half_flag = 0;
+        if (half_flag) {
+            if (*half_flag && fallback) fallback[0] += 1;
+            *half_flag = 0;
+        }
         if (xrange) { xrange[0] = INT_MAX; xrange[1] = INT_MIN; }   // re-arm the grid x-slab
     }
 }
@@ -1772,6 +1780,7 @@ static DirectArgs direct_args(Handle& h, const double* pos, int include_forces) 
     a.win_out = h.win_out;
     a.win_woff = h.win_woff;
     a.key_s = h.cell_key_sorted;
+    a.fallback = h.n_fallback_dev;
     return a;
 }
 
@@ -1850,7 +1859,7 @@ void launch_assemble_energy(Handle& h, double* forces_out, int include_energy, d
     hipLaunchKernelGGL(k_assemble_energy, dim3(nparts), dim3(kEChunk), 0, h.stream, h.lo, h.hi, h.ccsr_start,
                        h.ccsr_ent, h.dedq, h.dqdx, h.f_part, forces_out, h.e_atom, h.e_part, h.e_rec_part, nrec, h.pbc,
                        h.terms_dev, energy_out, h.energy_dev, h.e_ticket + kTicketEnergy, h.skin_flag, h.g_xrange,
-                       h.half ? h.half_flag : nullptr);
+                       h.half ? h.half_flag : nullptr, h.n_fallback_dev);
 }
 
 }  // namespace cf

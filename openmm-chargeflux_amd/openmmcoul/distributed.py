@@ -74,6 +74,11 @@ class ShardedCoulKernel:
 
     def execute(self, positions: torch.Tensor, box, forces: torch.Tensor | None, include_energy: bool = True):
         k = self.kernel
+        if self.world == 1 and hasattr(k, "execute_device"):
+            # one rank: a single cf_compute call (graph-replayable, cf_set_graph) into one energy buffer
+            self.energy = self._ebufs[0]
+            k.execute_device(positions, box, forces is not None, include_energy, forces, self.energy)
+            return self.energy
         k.begin(positions, box, forces is not None, include_energy)
         if self.world > 1 and self._sbuf is not None:
             # the direct-space kernels do not need S(k): they run while it is all-reduced

@@ -155,11 +155,30 @@ class HipCalcCoulForceKernel:
         _cabi.check(self._lib.cf_set_neighbor_skin(self._h, float(skin)), self._lib)
         return self
 
+    def set_graph(self, enable: bool = True):
+        """Replay single-rank evaluations as a captured hipGraph (cf_set_graph): the same kernels
+        in the same order, without the per-launch host cost."""
+        _cabi.check(self._lib.cf_set_graph(self._h, 1 if enable else 0), self._lib)
+        return self
+
+    def graph_stats(self):
+        """(captures, replays) since set_graph(True)."""
+        c, r = C.c_int64(), C.c_int64()
+        _cabi.check(self._lib.cf_get_graph_stats(self._h, C.byref(c), C.byref(r)), self._lib)
+        return c.value, r.value
+
     def neighbor_stats(self):
         """(list builds, evaluations) since initialize."""
         b, e = C.c_int64(), C.c_int64()
         _cabi.check(self._lib.cf_get_neighbor_stats(self._h, C.byref(b), C.byref(e)), self._lib)
         return b.value, e.value
+
+    def fallback_stats(self):
+        """(evaluations that fell back to the fp64 rescan of every atom, list rows rescanned
+        after a full-list overflow) since initialize: slow-path diagnostics."""
+        a, b = C.c_int64(), C.c_int64()
+        _cabi.check(self._lib.cf_get_fallback_stats(self._h, C.byref(a), C.byref(b)), self._lib)
+        return a.value, b.value
 
     def owned_range(self):
         lo, hi = C.c_int32(), C.c_int32()

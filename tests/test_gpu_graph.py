@@ -1,0 +1,83 @@
+"""hipGraph replay of single-rank evaluations (cf_set_graph): the captured launches must give
+the same bits as eager calls -- over a trajectory with a kept neighbour list (rebuilds decided
+on the device inside the graph), after a box change (re-capture) and with other output buffers
+(re-capture) -- and the cache must actually replay.  Bar: bitwise equality."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+from openmmcoul import HipCalcCoulForceKernel  # noqa: E402
+from openmmcoul import testsystems as ts  # noqa: E402
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+
+
+def _traj(k, pos, box, steps, f=None, e=None, box2=None):
+    pt = torch.tensor(pos, dtype=torch.float64, device="cuda")
+    f = torch.zeros_like(pt) if f is None else f
+    e = torch.zeros(1, dtype=torch.float64, device="cuda") if e is None else e
+    rng = np.random.default_rng(4)
+    out = []
+    for s in range(steps):
+        f.zero_()
+        k.execute_device(pt, box2 if (box2 is not None and s >= steps // 2) else box, True, True, f, e)
+        torch.cuda.synchronize()
+        out.append((e.item(), f.cpu().numpy().copy()))
+        pt += torch.tensor(rng.normal(scale=0.006, size=pos.shape), device="cuda")
+    return out
+
+
+@pytest.mark.parametrize("algo,precision,skin", [(2, "double", 0.1), (0, "double", 0.0), (2, "mixed", 0.15)])
+def test_graph_replay_is_bitwise_eager(algo, precision, skin):
+    system, force, pos, box = ts.water_box(4000, cutoff=1.0, ewald_tol=1e-4, every_bond_angle=5)
+    stream = torch.cuda.current_stream().cuda_stream
+    mk = lambda: HipCalcCoulForceKernel(stream=stream, kspace_algo=algo, precision=precision).initialize(system, force)
+    eager, graph = mk(), mk()
+    if skin:
+        eager.set_neighbor_skin(skin)
+        graph.set_neighbor_skin(skin)
+    graph.set_graph(True)
+    bigger = box * 1.01
+    a = _traj(eager, pos, box, 8, box2=bigger)
+    b = _traj(graph, pos, box, 8, box2=bigger)
+    for (ea, fa), (eb, fb) in zip(a, b):
+        assert ea == eb and np.array_equal(fa, fb)
+    caps, reps = graph.graph_stats()
+    assert reps >= 4 and caps <= 4, (caps, reps)
+    assert eager.neighbor_stats() == graph.neighbor_stats()
+
+
+def test_graph_recaptures_for_new_buffers_and_flags():
+    system, force, pos, box = ts.make("C2")
+    stream = torch.cuda.current_stream().cuda_stream
+    k = HipCalcCoulForceKernel(stream=stream, kspace_algo=2).initialize(system, force).set_graph(True)
+    ref = HipCalcCoulForceKernel(stream=stream, kspace_algo=2).initialize(system, force)
+    pt = torch.tensor(pos, dtype=torch.float64, device="cuda")
+    e0, f0 = ref.execute_host(pos, box)
+    for _ in range(2):
+        for buf in range(2):
+            f = torch.zeros_like(pt)
+            e = torch.zeros(1, dtype=torch.float64, device="cuda")
+            k.execute_device(pt, box, True, True, f, e)
+            torch.cuda.synchronize()
+            assert e.item() == e0 and np.array_equal(f.cpu().numpy(), f0)
+        e = torch.zeros(1, dtype=torch.float64, device="cuda")
+        k.execute_device(pt, box, False, True, None, e)   # energy only: another graph
+        torch.cuda.synchronize()
+        assert e.item() == pytest.approx(e0, rel=1e-12, abs=1e-9)
+    caps, reps = k.graph_stats()
+    assert caps >= 3
+    # timing on: eager, same answer
+    k.set_timing(True)
+    f = torch.zeros_like(pt)
+    k.execute_device(pt, box, True, True, f, None)
+    torch.cuda.synchronize()
+    assert np.array_equal(f.cpu().numpy(), f0)
+    assert k.graph_stats()[0] == caps

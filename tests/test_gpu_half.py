@@ -136,9 +136,12 @@ def test_half_list_fallbacks_persist_over_kept_lists(make):
     for step in range(5):
         e, f = k.execute_host(x, box)
         ef, ff = ref.execute_host(x, box)
-        assert np.abs(f - ff).max() <= 1e-9, (step, np.abs(f - ff).max())
+        # (the rescan of a kept rc + skin list walks cells of another size than the reference's
+        # full list: the same pairs in another summation order, ~2e-12 of |F|)
+        assert np.abs(f - ff).max() <= 1e-8, (step, np.abs(f - ff).max())
         assert abs(e - ef) <= 1e-12 * abs(ef) + 1e-9, (step, e, ef)
         x = x + rng.normal(scale=0.002, size=x.shape)
+    assert k.fallback_stats()[0] == 5   # every evaluation took the fp64 rescan
     builds, evals = k.neighbor_stats()
     assert evals == 5 and builds < evals   # the later steps did keep the list
 

@@ -32,8 +32,11 @@ def run(system, force, pos, box, warmup, evals):
         k.execute_device(pt, box, True, True, f, e)
     torch.cuda.synchronize()
     t = {p: v[0] / max(v[1], 1) for p, v in k.timing().items() if v[1]}
+    fb = k.fallback_stats()
     k.destroy()
-    return {p: round(t.get(p, 0.0), 4) for p in ("cell_sort", "neighbor_list", "direct_pairs", "direct_excl")}
+    out = {p: round(t.get(p, 0.0), 4) for p in ("cell_sort", "neighbor_list", "direct_pairs", "direct_excl")}
+    out["fallbacks_half_evals_rows"] = list(fb)
+    return out
 
 
 def main():
