@@ -182,12 +182,13 @@ CF_EXPORT int cf_kspace_buffer(cf_handle* h, double** buf_dev, int64_t* count);
 CF_EXPORT int cf_compute_direct(cf_handle* h);
 CF_EXPORT int cf_compute_end(cf_handle* h, double* forces_dev, double* energy_dev);
 
-/* Graph replay (single-rank cf_compute / cf_compute_host): enable = 1 captures the launches of an
- * evaluation into a hipGraph (on a private stream) and replays it on the handle's stream while
- * the calls look the same to the host: same device buffers, flags, box and neighbour-list
- * decision (a rebuild under a kept skin is decided on the device, inside the graph).  A change
- * re-captures.  Evaluations with timing on, the split-phase calls and multi-rank handles run
- * eagerly.  Results are identical either way (the same kernels in the same order). */
+/* Graph replay: enable = 1 captures the launches of an evaluation into hipGraphs (on a private
+ * stream) and replays them on the handle's stream while the calls look the same to the host:
+ * same device buffers, flags, box and neighbour-list decision (a rebuild under a kept skin is
+ * decided on the device, inside the graph).  A change re-captures.  A single-rank cf_compute /
+ * cf_compute_host is one graph; the split-phase calls of a multi-rank step are three (begin,
+ * direct, end: the caller's all-reduce runs between them on the same stream).  Evaluations with
+ * timing on run eagerly.  Results are identical either way (the same kernels in the same order). */
 CF_EXPORT int cf_set_graph(cf_handle* h, int enable);
 /* Number of graph captures and replays since cf_set_graph(h, 1). */
 CF_EXPORT int cf_get_graph_stats(const cf_handle* h, int64_t* captures, int64_t* replays);

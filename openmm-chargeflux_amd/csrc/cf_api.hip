@@ -44,6 +44,7 @@ struct cf_handle {
     double* ene_host_dev = nullptr;
     double default_box[9] = {};
     const double* pos_pending = nullptr;
+    double box9_last[9] = {};   // box of the begun evaluation (graph key of its end segment)
     // host copy of the topology cf_create was given (cf_update_parameters may change only
     // parameters, not which atoms the flux terms and exclusions connect)
     std::vector<int4> topo_terms;
@@ -827,6 +828,7 @@ CF_EXPORT int cf_get_owned_range(const cf_handle* H, int32_t* lo, int32_t* hi) {
 static bool host_prologue(cf_handle* H, const double* box9) {
     cf::Handle& h = H->h;
     set_box(H, box9);
+    if (h.pbc) std::memcpy(H->box9_last, box9, sizeof(H->box9_last));
     const double Lmin = std::min(h.box_L[0], std::min(h.box_L[1], h.box_L[2]));
     const double s_call = h.skin > 0 ? std::max(0.0, std::min(h.skin, 0.5 * Lmin - h.cutoff)) : 0.0;
     const bool reusable = h.pbc && h.skin > 0 && h.list_valid && s_call == h.list_skin &&
@@ -877,35 +879,10 @@ static void launch_begin(cf_handle* H, const double* pos_dev, int flags, bool re
     }
 }
 
-CF_EXPORT int cf_compute_begin(cf_handle* H, const double* pos_dev, const double* box9, int flags) {
-    return guarded([&] {
-        if (!H || !pos_dev) fail(CF_ERR_INVALID, "null argument");
-        cf::Handle& h = H->h;
-        if (h.pending_flags >= 0) fail(CF_ERR_STATE, "cf_compute_begin called twice without cf_compute_end");
-        check_hip(hipSetDevice(h.device), "hipSetDevice");
-        const bool reusable = host_prologue(H, box9);
-        launch_begin(H, pos_dev, flags, reusable);
-        launch_check("compute_begin");
-        h.pending_flags = flags;
-        h.direct_done = false;
-        H->pos_pending = pos_dev;
-    });
-}
-
-CF_EXPORT int cf_kspace_buffer(cf_handle* H, double** buf, int64_t* count) {
-    return guarded([&] {
-        if (!H || !buf || !count) fail(CF_ERR_INVALID, "null argument");
-        if (!H->h.pbc) { *buf = nullptr; *count = 0; return; }
-        *buf = cf::kspace_reduce_buffer(H->h, count);
-    });
-}
-
 // direct space + exclusion correction of a begun evaluation: independent of the
 // structure factors, so a multi-rank caller can run it while S(k) is being all-reduced
-static void run_direct(cf_handle* H) {
+static void launch_direct(cf_handle* H) {
     cf::Handle& h = H->h;
-    if (h.direct_done) return;
-    h.direct_done = true;
     if (h.hi <= h.lo) return;
     const int flags = h.pending_flags;
     const int forces = flags & CF_INCLUDE_FORCES, energy = flags & CF_INCLUDE_ENERGY;
@@ -916,16 +893,6 @@ static void run_direct(cf_handle* H) {
         Timed t(H, PH_DIRECT);
         cf::launch_nopbc(h, H->pos_pending, forces, energy);
     }
-}
-
-CF_EXPORT int cf_compute_direct(cf_handle* H) {
-    return guarded([&] {
-        if (!H) fail(CF_ERR_INVALID, "null handle");
-        if (H->h.pending_flags < 0) fail(CF_ERR_STATE, "cf_compute_direct without cf_compute_begin");
-        check_hip(hipSetDevice(H->h.device), "hipSetDevice");
-        run_direct(H);
-        launch_check("compute_direct");
-    });
 }
 
 // launches of cf_compute_end (after run_direct): k-space coefficients, reciprocal forces, chain
@@ -963,25 +930,15 @@ static void launch_end(cf_handle* H, int flags, double* forces_dev, double* ener
     }
 }
 
-CF_EXPORT int cf_compute_end(cf_handle* H, double* forces_dev, double* energy_dev) {
-    return guarded([&] {
-        if (!H) fail(CF_ERR_INVALID, "null handle");
-        cf::Handle& h = H->h;
-        if (h.pending_flags < 0) fail(CF_ERR_STATE, "cf_compute_end without cf_compute_begin");
-        check_hip(hipSetDevice(h.device), "hipSetDevice");
-        run_direct(H);
-        const int flags = h.pending_flags;
-        h.pending_flags = -1;
-        launch_end(H, flags, forces_dev, energy_dev);
-        launch_check("compute_end");
-    });
-}
+// ---- hipGraph replay (cf_set_graph) ------------------------------------------------------------
+// The launches of an evaluation are captured into hipGraphs on a private stream and replayed on
+// the handle's stream while the calls look the same to the host: the same device buffers,
+// flags, box and neighbour-list decision (a rebuild under a kept skin is decided on the device,
+// inside the graph).  Anything else re-captures.  Segments: the whole single-call evaluation
+// (cf_compute), and for the split-phase calls of a multi-rank step the begin, direct and end
+// launches separately (the caller's all-reduce runs between them on the same stream).
+enum GraphSeg { SEG_FULL, SEG_BEGIN, SEG_DIRECT, SEG_END, SEG_COUNT };
 
-// Graph replay of single-call evaluations (cf_set_graph): everything a call would launch is
-// captured once into a hipGraph on a private stream and replayed on the handle's stream as
-// long as the call looks the same to the host -- the same position / force / energy buffers and
-// flags, the same box and list decision (the rebuild itself is decided on the device, inside the
-// graph).  Anything else (a new box, other buffers, timing on) re-captures or runs eagerly.
 struct GraphKey {
     const void* pos = nullptr; void* frc = nullptr; void* ene = nullptr;
     int flags = -1; bool reusable = false;
@@ -995,12 +952,12 @@ struct GraphKey {
 struct GraphCache {
     bool enabled = false;
     hipStream_t cap = nullptr;
-    hipGraphExec_t exec = nullptr;
-    GraphKey key;
+    hipGraphExec_t exec[SEG_COUNT] = {};
+    GraphKey key[SEG_COUNT];
     int64_t captures = 0, replays = 0;
-    void drop() {
-        if (exec) (void)hipGraphExecDestroy(exec);
-        exec = nullptr;
+    void drop(int s) {
+        if (exec[s]) (void)hipGraphExecDestroy(exec[s]);
+        exec[s] = nullptr;
     }
 };
 
@@ -1019,11 +976,62 @@ static void graph_forget(cf_handle* H) {
     auto& v = graph_caches();
     for (size_t i = 0; i < v.size(); i++)
         if (v[i].first == H) {
-            v[i].second.drop();
+            for (int s = 0; s < SEG_COUNT; s++) v[i].second.drop(s);
             if (v[i].second.cap) (void)hipStreamDestroy(v[i].second.cap);
             v.erase(v.begin() + i);
             return;
         }
+}
+// graph mode for this call (timed evaluations run eagerly: replays could not record the events)
+static GraphCache* graph_active(cf_handle* H) {
+    GraphCache* g = graph_of(H, false);
+    return (g && g->enabled && !H->timing) ? g : nullptr;
+}
+
+// run `launches` (which enqueue on h.stream) as segment `seg`: replay the cached graph when the
+// key matches, else capture them afresh; g == null: eagerly
+}  // extern "C"
+template <class F>
+static void run_segment(cf_handle* H, GraphCache* g, int seg, const GraphKey& k, F&& launches) {
+    cf::Handle& h = H->h;
+    if (!g) { launches(); return; }
+    if (!g->exec[seg] || !(k == g->key[seg])) {
+        g->drop(seg);
+        hipStream_t user = h.stream;
+        h.stream = g->cap;
+        hipGraph_t graph = nullptr;
+        hipError_t e = hipStreamBeginCapture(g->cap, hipStreamCaptureModeThreadLocal);
+        if (e == hipSuccess) {
+            try {
+                launches();
+            } catch (...) {
+                (void)hipStreamEndCapture(g->cap, &graph);
+                if (graph) (void)hipGraphDestroy(graph);
+                h.stream = user;
+                throw;
+            }
+            e = hipStreamEndCapture(g->cap, &graph);
+        }
+        h.stream = user;
+        check_hip(e, "hipStreamBeginCapture / EndCapture");
+        e = hipGraphInstantiate(&g->exec[seg], graph, nullptr, nullptr, 0);
+        (void)hipGraphDestroy(graph);
+        check_hip(e, "hipGraphInstantiate");
+        g->key[seg] = k;
+        g->captures++;
+    } else {
+        g->replays++;
+    }
+    check_hip(hipGraphLaunch(g->exec[seg], h.stream), "hipGraphLaunch");
+}
+
+extern "C" {
+static GraphKey make_key(const cf::Handle& h, const void* pos, void* frc, void* ene, int flags, bool reusable,
+                         const double* box9) {
+    GraphKey k;
+    k.pos = pos; k.frc = frc; k.ene = ene; k.flags = flags; k.reusable = reusable;
+    if (h.pbc && box9) std::memcpy(k.box, box9, sizeof(k.box));
+    return k;
 }
 
 CF_EXPORT int cf_set_graph(cf_handle* H, int enable) {
@@ -1045,10 +1053,70 @@ CF_EXPORT int cf_get_graph_stats(const cf_handle* H, int64_t* captures, int64_t*
     return CF_OK;
 }
 
+// ---- the evaluation entry points -----------------------------------------------------------------
+CF_EXPORT int cf_compute_begin(cf_handle* H, const double* pos_dev, const double* box9, int flags) {
+    return guarded([&] {
+        if (!H || !pos_dev) fail(CF_ERR_INVALID, "null argument");
+        cf::Handle& h = H->h;
+        if (h.pending_flags >= 0) fail(CF_ERR_STATE, "cf_compute_begin called twice without cf_compute_end");
+        check_hip(hipSetDevice(h.device), "hipSetDevice");
+        const bool reusable = host_prologue(H, box9);
+        run_segment(H, graph_active(H), SEG_BEGIN, make_key(h, pos_dev, nullptr, nullptr, flags, reusable, box9),
+                    [&] { launch_begin(H, pos_dev, flags, reusable); });
+        launch_check("compute_begin");
+        h.pending_flags = flags;
+        h.direct_done = false;
+        H->pos_pending = pos_dev;
+    });
+}
+
+CF_EXPORT int cf_kspace_buffer(cf_handle* H, double** buf, int64_t* count) {
+    return guarded([&] {
+        if (!H || !buf || !count) fail(CF_ERR_INVALID, "null argument");
+        if (!H->h.pbc) { *buf = nullptr; *count = 0; return; }
+        *buf = cf::kspace_reduce_buffer(H->h, count);
+    });
+}
+
+static void run_direct(cf_handle* H) {
+    cf::Handle& h = H->h;
+    if (h.direct_done) return;
+    h.direct_done = true;
+    run_segment(H, graph_active(H), SEG_DIRECT, make_key(h, H->pos_pending, nullptr, nullptr, h.pending_flags, false, nullptr),
+                [&] { launch_direct(H); });
+}
+
+CF_EXPORT int cf_compute_direct(cf_handle* H) {
+    return guarded([&] {
+        if (!H) fail(CF_ERR_INVALID, "null handle");
+        if (H->h.pending_flags < 0) fail(CF_ERR_STATE, "cf_compute_direct without cf_compute_begin");
+        check_hip(hipSetDevice(H->h.device), "hipSetDevice");
+        run_direct(H);
+        launch_check("compute_direct");
+    });
+}
+
+CF_EXPORT int cf_compute_end(cf_handle* H, double* forces_dev, double* energy_dev) {
+    return guarded([&] {
+        if (!H) fail(CF_ERR_INVALID, "null handle");
+        cf::Handle& h = H->h;
+        if (h.pending_flags < 0) fail(CF_ERR_STATE, "cf_compute_end without cf_compute_begin");
+        check_hip(hipSetDevice(h.device), "hipSetDevice");
+        run_direct(H);
+        const int flags = h.pending_flags;
+        h.pending_flags = -1;
+        run_segment(H, graph_active(H), SEG_END,
+                    make_key(h, H->pos_pending, forces_dev, energy_dev, flags, false, h.pbc ? H->box9_last : nullptr),
+                    [&] { launch_end(H, flags, forces_dev, energy_dev); });
+        launch_check("compute_end");
+    });
+}
+
+// one evaluation = begin + end; in graph mode a single-rank call is one graph (SEG_FULL)
 CF_EXPORT int cf_compute(cf_handle* H, const double* pos_dev, const double* box9, int flags, double* forces_dev,
                          double* energy_dev) {
-    GraphCache* g = H ? graph_of(H, false) : nullptr;
-    if (!g || !g->enabled || H->timing || H->h.world > 1) {
+    GraphCache* g = H ? graph_active(H) : nullptr;
+    if (!g || H->h.world > 1) {
         int rc = cf_compute_begin(H, pos_dev, box9, flags);
         if (rc != CF_OK) return rc;
         return cf_compute_end(H, forces_dev, energy_dev);
@@ -1059,44 +1127,15 @@ CF_EXPORT int cf_compute(cf_handle* H, const double* pos_dev, const double* box9
         if (h.pending_flags >= 0) fail(CF_ERR_STATE, "cf_compute during a begun evaluation");
         check_hip(hipSetDevice(h.device), "hipSetDevice");
         const bool reusable = host_prologue(H, box9);
-        GraphKey k;
-        k.pos = pos_dev; k.frc = forces_dev; k.ene = energy_dev; k.flags = flags; k.reusable = reusable;
-        if (h.pbc && box9) std::memcpy(k.box, box9, sizeof(k.box));
-        if (!g->exec || !(k == g->key)) {
-            g->drop();
-            hipStream_t user = h.stream;
-            h.stream = g->cap;
-            hipGraph_t graph = nullptr;
-            hipError_t e = hipStreamBeginCapture(g->cap, hipStreamCaptureModeThreadLocal);
-            if (e == hipSuccess) {
-                try {
-                    H->pos_pending = pos_dev;
-                    h.pending_flags = flags;
-                    h.direct_done = false;
-                    launch_begin(H, pos_dev, flags, reusable);
-                    run_direct(H);
-                    h.pending_flags = -1;
-                    launch_end(H, flags, forces_dev, energy_dev);
-                } catch (...) {
-                    (void)hipStreamEndCapture(g->cap, &graph);
-                    if (graph) (void)hipGraphDestroy(graph);
-                    h.stream = user;
-                    h.pending_flags = -1;
-                    throw;
-                }
-                e = hipStreamEndCapture(g->cap, &graph);
-            }
-            h.stream = user;
-            check_hip(e, "hipStreamBeginCapture / EndCapture");
-            e = hipGraphInstantiate(&g->exec, graph, nullptr, nullptr, 0);
-            (void)hipGraphDestroy(graph);
-            check_hip(e, "hipGraphInstantiate");
-            g->key = k;
-            g->captures++;
-        } else {
-            g->replays++;
-        }
-        check_hip(hipGraphLaunch(g->exec, h.stream), "hipGraphLaunch");
+        H->pos_pending = pos_dev;
+        run_segment(H, g, SEG_FULL, make_key(h, pos_dev, forces_dev, energy_dev, flags, reusable, box9), [&] {
+            h.pending_flags = flags;
+            launch_begin(H, pos_dev, flags, reusable);
+            launch_direct(H);
+            h.pending_flags = -1;
+            launch_end(H, flags, forces_dev, energy_dev);
+        });
+        h.pending_flags = -1;
     });
 }
 

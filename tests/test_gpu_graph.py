@@ -81,3 +81,51 @@ def test_graph_recaptures_for_new_buffers_and_flags():
     torch.cuda.synchronize()
     assert np.array_equal(f.cpu().numpy(), f0)
     assert k.graph_stats()[0] == caps
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_graph_segments_of_a_decomposed_step_are_bitwise_eager(world):
+    """Multi-rank split calls (begin / direct / end) replayed as three graphs per rank, with the
+    k-space buffers summed between begin and end (the all-reduce, by hand on one GPU)."""
+    from openmmcoul.distributed import device_buffer_as_tensor
+    system, force, pos, box = ts.water_box(4000, cutoff=1.0, ewald_tol=1e-4, every_bond_angle=5)
+    stream = torch.cuda.current_stream().cuda_stream
+    pt = torch.tensor(pos, dtype=torch.float64, device="cuda")
+
+    def run(graph):
+        ks = [HipCalcCoulForceKernel(stream=stream, rank=r, world_size=world, kspace_algo=2).initialize(system, force)
+              for r in range(world)]
+        for k in ks:
+            k.set_neighbor_skin(0.1)
+            if graph:
+                k.set_graph(True)
+        bufs = [device_buffer_as_tensor(*k.kspace_buffer(), "cuda") for k in ks]
+        f = torch.zeros_like(pt)
+        es = [torch.zeros(1, dtype=torch.float64, device="cuda") for _ in ks]
+        x = pt.clone()
+        rng = np.random.default_rng(8)
+        out = []
+        for _ in range(5):
+            f.zero_()
+            for k in ks:
+                k.begin(x, box, True, True)
+            total = sum(bufs[1:], bufs[0].clone())
+            for b in bufs:
+                b.copy_(total)
+            for k in ks:
+                k.direct()
+            for k, e in zip(ks, es):
+                k.end(f, e)
+            torch.cuda.synchronize()
+            out.append((sum(e.item() for e in es), f.cpu().numpy().copy()))
+            x += torch.tensor(rng.normal(scale=0.006, size=pos.shape), device="cuda")
+        stats = [k.graph_stats() for k in ks]
+        for k in ks:
+            k.destroy()
+        return out, stats
+
+    a, _ = run(False)
+    b, stats = run(True)
+    for (ea, fa), (eb, fb) in zip(a, b):
+        assert ea == eb and np.array_equal(fa, fb)
+    assert all(reps > 0 for _, reps in stats), stats

@@ -24,12 +24,14 @@ from openmmcoul import testsystems as ts  # noqa: E402
 from openmmcoul.distributed import ShardedCoulKernel  # noqa: E402
 
 
-def probe(system, force, pos_np, box, world, steps, skin, algo=2, timing=True):
+def probe(system, force, pos_np, box, world, steps, skin, algo=2, timing=True, graph=False):
     dev = torch.device("cuda", 0)
     stream = torch.cuda.current_stream(dev).cuda_stream
     k = HipCalcCoulForceKernel(device=0, stream=stream, rank=0, world_size=world, kspace_algo=algo).initialize(system, force)
     if skin > 0:
         k.set_neighbor_skin(skin)
+    if graph:
+        k.set_graph(True)   # begin / direct / end replayed as hipGraphs (cf_set_graph)
     kern = ShardedCoulKernel(system, force, dev, kernel=k)
     lo, hi = kern.lo, kern.hi
     n = len(pos_np)
@@ -66,7 +68,7 @@ def probe(system, force, pos_np, box, world, steps, skin, algo=2, timing=True):
     tm = k.timing()
     k.set_timing(False)
     gpu = {p: v[0] / steps for p, v in tm.items()}
-    return {"world": world, "owned": hi - lo, "ms_per_step": round(wall, 4),
+    return {"world": world, "owned": hi - lo, "graph": graph, "ms_per_step": round(wall, 4),
             "host_enqueue_ms_per_step": round(host / steps * 1e3, 4),
             "lib_gpu_ms_per_step": round(sum(gpu.values()), 4),
             "phases": {p: round(v, 4) for p, v in gpu.items()}}
@@ -80,11 +82,12 @@ def main():
     ap.add_argument("--neighbor-skin", type=float, default=0.1)
     ap.add_argument("--kspace-algo", type=int, default=2)
     ap.add_argument("--no-timing", action="store_true", help="no per-phase events (clean wall time)")
+    ap.add_argument("--graph", action="store_true", help="replay the launches as hipGraphs (implies --no-timing)")
     args = ap.parse_args()
     system, force, pos_np, box = ts.make(args.config)
     for w in args.worlds:
         print(json.dumps(probe(system, force, pos_np, box, w, args.steps, args.neighbor_skin, args.kspace_algo,
-                               not args.no_timing)), flush=True)
+                               not (args.no_timing or args.graph), args.graph)), flush=True)
 
 
 if __name__ == "__main__":
