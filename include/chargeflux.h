@@ -146,12 +146,16 @@ CF_EXPORT int cf_update_parameters(cf_handle* h, const cf_params* params);
 /* Number of neighbour-list builds and evaluations since cf_create. */
 CF_EXPORT int cf_get_neighbor_stats(const cf_handle* h, int64_t* builds, int64_t* evaluations);
 /* Slow-path diagnostics since cf_create (synchronises the stream): evaluations whose half-list
- * partner sums could not be used -- a window over 4096 atoms, an overflowed list, a term beyond
- * the fixed-point range, rows the list builder could not place -- so that every atom's pair
- * sums were recomputed by the fp64 cell rescan (same results, several times slower); and list
- * rows rescanned after a full-list overflow.  Nonzero values on a production system mean the
- * neighbour-list capacity or the cell geometry does not suit it. */
-CF_EXPORT int cf_get_fallback_stats(const cf_handle* h, int64_t* half_list_fallbacks, int64_t* rows_rescanned);
+ * partner sums could not be used, so that every atom's pair sums were recomputed by the fp64 cell
+ * rescan (same results, several times slower); list rows rescanned after a full-list overflow;
+ * and the union of the reasons for the first (CF_FALLBACK_* bits).  Nonzero values on a
+ * production system mean the neighbour-list capacity or the cell geometry does not suit it
+ * (DESIGN.md §4.4).  Any output may be NULL. */
+#define CF_FALLBACK_WINDOW 1        /* a cell's 18-cell window held more than 4096 atoms */
+#define CF_FALLBACK_LIST 2          /* a list row overflowed, or the builder could not place it */
+#define CF_FALLBACK_FIXED_POINT 4   /* a partner-side term beyond the fixed-point range (|F| >= 2^16) */
+CF_EXPORT int cf_get_fallback_stats(const cf_handle* h, int64_t* half_list_fallbacks, int64_t* rows_rescanned,
+                                    int32_t* reasons);
 
 /*
  * Replaces ReferenceCalcCoulForceKernel::execute (ReferenceCoulKernels.cpp:424-636).

@@ -588,8 +588,8 @@ CF_EXPORT int cf_create(const cf_params* p, const cf_options* opt, cf_handle** o
             check_hip(hipMemset(h.half_flag, 0, sizeof(int)), "memset");
             h.n_builds_dev = dalloc<long long>(H, 1);
             check_hip(hipMemset(h.n_builds_dev, 0, sizeof(long long)), "memset");
-            h.n_fallback_dev = dalloc<long long>(H, 2);
-            check_hip(hipMemset(h.n_fallback_dev, 0, 2 * sizeof(long long)), "memset");
+            h.n_fallback_dev = dalloc<long long>(H, 3);
+            check_hip(hipMemset(h.n_fallback_dev, 0, 3 * sizeof(long long)), "memset");
             if (h.world > 1) h.own_s = dalloc<int>(H, std::max(nown, 1));  // owned atoms, cell-sorted
             std::copy(p->default_box, p->default_box + 9, H->default_box);
             alloc_nlist(H, 0.0);
@@ -780,9 +780,10 @@ CF_EXPORT int cf_get_neighbor_stats(const cf_handle* H, int64_t* builds, int64_t
     return CF_OK;
 }
 
-CF_EXPORT int cf_get_fallback_stats(const cf_handle* H, int64_t* half_list_fallbacks, int64_t* rows_rescanned) {
+CF_EXPORT int cf_get_fallback_stats(const cf_handle* H, int64_t* half_list_fallbacks, int64_t* rows_rescanned,
+                                    int32_t* reasons) {
     if (!H) { g_err = "null handle"; return CF_ERR_INVALID; }
-    long long v[2] = {0, 0};
+    long long v[3] = {0, 0, 0};
     if (H->h.n_fallback_dev) {
         (void)hipSetDevice(H->h.device);
         if (hipStreamSynchronize(H->h.stream) != hipSuccess ||
@@ -793,6 +794,7 @@ CF_EXPORT int cf_get_fallback_stats(const cf_handle* H, int64_t* half_list_fallb
     }
     if (half_list_fallbacks) *half_list_fallbacks = v[0];
     if (rows_rescanned) *rows_rescanned = v[1];
+    if (reasons) *reasons = (int32_t)v[2];
     return CF_OK;
 }
 

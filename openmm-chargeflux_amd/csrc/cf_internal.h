@@ -143,8 +143,9 @@ struct Handle {
     double* pos_ref = nullptr;  // [N*3] positions at the last build (skin > 0)
     int* skin_flag = nullptr;   // [1] device: rebuild this evaluation (host-forced or moved > skin/2)
     long long* n_builds_dev = nullptr;  // [1] list builds (device counter)
-    long long* n_fallback_dev = nullptr;  // [2] evaluations whose half-list sums were unusable (fp64
-                                          // rescan of every atom); list rows rescanned after an overflow
+    long long* n_fallback_dev = nullptr;  // [3] evaluations whose half-list sums were unusable (fp64
+                                          // rescan of every atom); list rows rescanned after an
+                                          // overflow; union of the half-list reasons (CF_FALLBACK_*)
     int64_t n_evals = 0;
     // cell-sort scratch (the sort kernels run only when the device flag asks for a rebuild;
     // k_cell_commit then copies the new order to the live arrays)

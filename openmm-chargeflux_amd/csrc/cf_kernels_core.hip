@@ -376,6 +376,10 @@ constexpr double kFixInv = 1.0 / 17179869184.0;
 constexpr double kFixMagic = 6755399441055744.0;       // 1.5 * 2^52
 constexpr long long kFixMagicBits = 0x4338000000000000LL;
 constexpr double kFixMax = 65536.0;
+// why half_flag was raised (bits; cf_get_fallback_stats reports their union)
+constexpr int kHalfWindowFull = 1;     // a cell's 18-cell window holds more than kHalfMaxWin atoms
+constexpr int kHalfListOverflow = 2;   // a row's sub-list overflowed, or the builder could not place it
+constexpr int kHalfFixedRange = 4;     // a partner-side term beyond the fixed-point range
 
 struct DirectArgs {
     int n, lo, hi, include_forces;
@@ -1109,7 +1113,7 @@ __global__ void __launch_bounds__(1024) k_pairs_half(DirectArgs a) {
             off += n;
         }
         wtot = off;
-        if (off > kHalfMaxWin) atomicOr(a.half_flag, 1);
+        if (off > kHalfMaxWin) atomicOr(a.half_flag, kHalfWindowFull);
     }
     __syncthreads();
     const int nw = wtot;
@@ -1121,13 +1125,13 @@ __global__ void __launch_bounds__(1024) k_pairs_half(DirectArgs a) {
     __syncthreads();
     const int r0 = win[kHalfOwn].x, nrows = a.cend[cell] - r0;
     const int g = threadIdx.x & 3;   // sub-list walked by this lane
-    bool bad = false;
+    bool bad = false, bad_list = false;
     for (int rb = 0; rb < nrows; rb += 256) {
         const int rr = rb + (threadIdx.x >> 2);
         bool active = rr < nrows;
         const int row = r0 + (active ? rr : 0);
         const int cnt = active ? a.nl_cnt[(size_t)g * a.nlr + row] : 0;
-        if (cnt > a.nb_cap) { bad = true; active = false; }
+        if (cnt > a.nb_cap) { bad_list = true; active = false; }
         std::conditional_t<MIXED, PairAccF, PairAcc> acc;
         if constexpr (MIXED) {
           if (active) {
@@ -1281,7 +1285,10 @@ __global__ void __launch_bounds__(1024) k_pairs_half(DirectArgs a) {
             }
         }
     }
-    if (__ballot(bad) && (threadIdx.x & 63) == 0) atomicOr(a.half_flag, 1);
+    {
+        const int why = (__ballot(bad_list) ? kHalfListOverflow : 0) | (__ballot(bad) ? kHalfFixedRange : 0);
+        if (why && (threadIdx.x & 63) == 0) atomicOr(a.half_flag, why);
+    }
     if (!a.include_forces) return;
     __syncthreads();
     unsigned long long* out = a.win_out + (size_t)cell * kHalfMaxWin * 4;
@@ -1640,7 +1647,7 @@ __global__ void __launch_bounds__(kEChunk) k_assemble_energy(int lo, int hi, con
         if (energy_out) *energy_out = e;
         if (flag) *flag = 0;
         if (half_flag) {
-            if (*half_flag && fallback) fallback[0] += 1;
+            if (*half_flag && fallback) { fallback[0] += 1; fallback[2] |= *half_flag; }
             *half_flag = 0;
         }
         if (xrange) { xrange[0] = INT_MAX; xrange[1] = INT_MIN; }   // re-arm the grid x-slab

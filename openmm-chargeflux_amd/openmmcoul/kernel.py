@@ -175,10 +175,11 @@ class HipCalcCoulForceKernel:
 
     def fallback_stats(self):
         """(evaluations that fell back to the fp64 rescan of every atom, list rows rescanned
-        after a full-list overflow) since initialize: slow-path diagnostics."""
-        a, b = C.c_int64(), C.c_int64()
-        _cabi.check(self._lib.cf_get_fallback_stats(self._h, C.byref(a), C.byref(b)), self._lib)
-        return a.value, b.value
+        after a full-list overflow, union of the reasons: 1 window > 4096 atoms, 2 list overflow /
+        unplaceable rows, 4 fixed-point range) since initialize: slow-path diagnostics."""
+        a, b, r = C.c_int64(), C.c_int64(), C.c_int32()
+        _cabi.check(self._lib.cf_get_fallback_stats(self._h, C.byref(a), C.byref(b), C.byref(r)), self._lib)
+        return a.value, b.value, r.value
 
     def owned_range(self):
         lo, hi = C.c_int32(), C.c_int32()

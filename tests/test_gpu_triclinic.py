@@ -166,7 +166,9 @@ def test_triclinic_cell_path_vs_oracle_12k(shear):
     system, force, pos, box = _big(shear)
     ref = Oracle(force, box).execute(pos, box)
     for half in (True, False):
-        _compare(_kernel(system, force, EXACT, half), pos, box, ref, 1e-8)
+        k = _kernel(system, force, EXACT, half)
+        _compare(k, pos, box, ref, 1e-8)
+        assert k.fallback_stats() == (0, 0, 0), k.fallback_stats()   # the fast paths, not the rescan
 
 
 def test_triclinic_cell_path_lattice_shifted_atoms_and_grid():

@@ -35,7 +35,7 @@ def run(system, force, pos, box, warmup, evals):
     fb = k.fallback_stats()
     k.destroy()
     out = {p: round(t.get(p, 0.0), 4) for p in ("cell_sort", "neighbor_list", "direct_pairs", "direct_excl")}
-    out["fallbacks_half_evals_rows"] = list(fb)
+    out["fallbacks_half_evals_rows_reasons"] = list(fb)
     return out
 
 
