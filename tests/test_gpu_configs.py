@@ -5,8 +5,8 @@
       charges of a seeded 2 000-atom subset; made by tests/golden/make_golden.py --c3)
   C4  the C3 box atom-decomposed over 8 ranks (here: 8 handles on one GPU, the S(k)
       all-reduce done by hand, exactly what openmmcoul.distributed does over RCCL)
-  C5  768 000 atoms, mixed precision, against the fp64 path on the same positions; and a
-      4-rank split of it
+  C5  768 000 atoms, mixed precision, against the fp64 path on the same positions; and its
+      4- and 8-rank splits
 plus the empty-rank case of the decomposition (a molecule larger than 1/world of the
 system leaves rank 0 without atoms; rank 0 still adds the reciprocal energy).
 
@@ -204,13 +204,17 @@ def test_c5_mixed_precision_vs_fp64(c5):
         assert abs(em - ed) <= 1e-8 * scale, (width, em, ed, td)
 
 
-def test_c5_mixed_four_rank_split(c5):
+@pytest.mark.parametrize("world", [4, 8])
+def test_c5_mixed_rank_split(c5, world):
+    """C5 over 4 and 8 ranks (BASELINE config 5 is an 8-GPU curve): here every rank's handle on
+    one GPU, the k-space all-reduce summed by hand."""
     system, force, pos, box = c5
     k = HipCalcCoulForceKernel(kspace_algo=GRID, precision="mixed").initialize(system, force)
     e1, f1 = k.execute_host(pos, box)
     t1 = k.energy_terms()
     k.destroy()
-    e4, f4, _, ranges = _decomposed(system, force, pos, box, 4, GRID, precision="mixed")
+    e4, f4, _, ranges = _decomposed(system, force, pos, box, world, GRID, precision="mixed")
+    assert len(ranges) == world
     assert all(hi > lo for lo, hi in ranges)
     # one rank walks the half list (each pair once), four ranks the full list: the fp32 pair
     # terms round differently (observed |dE| 2.6e-3 kJ/mol = 2e-11 of sum|terms|)
