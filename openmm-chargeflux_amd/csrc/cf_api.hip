@@ -123,6 +123,7 @@ void alloc_nlist(cf_handle* H, double skin) {
     h.nl = nullptr;
     h.nb_cap = cap;
     h.nl = dalloc<int>(H, (size_t)4 * h.nb_cap * rows);
+    h.alloc_epoch++;
     if (!h.nl_cnt) h.nl_cnt = dalloc<int>(H, (size_t)4 * rows);
 }
 
@@ -176,6 +177,7 @@ void set_cells(cf_handle* H, const double L[3]) {
     int64_t ncell = (int64_t)nc[0] * nc[1] * nc[2];
     if (ncell > h.ncell_alloc) {
         // grow (not graph-capture safe; only happens when the box grows past the initial grid)
+        h.alloc_epoch++;
         if (h.cell_start) { (void)hipFree(h.cell_start); (void)hipFree(h.cell_end); (void)hipFree(h.cell_cnt); }
         if (h.own_cnt) { (void)hipFree(h.own_cnt); (void)hipFree(h.own_start); h.own_cnt = h.own_start = nullptr; }
         cf::check_hip(hipMalloc(&h.cell_start, sizeof(int) * ncell), "cells");
@@ -203,6 +205,7 @@ void set_cells(cf_handle* H, const double L[3]) {
         cf::check_hip(hipMalloc(&h.win_out, sizeof(unsigned long long) * 4 * 4096 * (size_t)ncell), "half-list windows");
         cf::check_hip(hipMalloc(&h.win_woff, sizeof(int) * 18 * (size_t)ncell), "half-list windows");
         h.win_cells = (int)ncell;
+        h.alloc_epoch++;
     }
 }
 
@@ -944,9 +947,11 @@ enum GraphSeg { SEG_FULL, SEG_BEGIN, SEG_DIRECT, SEG_END, SEG_COUNT };
 struct GraphKey {
     const void* pos = nullptr; void* frc = nullptr; void* ene = nullptr;
     int flags = -1; bool reusable = false;
+    int64_t epoch = -1;   // Handle::alloc_epoch: a reallocated buffer invalidates the captured launches
     double box[9] = {};
     bool operator==(const GraphKey& o) const {
         return pos == o.pos && frc == o.frc && ene == o.ene && flags == o.flags && reusable == o.reusable &&
+               epoch == o.epoch &&
                std::memcmp(box, o.box, sizeof(box)) == 0;
     }
 };
@@ -1032,6 +1037,7 @@ static GraphKey make_key(const cf::Handle& h, const void* pos, void* frc, void* 
                          const double* box9) {
     GraphKey k;
     k.pos = pos; k.frc = frc; k.ene = ene; k.flags = flags; k.reusable = reusable;
+    k.epoch = h.alloc_epoch;
     if (h.pbc && box9) std::memcpy(k.box, box9, sizeof(k.box));
     return k;
 }

@@ -159,6 +159,7 @@ struct Handle {
     int* nl_cnt = nullptr;      // [4][N]
     // half list: one rank, fp64, >= 4 cells per axis
     bool half = false;
+    int64_t alloc_epoch = 0;    // bumped when a buffer a captured graph may point to is reallocated
     int* half_flag = nullptr;   // [1] device: half-list sums unusable this evaluation (fp64 rescan)
     unsigned long long* win_out = nullptr;   // [ncell][4096][4] window partials (fixed point)
     int* win_woff = nullptr;    // [ncell][18]

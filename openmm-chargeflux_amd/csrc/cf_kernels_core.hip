@@ -363,6 +363,7 @@ constexpr int kBruteShift = 31;  // shift code: minimum image by floor (brute-fo
 // cell k = ox*9 + (oy+1)*3 + (oz+1)) | LJ type << 26: the partner's address needs no table
 // lookup (the gather is not queued behind LDS work).
 constexpr int kHalfWin = 18;          // window cells per block: x offsets 0 and +1
+constexpr int kHalfBlock = 1024;      // threads per k_pairs_half block (one cell; 4 lanes per row)
 constexpr int kHalfOwn = 4;           // the row cell's own window index (0, 0, 0)
 constexpr int kHalfMaxWin = 4096;     // window atoms per block (LDS accumulators: 128 KB)
 constexpr int kHalfSlotBits = 21;     // sorted slots < 2^21 (cf_api.hip enables half lists below)
@@ -412,7 +413,7 @@ struct DirectArgs {
     unsigned long long* win_out;// [ncell][kHalfMaxWin][4] per-cell window partials (fixed point)
     int* win_woff;              // [ncell][kHalfWin] window offsets of the 18 window cells
     const int* key_s;           // cell key per sorted slot
-    long long* fallback;        // [2] diagnostics (Handle::n_fallback_dev)
+    long long* fallback;        // [3] diagnostics (Handle::n_fallback_dev)
 };
 
 __device__ __forceinline__ int own_slot(const DirectArgs& a, int c) { return a.own_s ? a.own_s[c] : c; }
@@ -1074,7 +1075,7 @@ __device__ __forceinline__ int wrap_cell(int v, int n) { return v < 0 ? v + n : 
 // point (an fp32 value times 2^34 is exact in fp64)
 // TRIC: reduced triclinic box (the box-vector minimum image, min_image); else the per-axis form
 template <bool TYPES, bool MIXED, bool TRIC>
-__global__ void __launch_bounds__(1024) k_pairs_half(DirectArgs a) {
+__global__ void __launch_bounds__(kHalfBlock) k_pairs_half(DirectArgs a) {
     __shared__ double tab[MIXED ? 1 : kErfcMaxM * (kErfcDeg + 1)];
     __shared__ float tabf[MIXED ? kErfcMaxMF * (kErfcDegF + 1) : 1];
     __shared__ double2 ljt[(TYPES && !MIXED) ? kMaxLjTypes : 1];
@@ -1093,15 +1094,15 @@ __global__ void __launch_bounds__(1024) k_pairs_half(DirectArgs a) {
         win[threadIdx.x] = make_int2(b, a.cend[w] - b);
     }
     if constexpr (TYPES) {
-        for (int e = threadIdx.x; e < a.lj_ntypes; e += blockDim.x) {
+        for (int e = threadIdx.x; e < a.lj_ntypes; e += kHalfBlock) {
             if constexpr (MIXED) ljtf[e] = make_float2((float)a.lj_tab[e].x, (float)a.lj_tab[e].y);
             else ljt[e] = a.lj_tab[e];
         }
     }
     if constexpr (MIXED) {
-        for (int e = threadIdx.x; e < a.erfc_m_f * (kErfcDegF + 1); e += blockDim.x) tabf[e] = a.erfc_tab_f[e];
+        for (int e = threadIdx.x; e < a.erfc_m_f * (kErfcDegF + 1); e += kHalfBlock) tabf[e] = a.erfc_tab_f[e];
     } else {
-        for (int e = threadIdx.x; e < kErfcMaxM * (kErfcDeg + 1); e += blockDim.x) tab[e] = a.erfc_tab[e];
+        for (int e = threadIdx.x; e < kErfcMaxM * (kErfcDeg + 1); e += kHalfBlock) tab[e] = a.erfc_tab[e];
     }
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -1119,7 +1120,7 @@ __global__ void __launch_bounds__(1024) k_pairs_half(DirectArgs a) {
     const int nw = wtot;
     if (nw > kHalfMaxWin) return;   // block-uniform; k_excl recomputes everything
     if (threadIdx.x < kHalfWin) a.win_woff[cell * kHalfWin + threadIdx.x] = win[threadIdx.x].y;
-    for (int e = threadIdx.x; e < nw; e += blockDim.x) {
+    for (int e = threadIdx.x; e < nw; e += kHalfBlock) {
         accw[0][e] = 0; accw[1][e] = 0; accw[2][e] = 0; accw[3][e] = 0;
     }
     __syncthreads();
@@ -1218,8 +1219,9 @@ __global__ void __launch_bounds__(1024) k_pairs_half(DirectArgs a) {
                 cd.slot = wdel[ok ? (e >> kHalfSlotBits) & 31 : 0] + t;
                 return cd;
             };
-            auto eval = [&](const Cand& cd) {
-                double dx = pi.x - cd.p.x, dy = pi.y - cd.p.y, dz = pi.z - cd.p.z;
+            // minimum-image pair vector d = x_i - x_j and r^2
+            auto sep = [&](const double4& pj, double& dx, double& dy, double& dz) {
+                dx = pi.x - pj.x; dy = pi.y - pj.y; dz = pi.z - pj.z;
                 if constexpr (TRIC) {
                     min_image(a, dx, dy, dz);
                 } else {
@@ -1227,39 +1229,46 @@ __global__ void __launch_bounds__(1024) k_pairs_half(DirectArgs a) {
                     dy -= a.L.y * rint(dy * a.invL.y);
                     dz -= a.L.z * rint(dz * a.invL.z);
                 }
-                const double r2 = dx * dx + dy * dy + dz * dz;
-                if (r2 <= a.rc2) {   // exact voxel-hash test
-                    const double ke = a.ke;
-                    const double two_over_sqrtpi = 1.1283791670955126;
-                    const double inv_r = rsqrt_fp64(r2);
-                    const double ar = a.alpha * (r2 * inv_r);
-                    double e2;
-                    const double ec = erfc_exp(ar, tab, a.erfc_scale, e2);
-                    const double sig = li.x + cd.lj.x;
-                    double s2 = inv_r * sig;
-                    s2 *= s2;
-                    const double sig6 = s2 * s2 * s2;
-                    const double es6 = sig6 * li.y * cd.lj.y;
-                    const double qj = ke * cd.p.w * inv_r;
-                    const double qq = pi.w * qj;
-                    if (a.include_forces) {
-                        // the force on j, -F_ij, in fixed-point units (x -2^34: exact), which the
-                        // i side also accumulates (negated and unscaled once at the end: the same
-                        // bits as summing F_ij) -- the conversion is then one add per value
-                        const double ndEdRs = fma(qq, ec + ar * e2 * two_over_sqrtpi, es6 * (12 * sig6 - 6)) *
-                                              ((inv_r * inv_r) * -kFixScale);
-                        const double nfx = ndEdRs * dx, nfy = ndEdRs * dy, nfz = ndEdRs * dz;
-                        const double dqjs = kqis * inv_r * ec;
-                        acc.fx += nfx; acc.fy += nfy; acc.fz += nfz;
-                        acc.dq += qj * ec;
-                        bad |= !(fmax(fmax(fabs(nfx), fabs(nfy)), fmax(fabs(nfz), fabs(dqjs))) < kFixMax * kFixScale);
-                        atomicAdd(&accw[0][cd.slot], scaled_to_fix(nfx));
-                        atomicAdd(&accw[1][cd.slot], scaled_to_fix(nfy));
-                        atomicAdd(&accw[2][cd.slot], scaled_to_fix(nfz));
-                        atomicAdd(&accw[3][cd.slot], scaled_to_fix(dqjs));
-                    }
-                    acc.e += qq * ec + es6 * (sig6 - 1);   // the whole pair energy: each pair once
+                return dx * dx + dy * dy + dz * dz;
+            };
+            // the pair term of a pair within rc: i side in registers, j side into the window
+            auto term = [&](const double4& pj, const double2& lj, int slot, double dx, double dy, double dz,
+                            double r2) {
+                const double ke = a.ke;
+                const double two_over_sqrtpi = 1.1283791670955126;
+                const double inv_r = rsqrt_fp64(r2);
+                const double ar = a.alpha * (r2 * inv_r);
+                double e2;
+                const double ec = erfc_exp(ar, tab, a.erfc_scale, e2);
+                const double sig = li.x + lj.x;
+                double s2 = inv_r * sig;
+                s2 *= s2;
+                const double sig6 = s2 * s2 * s2;
+                const double es6 = sig6 * li.y * lj.y;
+                const double qj = ke * pj.w * inv_r;
+                const double qq = pi.w * qj;
+                if (a.include_forces) {
+                    // the force on j, -F_ij, in fixed-point units (x -2^34: exact), which the
+                    // i side also accumulates (negated and unscaled once at the end: the same
+                    // bits as summing F_ij) -- the conversion is then one add per value
+                    const double ndEdRs = fma(qq, ec + ar * e2 * two_over_sqrtpi, es6 * (12 * sig6 - 6)) *
+                                          ((inv_r * inv_r) * -kFixScale);
+                    const double nfx = ndEdRs * dx, nfy = ndEdRs * dy, nfz = ndEdRs * dz;
+                    const double dqjs = kqis * inv_r * ec;
+                    acc.fx += nfx; acc.fy += nfy; acc.fz += nfz;
+                    acc.dq += qj * ec;
+                    bad |= !(fmax(fmax(fabs(nfx), fabs(nfy)), fmax(fabs(nfz), fabs(dqjs))) < kFixMax * kFixScale);
+                    atomicAdd(&accw[0][slot], scaled_to_fix(nfx));
+                    atomicAdd(&accw[1][slot], scaled_to_fix(nfy));
+                    atomicAdd(&accw[2][slot], scaled_to_fix(nfz));
+                    atomicAdd(&accw[3][slot], scaled_to_fix(dqjs));
                 }
+                acc.e += qq * ec + es6 * (sig6 - 1);   // the whole pair energy: each pair once
+            };
+            auto eval = [&](const Cand& cd) {
+                double dx, dy, dz;
+                const double r2 = sep(cd.p, dx, dy, dz);
+                if (r2 <= a.rc2) term(cd.p, cd.lj, cd.slot, dx, dy, dz, r2);   // exact voxel-hash test
             };
             walk_list(nl4, a.nlr, cnt, 0, 1, gather, eval);
         }
@@ -1292,7 +1301,7 @@ __global__ void __launch_bounds__(1024) k_pairs_half(DirectArgs a) {
     if (!a.include_forces) return;
     __syncthreads();
     unsigned long long* out = a.win_out + (size_t)cell * kHalfMaxWin * 4;
-    for (int e = threadIdx.x; e < nw; e += blockDim.x)
+    for (int e = threadIdx.x; e < nw; e += kHalfBlock)
         reinterpret_cast<ulonglong4*>(out)[e] = make_ulonglong4(accw[0][e], accw[1][e], accw[2][e], accw[3][e]);
 }
 
@@ -1804,8 +1813,8 @@ void launch_direct(Handle& h, const double* pos, int include_forces) {
     if (a.half) {
         const int ncell = h.nc[0] * h.nc[1] * h.nc[2];
 #define CF_PAIRS_HALF(TY_, MX_)                                                                              \
-    if (a.tric) hipLaunchKernelGGL((k_pairs_half<TY_, MX_, true>), dim3(ncell), dim3(1024), 0, h.stream, a); \
-    else hipLaunchKernelGGL((k_pairs_half<TY_, MX_, false>), dim3(ncell), dim3(1024), 0, h.stream, a)
+    if (a.tric) hipLaunchKernelGGL((k_pairs_half<TY_, MX_, true>), dim3(ncell), dim3(kHalfBlock), 0, h.stream, a); \
+    else hipLaunchKernelGGL((k_pairs_half<TY_, MX_, false>), dim3(ncell), dim3(kHalfBlock), 0, h.stream, a)
         if (h.mixed) {
             if (a.typ_s) { CF_PAIRS_HALF(true, true); } else { CF_PAIRS_HALF(false, true); }
         } else {

@@ -129,3 +129,26 @@ def test_graph_segments_of_a_decomposed_step_are_bitwise_eager(world):
     for (ea, fa), (eb, fb) in zip(a, b):
         assert ea == eb and np.array_equal(fa, fb)
     assert all(reps > 0 for _, reps in stats), stats
+
+
+def test_graph_recaptures_after_list_reallocation():
+    # a larger skin grows the neighbour-list buffer (alloc_nlist): launches captured before it
+    # point at the freed buffer, so the cache must re-capture (Handle::alloc_epoch in the key)
+    system, force, pos, box = ts.water_box(4000, cutoff=1.0, ewald_tol=1e-4)
+    stream = torch.cuda.current_stream().cuda_stream
+    mk = lambda: HipCalcCoulForceKernel(stream=stream, kspace_algo=2).initialize(system, force)
+    eager, graph = mk(), mk()
+    graph.set_graph(True)
+    for k in (eager, graph):
+        k.set_neighbor_skin(0.05)
+    a = _traj(eager, pos, box, 3)
+    b = _traj(graph, pos, box, 3)
+    caps0, _ = graph.graph_stats()
+    for k in (eager, graph):
+        k.set_neighbor_skin(0.3)   # capacity grows: nl reallocated
+    a += _traj(eager, pos, box, 3)
+    b += _traj(graph, pos, box, 3)
+    for (ea, fa), (eb, fb) in zip(a, b):
+        assert ea == eb and np.array_equal(fa, fb)
+    caps1, reps = graph.graph_stats()
+    assert caps1 > caps0 and reps >= 2, (caps0, caps1, reps)
