@@ -440,6 +440,7 @@ CF_EXPORT int cf_create(const cf_params* p, const cf_options* opt, cf_handle** o
         if (o.precision != CF_PRECISION_DOUBLE && o.precision != CF_PRECISION_MIXED)
             fail(CF_ERR_INVALID, "precision must be CF_PRECISION_DOUBLE or CF_PRECISION_MIXED");
         h.mixed = o.precision == CF_PRECISION_MIXED;
+        h.overlap = !(getenv("CF_OVERLAP") && std::string(getenv("CF_OVERLAP")) == "0");   // A/B
         h.kspace_algo = o.kspace_algo;
         h.stream = (hipStream_t)o.stream;  // NULL = the null stream (orders with torch's default stream)
 
@@ -681,6 +682,9 @@ CF_EXPORT int cf_destroy(cf_handle* H) {
         if (H->h.cell_cnt) (void)hipFree(H->h.cell_cnt);
         if (H->h.own_cnt) { (void)hipFree(H->h.own_cnt); (void)hipFree(H->h.own_start); }
         if (H->h.own_stream) (void)hipStreamDestroy(H->h.stream);
+        if (H->h.aux) (void)hipStreamDestroy(H->h.aux);
+        if (H->h.ev_fork) (void)hipEventDestroy(H->h.ev_fork);
+        if (H->h.ev_join) (void)hipEventDestroy(H->h.ev_join);
         delete H;
     });
 }
@@ -935,6 +939,82 @@ static void launch_end(cf_handle* H, int flags, double* forces_dev, double* ener
     }
 }
 
+// One single-rank evaluation.  With the grid k-space the reciprocal chain (bin sort, spread,
+// forward DFT, coefficients, inverse DFT, interpolation) depends on nothing the cell list and
+// the direct space produce -- both read the positions and k_atoms_prep's charges -- so it runs
+// on the handle's second stream while they run on the first: the small, latency-bound launches
+// of either chain (DFT stages, sorts, exclusions) fill the CUs the other leaves idle.  Joined
+// before k_assemble_energy, which adds the reciprocal dE/dq and forces (stored apart by the
+// interpolation) in the one-stream order: the same bits as launch_begin / direct / end.
+static bool overlap_ok(const cf::Handle& h, int flags) {
+    return h.overlap && h.aux && h.world == 1 && h.pbc && h.kspace_algo == 2 && h.hi > h.lo &&
+           (flags & (CF_INCLUDE_FORCES | CF_INCLUDE_ENERGY));
+}
+
+static void launch_full(cf_handle* H, const double* pos_dev, int flags, bool reusable, double* forces_dev,
+                        double* energy_dev) {
+    cf::Handle& h = H->h;
+    if (!overlap_ok(h, flags)) {
+        h.rec_split = false;
+        h.pending_flags = flags;
+        launch_begin(H, pos_dev, flags, reusable);
+        launch_direct(H);
+        h.pending_flags = -1;
+        launch_end(H, flags, forces_dev, energy_dev);
+        return;
+    }
+    const int forces = flags & CF_INCLUDE_FORCES, energy = flags & CF_INCLUDE_ENERGY;
+    { Timed t(H, PH_FLUX); cf::launch_flux_terms(h, pos_dev); }
+    { Timed t(H, PH_PREP); cf::launch_atoms_prep(h, pos_dev, reusable); }
+    const hipStream_t main = h.stream;
+    check_hip(hipEventRecord(h.ev_fork, main), "hipEventRecord (fork)");
+    check_hip(hipStreamWaitEvent(h.aux, h.ev_fork, 0), "hipStreamWaitEvent (fork)");
+    h.stream = h.aux;
+    try {
+        { Timed t(H, PH_GSORT); cf::launch_grid_sort(h, pos_dev); }
+        { Timed t(H, PH_GSPREAD); cf::launch_grid_spread(h); }
+        { Timed t(H, PH_GDFTF); cf::launch_grid_dft_fwd(h); }
+        { Timed t(H, PH_COEFFS); cf::launch_grid_coeffs(h, energy); }
+        if (forces) {
+            { Timed t(H, PH_GDFTI); cf::launch_grid_dft_inv(h); }
+            { Timed t(H, PH_GINTERP); cf::launch_grid_interp(h, true); }
+        }
+        check_hip(hipEventRecord(h.ev_join, h.aux), "hipEventRecord (join)");
+    } catch (...) {
+        h.stream = main;
+        throw;
+    }
+    h.stream = main;
+    {
+        Timed t(H, PH_CELLS);
+        if (!reusable) cf::launch_force_rebuild(h);
+        cf::launch_cell_sort(h, pos_dev);
+    }
+    { Timed t(H, PH_NLIST); cf::launch_nlist(h, pos_dev); }
+    h.pending_flags = flags;
+    launch_direct(H);
+    h.pending_flags = -1;
+    check_hip(hipStreamWaitEvent(main, h.ev_join, 0), "hipStreamWaitEvent (join)");
+    h.rec_split = forces != 0;
+    {
+        Timed t(H, PH_ENERGY);
+        cf::launch_assemble_energy(h, (forces && forces_dev) ? forces_dev : nullptr, energy, energy_dev);
+    }
+}
+
+// the second stream and its fork / join events (created outside any capture)
+static void ensure_aux(cf_handle* H) {
+    cf::Handle& h = H->h;
+    if (h.aux || !h.overlap || h.world != 1 || !h.pbc || h.kspace_algo != 2) return;
+    check_hip(hipStreamCreateWithFlags(&h.aux, hipStreamNonBlocking), "hipStreamCreate (reciprocal chain)");
+    check_hip(hipEventCreateWithFlags(&h.ev_fork, hipEventDisableTiming), "hipEventCreate");
+    check_hip(hipEventCreateWithFlags(&h.ev_join, hipEventDisableTiming), "hipEventCreate");
+    if (!h.dedq_rec) {
+        h.dedq_rec = dalloc<double>(H, (size_t)h.n);
+        h.f_rec = dalloc<double>(H, (size_t)4 * h.n);
+    }
+}
+
 // ---- hipGraph replay (cf_set_graph) ------------------------------------------------------------
 // The launches of an evaluation are captured into hipGraphs on a private stream and replayed on
 // the handle's stream while the calls look the same to the host: the same device buffers,
@@ -1069,6 +1149,7 @@ CF_EXPORT int cf_compute_begin(cf_handle* H, const double* pos_dev, const double
         if (h.pending_flags >= 0) fail(CF_ERR_STATE, "cf_compute_begin called twice without cf_compute_end");
         check_hip(hipSetDevice(h.device), "hipSetDevice");
         const bool reusable = host_prologue(H, box9);
+        h.rec_split = false;
         run_segment(H, graph_active(H), SEG_BEGIN, make_key(h, pos_dev, nullptr, nullptr, flags, reusable, box9),
                     [&] { launch_begin(H, pos_dev, flags, reusable); });
         launch_check("compute_begin");
@@ -1123,27 +1204,25 @@ CF_EXPORT int cf_compute_end(cf_handle* H, double* forces_dev, double* energy_de
 // one evaluation = begin + end; in graph mode a single-rank call is one graph (SEG_FULL)
 CF_EXPORT int cf_compute(cf_handle* H, const double* pos_dev, const double* box9, int flags, double* forces_dev,
                          double* energy_dev) {
-    GraphCache* g = H ? graph_active(H) : nullptr;
-    if (!g || H->h.world > 1) {
+    if (H && H->h.world > 1) {
         int rc = cf_compute_begin(H, pos_dev, box9, flags);
         if (rc != CF_OK) return rc;
         return cf_compute_end(H, forces_dev, energy_dev);
     }
     return guarded([&] {
-        if (!pos_dev) fail(CF_ERR_INVALID, "null argument");
+        if (!H || !pos_dev) fail(CF_ERR_INVALID, "null argument");
         cf::Handle& h = H->h;
         if (h.pending_flags >= 0) fail(CF_ERR_STATE, "cf_compute during a begun evaluation");
         check_hip(hipSetDevice(h.device), "hipSetDevice");
         const bool reusable = host_prologue(H, box9);
+        ensure_aux(H);
         H->pos_pending = pos_dev;
-        run_segment(H, g, SEG_FULL, make_key(h, pos_dev, forces_dev, energy_dev, flags, reusable, box9), [&] {
-            h.pending_flags = flags;
-            launch_begin(H, pos_dev, flags, reusable);
-            launch_direct(H);
-            h.pending_flags = -1;
-            launch_end(H, flags, forces_dev, energy_dev);
-        });
+        GraphCache* g = graph_active(H);
+        auto launches = [&] { launch_full(H, pos_dev, flags, reusable, forces_dev, energy_dev); };
+        if (g) run_segment(H, g, SEG_FULL, make_key(h, pos_dev, forces_dev, energy_dev, flags, reusable, box9), launches);
+        else launches();
         h.pending_flags = -1;
+        launch_check("compute");
     });
 }
 
@@ -1191,6 +1270,11 @@ CF_EXPORT int cf_get_dedq(cf_handle* H, double* out) {
         if (!H || !out) fail(CF_ERR_INVALID, "null argument");
         check_hip(hipStreamSynchronize(H->h.stream), "sync");
         check_hip(hipMemcpy(out, H->h.dedq, sizeof(double) * H->h.n, hipMemcpyDeviceToHost), "D2H dedq");
+        if (H->h.rec_split) {   // (direct + excl) + rec, as k_assemble_energy adds them
+            std::vector<double> r(H->h.n);
+            check_hip(hipMemcpy(r.data(), H->h.dedq_rec, sizeof(double) * H->h.n, hipMemcpyDeviceToHost), "D2H dedq");
+            for (int i = 0; i < H->h.n; i++) out[i] += r[i];
+        }
     });
 }
 

@@ -121,6 +121,15 @@ struct Handle {
     double* dedq = nullptr;     // [N] total dE/dq
     double* e_atom = nullptr;   // [N*3] per-atom (self, direct, exclusion) energy
     double* f_part = nullptr;   // [N*3] non-chain forces (recip + direct + excl)
+    // single rank, grid k-space: the reciprocal chain runs on a second stream beside the cell
+    // list and direct space (CF_OVERLAP=0: one stream); its interpolation then stores into
+    // dedq_rec / f_rec, added by k_assemble_energy in the one-stream order ((direct + excl) + rec)
+    bool overlap = true;
+    bool rec_split = false;     // the last evaluation left the reciprocal dE/dq in dedq_rec
+    hipStream_t aux = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    double* dedq_rec = nullptr; // [N]
+    double* f_rec = nullptr;    // [N][4]: the interpolated gradient p and -q (force = -q (ng/L) p)
     // cell list
     int ncell_alloc = 0;
     int nc[3] = {0, 0, 0};
@@ -255,7 +264,7 @@ void launch_grid_dft_fwd(Handle& h);
 double* grid_reduce_buffer(Handle& h, int64_t* count);
 void launch_grid_coeffs(Handle& h, int include_energy);
 void launch_grid_dft_inv(Handle& h);
-void launch_grid_interp(Handle& h);
+void launch_grid_interp(Handle& h, bool split = false);   // split: store into dedq_rec / f_rec
 
 void check_hip(hipError_t e, const char* what);
 

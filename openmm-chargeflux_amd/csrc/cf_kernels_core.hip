@@ -1589,6 +1589,8 @@ __global__ void __launch_bounds__(kEChunk) k_assemble_energy(int lo, int hi, con
                                                              const int2* __restrict__ ce, const double* __restrict__ dedq,
                                                              const double* __restrict__ dqdx,
                                                              const double* __restrict__ f_part, double* __restrict__ out,
+                                                             const double* __restrict__ dedq_rec,
+                                                             const double4* __restrict__ f_rec, double3 gscale,
                                                              const double* __restrict__ e_atom, double* __restrict__ part,
                                                              const double* __restrict__ e_rec_part, int nrec, int pbc,
                                                              double* __restrict__ terms, double* __restrict__ energy_out,
@@ -1602,6 +1604,12 @@ __global__ void __launch_bounds__(kEChunk) k_assemble_energy(int lo, int hi, con
     if (b < hi) {
         if (out) {
             double fx = f_part[3 * b], fy = f_part[3 * b + 1], fz = f_part[3 * b + 2];
+            if (f_rec) {   // reciprocal part from the second stream, added as k_g_interp adds it
+                const double4 r = f_rec[b];
+                fx = fma(r.w * gscale.x, r.x, fx);
+                fy = fma(r.w * gscale.y, r.y, fy);
+                fz = fma(r.w * gscale.z, r.z, fz);
+            }
             // entries in batches of 4: the entry loads, then their dE/dq and dq/dx gathers, all
             // in flight together (two memory latencies per batch, not per entry); the sums keep
             // the entry order
@@ -1615,6 +1623,10 @@ __global__ void __launch_bounds__(kEChunk) k_assemble_energy(int lo, int hi, con
                 for (int u = 0; u < 4; u++) {
                     g[u] = dedq[en[u].y];
                     d[u][0] = dqdx[3 * en[u].x]; d[u][1] = dqdx[3 * en[u].x + 1]; d[u][2] = dqdx[3 * en[u].x + 2];
+                }
+                if (dedq_rec) {
+#pragma unroll
+                    for (int u = 0; u < 4; u++) g[u] += dedq_rec[en[u].y];
                 }
 #pragma unroll
                 for (int u = 0; u < 4; u++) {
@@ -1873,7 +1885,9 @@ void launch_assemble_energy(Handle& h, double* forces_out, int include_energy, d
     int nrec = (h.pbc && include_energy && h.rank == 0) ? h.e_rec_nblk : 0;
     const int nparts = std::max(1, nblk(nown, kEChunk));
     hipLaunchKernelGGL(k_assemble_energy, dim3(nparts), dim3(kEChunk), 0, h.stream, h.lo, h.hi, h.ccsr_start,
-                       h.ccsr_ent, h.dedq, h.dqdx, h.f_part, forces_out, h.e_atom, h.e_part, h.e_rec_part, nrec, h.pbc,
+                       h.ccsr_ent, h.dedq, h.dqdx, h.f_part, forces_out, h.rec_split ? h.dedq_rec : nullptr,
+                       h.rec_split ? reinterpret_cast<const double4*>(h.f_rec) : nullptr,
+                       make_double3(h.gp.ng[0] / h.box_L[0], h.gp.ng[1] / h.box_L[1], h.gp.ng[2] / h.box_L[2]), h.e_atom, h.e_part, h.e_rec_part, nrec, h.pbc,
                        h.terms_dev, energy_out, h.energy_dev, h.e_ticket + kTicketEnergy, h.skin_flag, h.g_xrange,
                        h.half ? h.half_flag : nullptr, h.n_fallback_dev);
 }

@@ -1137,7 +1137,8 @@ __global__ void __launch_bounds__(kInterpThreads) k_g_interp(int3 ng, int3 nb, c
                                                              const int4* __restrict__ g0s,
                                                              const double4* __restrict__ srec, double beta,
                                                              double3 gscale, const double* __restrict__ G, int lo,
-                                                             double* __restrict__ dedq, double* __restrict__ f_part) {
+                                                             double* __restrict__ dedq, double* __restrict__ f_part,
+                                                             int store) {
     constexpr int R = 7 + W;
     constexpr int NJ = (W + 3) / 4;
     extern __shared__ double sg[];   // [R][R][R]
@@ -1244,10 +1245,16 @@ __global__ void __launch_bounds__(kInterpThreads) k_g_interp(int3 ng, int3 nb, c
         pz = wave_sum_lane63(pz);
         if (lane == 63) {   // each owned atom is in exactly one bin: no other writer
             const int i = lo + g.w;
-            dedq[i] += pv;
-            f_part[3 * i] += -sr.w * gscale.x * px;
-            f_part[3 * i + 1] += -sr.w * gscale.y * py;
-            f_part[3 * i + 2] += -sr.w * gscale.z * pz;
+            if (store) {   // the reciprocal chain on its own stream: dedq_rec, f_rec = (p, -q) per atom,
+                           // which k_assemble_energy folds in as the fused adds below
+                dedq[i] = pv;
+                reinterpret_cast<double4*>(f_part)[i] = make_double4(px, py, pz, -sr.w);
+            } else {
+                dedq[i] += pv;
+                f_part[3 * i] = fma(-sr.w * gscale.x, px, f_part[3 * i]);
+                f_part[3 * i + 1] = fma(-sr.w * gscale.y, py, f_part[3 * i + 1]);
+                f_part[3 * i + 2] = fma(-sr.w * gscale.z, pz, f_part[3 * i + 2]);
+            }
         }
     }
 }
@@ -1613,7 +1620,7 @@ void launch_grid_dft_inv(Handle& h) {
     cgemm<false, true>(h, CGemm{ngx * ngy, ngz, KZ, h.g_t1, KZ, 1, tzh, ngz, 0, 1, h.g_grid, ngz, 0, 1, ngz}, 1, ngy);
 }
 
-void launch_grid_interp(Handle& h) {
+void launch_grid_interp(Handle& h, bool split) {
     const GridPlan& p = h.gp;
     const int3 ng = make_int3(p.ng[0], p.ng[1], p.ng[2]), nb = make_int3(p.nb[0], p.nb[1], p.nb[2]);
     const double3 gs = make_double3(p.ng[0] / h.box_L[0], p.ng[1] / h.box_L[1], p.ng[2] / h.box_L[2]);
@@ -1621,7 +1628,8 @@ void launch_grid_interp(Handle& h) {
     const size_t lds = R * R * R * sizeof(double);
 #define CF_INTERP(W_)                                                                                               \
     hipLaunchKernelGGL(k_g_interp<W_>, dim3(p.nbins), dim3(kInterpThreads), lds, h.stream, ng, nb, h.g_start,       \
-                       h.g_g0s, h.g_srec, p.beta, gs, h.g_grid, h.lo, h.dedq, h.f_part)
+                       h.g_g0s, h.g_srec, p.beta, gs, h.g_grid, h.lo, split ? h.dedq_rec : h.dedq,            \
+                       split ? h.f_rec : h.f_part, split ? 1 : 0)
     CF_GRID_W_DISPATCH(p.W, CF_INTERP)
 #undef CF_INTERP
 }

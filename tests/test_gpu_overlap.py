@@ -1,0 +1,65 @@
+"""The single-rank reciprocal chain on a second stream: bin sort, spread,
+DFTs, coefficients and interpolation run beside the cell list and direct space, joined before
+k_assemble_energy, which folds the reciprocal dE/dq and forces in the one-stream order.  Bar:
+bitwise equality with CF_OVERLAP=0 (one stream) for energy, forces, dE/dq and the energy terms,
+with and without a kept list, energy-only calls in between, and graph replay."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+from openmmcoul import HipCalcCoulForceKernel  # noqa: E402
+from openmmcoul import testsystems as ts  # noqa: E402
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+
+
+def _run(monkeypatch, overlap, system, force, pos, box, skin, graph=False, steps=4):
+    monkeypatch.setenv("CF_OVERLAP", "1" if overlap else "0")
+    stream = torch.cuda.current_stream().cuda_stream
+    k = HipCalcCoulForceKernel(stream=stream, kspace_algo=2).initialize(system, force)
+    if skin:
+        k.set_neighbor_skin(skin)
+    if graph:
+        k.set_graph(True)
+    rng = np.random.default_rng(9)
+    pt = torch.tensor(pos, dtype=torch.float64, device="cuda")
+    out = []
+    for s in range(steps):
+        f = torch.zeros_like(pt)
+        e = torch.zeros(1, dtype=torch.float64, device="cuda")
+        forces = s != 2   # an energy-only evaluation in between
+        k.execute_device(pt, box, forces, True, f, e)
+        torch.cuda.synchronize()
+        out.append((e.item(), f.cpu().numpy(), k.dedq() if forces else None, k.energy_terms()))
+        pt += torch.tensor(rng.normal(scale=0.004, size=pos.shape), device="cuda")
+    k.destroy()
+    return out
+
+
+@pytest.mark.parametrize("skin,graph", [(0.0, False), (0.1, False), (0.1, True)])
+def test_overlap_is_bitwise_one_stream(monkeypatch, skin, graph):
+    system, force, pos, box = ts.water_box(4000, cutoff=1.0, ewald_tol=1e-4, every_bond_angle=5)
+    a = _run(monkeypatch, True, system, force, pos, box, skin, graph)
+    b = _run(monkeypatch, False, system, force, pos, box, skin, graph)
+    for (ea, fa, da, ta), (eb, fb, db, tb) in zip(a, b):
+        assert ea == eb and np.array_equal(fa, fb) and np.array_equal(ta, tb)
+        assert (da is None and db is None) or np.array_equal(da, db)
+
+
+def test_overlap_c2_matches_oracle(monkeypatch):
+    from oracle import Oracle
+    system, force, pos, box = ts.make("C2")
+    monkeypatch.setenv("CF_OVERLAP", "1")
+    k = HipCalcCoulForceKernel(kspace_algo=2).initialize(system, force)
+    e, f = k.execute_host(pos, box)
+    ref = Oracle(force, box).execute(pos, box)
+    assert np.abs(f - ref["forces"]).max() <= 1e-6
+    assert abs(e - ref["energy"]) <= 1e-9 * np.abs(ref["terms"]).sum() + 1e-6
+    assert np.abs(k.dedq() - ref["dedq"]).max() <= 1e-6 * max(1.0, np.abs(ref["dedq"]).max())
