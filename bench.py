@@ -123,11 +123,12 @@ def cpu_baseline(force, pos, box, k_sample):
     }
 
 
-# rocprofv3 kernel names of the library's timing phases at C3
-# (a phase timed as one bracket may be several launches: their bytes are summed)
-PMC_KERNEL = {"kspace_force": ["cf::k_force<2>"], "kspace_sfac": ["cf::k_sfac<4, 32>"],
-              "direct_pairs": ["cf::k_pairs_half<true, false>"],
-              "grid_spread": ["cf::k_g_spread_tile<3, 32>"], "grid_interp": ["cf::k_g_interp<14>"]}
+# rocprofv3 kernel names of the library's timing phases at C3, up to their template arguments
+# (the instantiation that runs in the profiled command; a phase timed as one bracket may be
+# several launches: their bytes are summed)
+PMC_KERNEL = {"kspace_force": ["cf::k_force<"], "kspace_sfac": ["cf::k_sfac<"],
+              "direct_pairs": ["cf::k_pairs_half<"],
+              "grid_spread": ["cf::k_g_spread_tile<"], "grid_interp": ["cf::k_g_interp<"]}
 
 
 def pair_count(force, pos, box):
@@ -162,11 +163,12 @@ def pmc_traffic(config, world, phase, precision):
         return None, None
     summary = json.load(open(files[-1]))
     total = 0
-    for name in PMC_KERNEL[phase]:
-        e = summary.get(name, {})
-        if "hbm_read_bytes_est" not in e or "hbm_write_bytes" not in e:
+    for prefix in PMC_KERNEL[phase]:
+        hits = [e for name, e in summary.items() if isinstance(e, dict) and name.startswith(prefix)
+                and "hbm_read_bytes_est" in e and "hbm_write_bytes" in e]
+        if len(hits) != 1:   # none, or several instantiations profiled: no unambiguous figure
             return None, None
-        total += e["hbm_read_bytes_est"] + e["hbm_write_bytes"]
+        total += hits[0]["hbm_read_bytes_est"] + hits[0]["hbm_write_bytes"]
     return int(total), os.path.relpath(files[-1], ROOT)
 
 

@@ -31,6 +31,8 @@ static const char* kPhaseNames[PH_COUNT] = {"flux_terms", "atoms_prep", "cell_so
 constexpr int kMaxTimed = 8192;
 
 static void graph_forget(cf_handle* H);   // hipGraph replay cache (cf_set_graph), below
+struct GraphCache;
+static GraphCache* graph_active(cf_handle* H);
 
 struct cf_handle {
     cf::Handle h;
@@ -1002,16 +1004,79 @@ static void launch_full(cf_handle* H, const double* pos_dev, int flags, bool reu
     }
 }
 
+// Multi-rank split-phase calls with the grid k-space: the direct chain (cell sort, list, pair
+// kernels, exclusions) runs on the second stream from cf_compute_begin on, forked after
+// k_atoms_prep, while the caller's stream runs the bin sort, spread and forward DFT, the
+// caller's all-reduce of B(n) and, in cf_compute_end, the coefficients, inverse DFT and the
+// interpolation (stored apart, as in launch_full); joined before k_assemble_energy.  So the
+// latency-bound launches of a rank's small share (DFT stages over its slab, sorts) and the
+// all-reduce overlap the direct space.  Results: the bits of the one-stream split-phase order.
+// Eager calls only (a captured begin segment cannot leave its fork unjoined).
+static bool split_overlap_ok(cf_handle* H, int flags) {
+    const cf::Handle& h = H->h;
+    return h.overlap && h.aux && h.world > 1 && h.pbc && h.kspace_algo == 2 && h.hi > h.lo &&
+           (flags & (CF_INCLUDE_FORCES | CF_INCLUDE_ENERGY)) && !graph_active(H);
+}
+
+static void launch_begin_split(cf_handle* H, const double* pos_dev, int flags, bool reusable) {
+    cf::Handle& h = H->h;
+    { Timed t(H, PH_FLUX); cf::launch_flux_terms(h, pos_dev); }
+    { Timed t(H, PH_PREP); cf::launch_atoms_prep(h, pos_dev, reusable); }
+    const hipStream_t main = h.stream;
+    check_hip(hipEventRecord(h.ev_fork, main), "hipEventRecord (fork)");
+    check_hip(hipStreamWaitEvent(h.aux, h.ev_fork, 0), "hipStreamWaitEvent (fork)");
+    h.stream = h.aux;
+    try {
+        {
+            Timed t(H, PH_CELLS);
+            if (!reusable) cf::launch_force_rebuild(h);
+            cf::launch_cell_sort(h, pos_dev);
+        }
+        { Timed t(H, PH_NLIST); cf::launch_nlist(h, pos_dev); }
+        h.pending_flags = flags;
+        launch_direct(H);
+        h.pending_flags = -1;
+        check_hip(hipEventRecord(h.ev_join, h.aux), "hipEventRecord (join)");
+    } catch (...) {
+        h.stream = main;
+        h.pending_flags = -1;
+        throw;
+    }
+    h.stream = main;
+    { Timed t(H, PH_GSORT); cf::launch_grid_sort(h, pos_dev); }
+    { Timed t(H, PH_GSPREAD); cf::launch_grid_spread(h); }
+    { Timed t(H, PH_GDFTF); cf::launch_grid_dft_fwd(h); }
+}
+
+static void launch_end_split(cf_handle* H, int flags, double* forces_dev, double* energy_dev) {
+    cf::Handle& h = H->h;
+    const int forces = flags & CF_INCLUDE_FORCES, energy = flags & CF_INCLUDE_ENERGY;
+    { Timed t(H, PH_COEFFS); cf::launch_grid_coeffs(h, energy); }
+    if (forces) {
+        { Timed t(H, PH_GDFTI); cf::launch_grid_dft_inv(h); }
+        { Timed t(H, PH_GINTERP); cf::launch_grid_interp(h, true); }
+    }
+    check_hip(hipStreamWaitEvent(h.stream, h.ev_join, 0), "hipStreamWaitEvent (join)");
+    h.rec_split = forces != 0;
+    {
+        Timed t(H, PH_ENERGY);
+        cf::launch_assemble_energy(h, (forces && forces_dev) ? forces_dev : nullptr, energy, energy_dev);
+    }
+}
+
 // the second stream and its fork / join events (created outside any capture)
 static void ensure_aux(cf_handle* H) {
     cf::Handle& h = H->h;
-    if (h.aux || !h.overlap || h.world != 1 || !h.pbc || h.kspace_algo != 2) return;
+    if (h.aux || !h.overlap || !h.pbc || h.kspace_algo != 2) return;
     check_hip(hipStreamCreateWithFlags(&h.aux, hipStreamNonBlocking), "hipStreamCreate (reciprocal chain)");
     check_hip(hipEventCreateWithFlags(&h.ev_fork, hipEventDisableTiming), "hipEventCreate");
     check_hip(hipEventCreateWithFlags(&h.ev_join, hipEventDisableTiming), "hipEventCreate");
     if (!h.dedq_rec) {
         h.dedq_rec = dalloc<double>(H, (size_t)h.n);
         h.f_rec = dalloc<double>(H, (size_t)4 * h.n);
+        // atoms a rank does not own are never written: zero, so that cf_get_dedq adds nothing
+        check_hip(hipMemset(h.dedq_rec, 0, sizeof(double) * h.n), "memset dedq_rec");
+        check_hip(hipMemset(h.f_rec, 0, sizeof(double) * 4 * h.n), "memset f_rec");
     }
 }
 
@@ -1149,13 +1214,19 @@ CF_EXPORT int cf_compute_begin(cf_handle* H, const double* pos_dev, const double
         if (h.pending_flags >= 0) fail(CF_ERR_STATE, "cf_compute_begin called twice without cf_compute_end");
         check_hip(hipSetDevice(h.device), "hipSetDevice");
         const bool reusable = host_prologue(H, box9);
+        ensure_aux(H);
         h.rec_split = false;
-        run_segment(H, graph_active(H), SEG_BEGIN, make_key(h, pos_dev, nullptr, nullptr, flags, reusable, box9),
-                    [&] { launch_begin(H, pos_dev, flags, reusable); });
+        H->pos_pending = pos_dev;
+        h.split_overlap = split_overlap_ok(H, flags);
+        if (h.split_overlap) {   // direct chain on the second stream (launch_begin_split)
+            launch_begin_split(H, pos_dev, flags, reusable);
+        } else {
+            run_segment(H, graph_active(H), SEG_BEGIN, make_key(h, pos_dev, nullptr, nullptr, flags, reusable, box9),
+                        [&] { launch_begin(H, pos_dev, flags, reusable); });
+        }
         launch_check("compute_begin");
         h.pending_flags = flags;
-        h.direct_done = false;
-        H->pos_pending = pos_dev;
+        h.direct_done = h.split_overlap;
     });
 }
 
@@ -1194,9 +1265,14 @@ CF_EXPORT int cf_compute_end(cf_handle* H, double* forces_dev, double* energy_de
         run_direct(H);
         const int flags = h.pending_flags;
         h.pending_flags = -1;
-        run_segment(H, graph_active(H), SEG_END,
-                    make_key(h, H->pos_pending, forces_dev, energy_dev, flags, false, h.pbc ? H->box9_last : nullptr),
-                    [&] { launch_end(H, flags, forces_dev, energy_dev); });
+        if (h.split_overlap) {
+            h.split_overlap = false;
+            launch_end_split(H, flags, forces_dev, energy_dev);
+        } else {
+            run_segment(H, graph_active(H), SEG_END,
+                        make_key(h, H->pos_pending, forces_dev, energy_dev, flags, false, h.pbc ? H->box9_last : nullptr),
+                        [&] { launch_end(H, flags, forces_dev, energy_dev); });
+        }
         launch_check("compute_end");
     });
 }

@@ -78,6 +78,7 @@ struct GridPlan {
     int mt[3] = {0, 0, 0};
     int rj[3][8] = {}, rc[3][8] = {};
     bool dft8 = false;       // every axis qualifies and CF_DFT8 != 0
+    bool spread_dpp = true;  // spread FMAs take the x taps by DPP row broadcast (CF_SPREAD_DPP=0: scalar loads)
 };
 
 struct Handle {
@@ -126,6 +127,7 @@ struct Handle {
     // dedq_rec / f_rec, added by k_assemble_energy in the one-stream order ((direct + excl) + rec)
     bool overlap = true;
     bool rec_split = false;     // the last evaluation left the reciprocal dE/dq in dedq_rec
+    bool split_overlap = false; // a begun multi-rank evaluation runs its direct chain on aux (cf_api.hip)
     hipStream_t aux = nullptr;
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     double* dedq_rec = nullptr; // [N]

@@ -311,7 +311,25 @@ __device__ __forceinline__ int wrapb(int b, int n) { return b < 0 ? b + n : (b >
 constexpr int kSpWin = 24;         // doubles staged per atom: x, y, z windows of 8
 constexpr int kSpMaxSrc = 1024;    // source atoms whose slots are resolved per segment
 
-template <int NS, int kSpPass>
+// acc[i] = fma(x_i, yz, acc[i]), i < 8, where x_i is the value lane i of this lane's 16-lane row
+// holds in xv (v_fmac_f64 with a 64-bit DPP row_newbcast:i source; the s_nop gives the DPP
+// source the wait states it needs after a VALU write)
+__device__ __forceinline__ void fma8_row_bcast(double (&acc)[8], double xv, double yz) {
+    asm("s_nop 1\n\t"
+        "v_fmac_f64_dpp %0, %8, %9 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, %8, %9 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %2, %8, %9 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %3, %8, %9 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %4, %8, %9 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %5, %8, %9 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %6, %8, %9 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %7, %8, %9 row_newbcast:7 row_mask:0xf bank_mask:0xf"
+        : "+v"(acc[0]), "+v"(acc[1]), "+v"(acc[2]), "+v"(acc[3]), "+v"(acc[4]), "+v"(acc[5]), "+v"(acc[6]),
+          "+v"(acc[7])
+        : "v"(xv), "v"(yz));
+}
+
+template <int NS, int kSpPass, bool DPP>
 __global__ void __launch_bounds__(256) k_g_spread_tile(int3 ng, int3 nb, const int* __restrict__ start,
                                                        const double* __restrict__ taps, const int4* __restrict__ g0s,
                                                        double* __restrict__ grid, const int* __restrict__ xr, int W) {
@@ -438,6 +456,27 @@ __global__ void __launch_bounds__(256) k_g_spread_tile(int3 ng, int3 nb, const i
             if (p + 1 < npass) fetch(base + kSpPass, min(kSpPass, nseg - base - kSpPass));
             const double* buf = st + (p & 1) * kSpPass * kSpWin;
             const int* xb = xoff[p & 1];
+            if constexpr (DPP) {
+                // lane l reads x tap (l & 7) of the staged window, so lane i of every 16-lane row
+                // holds tap i, and each FMA takes tap i by a row broadcast of its operand
+                // (row_newbcast:i, 64-bit DPP): every operand comes from the LDS with 8-B per-lane
+                // reads, no scalar-load latency.  Same products and order as the scalar form.
+                // Four atoms per iteration: their twelve reads in flight together, one wait (a
+                // branch-free body; atoms past the pass end read the last one with y*z = 0,
+                // which adds exact zeros).
+                const double* rb = buf + (lane & 7);   // x tap; y tap at +8 + y - (lane & 7), z at +16
+                const int oy = 8 + y - (lane & 7);
+                for (int a = w; a < n; a += 16) {
+                    double xv[4], yv[4], zv[4];
+#pragma unroll
+                    for (int u = 0; u < 4; u++) {
+                        const double* r = rb + min(a + 4 * u, n - 1) * kSpWin;
+                        xv[u] = r[0]; yv[u] = r[oy]; zv[u] = r[16];
+                    }
+#pragma unroll
+                    for (int u = 0; u < 4; u++) fma8_row_bcast(acc, xv[u], a + 4 * u < n ? yv[u] * zv[u] : 0.0);
+                }
+            } else
             // the x window is the same for every lane: scalar loads (SGPR operands of the FMAs),
             // so the LDS serves only the per-lane y and z taps (2 of the 6 reads per atom)
             // (two atoms per iteration: one wait covers both windows' scalar loads; four measured
@@ -1109,27 +1148,56 @@ __global__ void __launch_bounds__(256) k_g_coeffs(int KX, int KY, int KZ, double
 // ---------------------------------------------------------------------------------
 constexpr int kInterpThreads = 512;
 
-// Sum of v over the 64 lanes of a wave into lane 63, by DPP moves (VALU) in a fixed order:
-// quad xor 1, quad xor 2, half-row mirror, row mirror (every row of 16 then holds its sum),
-// row_bcast15 into rows 1 and 3, row_bcast31 into rows 2 and 3.  The __shfl_xor butterfly
-// this replaces costs two ds_bpermute (LDS instructions) per step and value: 48 per atom in
-// the interpolation, whose LDS issue queue is its bottleneck.
+// A 64-bit value of another lane by two DPP moves (VALU; a __shfl_xor costs two ds_bpermute,
+// LDS instructions, per step and value -- the interpolation's LDS issue queue is its bottleneck).
 template <int CTRL, int ROWS>
 __device__ __forceinline__ double dpp_f64(double v) {
     const long long b = __double_as_longlong(v);
-    const int lo = __builtin_amdgcn_update_dpp(0, (int)b, CTRL, ROWS, 0xF, false);
-    const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, ROWS, 0xF, false);
+    int lo, hi;
+    if constexpr (ROWS == 0xF) {
+        // every lane has a valid source (quad permutations, mirrors): no "old" value, so no
+        // zeroed destination register per move (the update form cost one v_mov per DPP move)
+        lo = __builtin_amdgcn_mov_dpp((int)b, CTRL, ROWS, 0xF, false);
+        hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), CTRL, ROWS, 0xF, false);
+    } else {   // rows outside the mask keep the old value: 0, so that they add nothing
+        lo = __builtin_amdgcn_update_dpp(0, (int)b, CTRL, ROWS, 0xF, false);
+        hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, ROWS, 0xF, false);
+    }
     return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
 }
 
-__device__ __forceinline__ double wave_sum_lane63(double v) {
-    v += dpp_f64<0xB1, 0xF>(v);    // quad_perm [1,0,3,2]
-    v += dpp_f64<0x4E, 0xF>(v);    // quad_perm [2,3,0,1]
-    v += dpp_f64<0x141, 0xF>(v);   // row_half_mirror
-    v += dpp_f64<0x140, 0xF>(v);   // row_mirror
-    v += dpp_f64<0x142, 0xA>(v);   // row_bcast15 -> rows 1, 3 (rows 0, 2 add 0)
-    v += dpp_f64<0x143, 0xC>(v);   // row_bcast31 -> rows 2, 3
-    return v;
+// v + (the same lane of the partner row / half-wave): gfx950 v_permlane16_swap / 32_swap of two
+// copies of v leave row r's and row r ^ 1's values (halves: lanes l and l ^ 32) in the two
+// outputs at each lane's own position, so every lane gets the same two-term sum
+__device__ __forceinline__ double add_swap16(double v) {
+    const long long b = __double_as_longlong(v);
+    const auto lo = __builtin_amdgcn_permlane16_swap((unsigned)b, (unsigned)b, false, false);
+    const auto hi = __builtin_amdgcn_permlane16_swap((unsigned)(b >> 32), (unsigned)(b >> 32), false, false);
+    return __longlong_as_double(((long long)hi[0] << 32) | lo[0]) + __longlong_as_double(((long long)hi[1] << 32) | lo[1]);
+}
+
+__device__ __forceinline__ double add_swap32(double v) {
+    const long long b = __double_as_longlong(v);
+    const auto lo = __builtin_amdgcn_permlane32_swap((unsigned)b, (unsigned)b, false, false);
+    const auto hi = __builtin_amdgcn_permlane32_swap((unsigned)(b >> 32), (unsigned)(b >> 32), false, false);
+    return __longlong_as_double(((long long)hi[0] << 32) | lo[0]) + __longlong_as_double(((long long)hi[1] << 32) | lo[1]);
+}
+
+// Wave sums of four values at once, halving the values carried per lane at every exchange:
+// quad xor 1 (even lanes keep pv / px, odd lanes py / pz), quad xor 2 (one value per lane: lane
+// l holds quantity (pv, py, px, pz)[l & 3] over its quad), row rotations by 4 and 8 (the row's
+// four quads, same l & 3), then the partner row and the other half-wave.  13 exchanges instead
+// of 4 x 6 DPP reductions.  Lane l < 4 (every lane, for its l & 3) ends with the wave total of
+// quantity (pv, py, px, pz)[l & 3]; one fixed order per lane: deterministic.
+__device__ __forceinline__ double wave_sum4(double pv, double px, double py, double pz, int lane) {
+    const bool odd = lane & 1, hi = lane & 2;
+    const double a = (odd ? py : pv) + dpp_f64<0xB1, 0xF>(odd ? pv : py);    // quad_perm [1,0,3,2]
+    const double b = (odd ? pz : px) + dpp_f64<0xB1, 0xF>(odd ? px : pz);
+    double c = (hi ? b : a) + dpp_f64<0x4E, 0xF>(hi ? a : b);                // quad_perm [2,3,0,1]
+    c += dpp_f64<0x124, 0xF>(c);   // row_ror:4
+    c += dpp_f64<0x128, 0xF>(c);   // row_ror:8
+    c = add_swap16(c);
+    return add_swap32(c);
 }
 
 template <int W>
@@ -1239,21 +1307,24 @@ __global__ void __launch_bounds__(kInterpThreads) k_g_interp(int3 ng, int3 nb, c
         }
         pz = pv * dzt;
         pv *= zt; px *= zt; py *= zt;
-        pv = wave_sum_lane63(pv);
-        px = wave_sum_lane63(px);
-        py = wave_sum_lane63(py);
-        pz = wave_sum_lane63(pz);
-        if (lane == 63) {   // each owned atom is in exactly one bin: no other writer
+        // lane l < 4 ends with the wave total of quantity (pv, py, px, pz)[l]
+        const double tot = wave_sum4(pv, px, py, pz, lane);
+        if (lane < 4) {   // each owned atom is in exactly one bin: no other writer
             const int i = lo + g.w;
+            const int c = lane == 2 ? 0 : (lane == 1 ? 1 : 2);   // force component of lanes 1..3
             if (store) {   // the reciprocal chain on its own stream: dedq_rec, f_rec = (p, -q) per atom,
                            // which k_assemble_energy folds in as the fused adds below
-                dedq[i] = pv;
-                reinterpret_cast<double4*>(f_part)[i] = make_double4(px, py, pz, -sr.w);
+                if (lane == 0) {
+                    dedq[i] = tot;
+                    f_part[4 * i + 3] = -sr.w;
+                } else {
+                    f_part[4 * i + c] = tot;
+                }
+            } else if (lane == 0) {
+                dedq[i] += tot;
             } else {
-                dedq[i] += pv;
-                f_part[3 * i] = fma(-sr.w * gscale.x, px, f_part[3 * i]);
-                f_part[3 * i + 1] = fma(-sr.w * gscale.y, py, f_part[3 * i + 1]);
-                f_part[3 * i + 2] = fma(-sr.w * gscale.z, pz, f_part[3 * i + 2]);
+                const double gs = c == 0 ? gscale.x : (c == 1 ? gscale.y : gscale.z);
+                f_part[3 * i + c] = fma(-sr.w * gs, tot, f_part[3 * i + c]);
             }
         }
     }
@@ -1314,6 +1385,8 @@ void grid_plan(Handle& h, int width, double sigma) {
     // factorized stages: mode set k0 + j, j < J per axis (x, y: |n| < K; z: 0 <= nz < K)
     const char* env = getenv("CF_DFT8");
     p.dft8 = !(env && env[0] == '0');
+    const char* sd = getenv("CF_SPREAD_DPP");
+    p.spread_dpp = !(sd && sd[0] == '0');
     for (int d = 0; d < 3; d++) {
         const int K = h.kmax[d], J = d == 2 ? K : 2 * K - 1, k0 = d == 2 ? 0 : -(K - 1);
         int mx = 0;
@@ -1419,12 +1492,15 @@ void launch_grid_sort(Handle& h, const double* pos) {
 void launch_grid_spread(Handle& h) {
     const GridPlan& p = h.gp;
     const int3 ng = make_int3(p.ng[0], p.ng[1], p.ng[2]), nb = make_int3(p.nb[0], p.nb[1], p.nb[2]);
-#define CF_SPT(NS_, P_) hipLaunchKernelGGL((k_g_spread_tile<NS_, P_>), dim3(p.nbins), dim3(256), 0, h.stream, ng, nb, \
-                                           h.g_start, h.g_taps, h.g_g0s, h.g_grid, h.g_xrange, p.W)
+#define CF_SPT(NS_, P_, D_) hipLaunchKernelGGL((k_g_spread_tile<NS_, P_, D_>), dim3(p.nbins), dim3(256), 0, h.stream, \
+                                               ng, nb, h.g_start, h.g_taps, h.g_g0s, h.g_grid, h.g_xrange, p.W)
     // a first tap in bin B reaches tiles B .. B + NS - 1: NS = 2 when W <= 9 (8 source bins per
     // tile instead of 27).  Passes of 32 atoms at W = 14 (64 / 128 measured slower at C3)
-    if (p.W <= 9) { CF_SPT(2, 64); }
-    else { CF_SPT(3, 32); }
+    if (p.W <= 9) {
+        if (p.spread_dpp) { CF_SPT(2, 64, true); } else { CF_SPT(2, 64, false); }
+    } else {
+        if (p.spread_dpp) { CF_SPT(3, 32, true); } else { CF_SPT(3, 32, false); }
+    }
 #undef CF_SPT
 }
 

@@ -63,3 +63,53 @@ def test_overlap_c2_matches_oracle(monkeypatch):
     assert np.abs(f - ref["forces"]).max() <= 1e-6
     assert abs(e - ref["energy"]) <= 1e-9 * np.abs(ref["terms"]).sum() + 1e-6
     assert np.abs(k.dedq() - ref["dedq"]).max() <= 1e-6 * max(1.0, np.abs(ref["dedq"]).max())
+
+
+def _run_ranks(monkeypatch, overlap, world, system, force, pos, box, skin, steps=3):
+    """`world` ranks of an atom decomposition driven on one GPU through the split-phase calls
+    (cf_compute_begin / direct / end), the all-reduce of B(n) done by hand on the caller's
+    stream between begin and end, as openmmcoul.distributed does with RCCL."""
+    from openmmcoul.distributed import device_buffer_as_tensor
+    monkeypatch.setenv("CF_OVERLAP", "1" if overlap else "0")
+    stream = torch.cuda.current_stream().cuda_stream
+    ks = [HipCalcCoulForceKernel(stream=stream, rank=r, world_size=world, kspace_algo=2).initialize(system, force)
+          for r in range(world)]
+    for k in ks:
+        if skin:
+            k.set_neighbor_skin(skin)
+    rng = np.random.default_rng(5)
+    pt = torch.tensor(pos, dtype=torch.float64, device="cuda")
+    out = []
+    for s in range(steps):
+        forces = s != 1   # an energy-only evaluation in between
+        for k in ks:
+            k.begin(pt, box, forces, True)
+        bufs = [device_buffer_as_tensor(*k.kspace_buffer(), "cuda") for k in ks]
+        total = sum(bufs[1:], bufs[0].clone())
+        for b in bufs:
+            b.copy_(total)
+        f = torch.zeros_like(pt)
+        es = []
+        for k in ks:
+            e = torch.zeros(1, dtype=torch.float64, device="cuda")
+            k.end(f if forces else None, e)
+            es.append(e)
+        torch.cuda.synchronize()
+        out.append(([x.item() for x in es], f.cpu().numpy(),
+                    [k.dedq()[slice(*k.owned_range())] for k in ks] if forces else None))   # owned atoms
+        pt += torch.tensor(rng.normal(scale=0.004, size=pos.shape), device="cuda")
+    for k in ks:
+        k.destroy()
+    return out
+
+
+@pytest.mark.parametrize("world,skin", [(2, 0.0), (4, 0.1)])
+def test_multi_rank_overlap_is_bitwise_one_stream(monkeypatch, world, skin):
+    """Multi-rank split-phase calls: the direct chain on the second stream from cf_compute_begin
+    on (cf_api.hip launch_begin_split / launch_end_split) against one stream, bitwise."""
+    system, force, pos, box = ts.water_box(4000, cutoff=1.0, ewald_tol=1e-4, every_bond_angle=5)
+    a = _run_ranks(monkeypatch, True, world, system, force, pos, box, skin)
+    b = _run_ranks(monkeypatch, False, world, system, force, pos, box, skin)
+    for (ea, fa, da), (eb, fb, db) in zip(a, b):
+        assert ea == eb and np.array_equal(fa, fb)
+        assert (da is None and db is None) or all(np.array_equal(x, y) for x, y in zip(da, db))
