@@ -21,6 +21,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <cmath>
+#include <utility>
 #include <vector>
 
 #include "cf_internal.h"
@@ -1200,6 +1201,38 @@ __device__ __forceinline__ double wave_sum4(double pv, double px, double py, dou
     return add_swap32(c);
 }
 
+// the potential grid over tile (tx, ty, tz) plus the W - 1 halo, wrapped, into sg[R][R][R]:
+// rows of R consecutive z; thread t covers column c = t % R of rows t / R, t / R + RPP, ...
+template <int W>
+__device__ __forceinline__ void interp_stage(int3 ng, const double* __restrict__ G, int tx, int ty, int tz,
+                                             double* __restrict__ sg) {
+    constexpr int R = 7 + W;
+    constexpr int RPP = kInterpThreads / R;   // rows per pass
+    const int c = threadIdx.x % R, r0 = threadIdx.x / R;
+    int z = 8 * tz + c;
+    z -= z >= ng.z ? ng.z : 0;
+    // every load of the staging issued before the first LDS store (one memory latency per
+    // block instead of one per group of 4 rows): the block's halo comes from L2 / MALL
+    constexpr int kRows = (R * R + RPP - 1) / RPP;
+    if (r0 < RPP) {
+        double gv[kRows];
+#pragma unroll
+        for (int q = 0; q < kRows; q++) {
+            const int row = min(r0 + q * RPP, R * R - 1);
+            const int a = row / R, b = row - a * R;
+            int x = 8 * tx + a, y = 8 * ty + b;
+            x -= x >= ng.x ? ng.x : 0;
+            y -= y >= ng.y ? ng.y : 0;
+            gv[q] = G[((size_t)x * ng.y + y) * ng.z + z];
+        }
+#pragma unroll
+        for (int q = 0; q < kRows; q++) {
+            const int row = r0 + q * RPP;
+            if (row < R * R) sg[row * R + c] = gv[q];
+        }
+    }
+}
+
 template <int W>
 __global__ void __launch_bounds__(kInterpThreads) k_g_interp(int3 ng, int3 nb, const int* __restrict__ start,
                                                              const int4* __restrict__ g0s,
@@ -1222,33 +1255,7 @@ __global__ void __launch_bounds__(kInterpThreads) k_g_interp(int3 ng, int3 nb, c
     const int s0 = start[tile], s1 = start[tile + 1];
     if (s0 == s1) return;
     const int tz = tile % nb.z, ty = (tile / nb.z) % nb.y, tx = tile / (nb.z * nb.y);
-    // rows of R consecutive z: thread t covers column c = t % R of rows t / R, t / R + RPP, ...
-    {
-        constexpr int RPP = kInterpThreads / R;   // rows per pass
-        const int c = threadIdx.x % R, r0 = threadIdx.x / R;
-        int z = 8 * tz + c;
-        z -= z >= ng.z ? ng.z : 0;
-        // every load of the staging issued before the first LDS store (one memory latency per
-        // block instead of one per group of 4 rows): the block's halo comes from L2 / MALL
-        constexpr int kRows = (R * R + RPP - 1) / RPP;
-        if (r0 < RPP) {
-            double gv[kRows];
-#pragma unroll
-            for (int q = 0; q < kRows; q++) {
-                const int row = min(r0 + q * RPP, R * R - 1);
-                const int a = row / R, b = row - a * R;
-                int x = 8 * tx + a, y = 8 * ty + b;
-                x -= x >= ng.x ? ng.x : 0;
-                y -= y >= ng.y ? ng.y : 0;
-                gv[q] = G[((size_t)x * ng.y + y) * ng.z + z];
-            }
-#pragma unroll
-            for (int q = 0; q < kRows; q++) {
-                const int row = r0 + q * RPP;
-                if (row < R * R) sg[row * R + c] = gv[q];
-            }
-        }
-    }
+    interp_stage<W>(ng, G, tx, ty, tz, sg);
     __syncthreads();
     const int lane = threadIdx.x & 63, w = wave_id();
     const int d = lane >> 4, m = lane & 15;
@@ -1333,6 +1340,156 @@ __global__ void __launch_bounds__(kInterpThreads) k_g_interp(int3 ng, int3 nb, c
 // ---------------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------------
+// acc += x_I * y, x_I = the value lane I of this lane's 16-lane row holds in x (v_fmac_f64 with
+// a 64-bit DPP row_newbcast:I source).  NOP: an s_nop 1 ahead of it, for a DPP source written
+// by a VALU instruction just before (2 wait states; the compiler does not see inside the asm).
+template <int I, bool NOP = false>
+__device__ __forceinline__ void fmac_row_bcast(double& acc, double x, double y) {
+    if constexpr (NOP)
+        asm("s_nop 1\n\tv_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+            : "+v"(acc) : "v"(x), "v"(y), "i"(I));
+    else
+        asm("v_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(x), "v"(y), "i"(I));
+}
+
+// a VALU-written value made safe as a DPP source: every reader comes after this s_nop
+__device__ __forceinline__ double dpp_ready(double v) {
+    asm("s_nop 1" : "+v"(v));
+    return v;
+}
+
+template <int... Is, class F>
+__device__ __forceinline__ void static_for_impl(std::integer_sequence<int, Is...>, F&& f) {
+    (f(std::integral_constant<int, Is>{}), ...);
+}
+template <int N, class F>
+__device__ __forceinline__ void static_for(F&& f) { static_for_impl(std::make_integer_sequence<int, N>{}, f); }
+
+// Sums of four values over each 32-lane half of the wave (wave_sum4 without the half-wave
+// exchange): lane l with (l & 31) < 4 holds its half's total of (pv, py, px, pz)[l & 3].
+__device__ __forceinline__ double half_sum4(double pv, double px, double py, double pz, int lane) {
+    const bool odd = lane & 1, hi = lane & 2;
+    const double a = (odd ? py : pv) + dpp_f64<0xB1, 0xF>(odd ? pv : py);
+    const double b = (odd ? pz : px) + dpp_f64<0xB1, 0xF>(odd ? px : pz);
+    double c = (hi ? b : a) + dpp_f64<0x4E, 0xF>(hi ? a : b);
+    c += dpp_f64<0x124, 0xF>(c);   // row_ror:4
+    c += dpp_f64<0x128, 0xF>(c);   // row_ror:8
+    return add_swap16(c);
+}
+
+// Two atoms per wave, one per 32-lane half h.  Lane (h, jg, k): z column k of the tile's halo,
+// rows j = 2jj + jg (jj < NJ = ceil(W/2): no padded j rows at even W, 14 = 2 x 7).  Every tap
+// lives in a register: each lane evaluates x tap k, z tap k and y tap 2k + jg (k < NJ) of its
+// half's atom, and the contractions take the x and y taps they need from the lane that holds
+// them by DPP row broadcast (x tap i is in lane i of every row, y tap 2jj + jg in lane jj of
+// row jg), so the LDS serves only the potential halo (49 reads per atom instead of 56 plus 14
+// broadcast tap reads, no tap stores, no wave barriers).  t0 = sum_i G X_i, t1 = sum_i G dX_i
+// per (j, k), then pot / gradient by y and z as in k_g_interp; the four sums per half reduced
+// in a fixed order; lanes (h, 0..3) store.
+template <int W>
+__global__ void __launch_bounds__(kInterpThreads) k_g_interp2(int3 ng, int3 nb, const int* __restrict__ start,
+                                                              const int4* __restrict__ g0s,
+                                                              const double4* __restrict__ srec, double beta,
+                                                              double3 gscale, const double* __restrict__ G, int lo,
+                                                              double* __restrict__ dedq, double* __restrict__ f_part,
+                                                              int store) {
+    constexpr int R = 7 + W;
+    constexpr int NJ = (W + 1) / 2;
+    constexpr int NW = kInterpThreads / 64;
+    static_assert(W <= 16, "row broadcast reaches lanes 0..15");
+    extern __shared__ double sg[];   // [R][R][R]
+    const int nyz = nb.y * nb.z;
+    int tile = blockIdx.x;
+    if (nyz % 8 == 0) {
+        const int per = nyz / 8, i = blockIdx.x / 8;
+        tile = (i / per) * nyz + (blockIdx.x % 8) * per + i % per;
+    }
+    const int s0 = start[tile], s1 = start[tile + 1];
+    if (s0 == s1) return;
+    const int tz = tile % nb.z, ty = (tile / nb.z) % nb.y, tx = tile / (nb.z * nb.y);
+    interp_stage<W>(ng, G, tx, ty, tz, sg);
+    __syncthreads();
+    const int lane = threadIdx.x & 63, w = wave_id();
+    const int h = lane >> 5, jg = (lane >> 4) & 1, k = lane & 15;
+    const double hw_inv = 2.0 / W;
+    // this half's next atom (bin entry, coordinates) loaded while the current one is evaluated
+    int4 g_n = make_int4(0, 0, 0, 0);
+    if (s0 + 2 * w + h < s1) g_n = g0s[s0 + 2 * w + h];
+    double4 sr_n = srec[g_n.w];
+    for (int sb = s0 + 2 * w; sb < s1; sb += 2 * NW) {   // wave-uniform
+        const bool valid = sb + h < s1;
+        const int4 g = g_n;
+        const double4 sr = sr_n;
+        if (sb + 2 * NW + h < s1) {
+            g_n = g0s[sb + 2 * NW + h];
+            sr_n = srec[g_n.w];
+        }
+        // taps (t = g0 + m - s, g0 = ceil(s - W/2)): x tap k, y tap 2k + jg, z tap k; zero
+        // beyond the support
+        double xv = 0, xd = 0, yv = 0, yd = 0, zv = 0, zd = 0;
+        if (k < W) es_tap(ceil(sr.x - 0.5 * W) + k - sr.x, hw_inv, beta, xv, xd);
+        if (k < NJ && 2 * k + jg < W) es_tap(ceil(sr.y - 0.5 * W) + (2 * k + jg) - sr.y, hw_inv, beta, yv, yd);
+        if (k < W) es_tap(ceil(sr.z - 0.5 * W) + k - sr.z, hw_inv, beta, zv, zd);
+        xv = dpp_ready(xv); xd = dpp_ready(xd); yv = dpp_ready(yv); yd = dpp_ready(yd);
+        const int rx = g.x & 7, ry = g.y & 7, rz = g.z & 7;
+        const double* base = sg + (rx * R + ry) * R + rz + (k < W ? k : 0);
+        double t0[NJ], t1[NJ];
+#pragma unroll
+        for (int jj = 0; jj < NJ; jj++) { t0[jj] = 0; t1[jj] = 0; }
+        // x rows i in order; the NJ halo reads of row i + 1 are issued before row i's FMAs (the
+        // scheduling barriers keep them there: the compiler otherwise sinks each read to its
+        // first use, behind the inline asm, one LDS latency per read)
+        double gv[2][NJ];
+        auto load_row = [&](int i, double (&g)[NJ]) {
+#pragma unroll
+            for (int jj = 0; jj < NJ; jj++) {
+                const int j = 2 * jj + jg;
+                g[jj] = base[(i * R + (j < W ? j : 0)) * R];
+            }
+        };
+        load_row(0, gv[0]);
+        static_for<W>([&](auto I) {
+            constexpr int i = decltype(I)::value;
+            if constexpr (i + 1 < W) load_row(i + 1, gv[(i + 1) & 1]);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int jj = 0; jj < NJ; jj++) {
+                fmac_row_bcast<i>(t0[jj], xv, gv[i & 1][jj]);
+                fmac_row_bcast<i>(t1[jj], xd, gv[i & 1][jj]);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        });
+        double pv = 0, px = 0, py = 0;
+        static_for<NJ>([&](auto J) {
+            constexpr int jj = decltype(J)::value;
+            fmac_row_bcast<jj>(pv, yv, t0[jj]);
+            fmac_row_bcast<jj>(px, yv, t1[jj]);
+            fmac_row_bcast<jj>(py, yd, t0[jj]);
+        });
+        const double pz = pv * zd;
+        pv *= zv; px *= zv; py *= zv;
+        const double tot = half_sum4(pv, px, py, pz, lane);
+        const int hl = lane & 31;
+        if (hl < 4 && valid) {   // each owned atom is in exactly one bin: no other writer
+            const int i = lo + g.w;
+            const int c = hl == 2 ? 0 : (hl == 1 ? 1 : 2);   // force component of lanes 1..3
+            if (store) {
+                if (hl == 0) {
+                    dedq[i] = tot;
+                    f_part[4 * i + 3] = -sr.w;
+                } else {
+                    f_part[4 * i + c] = tot;
+                }
+            } else if (hl == 0) {
+                dedq[i] += tot;
+            } else {
+                const double gs = c == 0 ? gscale.x : (c == 1 ? gscale.y : gscale.z);
+                f_part[3 * i + c] = fma(-sr.w * gs, tot, f_part[3 * i + c]);
+            }
+        }
+    }
+}
+
 static double es_host(double t, int W, double beta) {
     double z = 2.0 * t / W, u = 1.0 - z * z;
     return u > 0 ? std::exp(beta * (std::sqrt(u) - 1.0)) : 0.0;
@@ -1387,6 +1544,8 @@ void grid_plan(Handle& h, int width, double sigma) {
     p.dft8 = !(env && env[0] == '0');
     const char* sd = getenv("CF_SPREAD_DPP");
     p.spread_dpp = !(sd && sd[0] == '0');
+    const char* i2 = getenv("CF_INTERP2");
+    p.interp2 = !(i2 && i2[0] == '0');
     for (int d = 0; d < 3; d++) {
         const int K = h.kmax[d], J = d == 2 ? K : 2 * K - 1, k0 = d == 2 ? 0 : -(K - 1);
         int mx = 0;
@@ -1703,9 +1862,9 @@ void launch_grid_interp(Handle& h, bool split) {
     const size_t R = 7 + p.W;
     const size_t lds = R * R * R * sizeof(double);
 #define CF_INTERP(W_)                                                                                               \
-    hipLaunchKernelGGL(k_g_interp<W_>, dim3(p.nbins), dim3(kInterpThreads), lds, h.stream, ng, nb, h.g_start,       \
-                       h.g_g0s, h.g_srec, p.beta, gs, h.g_grid, h.lo, split ? h.dedq_rec : h.dedq,            \
-                       split ? h.f_rec : h.f_part, split ? 1 : 0)
+    hipLaunchKernelGGL(p.interp2 ? k_g_interp2<W_> : k_g_interp<W_>, dim3(p.nbins), dim3(kInterpThreads), lds,        \
+                       h.stream, ng, nb, h.g_start, h.g_g0s, h.g_srec, p.beta, gs, h.g_grid, h.lo,                   \
+                       split ? h.dedq_rec : h.dedq, split ? h.f_rec : h.f_part, split ? 1 : 0)
     CF_GRID_W_DISPATCH(p.W, CF_INTERP)
 #undef CF_INTERP
 }

@@ -252,3 +252,28 @@ def test_grid_dft8_matches_gemm_stages(case):
     assert abs(e1 - e0) <= 1e-12 * scale, (e0, e1)
     assert np.abs(f1 - f0).max() <= 1e-12 * np.abs(f0).max(), np.abs(f1 - f0).max()
     assert np.abs(d1 - d0).max() <= 1e-12 * np.abs(d0).max(), np.abs(d1 - d0).max()
+
+
+@pytest.mark.parametrize("case,width,spread_dpp", [("C2", 14, "1"), ("C2", 13, "1"), ("w4k", 14, "1"), ("w4k", 14, "0"),
+                                                   ("w4k", 8, "1"), ("w4k", 11, "1")])
+def test_grid_interp2_matches_interp(monkeypatch, case, width, spread_dpp):
+    """The two-atoms-per-wave interpolation (k_g_interp2: taps in registers, DPP row broadcasts)
+    against the one-atom form (CF_INTERP2=0), even and odd kernel widths, with either spread
+    form (CF_SPREAD_DPP; the spread forms are bitwise equal): the same sums in another order,
+    forces and dE/dq equal to <= 1e-12 relative, energy unchanged (not interpolated)."""
+    if case == "C2":
+        system, force, pos, box = ts.make("C2")
+    else:
+        system, force, pos, box = ts.water_box(4000, cutoff=1.0, ewald_tol=1e-4, every_bond_angle=5)
+    monkeypatch.setenv("CF_SPREAD_DPP", spread_dpp)
+    out = []
+    for flag in ("0", "1"):
+        monkeypatch.setenv("CF_INTERP2", flag)
+        k = HipCalcCoulForceKernel(kspace_algo=GRID, grid_width=width).initialize(system, force)
+        e, f = k.execute_host(pos, box)
+        out.append((e, f, k.dedq()))
+        k.destroy()
+    (e0, f0, d0), (e1, f1, d1) = out
+    assert e1 == e0
+    assert np.abs(f1 - f0).max() <= 1e-12 * np.abs(f0).max(), np.abs(f1 - f0).max()
+    assert np.abs(d1 - d0).max() <= 1e-12 * np.abs(d0).max(), np.abs(d1 - d0).max()
