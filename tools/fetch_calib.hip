@@ -9,6 +9,8 @@
 //                (k_pairs_half's partner gathers, each record once here)
 //   c_gather8    8 B per lane, permuted 8-B words
 //   c_scalar64   wave-uniform 64 B (s_load_dwordx16), permuted 64-B pieces (spread's x window)
+//   c_rows168    runs of 21 doubles (168 B, 8-B aligned) per 21 lanes at permuted row starts
+//                (k_g_interp's halo rows: lane t reads z = t % 21 of row t / 21)
 //   w_stream16   16 B per lane coalesced stores
 //   w_seg64      64-B pieces (8 doubles) at permuted offsets (spread's grid tile rows)
 // Run: rocprofv3 --pmc FETCH_SIZE -- ./fetch_calib ; rocprofv3 --pmc WRITE_SIZE -- ./fetch_calib
@@ -73,6 +75,18 @@ __global__ void c_scalar64(const double* __restrict__ a, unsigned nseg, double* 
     if (s == 12345.678) out[0] = s;
 }
 
+// 21 lanes per 168-B run; the run starts are a permutation of the region's 168-B slots
+__global__ void c_rows168(const double* __restrict__ a, unsigned nrun, double* __restrict__ out) {
+    double s = 0.0;
+    const unsigned t = blockIdx.x * blockDim.x + threadIdx.x, nt = gridDim.x * blockDim.x;
+    // lanes past the last full run of a wave idle, as in the interpolation's staging (21 * 3 = 63)
+    const unsigned lane = threadIdx.x & 63, wave = t >> 6, nwave = nt >> 6;
+    if (lane < 63) {
+        for (unsigned g = wave * 3 + lane / 21; g < nrun; g += nwave * 3) s += a[(size_t)perm(g, nrun) * 21 + lane % 21];
+    }
+    if (s == 12345.678) out[0] = s;
+}
+
 __global__ void w_stream16(v2d* __restrict__ a, size_t n16) {
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n16; i += (size_t)gridDim.x * blockDim.x)
         a[i] = v2d{(double)i, 1.0};
@@ -107,6 +121,13 @@ int main() {
     run("c_gather32", [&] { c_gather32<<<grid, blk>>>((const v2d*)buf + 2 * (moved / 16), (unsigned)(moved / 32), out); });
     run("c_gather8", [&] { c_gather8<<<grid, blk>>>((const double*)buf + 3 * (moved / 8), (unsigned)(moved / 8), out); });
     run("c_scalar64", [&] { c_scalar64<<<grid, blk>>>((const double*)buf, (unsigned)(moved / 64), out); });
+    // 2^21 runs of 168 B (336 MiB) in region 0..1, every run once; bytes = 2^21 * 168
+    {
+        const unsigned nrun = 1u << 21;
+        c_rows168<<<grid, blk>>>((const double*)buf, nrun, out);
+        CK(hipDeviceSynchronize());
+        std::printf("%-12s bytes %zu\n", "c_rows168", (size_t)nrun * 168);
+    }
     run("w_stream16", [&] { w_stream16<<<grid, blk>>>((v2d*)buf + moved / 16, moved / 16); });
     run("w_seg64", [&] { w_seg64<<<grid, blk>>>((v2d*)buf + 2 * (moved / 16), (unsigned)(moved / 64)); });
     CK(hipFree(buf));

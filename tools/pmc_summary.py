@@ -4,11 +4,23 @@
 usage: pmc_summary.py OUT.json KERNEL_TRACE.csv [COUNTER_COLLECTION.csv ...]
 
 Per kernel: launches, average duration (kernel trace) and, for every PMC counter,
-the average value per launch.  HBM bytes follow MI355X_MICROARCH.md §HBM: FETCH_SIZE and
-WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE reports half the bytes of a wide streaming
-read, so hbm_read_bytes = 2 * 1024 * FETCH_SIZE (upper estimate; the exact factor depends
-on access width), hbm_write_bytes = 1024 * WRITE_SIZE.
+the average value per launch.  HBM bytes: FETCH_SIZE and WRITE_SIZE are in KiB.  FETCH_SIZE
+counts 64-B memory requests; on gfx950 it reports half the bytes of a 16-B/lane coalesced
+streaming read (MI355X_MICROARCH.md §HBM) and exactly the bytes of 64-B pieces, wave-uniform
+64-B scalar loads and scattered gathers (whose 64-B granules are the real traffic), per the
+calibration kernels of tools/fetch_calib.hip (profiles/r03_fetch_calibration.json).  So
+hbm_read_bytes_est = fetch_factor * 1024 * FETCH_SIZE with the factor of the kernel's dominant
+read pattern (FETCH_FACTOR below; 2, the upper estimate, for kernels not listed), and
+hbm_write_bytes = 1024 * WRITE_SIZE (calibrated exact for 16-B and 64-B stores).
 """
+
+# kernel-name prefix -> FETCH_SIZE factor of its dominant read pattern (tools/fetch_calib.hip)
+FETCH_FACTOR = {
+    "cf::k_pairs_half": 2.0,       # the neighbour list: 16-B chunks, consecutive rows per lane (streaming)
+    "cf::k_pairs<": 2.0,
+    "cf::k_g_spread_tile": 1.0,    # 64-B window pieces + wave-uniform 64-B x windows (c_seg64, c_scalar64)
+    "cf::k_excl": 1.0,             # 32-B window-sum gathers (c_gather32: 64-B granules = real traffic)
+}
 import collections
 import csv
 import json
@@ -42,7 +54,8 @@ def main():
         for c, vals in ctr.get(k, {}).items():
             e[c] = sum(vals) / len(vals)
         if "FETCH_SIZE" in e:
-            e["hbm_read_bytes_est"] = 2 * 1024 * e["FETCH_SIZE"]
+            e["fetch_factor"] = next((f for p, f in FETCH_FACTOR.items() if k.startswith(p)), 2.0)
+            e["hbm_read_bytes_est"] = e["fetch_factor"] * 1024 * e["FETCH_SIZE"]
         if "WRITE_SIZE" in e:
             e["hbm_write_bytes"] = 1024 * e["WRITE_SIZE"]
         res[k] = e
