@@ -260,15 +260,18 @@ def main():
         energy = step(False)
     torch.cuda.synchronize()
     # breakdown pass (not the timed region): every phase bracketed by HIP events on the
-    # library's stream.  Those event records cost ~10% of a step, so the timed region below
-    # brackets only the dominant kernel.
+    # library's stream, with the second stream off (cf_set_overlap) so that each phase's time is
+    # its own, not stretched by kernels of the other chain sharing the CUs.  Those event records
+    # cost ~10% of a step, so the timed region below brackets only the dominant kernel.
     HOT = ("direct_pairs", "grid_spread", "grid_interp", "kspace_sfac", "kspace_force")
+    kern.kernel.set_overlap(False)
     kern.kernel.set_timing(True)
     for _ in range(args.steps):
         energy = step(True)
     torch.cuda.synchronize()
     timing_all = kern.kernel.timing()
     kern.kernel.set_timing(False)
+    kern.kernel.set_overlap(True)
     ms_eval = float(np.mean([a.elapsed_time(b) for a, b in ev])) if ev else float("nan")
     per_step = {k: v[0] / args.steps for k, v in timing_all.items()}   # amortized (list phases are not every step)
     dom = max((k for k in HOT if per_step.get(k, 0.0) > 0), key=lambda k: per_step[k], default=None)
@@ -324,7 +327,8 @@ def main():
     ms_step = elapsed / args.steps * 1e3
     ns_day = 86.4 / ms_step * (dt / 0.001)
 
-    per_launch = {k: (v[0] / v[1] if v[1] else 0.0) for k, v in timing_all.items()}
+    per_launch = {k: (v[0] / v[1] if v[1] else 0.0) for k, v in timing_all.items()}   # isolated (breakdown pass)
+    dom_isolated_ms = per_launch.get(dom) if dom is not None else None
     if dom is not None and timing.get(dom, (0, 0))[1]:
         per_launch[dom] = timing[dom][0] / timing[dom][1]   # measured inside the timed region
     n_own = hi - lo
@@ -373,6 +377,14 @@ def main():
                     "hbm_gbs": round(r["gbs"], 1), "tflops": round(r["tflops"], 3),
                     "avg_launch_ms": per_launch[dom], "pairs_within_cutoff": int(p_c),
                     "frac_definition": "max(alg_bytes/8 TB/s, alg_flops/peak)/t (SURVEY 8(d))"}
+        if dom_isolated_ms:
+            ri = roof(dom, dom_isolated_ms)
+            roofline["isolated"] = {
+                "avg_launch_ms": dom_isolated_ms, "frac": round(ri["frac"], 4), "tflops": round(ri["tflops"], 3),
+                "hbm_gbs": round(ri["gbs"], 1),
+                "note": "the same kernel in the breakdown pass, second stream off (cf_set_overlap): its own "
+                        "duration; the timed region's avg_launch_ms includes CUs shared with the reciprocal "
+                        "chain running beside it"}
         others = {}
         for k in present:
             if k == dom:
@@ -454,7 +466,8 @@ def main():
             "timing_note": (f"value: K steps with HIP events around {dom} launches only; ms_per_force_eval: a "
                             f"separate K-step pass with two events around each execute and no library timing; "
                             f"kernels_ms_per_step and ms_per_force_eval_instrumented: a K-step pass with every "
-                            f"phase bracketed by events"),
+                            f"phase bracketed by events and the second stream off (one stream: each phase's "
+                            f"own time; kernels_roofline is from that pass)"),
             "roofline": roofline,
             "kernels_roofline": others,
             "exact_kspace": exact,

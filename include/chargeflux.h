@@ -197,6 +197,13 @@ CF_EXPORT int cf_set_graph(cf_handle* h, int enable);
 /* Number of graph captures and replays since cf_set_graph(h, 1). */
 CF_EXPORT int cf_get_graph_stats(const cf_handle* h, int64_t* captures, int64_t* replays);
 
+/* Second stream (default on; CF_OVERLAP=0 in the environment at cf_create turns it off): with the
+ * grid k-space a single-rank cf_compute runs the reciprocal chain, and the split-phase calls of
+ * a multi-rank step run the direct-space chain, on a second stream of the handle, joined before
+ * the chain rule.  Results are bitwise those of the one-stream order.  enable = 0 launches
+ * everything on the handle's stream (kernel durations are then the kernels' own). */
+CF_EXPORT int cf_set_overlap(cf_handle* h, int enable);
+
 /* Synchronous host-memory convenience (H2D positions, D2H forces/energy): what an
  * OpenMM Reference/CPU-platform adapter calls.  forces_host is ADDED to. */
 CF_EXPORT int cf_compute_host(cf_handle* h, const double* pos_host, const double* box9, int flags,

@@ -1199,6 +1199,18 @@ CF_EXPORT int cf_set_graph(cf_handle* H, int enable) {
     });
 }
 
+CF_EXPORT int cf_set_overlap(cf_handle* H, int enable) {
+    return guarded([&] {
+        if (!H) fail(CF_ERR_INVALID, "null handle");
+        if (H->h.pending_flags >= 0) fail(CF_ERR_STATE, "cf_set_overlap during a begun evaluation");
+        check_hip(hipSetDevice(H->h.device), "hipSetDevice");
+        H->h.overlap = enable != 0;
+        if (GraphCache* g = graph_of(H, false))   // captured launches follow the old stream layout
+            for (int seg = 0; seg < SEG_COUNT; seg++) g->drop(seg);
+        if (H->h.overlap) ensure_aux(H);
+    });
+}
+
 CF_EXPORT int cf_get_graph_stats(const cf_handle* H, int64_t* captures, int64_t* replays) {
     GraphCache* g = graph_of(const_cast<cf_handle*>(H), false);
     if (captures) *captures = g ? g->captures : 0;

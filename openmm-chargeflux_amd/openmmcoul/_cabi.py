@@ -96,6 +96,7 @@ SIGNATURES = [
     ("cf_update_parameters", C.c_int, [C.c_void_p, C.POINTER(cf_params)]),
     ("cf_get_neighbor_stats", C.c_int, [C.c_void_p, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
     ("cf_set_graph", C.c_int, [C.c_void_p, C.c_int]),
+    ("cf_set_overlap", C.c_int, [C.c_void_p, C.c_int]),
     ("cf_get_fallback_stats", C.c_int, [C.c_void_p, C.POINTER(C.c_int64), C.POINTER(C.c_int64),
                                         C.POINTER(C.c_int32)]),
     ("cf_get_graph_stats", C.c_int, [C.c_void_p, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),

@@ -161,6 +161,12 @@ class HipCalcCoulForceKernel:
         _cabi.check(self._lib.cf_set_graph(self._h, 1 if enable else 0), self._lib)
         return self
 
+    def set_overlap(self, enable: bool = True):
+        """Second stream for the grid path (cf_set_overlap, default on): off launches every kernel
+        on the handle's stream, so that kernel durations are the kernels' own; same results."""
+        _cabi.check(self._lib.cf_set_overlap(self._h, 1 if enable else 0), self._lib)
+        return self
+
     def graph_stats(self):
         """(captures, replays) since set_graph(True)."""
         c, r = C.c_int64(), C.c_int64()

@@ -113,3 +113,25 @@ def test_multi_rank_overlap_is_bitwise_one_stream(monkeypatch, world, skin):
     for (ea, fa, da), (eb, fb, db) in zip(a, b):
         assert ea == eb and np.array_equal(fa, fb)
         assert (da is None and db is None) or all(np.array_equal(x, y) for x, y in zip(da, db))
+
+
+def test_set_overlap_at_run_time_is_bitwise(monkeypatch):
+    """cf_set_overlap switches the second stream off and on between evaluations of one handle
+    (the bench's breakdown pass runs one-stream): the same bits every time."""
+    monkeypatch.setenv("CF_OVERLAP", "1")
+    system, force, pos, box = ts.water_box(4000, cutoff=1.0, ewald_tol=1e-4, every_bond_angle=5)
+    stream = torch.cuda.current_stream().cuda_stream
+    k = HipCalcCoulForceKernel(stream=stream, kspace_algo=2).initialize(system, force)
+    k.set_neighbor_skin(0.1)
+    pt = torch.tensor(pos, dtype=torch.float64, device="cuda")
+    res = []
+    for on in (True, False, True, False):
+        k.set_overlap(on)
+        f = torch.zeros_like(pt)
+        e = torch.zeros(1, dtype=torch.float64, device="cuda")
+        k.execute_device(pt, box, True, True, f, e)
+        torch.cuda.synchronize()
+        res.append((e.item(), f.cpu().numpy(), k.dedq()))
+    k.destroy()
+    for e, f, d in res[1:]:
+        assert e == res[0][0] and np.array_equal(f, res[0][1]) and np.array_equal(d, res[0][2])
