@@ -79,6 +79,7 @@ struct GridPlan {
     int rj[3][8] = {}, rc[3][8] = {};
     bool dft8 = false;       // every axis qualifies and CF_DFT8 != 0
     bool spread_dpp = true;  // spread FMAs take the x taps by DPP row broadcast (CF_SPREAD_DPP=0: scalar loads)
+    int spread_pass = 32;    // atoms per staging pass of the W > 9 spread (CF_SPREAD_PASS=64: A/B)
     bool interp2 = true;     // two atoms per wave, taps by DPP row broadcast (CF_INTERP2=0: k_g_interp)
 };
 

@@ -436,6 +436,9 @@ __global__ void __launch_bounds__(256) k_g_spread_tile(int3 ng, int3 nb, const i
                 const int off = (sb >> 5) * kTapStride + d * kRow + 8 * db;
                 xo_r[q] = off;
                 r[q] = *reinterpret_cast<const v2d*>(taps + off + 2 * h);
+                // DPP form: atoms past the pass end are staged as zero windows, so that the
+                // compute loop reads whole groups of four without bounds checks (adds exact zeros)
+                if (DPP && a >= n) r[q] = v2d{0.0, 0.0};
             }
         };
         auto stage = [&](double* buf, int* xb) {
@@ -463,19 +466,20 @@ __global__ void __launch_bounds__(256) k_g_spread_tile(int3 ng, int3 nb, const i
                 // (row_newbcast:i, 64-bit DPP): every operand comes from the LDS with 8-B per-lane
                 // reads, no scalar-load latency.  Same products and order as the scalar form.
                 // Four atoms per iteration: their twelve reads in flight together, one wait (a
-                // branch-free body; atoms past the pass end read the last one with y*z = 0,
-                // which adds exact zeros).
+                // branch-free body at fixed offsets; the windows of atoms past the pass end are
+                // staged as zeros, kSpPass is a multiple of 16, so every read is in the buffer).
+                static_assert(kSpPass % 16 == 0, "four-atom groups");
                 const double* rb = buf + (lane & 7);   // x tap; y tap at +8 + y - (lane & 7), z at +16
                 const int oy = 8 + y - (lane & 7);
                 for (int a = w; a < n; a += 16) {
+                    const double* r = rb + a * kSpWin;
                     double xv[4], yv[4], zv[4];
 #pragma unroll
                     for (int u = 0; u < 4; u++) {
-                        const double* r = rb + min(a + 4 * u, n - 1) * kSpWin;
-                        xv[u] = r[0]; yv[u] = r[oy]; zv[u] = r[16];
+                        xv[u] = r[4 * u * kSpWin]; yv[u] = r[4 * u * kSpWin + oy]; zv[u] = r[4 * u * kSpWin + 16];
                     }
 #pragma unroll
-                    for (int u = 0; u < 4; u++) fma8_row_bcast(acc, xv[u], a + 4 * u < n ? yv[u] * zv[u] : 0.0);
+                    for (int u = 0; u < 4; u++) fma8_row_bcast(acc, xv[u], yv[u] * zv[u]);
                 }
             } else
             // the x window is the same for every lane: scalar loads (SGPR operands of the FMAs),
@@ -1212,18 +1216,26 @@ __device__ __forceinline__ void interp_stage(int3 ng, const double* __restrict__
     int z = 8 * tz + c;
     z -= z >= ng.z ? ng.z : 0;
     // every load of the staging issued before the first LDS store (one memory latency per
-    // block instead of one per group of 4 rows): the block's halo comes from L2 / MALL
+    // block instead of one per group of 4 rows): the block's halo comes from L2 / MALL.  Row
+    // (a, b) = (x, y) halo offsets stepped incrementally by RPP rows (no divisions per row) and
+    // 32-bit element offsets (ng^3 < 2^31) from the grid base
     constexpr int kRows = (R * R + RPP - 1) / RPP;
+    constexpr int kDA = RPP / R, kDB = RPP % R;
     if (r0 < RPP) {
         double gv[kRows];
+        int a = r0 / R, b = r0 - (r0 / R) * R;
+        const int zy = ng.y * ng.z;
 #pragma unroll
         for (int q = 0; q < kRows; q++) {
-            const int row = min(r0 + q * RPP, R * R - 1);
-            const int a = row / R, b = row - a * R;
-            int x = 8 * tx + a, y = 8 * ty + b;
+            const bool in = r0 + q * RPP < R * R;   // rows past the halo re-read row 0 (not stored)
+            int x = 8 * tx + (in ? a : 0), y = 8 * ty + (in ? b : 0);
             x -= x >= ng.x ? ng.x : 0;
             y -= y >= ng.y ? ng.y : 0;
-            gv[q] = G[((size_t)x * ng.y + y) * ng.z + z];
+            // 32-bit byte offset from the uniform base: one global_load with an SGPR base
+            const unsigned off = (unsigned)(x * zy + y * ng.z + z) * 8u;
+            gv[q] = *reinterpret_cast<const double*>(reinterpret_cast<const char*>(G) + off);
+            a += kDA; b += kDB;
+            if (b >= R) { b -= R; a += 1; }
         }
 #pragma unroll
         for (int q = 0; q < kRows; q++) {
@@ -1544,6 +1556,8 @@ void grid_plan(Handle& h, int width, double sigma) {
     p.dft8 = !(env && env[0] == '0');
     const char* sd = getenv("CF_SPREAD_DPP");
     p.spread_dpp = !(sd && sd[0] == '0');
+    const char* sp = getenv("CF_SPREAD_PASS");
+    p.spread_pass = sp ? std::atoi(sp) : 32;
     const char* i2 = getenv("CF_INTERP2");
     p.interp2 = !(i2 && i2[0] == '0');
     for (int d = 0; d < 3; d++) {
@@ -1657,6 +1671,8 @@ void launch_grid_spread(Handle& h) {
     // tile instead of 27).  Passes of 32 atoms at W = 14 (64 / 128 measured slower at C3)
     if (p.W <= 9) {
         if (p.spread_dpp) { CF_SPT(2, 64, true); } else { CF_SPT(2, 64, false); }
+    } else if (p.spread_dpp && p.spread_pass == 64) {   // A/B (CF_SPREAD_PASS=64)
+        CF_SPT(3, 64, true);
     } else {
         if (p.spread_dpp) { CF_SPT(3, 32, true); } else { CF_SPT(3, 32, false); }
     }
