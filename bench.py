@@ -264,6 +264,7 @@ def main():
     # its own, not stretched by kernels of the other chain sharing the CUs.  Those event records
     # cost ~10% of a step, so the timed region below brackets only the dominant kernel.
     HOT = ("direct_pairs", "grid_spread", "grid_interp", "kspace_sfac", "kspace_force")
+    overlap = os.environ.get("CF_OVERLAP", "1") != "0"   # the library's setting at create
     kern.kernel.set_overlap(False)
     kern.kernel.set_timing(True)
     for _ in range(args.steps):
@@ -271,7 +272,7 @@ def main():
     torch.cuda.synchronize()
     timing_all = kern.kernel.timing()
     kern.kernel.set_timing(False)
-    kern.kernel.set_overlap(True)
+    kern.kernel.set_overlap(overlap)
     ms_eval = float(np.mean([a.elapsed_time(b) for a, b in ev])) if ev else float("nan")
     per_step = {k: v[0] / args.steps for k, v in timing_all.items()}   # amortized (list phases are not every step)
     dom = max((k for k in HOT if per_step.get(k, 0.0) > 0), key=lambda k: per_step[k], default=None)

@@ -1,0 +1,23 @@
+#!/bin/bash
+# GPU session (round 3): LJ-first rows + wave-uniform LJ skip in the pair kernels; full GPU test
+# suite, isolated kernel times (CF_OVERLAP=0) of the current tree, C3 bench.  Each GPU step
+# time-limited; stops at the first step that faults, aborts or times out.
+out=gpurun_out/r3h
+mkdir -p $out
+step() { local rc=$1 name=$2; echo "$name rc=$rc"; [ $rc -eq 0 ] || exit $rc; }
+timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread -p no:cacheprovider > $out/tests.log 2>&1
+rc=$?; tail -3 $out/tests.log; echo "tests rc=$rc"; [ $rc -le 1 ] || exit $rc
+R=$GRAFT_REPO_ROOT
+ARGS="--steps 10 --warmup 3 --no-cpu-baseline --no-exact-compare"
+cd /tmp && export TMPDIR=/tmp
+CF_OVERLAP=0 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/$out/tr_iso -o run --output-format csv -- python3 $R/bench.py $ARGS > $R/$out/tr_iso.log 2>&1; step $? tr_iso
+cd $R
+echo "== isolated"; python3 tools/prof_stats.py $out/tr_iso/run_kernel_stats.csv 24
+timeout -k 10 300 python -u bench.py --steps 40 --warmup 5 --no-cpu-baseline --no-exact-compare > $out/bench.json 2> $out/bench.err; step $? bench
+python - <<'P'
+import json
+d = json.loads(open("gpurun_out/r3h/bench.json").read().strip().splitlines()[-1])
+print(d["ms_per_step"], d["ms_per_force_eval"], d["graph_replay_ms_per_step"], d["roofline"]["avg_launch_ms"], d["roofline"].get("isolated"))
+print(d["kernels_ms_per_step"])
+P
+exit 0
