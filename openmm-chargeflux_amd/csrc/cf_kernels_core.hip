@@ -395,6 +395,7 @@ struct DirectArgs {
     double3 L; double3 invL; int3 nc; int brute;
     double3 T; int tric;        // reduced triclinic box: off-diagonals (bx, cx, cy); tric = any nonzero
     double rc2, alpha;
+    double rc;                  // cutoff (the half list's fixed-point range bound)
     double ke;                  // Coulomb constant ONE_4PI_EPS0 (Handle::ke)
     const double* erfc_tab;     // [kErfcDeg+1][kErfcMaxM] erfcx(x) on intervals of width 1/erfc_scale
     const float* erfc_tab_f;    // [erfc_m_f][kErfcDegF+1] fp32 (mixed precision), width 1/erfc_scale_f
@@ -1277,7 +1278,9 @@ __global__ void __launch_bounds__(kHalfBlock) k_pairs_half(DirectArgs a) {
                     const double dqjs = kqis * inv_r * ec;
                     acc.fx += nfx; acc.fy += nfy; acc.fz += nfz;
                     acc.dq += qj * ec;
-                    bad |= !(fmax(fmax(fabs(nfx), fabs(nfy)), fmax(fabs(nfz), fabs(dqjs))) < kFixMax * kFixScale);
+                    // fixed-point range: |nf_c| <= |ndEdRs| r <= |ndEdRs| rc (one bound for the three
+                    // components; an infinite or NaN term fails it)
+                    bad |= !(fmax(fabs(ndEdRs) * a.rc, fabs(dqjs)) < kFixMax * kFixScale);
                     atomicAdd(&accw[0][slot], scaled_to_fix(nfx));
                     atomicAdd(&accw[1][slot], scaled_to_fix(nfy));
                     atomicAdd(&accw[2][slot], scaled_to_fix(nfz));
@@ -1806,7 +1809,7 @@ static DirectArgs direct_args(Handle& h, const double* pos, int include_forces) 
     a.invL = make_double3(1.0 / h.box_L[0], 1.0 / h.box_L[1], 1.0 / h.box_L[2]);
     a.nc = make_int3(h.nc[0], h.nc[1], h.nc[2]);
     a.brute = (h.nc[0] < 3 || h.nc[1] < 3 || h.nc[2] < 3) ? 1 : 0;
-    a.rc2 = h.cutoff * h.cutoff; a.alpha = h.alpha; a.ke = h.ke;
+    a.rc2 = h.cutoff * h.cutoff; a.rc = h.cutoff; a.alpha = h.alpha; a.ke = h.ke;
     a.erfc_tab = h.erfc_tab; a.erfc_scale = h.erfc_scale; a.erfc_m = h.erfc_m;
     a.erfc_tab_f = h.erfc_tab_f; a.erfc_scale_f = h.erfc_scale_f; a.erfc_m_f = h.erfc_m_f;
     a.rl2 = (h.cutoff + h.list_skin) * (h.cutoff + h.list_skin);

@@ -1639,6 +1639,8 @@ void launch_grid_sort(Handle& h, const double* pos) {
                        h.g_tmp, p.nbins, h.g_cnt);
     if (p.W == 14) hipLaunchKernelGGL(k_g_order_taps<14>, dim3(nblk(p.nbins, kOtWaves)), dim3(256), 0, h.stream, p.nbins, h.g_start, h.g_tmp,
                        h.g_order, p.W, p.beta, ng, h.g_srec, h.g_g0u, h.g_taps, h.g_g0s);
+    else if (p.W == 13) hipLaunchKernelGGL(k_g_order_taps<13>, dim3(nblk(p.nbins, kOtWaves)), dim3(256), 0, h.stream, p.nbins, h.g_start, h.g_tmp,
+                       h.g_order, p.W, p.beta, ng, h.g_srec, h.g_g0u, h.g_taps, h.g_g0s);
     else if (p.W == 8) hipLaunchKernelGGL(k_g_order_taps<8>, dim3(nblk(p.nbins, kOtWaves)), dim3(256), 0, h.stream, p.nbins, h.g_start, h.g_tmp,
                        h.g_order, p.W, p.beta, ng, h.g_srec, h.g_g0u, h.g_taps, h.g_g0s);
     else hipLaunchKernelGGL(k_g_order_taps<0>, dim3(nblk(p.nbins, kOtWaves)), dim3(256), 0, h.stream, p.nbins, h.g_start, h.g_tmp,

@@ -20,4 +20,14 @@ d = json.loads(open("gpurun_out/r3h/bench.json").read().strip().splitlines()[-1]
 print(d["ms_per_step"], d["ms_per_force_eval"], d["graph_replay_ms_per_step"], d["roofline"]["avg_launch_ms"], d["roofline"].get("isolated"))
 print(d["kernels_ms_per_step"])
 P
+# accuracy / speed of the kernel width: W = 13 and 14 with the exact k-sum comparison
+for w in 13 14; do
+    timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline --grid-width $w > $out/bench_w$w.json 2> $out/bench_w$w.err; step $? bench_w$w
+done
+python - <<'P'
+import json
+for w in (13, 14):
+    d = json.loads(open(f"gpurun_out/r3h/bench_w{w}.json").read().strip().splitlines()[-1])
+    print(w, d["ms_per_step"], d["exact_kspace"], {k: d["kernels_ms_per_step"][k] for k in ("grid_sort", "grid_spread", "grid_interp")})
+P
 exit 0
