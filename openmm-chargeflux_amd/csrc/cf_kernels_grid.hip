@@ -1364,6 +1364,16 @@ __device__ __forceinline__ void fmac_row_bcast(double& acc, double x, double y) 
         asm("v_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(x), "v"(y), "i"(I));
 }
 
+// v_permlane16_swap of two copies of v: `even` = v of the even row of this lane's row pair
+// (rows 0, 2), `odd` = v of the odd row (rows 1, 3), at this lane's position in the row
+__device__ __forceinline__ void rows_even_odd(double v, double& even, double& odd) {
+    const long long b = __double_as_longlong(v);
+    const auto lo = __builtin_amdgcn_permlane16_swap((unsigned)b, (unsigned)b, false, false);
+    const auto hi = __builtin_amdgcn_permlane16_swap((unsigned)(b >> 32), (unsigned)(b >> 32), false, false);
+    even = __longlong_as_double(((long long)hi[0] << 32) | lo[0]);
+    odd = __longlong_as_double(((long long)hi[1] << 32) | lo[1]);
+}
+
 // a VALU-written value made safe as a DPP source: every reader comes after this s_nop
 __device__ __forceinline__ double dpp_ready(double v) {
     asm("s_nop 1" : "+v"(v));
@@ -1438,10 +1448,17 @@ __global__ void __launch_bounds__(kInterpThreads) k_g_interp2(int3 ng, int3 nb, 
         }
         // taps (t = g0 + m - s, g0 = ceil(s - W/2)): x tap k, y tap 2k + jg, z tap k; zero
         // beyond the support
+        // (one pass for x and z: row jg = 0 of each half evaluates x tap k, row 1 z tap k, and a
+        // v_permlane16_swap copies each row's values into the other, so every lane ends with both)
         double xv = 0, xd = 0, yv = 0, yd = 0, zv = 0, zd = 0;
-        if (k < W) es_tap(ceil(sr.x - 0.5 * W) + k - sr.x, hw_inv, beta, xv, xd);
+        {
+            const double sd = jg ? sr.z : sr.x;
+            double v = 0, dv = 0;
+            if (k < W) es_tap(ceil(sd - 0.5 * W) + k - sd, hw_inv, beta, v, dv);
+            rows_even_odd(v, xv, zv);
+            rows_even_odd(dv, xd, zd);
+        }
         if (k < NJ && 2 * k + jg < W) es_tap(ceil(sr.y - 0.5 * W) + (2 * k + jg) - sr.y, hw_inv, beta, yv, yd);
-        if (k < W) es_tap(ceil(sr.z - 0.5 * W) + k - sr.z, hw_inv, beta, zv, zd);
         xv = dpp_ready(xv); xd = dpp_ready(xd); yv = dpp_ready(yv); yd = dpp_ready(yd);
         const int rx = g.x & 7, ry = g.y & 7, rz = g.z & 7;
         const double* base = sg + (rx * R + ry) * R + rz + (k < W ? k : 0);
