@@ -11,7 +11,10 @@ R=$GRAFT_REPO_ROOT
 ARGS="--steps 10 --warmup 3 --no-cpu-baseline --no-exact-compare"
 cd /tmp && export TMPDIR=/tmp
 CF_OVERLAP=0 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/$out/tr_iso -o run --output-format csv -- python3 $R/bench.py $ARGS > $R/$out/tr_iso.log 2>&1; step $? tr_iso
+CF_OVERLAP=0 timeout -k 10 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS GRBM_GUI_ACTIVE -d $R/$out/pmc_a -o run --output-format csv -- python3 $R/bench.py $ARGS > $R/$out/pmc_a.log 2>&1; step $? pmc_a
 cd $R
+python3 tools/pmc_summary.py $out/summary.json $out/tr_iso/run_kernel_trace.csv $out/pmc_a/run_counter_collection.csv > $out/summary.txt
+head -6 $out/summary.txt | cut -c1-300
 echo "== isolated"; python3 tools/prof_stats.py $out/tr_iso/run_kernel_stats.csv 24
 timeout -k 10 300 python -u bench.py --steps 40 --warmup 5 --no-cpu-baseline --no-exact-compare > $out/bench.json 2> $out/bench.err; step $? bench
 python - <<'P'
@@ -20,6 +23,8 @@ d = json.loads(open("gpurun_out/r3h/bench.json").read().strip().splitlines()[-1]
 print(d["ms_per_step"], d["ms_per_force_eval"], d["graph_replay_ms_per_step"], d["roofline"]["avg_launch_ms"], d["roofline"].get("isolated"))
 print(d["kernels_ms_per_step"])
 P
+timeout -k 10 300 python -u tools/scaling_probe.py --worlds 1 8 --no-timing > $out/probe.json 2> $out/probe.err; step $? probe
+cut -c1-120 $out/probe.json
 # accuracy / speed of the kernel width: W = 13 and 14 with the exact k-sum comparison
 for w in 13 14; do
     timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline --grid-width $w > $out/bench_w$w.json 2> $out/bench_w$w.err; step $? bench_w$w
