@@ -118,9 +118,12 @@ void alloc_nlist(cf_handle* H, double skin) {
     double r = h.cutoff + skin;
     double mean = 4.0 / 3.0 * M_PI * r * r * r * h.n / V;
     int cap = (int)std::min<double>(h.n, 0.5 * mean + 64);
+    const size_t rows = std::max(h.hi - h.lo, 1);  // one row per owned atom
+    // a sub-list's entries are addressed by 32-bit offsets from its row (k_nlist_wave): cap * rows
+    // < 2^31 (a clamped capacity only sends more rows to the overflow rescan)
+    cap = (int)std::min<size_t>((size_t)cap, ((size_t)1 << 31) / rows - 4);
     cap = (cap + 3) / 4 * 4;   // whole 4-entry chunks (list layout, cf_kernels_core.hip nl_index)
     if (h.nl && cap <= h.nb_cap) return;
-    const size_t rows = std::max(h.hi - h.lo, 1);  // one row per owned atom
     dfree(H, h.nl);
     h.nl = nullptr;
     h.nb_cap = cap;

@@ -608,11 +608,11 @@ __global__ void __launch_bounds__(kWaveNL * kSeg) k_nlist_wave(DirectArgs a) {
     const int ex_min = exc ? a.ex_list[ex0] : 1, ex_max = exc ? a.ex_list[ex0 + exc - 1] : 0;
     int cnt = 0;
     int* const nl_row = a.nl + ((size_t)seg * (a.nb_cap / kChunk) * a.nlr + c) * kChunk;   // = nl_index(a, seg, 0, c)
-    const size_t nl_qstride = (size_t)a.nlr * kChunk;
+    const unsigned nl_qstride = (unsigned)a.nlr * kChunk;   // a row's entries lie within nb_cap * nlr < 2^31 ints of nl_row
     // store list entry `entry` unless partner j is excluded (one branch: the store)
     auto put_entry = [&](int entry, int j) {
         const bool keep = !(j >= ex_min && j <= ex_max && in_excl(j, reg, exc, a.ex_list, ex0));
-        if (keep && cnt < a.nb_cap) nl_row[(size_t)(cnt >> 2) * nl_qstride + (cnt & 3)] = entry;
+        if (keep && cnt < a.nb_cap) nl_row[(unsigned)(cnt >> 2) * nl_qstride + (unsigned)(cnt & 3)] = entry;
         cnt += keep;
     };
     // high bits of a list entry: the partner's LJ type when types are used, else the image code

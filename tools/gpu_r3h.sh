@@ -35,4 +35,11 @@ for w in (13, 14):
     d = json.loads(open(f"gpurun_out/r3h/bench_w{w}.json").read().strip().splitlines()[-1])
     print(w, d["ms_per_step"], d["exact_kspace"], {k: d["kernels_ms_per_step"][k] for k in ("grid_sort", "grid_spread", "grid_interp")})
 P
+# C5 (768k atoms, mixed precision): the BASELINE config-5 workload on one GPU
+timeout -k 10 600 python -u bench.py --config C5 --precision mixed --steps 10 --warmup 3 --no-cpu-baseline --no-exact-compare > $out/bench_c5.json 2> $out/bench_c5.err; step $? bench_c5
+python - <<'P'
+import json
+d = json.loads(open("gpurun_out/r3h/bench_c5.json").read().strip().splitlines()[-1])
+print("C5", d["ms_per_step"], d["value"], d["kernels_ms_per_step"])
+P
 exit 0
