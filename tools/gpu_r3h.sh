@@ -5,17 +5,24 @@
 out=gpurun_out/r3h
 mkdir -p $out
 step() { local rc=$1 name=$2; echo "$name rc=$rc"; [ $rc -eq 0 ] || exit $rc; }
+# list builder: per-candidate emission (default) vs the hit-mask form (CF_NLIST_MASKS=1): same list, same bits
+CF_NLIST_MASKS=1 timeout -k 10 300 python -u tools/ab_bits.py run openmm-chargeflux_amd/libchargeflux_hip.so $out/ab0.npz > $out/ab0.log 2>&1; step $? ab0
+timeout -k 10 300 python -u tools/ab_bits.py run openmm-chargeflux_amd/libchargeflux_hip.so $out/ab1.npz > $out/ab1.log 2>&1; step $? ab1
+python tools/ab_bits.py cmp $out/ab0.npz $out/ab1.npz > $out/ab.txt 2>&1; echo "ab cmp rc=$?"; tail -2 $out/ab.txt
+rm -f $out/ab0.npz $out/ab1.npz
 timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread -p no:cacheprovider > $out/tests.log 2>&1
 rc=$?; tail -3 $out/tests.log; echo "tests rc=$rc"; [ $rc -le 1 ] || exit $rc
 R=$GRAFT_REPO_ROOT
 ARGS="--steps 10 --warmup 3 --no-cpu-baseline --no-exact-compare"
 cd /tmp && export TMPDIR=/tmp
 CF_OVERLAP=0 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/$out/tr_iso -o run --output-format csv -- python3 $R/bench.py $ARGS > $R/$out/tr_iso.log 2>&1; step $? tr_iso
+CF_OVERLAP=0 CF_NLIST_MASKS=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/$out/tr_masks -o run --output-format csv -- python3 $R/bench.py $ARGS > $R/$out/tr_masks.log 2>&1; step $? tr_masks
 CF_OVERLAP=0 timeout -k 10 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS GRBM_GUI_ACTIVE -d $R/$out/pmc_a -o run --output-format csv -- python3 $R/bench.py $ARGS > $R/$out/pmc_a.log 2>&1; step $? pmc_a
 cd $R
 python3 tools/pmc_summary.py $out/summary.json $out/tr_iso/run_kernel_trace.csv $out/pmc_a/run_counter_collection.csv > $out/summary.txt
 head -6 $out/summary.txt | cut -c1-300
 echo "== isolated"; python3 tools/prof_stats.py $out/tr_iso/run_kernel_stats.csv 24
+echo "== isolated, hit-mask builder"; python3 tools/prof_stats.py $out/tr_masks/run_kernel_stats.csv 6
 timeout -k 10 300 python -u bench.py --steps 40 --warmup 5 --no-cpu-baseline --no-exact-compare > $out/bench.json 2> $out/bench.err; step $? bench
 python - <<'P'
 import json
