@@ -253,47 +253,39 @@ __global__ void __launch_bounds__(256) k_cell_scatter(int n, const int* __restri
     tmp[cstart[key[i]] + rank[i]] = i;
 }
 
-// one wave per cell: final position of each member = cell start + number of members before it
-// in (LJ class, atom index) order -- atoms with LJ (epsilon != 0) first, then those without,
-// each by atom index -- (members staged in LDS and read by broadcast); multi-rank: an owned
-// member's list row = the cell's first row + number of owned members before it.  The LJ-first
-// order makes the rows of a water cell's H atoms contiguous, so most pair-kernel waves hold
-// only rows without LJ and skip its terms (wave-uniform branch, k_pairs_half / k_pairs).
+// one wave per cell: final position of each member = cell start + number of members with
+// a smaller atom index (members staged in LDS and read by broadcast); multi-rank: an owned
+// member's list row = the cell's first row + number of owned members with a smaller index
 constexpr int kOrderLds = 1024;
-constexpr int kNoLjBit = 30;   // sort key = atom index | (no LJ) << 30 (indices < 2^26)
 
 __global__ void __launch_bounds__(256) k_cell_order(int ncell, const int* __restrict__ flag,
                                                     const int* __restrict__ cstart, const int* __restrict__ cend,
                                                     const int* __restrict__ tmp, int* __restrict__ out, int lo, int hi,
-                                                    const int* __restrict__ own_start, int* __restrict__ own_s,
-                                                    const double2* __restrict__ lj) {
+                                                    const int* __restrict__ own_start, int* __restrict__ own_s) {
     __shared__ int mem[4][kOrderLds];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int c = blockIdx.x * 4 + w;
     if (c >= ncell || !*flag) return;
     const int b = cstart[c], m = cend[c] - b;
-    auto key_of = [&](int i) { return i | ((lj[i].y == 0.0 ? 1 : 0) << kNoLjBit); };
-    constexpr int kIdx = (1 << kNoLjBit) - 1;
-    // keys in LDS (cells of up to kOrderLds members; denser cells compute them per comparison)
-    const bool in_lds = m <= kOrderLds;
-    if (in_lds) {
-        for (int e = lane; e < m; e += 64) mem[w][e] = key_of(tmp[b + e]);
+    const int* src = tmp + b;
+    if (m <= kOrderLds) {
+        for (int e = lane; e < m; e += 64) mem[w][e] = src[e];
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        src = mem[w];
     }
-    auto key_at = [&](int j) { return in_lds ? mem[w][j] : key_of(tmp[b + j]); };
     for (int e = lane; e < m; e += 64) {
-        const int kv = key_at(e), v = kv & kIdx;
+        const int v = src[e];
         int r = 0, ro = 0;
         if (own_s) {
             for (int j = 0; j < m; j++) {
-                const int ku = key_at(j), u = ku & kIdx;
-                r += ku < kv;
-                ro += ku < kv && u >= lo && u < hi;
+                const int u = src[j];
+                r += u < v;
+                ro += u < v && u >= lo && u < hi;
             }
         } else {
-            for (int j = 0; j < m; j++) r += key_at(j) < kv;
+            for (int j = 0; j < m; j++) r += src[j] < v;
         }
         out[b + r] = v;
         if (own_s && v >= lo && v < hi) own_s[own_start[c] + ro] = b + r;
@@ -889,11 +881,9 @@ __device__ __forceinline__ double erfc_exp(double x, const double* __restrict__ 
 
 // real-space Ewald + LJ pair (RCK:567-592), d = pos_i - pos_j (minimum image); tab = LDS
 // copy of the erfcx table (the cutoff test r <= rc guarantees alpha r lies inside it)
-// lj: the wave has a row with LJ (wave-uniform; otherwise es6 = sig6 = 0, the values a row
-// without LJ, epsilon_i = 0, gives anyway: the same bits)
 __device__ __forceinline__ void pair_term(PairAcc& acc, const DirectArgs& a, const double* __restrict__ tab,
                                           double4 pi, double2 li, double4 pj, double2 lj2, double dx, double dy,
-                                          double dz, double r2, bool lj = true) {
+                                          double dz, double r2) {
     const double ke = a.ke;
     const double two_over_sqrtpi = 1.1283791670955126;
     double inv_r = rsqrt_fp64(r2);
@@ -903,13 +893,10 @@ __device__ __forceinline__ void pair_term(PairAcc& acc, const DirectArgs& a, con
     double ec = erfc_exp(ar, tab, a.erfc_scale, e2);
     const double qj = ke * pj.w * inv_r;   // potential of j at i per unit erfc; qq = q_i qj
     const double qq = pi.w * qj;
-    double sig6 = 0.0, es6 = 0.0;
-    if (lj) {
-        double sig = li.x + lj2.x;
-        double s2 = inv_r * sig; s2 *= s2;
-        sig6 = s2 * s2 * s2;
-        es6 = sig6 * li.y * lj2.y;
-    }
+    double sig = li.x + lj2.x;
+    double s2 = inv_r * sig; s2 *= s2;
+    const double sig6 = s2 * s2 * s2;
+    const double es6 = sig6 * li.y * lj2.y;
     if (a.include_forces) {
         const double dEdR = fma(qq, ec + ar * e2 * two_over_sqrtpi, es6 * (12 * sig6 - 6)) * (inv_r * inv_r);
         acc.fx += dEdR * dx; acc.fy += dEdR * dy; acc.fz += dEdR * dz;
@@ -1066,7 +1053,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))
     for (int m = 1; m < LPA; m <<= 1) over = __shfl_xor(over, m) || over;
     if (over) active = false;
     PairAcc acc;
-    const bool lj_wave = __ballot(active && a.ljs[ss].y != 0.0) != 0;   // a row of this wave has LJ
     if (active) {
         const double4 pi = a.pos4s[ss];
         const double2 li = a.ljs[ss];
@@ -1087,7 +1073,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))
             double dx = pi.x - cd.p.x, dy = pi.y - cd.p.y, dz = pi.z - cd.p.z;
             min_image(a, dx, dy, dz);
             const double r2 = dx * dx + dy * dy + dz * dz;
-            if (r2 <= a.rc2) pair_term(acc, a, tab, pi, li, cd.p, cd.lj, dx, dy, dz, r2, lj_wave);  // exact voxel-hash test
+            if (r2 <= a.rc2) pair_term(acc, a, tab, pi, li, cd.p, cd.lj, dx, dy, dz, r2);  // exact voxel-hash test
         };
         walk_list(nl4, a.nlr, cnt, part, LPA / kSeg, gather, eval);
     }
@@ -1191,7 +1177,6 @@ __global__ void __launch_bounds__(kHalfBlock) k_pairs_half(DirectArgs a) {
         const int row = r0 + (active ? rr : 0);
         const int cnt = active ? a.nl_cnt[(size_t)g * a.nlr + row] : 0;
         if (cnt > a.nb_cap) { bad_list = true; active = false; }
-        const bool lj_wave = __ballot(active && a.ljs[row].y != 0.0) != 0;   // a row of this wave has LJ
         std::conditional_t<MIXED, PairAccF, PairAcc> acc;
         if constexpr (MIXED) {
           if (active) {
@@ -1301,16 +1286,11 @@ __global__ void __launch_bounds__(kHalfBlock) k_pairs_half(DirectArgs a) {
                 const double ec = erfc_exp(ar, tab, a.erfc_scale, e2);
                 const double qj = ke * pj.w * inv_r;
                 const double qq = pi.w * qj;
-                // LJ only when a row of this wave has it (wave-uniform; otherwise es6 = sig6 = 0,
-                // which adds the same -0 / exact zeros as a row without LJ: the same bits)
-                double es6 = 0.0, sig6 = 0.0;
-                if (lj_wave) {
-                    const double sig = li.x + lj.x;
-                    double s2 = inv_r * sig;
-                    s2 *= s2;
-                    sig6 = s2 * s2 * s2;
-                    es6 = sig6 * li.y * lj.y;
-                }
+                const double sig = li.x + lj.x;
+                double s2 = inv_r * sig;
+                s2 *= s2;
+                const double sig6 = s2 * s2 * s2;
+                const double es6 = sig6 * li.y * lj.y;
                 if (a.include_forces) {
                     // the force on j, -F_ij, in fixed-point units (x -2^34: exact), which the
                     // i side also accumulates (negated and unscaled once at the end: the same
@@ -1832,7 +1812,7 @@ void launch_cell_sort(Handle& h, const double* pos) {
     hipLaunchKernelGGL(k_cell_scatter, dim3(nblk(h.n, 256)), dim3(256), 0, h.stream, h.n, f, h.cell_key, h.atom_val,
                        h.cell_start, h.atom_tmp, ncell, h.cell_cnt, oc);
     hipLaunchKernelGGL(k_cell_order, dim3(nblk(ncell, 4)), dim3(256), 0, h.stream, ncell, f, h.cell_start,
-                       h.cell_end, h.atom_tmp, h.key_tmp, h.lo, h.hi, h.own_start, oc ? h.own_s : nullptr, h.lj);
+                       h.cell_end, h.atom_tmp, h.key_tmp, h.lo, h.hi, h.own_start, oc ? h.own_s : nullptr);
     hipLaunchKernelGGL(k_cell_commit, dim3(nblk(h.n, 256)), dim3(256), 0, h.stream, h.n, f, h.cell_key, h.key_tmp,
                        pos, h.q, h.lj, L, T, h.cell_key_sorted, h.atom_sorted, h.pos4s, h.ljs,
                        h.atom_type, h.typ_s,
