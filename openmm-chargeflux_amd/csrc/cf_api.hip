@@ -446,7 +446,6 @@ CF_EXPORT int cf_create(const cf_params* p, const cf_options* opt, cf_handle** o
             fail(CF_ERR_INVALID, "precision must be CF_PRECISION_DOUBLE or CF_PRECISION_MIXED");
         h.mixed = o.precision == CF_PRECISION_MIXED;
         h.overlap = !(getenv("CF_OVERLAP") && std::string(getenv("CF_OVERLAP")) == "0");   // A/B
-        h.nl_masks = getenv("CF_NLIST_MASKS") && std::string(getenv("CF_NLIST_MASKS")) == "1";   // A/B
         h.kspace_algo = o.kspace_algo;
         h.stream = (hipStream_t)o.stream;  // NULL = the null stream (orders with torch's default stream)
 

@@ -128,7 +128,6 @@ struct Handle {
     // list and direct space (CF_OVERLAP=0: one stream); its interpolation then stores into
     // dedq_rec / f_rec, added by k_assemble_energy in the one-stream order ((direct + excl) + rec)
     bool overlap = true;
-    int nl_masks = 0;           // list builder A/B: CF_NLIST_MASKS=1 selects the hit-mask emission (cf_create)
     bool rec_split = false;     // the last evaluation left the reciprocal dE/dq in dedq_rec
     bool split_overlap = false; // a begun multi-rank evaluation runs its direct chain on aux (cf_api.hip)
     hipStream_t aux = nullptr;

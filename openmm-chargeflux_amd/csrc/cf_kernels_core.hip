@@ -388,7 +388,6 @@ struct DirectArgs {
     double3 T; int tric;        // reduced triclinic box: off-diagonals (bx, cx, cy); tric = any nonzero
     double rc2, alpha;
     double rc;                  // cutoff (the half list's fixed-point range bound)
-    int nl_masks;               // list builder: the hit-mask form (CF_NLIST_MASKS=1, A/B)
     double ke;                  // Coulomb constant ONE_4PI_EPS0 (Handle::ke)
     const double* erfc_tab;     // [kErfcDeg+1][kErfcMaxM] erfcx(x) on intervals of width 1/erfc_scale
     const float* erfc_tab_f;    // [erfc_m_f][kErfcDegF+1] fp32 (mixed precision), width 1/erfc_scale_f
@@ -553,7 +552,7 @@ __global__ void __launch_bounds__(kWaveNL * kSeg) k_nlist_wave(DirectArgs a) {
     // staged candidates, SoA so that one ds_read_b128 gives 4 candidates' x (two packed-fp32
     // operands): x, y, z in the block frame, (half lists) the x key; atom index | LJ type << 26
     __shared__ __attribute__((aligned(16))) float cand_all[kSeg][4][kStage + 16];
-    __shared__ __attribute__((aligned(16))) int cand_j_all[kSeg][kStage + 16];
+    __shared__ int cand_j_all[kSeg][kStage + 16];
     const int lane = threadIdx.x & 63;
     const int seg = threadIdx.x >> 6;   // this wave's share of the cell box and its sub-list
     float* cx = cand_all[seg][0];
@@ -697,54 +696,15 @@ __global__ void __launch_bounds__(kWaveNL * kSeg) k_nlist_wave(DirectArgs a) {
             if (u < nu) put(u, rp[v], rj[v], rt[v], off);
         }
     };
-    // Candidates in order, four per step (one ds_read_b128 of each staged array), their
-    // distances two at a time in packed fp32 (v_pk_add/mul/fma_f32), and each candidate emitted
-    // at once by the lanes it hits (an exec-masked block per candidate: no per-lane loops over
-    // hit masks, whose trip count was the largest hit count of the wave's lanes; the entries
-    // come out in the same order).  Staged candidate u is candidate u0 + u of cell cb.
-    // CF_NLIST_MASKS (old form, A/B): 16-candidate hit masks per lane, emitted by ctz loops.
+    // 16 candidates per chunk, tested two at a time in packed fp32 (v_pk_add/mul/fma_f32: half
+    // the VALU instructions of scalar fp32), then the lane's hits of the chunk are emitted
+    // (a longer chunk amortizes the divergent emit loop: its trip count is the maximum hit
+    // count over the wave's lanes).  Staged candidate u is candidate u0 + u of cell cb.
+    // (Measured against emitting each candidate at once by the lanes it hits, exec-masked:
+    // 54.8 vs 67.7 us per step at C3, profiles/r03i_*; the same list either way.)
     typedef float v2f __attribute__((ext_vector_type(2)));
     typedef float v4f __attribute__((ext_vector_type(4)));
-    typedef int v4i_ __attribute__((ext_vector_type(4)));
-    const bool same_x_rule = a.half;
     auto test = [&](int cb, int u0, int m, int code, int hk) {
-        if (!active) return;
-        if (a.half && hk < 0) return;   // x offset -1: those pairs belong to the partner's row
-        const bool same_x = same_x_rule && hk < 9;   // same x cell: the smaller x key keeps the pair
-        const int ds = s - cb;                      // full lists: this atom itself, if it is a candidate
-        const int us_self = (!a.half && ds >= 0 && ((ds >> 2) & 3) == seg) ? (((ds >> 4) << 2) | (ds & 3)) - u0 : -1;
-        const v2f px = {pf.x, pf.x}, py = {pf.y, pf.y}, pz = {pf.z, pf.z};
-        for (int c0 = 0; c0 < m; c0 += 4) {
-            const v4f X = *reinterpret_cast<const v4f*>(cx + c0);
-            const v4f Y = *reinterpret_cast<const v4f*>(cy + c0);
-            const v4f Z = *reinterpret_cast<const v4f*>(cz + c0);
-            const v4f K = *reinterpret_cast<const v4f*>(cxk + c0);
-            const v4i_ J = *reinterpret_cast<const v4i_*>(cand_j + c0);
-            v2f r2[2];
-#pragma unroll
-            for (int h = 0; h < 2; h++) {
-                const v2f dx = px - (h ? X.zw : X.xy), dy = py - (h ? Y.zw : Y.xy), dz = pz - (h ? Z.zw : Z.xy);
-                r2[h] = dx * dx + dy * dy + dz * dz;
-            }
-#pragma unroll
-            for (int v = 0; v < 4; v++) {
-                const int u = c0 + v;
-                const float d2 = v == 0 ? r2[0].x : (v == 1 ? r2[0].y : (v == 2 ? r2[1].x : r2[1].y));
-                // (bitwise logic, no short-circuit branches: one exec-masked block per candidate)
-                const float kv = v == 0 ? K.x : (v == 1 ? K.y : (v == 2 ? K.z : K.w));
-                // same x cell: the smaller x key keeps the pair; ties (rare; and the row atom
-                // itself, dropped): the lower slot
-                const bool ahead = (kv > xki) | ((kv == xki) & (slot_of(cb, u0 + u) > s));
-                const bool hit = (u < m) & (d2 <= rc2f) & (!same_x | ahead) & (u != us_self);
-                if (hit) {
-                    const int cj = v == 0 ? J.x : (v == 1 ? J.y : (v == 2 ? J.z : J.w));
-                    if (a.half) put_entry(slot_of(cb, u0 + u) | (hk << kHalfSlotBits) | (cj & ~kJMask), cj & kJMask);
-                    else emit(slot_of(cb, u0 + u), cj & kJMask, a.typ_s ? (int)((unsigned)cj >> kShiftBits) : code);
-                }
-            }
-        }
-    };
-    auto test_masks = [&](int cb, int u0, int m, int code, int hk) {
         if (!active) return;
         if (a.half && hk < 0) return;   // x offset -1: those pairs belong to the partner's row
         const v2f px = {pf.x, pf.x}, py = {pf.y, pf.y}, pz = {pf.z, pf.z};
@@ -826,8 +786,7 @@ __global__ void __launch_bounds__(kWaveNL * kSeg) k_nlist_wave(DirectArgs a) {
             nu_n = count_of(cb_n, a.cend[cc]);
             fetch(cb_n, nu_n);
         }
-        if (a.nl_masks) test_masks(cb, 0, min(nu, kStage), code, hk);
-        else test(cb, 0, min(nu, kStage), code, hk);
+        test(cb, 0, min(nu, kStage), code, hk);
         // rare: more than kStage candidates per wave in a cell (synchronous remainder)
         for (int u0 = kStage; u0 < nu; u0 += kStage) {
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -843,8 +802,7 @@ __global__ void __launch_bounds__(kWaveNL * kSeg) k_nlist_wave(DirectArgs a) {
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            if (a.nl_masks) test_masks(cb, u0, min(nu - u0, kStage), code, hk);
-            else test(cb, u0, min(nu - u0, kStage), code, hk);
+            test(cb, u0, min(nu - u0, kStage), code, hk);
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     }
@@ -1833,7 +1791,6 @@ static DirectArgs direct_args(Handle& h, const double* pos, int include_forces) 
     a.nc = make_int3(h.nc[0], h.nc[1], h.nc[2]);
     a.brute = (h.nc[0] < 3 || h.nc[1] < 3 || h.nc[2] < 3) ? 1 : 0;
     a.rc2 = h.cutoff * h.cutoff; a.rc = h.cutoff; a.alpha = h.alpha; a.ke = h.ke;
-    a.nl_masks = h.nl_masks;
     a.erfc_tab = h.erfc_tab; a.erfc_scale = h.erfc_scale; a.erfc_m = h.erfc_m;
     a.erfc_tab_f = h.erfc_tab_f; a.erfc_scale_f = h.erfc_scale_f; a.erfc_m_f = h.erfc_m_f;
     a.rl2 = (h.cutoff + h.list_skin) * (h.cutoff + h.list_skin);
