@@ -1071,7 +1071,16 @@ static void launch_end_split(cf_handle* H, int flags, double* forces_dev, double
 static void ensure_aux(cf_handle* H) {
     cf::Handle& h = H->h;
     if (h.aux || !h.overlap || !h.pbc || h.kspace_algo != 2) return;
-    check_hip(hipStreamCreateWithFlags(&h.aux, hipStreamNonBlocking), "hipStreamCreate (reciprocal chain)");
+    // CF_AUX_PRIORITY=low / high (A/B): the second stream's priority against the caller's
+    const char* pr = getenv("CF_AUX_PRIORITY");
+    if (pr && (std::string(pr) == "low" || std::string(pr) == "high")) {
+        int least = 0, greatest = 0;
+        check_hip(hipDeviceGetStreamPriorityRange(&least, &greatest), "hipDeviceGetStreamPriorityRange");
+        check_hip(hipStreamCreateWithPriority(&h.aux, hipStreamNonBlocking, std::string(pr) == "low" ? least : greatest),
+                  "hipStreamCreateWithPriority (second stream)");
+    } else {
+        check_hip(hipStreamCreateWithFlags(&h.aux, hipStreamNonBlocking), "hipStreamCreate (second stream)");
+    }
     check_hip(hipEventCreateWithFlags(&h.ev_fork, hipEventDisableTiming), "hipEventCreate");
     check_hip(hipEventCreateWithFlags(&h.ev_join, hipEventDisableTiming), "hipEventCreate");
     if (!h.dedq_rec) {
