@@ -81,6 +81,7 @@ struct GridPlan {
     bool spread_dpp = true;  // spread FMAs take the x taps by DPP row broadcast (CF_SPREAD_DPP=0: scalar loads)
     int spread_pass = 32;    // atoms per staging pass of the W > 9 spread (CF_SPREAD_PASS=64: A/B)
     bool interp2 = true;     // two atoms per wave, taps by DPP row broadcast (CF_INTERP2=0: k_g_interp)
+    bool interp4 = true;     // W <= 8: four atoms per wave (CF_INTERP4=0: k_g_interp2)
 };
 
 struct Handle {

@@ -1519,6 +1519,144 @@ __global__ void __launch_bounds__(kInterpThreads) k_g_interp2(int3 ng, int3 nb, 
     }
 }
 
+// acc += x_I * y on the lanes of banks BANKS of every row (row_newbcast:I, bank_mask): the
+// other lanes keep acc
+template <int I, int BANKS>
+__device__ __forceinline__ void fmac_row_bcast_banks(double& acc, double x, double y) {
+    asm("v_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:%4" : "+v"(acc) : "v"(x), "v"(y), "i"(I),
+        "i"(BANKS));
+}
+
+// 64-bit row rotation by 8 lanes (lane l of a row gets lane (l - 8) mod 16's value)
+__device__ __forceinline__ double row_ror8(double v) { return dpp_f64<0x128, 0xF>(v); }
+
+// Sums of four values over each 16-lane row (rows are atoms here): lane l with (l & 15) < 4 holds
+// its row's total of (pv, py, px, pz)[l & 3]
+__device__ __forceinline__ double row_sum4(double pv, double px, double py, double pz, int lane) {
+    const bool odd = lane & 1, hi = lane & 2;
+    const double a = (odd ? py : pv) + dpp_f64<0xB1, 0xF>(odd ? pv : py);
+    const double b = (odd ? pz : px) + dpp_f64<0xB1, 0xF>(odd ? px : pz);
+    double c = (hi ? b : a) + dpp_f64<0x4E, 0xF>(hi ? a : b);
+    c += dpp_f64<0x124, 0xF>(c);   // row_ror:4
+    c += dpp_f64<0x128, 0xF>(c);   // row_ror:8
+    return c;
+}
+
+// W <= 8 (the mixed-precision grid): four atoms per wave, one per 16-lane row.  Lane (jg, k) of a
+// row (jg = bit 3, k = bits 0-2) owns z column k and rows j = 2jj + jg (jj < ceil(W/2)), so every
+// lane of the wave does useful work (k_g_interp2 leaves lanes k >= W of its 16-lane columns idle
+// at W <= 8).  Taps: lanes jg = 0 evaluate x tap k, lanes jg = 1 z tap k (one pass; a row rotation
+// by 8 gives the jg = 0 lanes their z tap); y taps 2n + jg in lane (jg, n < NJ), broadcast to the
+// lanes of each half-row by row_newbcast with a bank mask.  Otherwise as k_g_interp2.
+template <int W>
+__global__ void __launch_bounds__(kInterpThreads) k_g_interp4(int3 ng, int3 nb, const int* __restrict__ start,
+                                                              const int4* __restrict__ g0s,
+                                                              const double4* __restrict__ srec, double beta,
+                                                              double3 gscale, const double* __restrict__ G, int lo,
+                                                              double* __restrict__ dedq, double* __restrict__ f_part,
+                                                              int store) {
+    static_assert(W <= 8, "one 8-lane half-row per z column");
+    constexpr int R = 7 + W;
+    constexpr int NJ = (W + 1) / 2;
+    constexpr int NW = kInterpThreads / 64;
+    extern __shared__ double sg[];   // [R][R][R]
+    const int nyz = nb.y * nb.z;
+    int tile = blockIdx.x;
+    if (nyz % 8 == 0) {
+        const int per = nyz / 8, i = blockIdx.x / 8;
+        tile = (i / per) * nyz + (blockIdx.x % 8) * per + i % per;
+    }
+    const int s0 = start[tile], s1 = start[tile + 1];
+    if (s0 == s1) return;
+    const int tz = tile % nb.z, ty = (tile / nb.z) % nb.y, tx = tile / (nb.z * nb.y);
+    interp_stage<W>(ng, G, tx, ty, tz, sg);
+    __syncthreads();
+    const int lane = threadIdx.x & 63, w = wave_id();
+    const int q = lane >> 4, jg = (lane >> 3) & 1, k = lane & 7;
+    const double hw_inv = 2.0 / W;
+    int4 g_n = make_int4(0, 0, 0, 0);
+    if (s0 + 4 * w + q < s1) g_n = g0s[s0 + 4 * w + q];
+    double4 sr_n = srec[g_n.w];
+    for (int sb = s0 + 4 * w; sb < s1; sb += 4 * NW) {   // wave-uniform
+        const bool valid = sb + q < s1;
+        const int4 g = g_n;
+        const double4 sr = sr_n;
+        if (sb + 4 * NW + q < s1) {
+            g_n = g0s[sb + 4 * NW + q];
+            sr_n = srec[g_n.w];
+        }
+        double xv, xd, yv = 0, yd = 0, zv, zd;
+        {
+            const double sd = jg ? sr.z : sr.x;
+            double v = 0, dv = 0;
+            if (k < W) es_tap(ceil(sd - 0.5 * W) + k - sd, hw_inv, beta, v, dv);
+            xv = v; xd = dv;                              // lanes jg = 0: x tap k (the DPP sources)
+            const double rv = row_ror8(v), rdv = row_ror8(dv);   // lane (0, k) <- lane (1, k)
+            zv = jg ? v : rv; zd = jg ? dv : rdv;
+        }
+        if (k < NJ && 2 * k + jg < W) es_tap(ceil(sr.y - 0.5 * W) + (2 * k + jg) - sr.y, hw_inv, beta, yv, yd);
+        xv = dpp_ready(xv); xd = dpp_ready(xd); yv = dpp_ready(yv); yd = dpp_ready(yd);
+        const int rx = g.x & 7, ry = g.y & 7, rz = g.z & 7;
+        const double* base = sg + (rx * R + ry) * R + rz + (k < W ? k : 0);
+        double t0[NJ], t1[NJ];
+#pragma unroll
+        for (int jj = 0; jj < NJ; jj++) { t0[jj] = 0; t1[jj] = 0; }
+        double gv[2][NJ];
+        auto load_row = [&](int i, double (&gg)[NJ]) {
+#pragma unroll
+            for (int jj = 0; jj < NJ; jj++) {
+                const int j = 2 * jj + jg;
+                gg[jj] = base[(i * R + (j < W ? j : 0)) * R];
+            }
+        };
+        load_row(0, gv[0]);
+        static_for<W>([&](auto I) {
+            constexpr int i = decltype(I)::value;
+            if constexpr (i + 1 < W) load_row(i + 1, gv[(i + 1) & 1]);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int jj = 0; jj < NJ; jj++) {
+                fmac_row_bcast<i>(t0[jj], xv, gv[i & 1][jj]);
+                fmac_row_bcast<i>(t1[jj], xd, gv[i & 1][jj]);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        });
+        // y: lanes jg = 0 (banks 0, 1) take y tap 2jj from lane jj, lanes jg = 1 (banks 2, 3) tap
+        // 2jj + 1 from lane 8 + jj
+        double pv = 0, px = 0, py = 0;
+        static_for<NJ>([&](auto J) {
+            constexpr int jj = decltype(J)::value;
+            fmac_row_bcast_banks<jj, 0x3>(pv, yv, t0[jj]);
+            fmac_row_bcast_banks<8 + jj, 0xC>(pv, yv, t0[jj]);
+            fmac_row_bcast_banks<jj, 0x3>(px, yv, t1[jj]);
+            fmac_row_bcast_banks<8 + jj, 0xC>(px, yv, t1[jj]);
+            fmac_row_bcast_banks<jj, 0x3>(py, yd, t0[jj]);
+            fmac_row_bcast_banks<8 + jj, 0xC>(py, yd, t0[jj]);
+        });
+        const double pz = pv * zd;
+        pv *= zv; px *= zv; py *= zv;
+        const double tot = row_sum4(pv, px, py, pz, lane);
+        const int rl = lane & 15;
+        if (rl < 4 && valid) {   // each owned atom is in exactly one bin: no other writer
+            const int i = lo + g.w;
+            const int c = rl == 2 ? 0 : (rl == 1 ? 1 : 2);   // force component of lanes 1..3
+            if (store) {
+                if (rl == 0) {
+                    dedq[i] = tot;
+                    f_part[4 * i + 3] = -sr.w;
+                } else {
+                    f_part[4 * i + c] = tot;
+                }
+            } else if (rl == 0) {
+                dedq[i] += tot;
+            } else {
+                const double gs = c == 0 ? gscale.x : (c == 1 ? gscale.y : gscale.z);
+                f_part[3 * i + c] = fma(-sr.w * gs, tot, f_part[3 * i + c]);
+            }
+        }
+    }
+}
+
 static double es_host(double t, int W, double beta) {
     double z = 2.0 * t / W, u = 1.0 - z * z;
     return u > 0 ? std::exp(beta * (std::sqrt(u) - 1.0)) : 0.0;
@@ -1577,6 +1715,8 @@ void grid_plan(Handle& h, int width, double sigma) {
     p.spread_pass = sp ? std::atoi(sp) : 32;
     const char* i2 = getenv("CF_INTERP2");
     p.interp2 = !(i2 && i2[0] == '0');
+    const char* i4 = getenv("CF_INTERP4");
+    p.interp4 = !(i4 && i4[0] == '0');
     for (int d = 0; d < 3; d++) {
         const int K = h.kmax[d], J = d == 2 ? K : 2 * K - 1, k0 = d == 2 ? 0 : -(K - 1);
         int mx = 0;
@@ -1896,8 +2036,11 @@ void launch_grid_interp(Handle& h, bool split) {
     const double3 gs = make_double3(p.ng[0] / h.box_L[0], p.ng[1] / h.box_L[1], p.ng[2] / h.box_L[2]);
     const size_t R = 7 + p.W;
     const size_t lds = R * R * R * sizeof(double);
+    // W <= 8: four atoms per wave (k_g_interp4); else two (k_g_interp2); CF_INTERP2=0: one (k_g_interp)
 #define CF_INTERP(W_)                                                                                               \
-    hipLaunchKernelGGL(p.interp2 ? k_g_interp2<W_> : k_g_interp<W_>, dim3(p.nbins), dim3(kInterpThreads), lds,        \
+    hipLaunchKernelGGL(!p.interp2 ? k_g_interp<W_> : (W_ <= 8 && p.interp4) ? k_g_interp4<(W_ <= 8 ? W_ : 8)>      \
+                                                                           : k_g_interp2<W_>,                          \
+                       dim3(p.nbins), dim3(kInterpThreads), lds,                                                    \
                        h.stream, ng, nb, h.g_start, h.g_g0s, h.g_srec, p.beta, gs, h.g_grid, h.lo,                   \
                        split ? h.dedq_rec : h.dedq, split ? h.f_rec : h.f_part, split ? 1 : 0)
     CF_GRID_W_DISPATCH(p.W, CF_INTERP)

@@ -277,3 +277,28 @@ def test_grid_interp2_matches_interp(monkeypatch, case, width, spread_dpp):
     assert e1 == e0
     assert np.abs(f1 - f0).max() <= 1e-12 * np.abs(f0).max(), np.abs(f1 - f0).max()
     assert np.abs(d1 - d0).max() <= 1e-12 * np.abs(d0).max(), np.abs(d1 - d0).max()
+
+
+@pytest.mark.parametrize("case,width", [("C2", 8), ("w4k", 8), ("w4k", 7), ("w4k", 6), ("w4k", 5), ("w4k", 4)])
+def test_grid_interp4_matches_interp(monkeypatch, case, width):
+    """The four-atoms-per-wave interpolation (k_g_interp4, W <= 8: one atom per 16-lane row, y
+    taps by bank-masked row broadcasts) against the one-atom form (CF_INTERP2=0) and the
+    two-atom form (CF_INTERP4=0), even and odd widths: forces and dE/dq equal to <= 1e-12
+    relative, energy unchanged (not interpolated)."""
+    if case == "C2":
+        system, force, pos, box = ts.make("C2")
+    else:
+        system, force, pos, box = ts.water_box(4000, cutoff=1.0, ewald_tol=1e-4, every_bond_angle=5)
+    out = []
+    for i2, i4 in (("0", "1"), ("1", "0"), ("1", "1")):
+        monkeypatch.setenv("CF_INTERP2", i2)
+        monkeypatch.setenv("CF_INTERP4", i4)
+        k = HipCalcCoulForceKernel(kspace_algo=GRID, grid_width=width).initialize(system, force)
+        e, f = k.execute_host(pos, box)
+        out.append((e, f, k.dedq()))
+        k.destroy()
+    e0, f0, d0 = out[0]
+    for e1, f1, d1 in out[1:]:
+        assert e1 == e0
+        assert np.abs(f1 - f0).max() <= 1e-12 * np.abs(f0).max(), np.abs(f1 - f0).max()
+        assert np.abs(d1 - d0).max() <= 1e-12 * np.abs(d0).max(), np.abs(d1 - d0).max()
