@@ -122,7 +122,6 @@ void alloc_nlist(cf_handle* H, double skin) {
     // a sub-list's entries are addressed by 32-bit offsets from its row (k_nlist_wave): cap * rows
     // < 2^31 (a clamped capacity only sends more rows to the overflow rescan)
     cap = (int)std::min<size_t>((size_t)cap, ((size_t)1 << 31) / rows - 4);
-    cap = std::min(cap, 65532);   // a half-list row's chunks count in 16 bits (k_pairs_half walk_row)
     cap = (cap + 3) / 4 * 4;   // whole 4-entry chunks (list layout, cf_kernels_core.hip nl_index)
     if (h.nl && cap <= h.nb_cap) return;
     dfree(H, h.nl);

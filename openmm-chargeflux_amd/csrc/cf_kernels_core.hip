@@ -363,12 +363,11 @@ constexpr int kBruteShift = 31;  // shift code: minimum image by floor (brute-fo
 // cell k = ox*9 + (oy+1)*3 + (oz+1)) | LJ type << 26: the partner's address needs no table
 // lookup (the gather is not queued behind LDS work).
 constexpr int kHalfWin = 18;          // window cells per block: x offsets 0 and +1
-constexpr int kHalfBlock = 1024;      // threads per k_pairs_half block (one cell; 4-8 lanes per row)
+constexpr int kHalfBlock = 1024;      // threads per k_pairs_half block (one cell; 4 lanes per row)
 constexpr int kHalfOwn = 4;           // the row cell's own window index (0, 0, 0)
 constexpr int kHalfMaxWin = 4096;     // window atoms per block (LDS accumulators: 128 KB)
 constexpr int kHalfSlotBits = 21;     // sorted slots < 2^21 (cf_api.hip enables half lists below)
 constexpr int kHalfSlotMask = (1 << kHalfSlotBits) - 1;
-constexpr int kHalfPad = -1;          // half-list padding after a sub-list's last entry (window 31: never real)
 static_assert(kHalfSlotBits + 5 <= kShiftBits, "window cell bits overlap the LJ type bits");
 // j-side sums in 64-bit fixed point (integer adds: exact, so any order gives the same bits):
 // v -> round(v 2^34) via the 1.5 * 2^52 magic add (exact for |v 2^34| < 2^51); a contribution
@@ -389,7 +388,6 @@ struct DirectArgs {
     double3 T; int tric;        // reduced triclinic box: off-diagonals (bx, cx, cy); tric = any nonzero
     double rc2, alpha;
     double rc;                  // cutoff (the half list's fixed-point range bound)
-    int half_lpr;               // k_pairs_half: most lanes per row (4..8; CF_HALF_LPR, A/B)
     double ke;                  // Coulomb constant ONE_4PI_EPS0 (Handle::ke)
     const double* erfc_tab;     // [kErfcDeg+1][kErfcMaxM] erfcx(x) on intervals of width 1/erfc_scale
     const float* erfc_tab_f;    // [erfc_m_f][kErfcDegF+1] fp32 (mixed precision), width 1/erfc_scale_f
@@ -808,13 +806,7 @@ __global__ void __launch_bounds__(kWaveNL * kSeg) k_nlist_wave(DirectArgs a) {
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     }
-    if (active) {
-        a.nl_cnt[(size_t)seg * a.nlr + c] = cnt;
-        // half lists: the rest of the last chunk is padding (k_pairs_half's walk_row)
-        if (a.half)
-            for (int k = cnt; k < min((cnt + kChunk - 1) & ~(kChunk - 1), a.nb_cap); k++)
-                nl_row[(unsigned)(k >> 2) * nl_qstride + (unsigned)(k & 3)] = kHalfPad;
-    }
+    if (active) a.nl_cnt[(size_t)seg * a.nlr + c] = cnt;
 }
 
 struct PairAcc {
@@ -992,62 +984,6 @@ __device__ __forceinline__ void walk_list(const v4i* __restrict__ nl4, size_t st
     }
 }
 
-// The same pipeline over a row's four sub-lists of a half list taken as one sequence of chunks
-// (sub-list 0's, then 1's, ...): this lane walks chunks part, part + step, ... of it, so a row
-// can be shared by any number of lanes (k_pairs_half: 4 to 8, as many as the block holds for
-// its cell) and the lanes of a row finish together (one sub-list per lane: the longest of the
-// four sets the row's time).  The builder ends each sub-list's last chunk with kHalfPad
-// entries, so only the chunk sequence needs bounds: p1, p2, p3 = the chunks before sub-lists
-// 1, 2, 3; total = all.  nl4 points at the row's entry of sub-list 0; gstride = chunks per
-// sub-list x rows.
-template <class G, class E>
-__device__ __forceinline__ void walk_row(const v4i* __restrict__ nl4, size_t stride, size_t gstride, int4 cnt,
-                                         int part, int step, G&& gather, E&& eval) {
-    // (p1, p2) and (p3, total) packed in 16-bit halves: chunk counts < 2^16 (alloc_nlist caps
-    // nb_cap), two registers instead of four over the whole walk
-    const unsigned p1 = (cnt.x + kChunk - 1) / kChunk;
-    const unsigned p2 = p1 + (cnt.y + kChunk - 1) / kChunk;
-    const unsigned p3 = p2 + (cnt.z + kChunk - 1) / kChunk;
-    const int total = (int)(p3 + (cnt.w + kChunk - 1) / kChunk);
-    if (part >= total) return;
-    const unsigned k12 = p1 | (p2 << 16), k3t = p3 | ((unsigned)total << 16);
-    auto chunk = [&](int c) {   // chunk c (the last one past the end: valid memory, not evaluated)
-        const int t = (int)(k3t >> 16);
-        c = min(c, t - 1);
-        const int b1 = (int)(k12 & 0xffff), b2 = (int)(k12 >> 16), b3 = (int)(k3t & 0xffff);
-        const int g = (c >= b1) + (c >= b2) + (c >= b3);
-        const int q = c - (g == 0 ? 0 : (g == 1 ? b1 : (g == 2 ? b2 : b3)));
-        return __builtin_nontemporal_load(nl4 + (size_t)g * gstride + (size_t)q * stride);
-    };
-    auto ok = [](int e) { return e != kHalfPad; };
-    v4i A = chunk(part), B = chunk(part + step);
-    auto c0 = gather(A.x, true);   // a chunk's first entry is never padding
-    for (int c = part; c < total; c += 2 * step) {
-        const bool hb = c + step < total;
-        bool o1 = ok(A.y), o2 = ok(A.z), o3 = ok(A.w);
-        auto c1 = gather(A.y, o1);
-        eval(c0);
-        c0 = gather(A.z, o2);
-        if (o1) eval(c1);
-        c1 = gather(A.w, o3);
-        A = chunk(c + 2 * step);
-        if (o2) eval(c0);
-        c0 = gather(B.x, hb);
-        if (o3) eval(c1);
-        if (!hb) break;
-        o1 = ok(B.y); o2 = ok(B.z); o3 = ok(B.w);
-        c1 = gather(B.y, o1);
-        eval(c0);
-        c0 = gather(B.z, o2);
-        if (o1) eval(c1);
-        c1 = gather(B.w, o3);
-        B = chunk(c + 3 * step);
-        if (o2) eval(c0);
-        c0 = gather(A.x, c + 2 * step < total);
-        if (o3) eval(c1);
-    }
-}
-
 // 4b: walk the list — kSeg adjacent lanes per atom, lane g walks sub-list g; partial sums
 // are combined with two xor-shuffles (fixed order: deterministic).  Atoms with an
 // overflowed sub-list are left to k_excl (cell rescan).
@@ -1109,9 +1045,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))
 }
 
 // ---------------------------------------------------------------------------------
-// 4b'' half list: one 1024-thread workgroup per cell, 4 to 8 lanes per row
-//     (whole rows per wave; the most lanes that still take the cell's rows in one pass, so a
-//     cell of ~190 rows fills 15 of the 16 waves instead of 12; walk_row).  Each pair is evaluated once, by the row that keeps it (the x
+// 4b'' half list: one 1024-thread workgroup per cell, 4 lanes per row
+//     (passes of 256 rows).  Each pair is evaluated once, by the row that keeps it (the x
 //     half-space rule above): the i side accumulates in fp64 registers as in k_pairs; the j
 //     side (force -F_ij and dE/dq_j += k_e q_i erfc/r) is added in 64-bit fixed point to the
 //     block's LDS window -- the atoms of the 18 cells at x offset 0 and +1 -- with integer LDS
@@ -1192,25 +1127,14 @@ __global__ void __launch_bounds__(kHalfBlock) k_pairs_half(DirectArgs a) {
     }
     __syncthreads();
     const int r0 = win[kHalfOwn].x, nrows = a.cend[cell] - r0;
-    // lanes per row: the most (4..8) with which the 16 waves hold every row of the cell in one
-    // pass (whole rows per wave; 4 and several passes beyond 256 rows).  Block-uniform.
-    int lpr = 4;
-    for (int l = a.half_lpr; l > 4; l--)
-        if ((kHalfBlock / 64) * (64 / l) >= nrows) { lpr = l; break; }
-    const int rpw = 64 / lpr, lane = threadIdx.x & 63;
-    const int lr = lane / lpr, part = lane - lr * lpr;   // row in the wave, lane in the row
-    const size_t gstride = (size_t)(a.nb_cap / kChunk) * a.nlr;
+    const int g = threadIdx.x & 3;   // sub-list walked by this lane
     bool bad = false, bad_list = false;
-    for (int rb = 0; rb < nrows; rb += (kHalfBlock / 64) * rpw) {
-        const int rr = rb + (threadIdx.x >> 6) * rpw + lr;
-        bool active = lr < rpw && rr < nrows;
+    for (int rb = 0; rb < nrows; rb += 256) {
+        const int rr = rb + (threadIdx.x >> 2);
+        bool active = rr < nrows;
         const int row = r0 + (active ? rr : 0);
-        int4 cnt = make_int4(0, 0, 0, 0);
-        if (active) {
-            cnt = make_int4(a.nl_cnt[row], a.nl_cnt[(size_t)a.nlr + row], a.nl_cnt[(size_t)2 * a.nlr + row],
-                            a.nl_cnt[(size_t)3 * a.nlr + row]);
-            if (max(max(cnt.x, cnt.y), max(cnt.z, cnt.w)) > a.nb_cap) { bad_list = true; active = false; }
-        }
+        const int cnt = active ? a.nl_cnt[(size_t)g * a.nlr + row] : 0;
+        if (cnt > a.nb_cap) { bad_list = true; active = false; }
         std::conditional_t<MIXED, PairAccF, PairAcc> acc;
         if constexpr (MIXED) {
           if (active) {
@@ -1218,7 +1142,7 @@ __global__ void __launch_bounds__(kHalfBlock) k_pairs_half(DirectArgs a) {
             const float2 li = make_float2((float)a.ljs[row].x, (float)a.ljs[row].y);
             const float qi = (float)pi.w, ke = (float)a.ke, keqi = ke * qi;
             const float rc2 = (float)a.rc2, alpha = (float)a.alpha, escale = (float)a.erfc_scale_f;
-            const v4i* nl4 = reinterpret_cast<const v4i*>(a.nl) + row;
+            const v4i* nl4 = reinterpret_cast<const v4i*>(a.nl) + (size_t)g * (a.nb_cap / kChunk) * a.nlr + row;
             struct Cand { double4 p; float2 lj; int slot; };
             auto gather = [&](int e, bool ok) {
                 const int t = ok ? (e & kHalfSlotMask) : 0;
@@ -1280,21 +1204,19 @@ __global__ void __launch_bounds__(kHalfBlock) k_pairs_half(DirectArgs a) {
                     acc.e += (double)fmaf(qq, ec, es6 * (sig6 - 1.0f));   // the whole pair energy
                 }
             };
-            walk_row(nl4, a.nlr, gstride, cnt, part, lpr, gather, eval);
+            walk_list(nl4, a.nlr, cnt, 0, 1, gather, eval);
           }
         } else if (active) {
             const double4 pi = a.pos4s[row];
             const double2 li = a.ljs[row];
             const double kqis = a.ke * pi.w * kFixScale;   // k_e q_i in fixed-point units
-            const v4i* nl4 = reinterpret_cast<const v4i*>(a.nl) + row;
-            // TYPES: the partner's LJ type index is carried, its parameters read from LDS at
-            // evaluation (two fewer 64-bit registers per candidate in flight)
-            struct Cand { double4 p; std::conditional_t<TYPES, int, double2> lj; int slot; };
+            const v4i* nl4 = reinterpret_cast<const v4i*>(a.nl) + (size_t)g * (a.nb_cap / kChunk) * a.nlr + row;
+            struct Cand { double4 p; double2 lj; int slot; };
             auto gather = [&](int e, bool ok) {
                 const int t = ok ? (e & kHalfSlotMask) : 0;
                 Cand cd;
                 cd.p = a.pos4s[t];
-                if constexpr (TYPES) cd.lj = (unsigned)e >> kShiftBits;
+                if constexpr (TYPES) cd.lj = ljt[(unsigned)e >> kShiftBits];
                 else cd.lj = a.ljs[t];
                 cd.slot = wdel[ok ? (e >> kHalfSlotBits) & 31 : 0] + t;
                 return cd;
@@ -1350,30 +1272,16 @@ __global__ void __launch_bounds__(kHalfBlock) k_pairs_half(DirectArgs a) {
             auto eval = [&](const Cand& cd) {
                 double dx, dy, dz;
                 const double r2 = sep(cd.p, dx, dy, dz);
-                if (r2 <= a.rc2) {   // exact voxel-hash test
-                    if constexpr (TYPES) term(cd.p, ljt[cd.lj], cd.slot, dx, dy, dz, r2);
-                    else term(cd.p, cd.lj, cd.slot, dx, dy, dz, r2);
-                }
+                if (r2 <= a.rc2) term(cd.p, cd.lj, cd.slot, dx, dy, dz, r2);   // exact voxel-hash test
             };
-            walk_row(nl4, a.nlr, gstride, cnt, part, lpr, gather, eval);
+            walk_list(nl4, a.nlr, cnt, 0, 1, gather, eval);
         }
-        // the row's first lane adds the others' partials in lane order (fixed: deterministic)
-        {
-            auto acc0 = acc;
 #pragma unroll
-            for (int l = 1; l < 8; l++) {
-                if (l < lpr) {   // block-uniform
-                    // (formed here: hoisted out of the row loop, the 7 indices would be spilled)
-                    int src = lane + l;
-                    asm volatile("" : "+v"(src));
-                    acc0.fx += __shfl(acc.fx, src); acc0.fy += __shfl(acc.fy, src);
-                    acc0.fz += __shfl(acc.fz, src); acc0.dq += __shfl(acc.dq, src);
-                    acc0.e += __shfl(acc.e, src);
-                }
-            }
-            acc = acc0;
+        for (int m = 1; m < 4; m <<= 1) {
+            acc.fx += __shfl_xor(acc.fx, m); acc.fy += __shfl_xor(acc.fy, m); acc.fz += __shfl_xor(acc.fz, m);
+            acc.dq += __shfl_xor(acc.dq, m); acc.e += __shfl_xor(acc.e, m);
         }
-        if (active && part == 0) {
+        if (active && g == 0) {
             const int i = a.atom_sorted[row];
             a.e_atom[3 * i + 1] = acc.e;
             if (a.include_forces) {
@@ -1883,13 +1791,6 @@ static DirectArgs direct_args(Handle& h, const double* pos, int include_forces) 
     a.nc = make_int3(h.nc[0], h.nc[1], h.nc[2]);
     a.brute = (h.nc[0] < 3 || h.nc[1] < 3 || h.nc[2] < 3) ? 1 : 0;
     a.rc2 = h.cutoff * h.cutoff; a.rc = h.cutoff; a.alpha = h.alpha; a.ke = h.ke;
-    {
-        static const int lpr = [] {
-            const char* e = getenv("CF_HALF_LPR");
-            return e ? std::min(8, std::max(4, atoi(e))) : 8;
-        }();
-        a.half_lpr = lpr;
-    }
     a.erfc_tab = h.erfc_tab; a.erfc_scale = h.erfc_scale; a.erfc_m = h.erfc_m;
     a.erfc_tab_f = h.erfc_tab_f; a.erfc_scale_f = h.erfc_scale_f; a.erfc_m_f = h.erfc_m_f;
     a.rl2 = (h.cutoff + h.list_skin) * (h.cutoff + h.list_skin);
