@@ -335,10 +335,11 @@ __global__ void __launch_bounds__(256) k_g_spread_tile(int3 ng, int3 nb, const i
                                                        const double* __restrict__ taps, const int4* __restrict__ g0s,
                                                        double* __restrict__ grid, const int* __restrict__ xr, int W) {
     constexpr int NB3 = NS * NS * NS;
+    static_assert(NS <= 3, "tile offsets are packed in 2 bits per axis");
     constexpr int kStD = 2 * kSpPass * kSpWin > 4 * 8 * 64 ? 2 * kSpPass * kSpWin : 4 * 8 * 64;
     __shared__ __attribute__((aligned(16))) double st[kStD];   // 2 staging buffers; reused by the reduction
     __shared__ int bin_start[NB3], bin_pre[NB3 + 1], bin_db[NB3];
-    __shared__ int src[kSpMaxSrc];   // slot << 5 | source bin, of the segment's atoms that reach this tile
+    __shared__ int src[kSpMaxSrc];   // slot << 6 | (dx, dy, dz) 2 bits each, of the segment's atoms that reach this tile
     __shared__ int wcnt[4 * (kSpMaxSrc / 256)];
     __shared__ int xoff[2][kSpPass];   // offset in taps of each staged atom's x window
     // XCD-aware tile order (as in k_g_interp)
@@ -399,9 +400,11 @@ __global__ void __launch_bounds__(256) k_g_spread_tile(int3 ng, int3 nb, const i
         for (int k = 0; k < kRounds; k++) g[k] = 256 * k + t < nall ? g0s[sb[k].x] : make_int4(0, 0, 0, 0);
         bool keep[kRounds];
         unsigned long long m[kRounds];
+        int dbits[kRounds];   // the source bin's tile offsets, 2 bits per axis (NS <= 3)
 #pragma unroll
         for (int k = 0; k < kRounds; k++) {
             const int db = bin_db[sb[k].y];
+            dbits[k] = ((db >> 4) & 0x30) | ((db >> 2) & 0xC) | (db & 3);
             keep[k] = 256 * k + t < nall && (g[k].x & 7) + W > 8 * (db >> 8) &&
                       (g[k].y & 7) + W > 8 * ((db >> 4) & 15) && (g[k].z & 7) + W > 8 * (db & 15);
             m[k] = __ballot(keep[k]);
@@ -413,7 +416,7 @@ __global__ void __launch_bounds__(256) k_g_spread_tile(int3 ng, int3 nb, const i
         for (int k = 0; k < kRounds; k++) {   // kept sources in source order: (round, wave, lane)
             int off = nseg;
             for (int q = 0; q < (t >> 6); q++) off += wcnt[4 * k + q];
-            if (keep[k]) src[off + __popcll(m[k] & ((1ull << (t & 63)) - 1))] = (sb[k].x << 5) | sb[k].y;
+            if (keep[k]) src[off + __popcll(m[k] & ((1ull << (t & 63)) - 1))] = (sb[k].x << 6) | dbits[k];
             nseg += wcnt[4 * k] + wcnt[4 * k + 1] + wcnt[4 * k + 2] + wcnt[4 * k + 3];
         }
         __syncthreads();
@@ -431,9 +434,9 @@ __global__ void __launch_bounds__(256) k_g_spread_tile(int3 ng, int3 nb, const i
                 const int e = min(t + 256 * q, kPieces - 1);
                 const int a = e / 12, c = e - 12 * a, d = c >> 2, h = c & 3;
                 const int u = base + min(a, n - 1);
-                const int sb = src[u], bin = sb & 31;
-                const int db = (bin_db[bin] >> (8 - 4 * d)) & 15;
-                const int off = (sb >> 5) * kTapStride + d * kRow + 8 * db;
+                const int sb = src[u];
+                const int db = (sb >> (4 - 2 * d)) & 3;
+                const int off = (sb >> 6) * kTapStride + d * kRow + 8 * db;
                 xo_r[q] = off;
                 r[q] = *reinterpret_cast<const v2d*>(taps + off + 2 * h);
                 // DPP form: atoms past the pass end are staged as zero windows, so that the
@@ -1364,6 +1367,14 @@ __device__ __forceinline__ void fmac_row_bcast(double& acc, double x, double y) 
         asm("v_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(x), "v"(y), "i"(I));
 }
 
+// x_0 of this lane's 16-lane row (v_mov_b64 with a 64-bit DPP row_newbcast:0 source; the source
+// must be fenced by dpp_ready after its last VALU write)
+__device__ __forceinline__ double row_bcast0(double x) {
+    double r;
+    asm("v_mov_b64_dpp %0, %1 row_newbcast:0 row_mask:0xf bank_mask:0xf" : "=v"(r) : "v"(x));
+    return r;
+}
+
 // v_permlane16_swap of two copies of v: `even` = v of the even row of this lane's row pair
 // (rows 0, 2), `odd` = v of the odd row (rows 1, 3), at this lane's position in the row
 __device__ __forceinline__ void rows_even_odd(double v, double& even, double& odd) {
@@ -1462,9 +1473,7 @@ __global__ void __launch_bounds__(kInterpThreads) k_g_interp2(int3 ng, int3 nb, 
         xv = dpp_ready(xv); xd = dpp_ready(xd); yv = dpp_ready(yv); yd = dpp_ready(yd);
         const int rx = g.x & 7, ry = g.y & 7, rz = g.z & 7;
         const double* base = sg + (rx * R + ry) * R + rz + (k < W ? k : 0);
-        double t0[NJ], t1[NJ];
-#pragma unroll
-        for (int jj = 0; jj < NJ; jj++) { t0[jj] = 0; t1[jj] = 0; }
+        double t0[NJ], t1[NJ];   // row 0 initialises them (products: no zero fill)
         // x rows i in order; the NJ halo reads of row i + 1 are issued before row i's FMAs (the
         // scheduling barriers keep them there: the compiler otherwise sinks each read to its
         // first use, behind the inline asm, one LDS latency per read)
@@ -1481,10 +1490,19 @@ __global__ void __launch_bounds__(kInterpThreads) k_g_interp2(int3 ng, int3 nb, 
             constexpr int i = decltype(I)::value;
             if constexpr (i + 1 < W) load_row(i + 1, gv[(i + 1) & 1]);
             __builtin_amdgcn_sched_barrier(0);
+            if constexpr (i == 0) {
+                const double x0 = row_bcast0(xv), d0 = row_bcast0(xd);
 #pragma unroll
-            for (int jj = 0; jj < NJ; jj++) {
-                fmac_row_bcast<i>(t0[jj], xv, gv[i & 1][jj]);
-                fmac_row_bcast<i>(t1[jj], xd, gv[i & 1][jj]);
+                for (int jj = 0; jj < NJ; jj++) {
+                    t0[jj] = x0 * gv[0][jj];
+                    t1[jj] = d0 * gv[0][jj];
+                }
+            } else {
+#pragma unroll
+                for (int jj = 0; jj < NJ; jj++) {
+                    fmac_row_bcast<i>(t0[jj], xv, gv[i & 1][jj]);
+                    fmac_row_bcast<i>(t1[jj], xd, gv[i & 1][jj]);
+                }
             }
             __builtin_amdgcn_sched_barrier(0);
         });
@@ -1598,9 +1616,7 @@ __global__ void __launch_bounds__(kInterpThreads) k_g_interp4(int3 ng, int3 nb, 
         xv = dpp_ready(xv); xd = dpp_ready(xd); yv = dpp_ready(yv); yd = dpp_ready(yd);
         const int rx = g.x & 7, ry = g.y & 7, rz = g.z & 7;
         const double* base = sg + (rx * R + ry) * R + rz + (k < W ? k : 0);
-        double t0[NJ], t1[NJ];
-#pragma unroll
-        for (int jj = 0; jj < NJ; jj++) { t0[jj] = 0; t1[jj] = 0; }
+        double t0[NJ], t1[NJ];   // row 0 initialises them (products: no zero fill)
         double gv[2][NJ];
         auto load_row = [&](int i, double (&gg)[NJ]) {
 #pragma unroll
@@ -1614,10 +1630,19 @@ __global__ void __launch_bounds__(kInterpThreads) k_g_interp4(int3 ng, int3 nb, 
             constexpr int i = decltype(I)::value;
             if constexpr (i + 1 < W) load_row(i + 1, gv[(i + 1) & 1]);
             __builtin_amdgcn_sched_barrier(0);
+            if constexpr (i == 0) {
+                const double x0 = row_bcast0(xv), d0 = row_bcast0(xd);
 #pragma unroll
-            for (int jj = 0; jj < NJ; jj++) {
-                fmac_row_bcast<i>(t0[jj], xv, gv[i & 1][jj]);
-                fmac_row_bcast<i>(t1[jj], xd, gv[i & 1][jj]);
+                for (int jj = 0; jj < NJ; jj++) {
+                    t0[jj] = x0 * gv[0][jj];
+                    t1[jj] = d0 * gv[0][jj];
+                }
+            } else {
+#pragma unroll
+                for (int jj = 0; jj < NJ; jj++) {
+                    fmac_row_bcast<i>(t0[jj], xv, gv[i & 1][jj]);
+                    fmac_row_bcast<i>(t1[jj], xd, gv[i & 1][jj]);
+                }
             }
             __builtin_amdgcn_sched_barrier(0);
         });
