@@ -178,7 +178,10 @@ constexpr int kRow = 24;
 constexpr int kTapStride = 3 * kRow;
 constexpr int kOtWaves = 4;     // bins per 256-thread block: one wave per bin, no block barriers
 constexpr int kOtLds = 128;     // members per bin staged in LDS (denser bins read global memory)
-constexpr int kOtChunk = 8;     // atoms whose tap rows are assembled in LDS at a time
+#ifndef CF_OT_CHUNK
+#define CF_OT_CHUNK 8   // build-time knob for A/B builds (-DCF_OT_CHUNK=16)
+#endif
+constexpr int kOtChunk = CF_OT_CHUNK;   // atoms whose tap rows are assembled in LDS at a time
 
 // LDS written by some lanes of a wave, then read by others of the same wave
 __device__ __forceinline__ void wave_sync() {
