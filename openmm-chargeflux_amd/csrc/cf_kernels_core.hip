@@ -1310,37 +1310,34 @@ __global__ void __launch_bounds__(kHalfBlock) k_pairs_half(DirectArgs a) {
 }
 
 // sorted slot s: the j-side sums of the 18 windows holding s (those of the cells at x offset
-// 0 and -1 from its own), converted from fixed point once (k_excl, before the exclusions)
-__device__ __forceinline__ void half_window_sums(const DirectArgs& a, int s, double3& f, double& dq) {
+// 0 and -1 from its own), as 64-bit fixed-point integers, over windows part, part + kExclLanes,
+// ... (k_excl's lanes of one atom; integer sums, so the split does not change the result).
+// Every offset load of the lane in flight, then every window load.
+constexpr int kExclLanes = 4;
+__device__ __forceinline__ void half_window_part(const DirectArgs& a, int s, int part, long long (&w)[4]) {
     const int key = a.key_s[s];
     const int3 nc = a.nc;
     const int cz = key % nc.z, cy = (key / nc.z) % nc.y, cx = key / (nc.y * nc.z);
     const int jj = s - a.cstart[key];
-    long long sx = 0, sy = 0, sz = 0, sq = 0;
-    // batches of kBatch windows: every offset load of a batch in flight, then every window
-    // load (two memory latencies per batch instead of two per window; integer sums, so the
-    // order does not change the result)
-    constexpr int kBatch = 6;
-    static_assert(kHalfWin % kBatch == 0, "window batches");
+    constexpr int kPer = (kHalfWin + kExclLanes - 1) / kExclLanes;
+    int b[kPer], slot[kPer];
 #pragma unroll
-    for (int k0 = 0; k0 < kHalfWin; k0 += kBatch) {
-        int b[kBatch], slot[kBatch];
+    for (int u = 0; u < kPer; u++) {
+        const int k = min(part + kExclLanes * u, kHalfWin - 1);
+        const int3 o = half_offset(k);
+        b[u] = (wrap_cell(cx - o.x, nc.x) * nc.y + wrap_cell(cy - o.y, nc.y)) * nc.z + wrap_cell(cz - o.z, nc.z);
+        slot[u] = a.win_woff[b[u] * kHalfWin + k] + jj;
+    }
+    ulonglong4 v[kPer];
 #pragma unroll
-        for (int u = 0; u < kBatch; u++) {
-            const int3 o = half_offset(k0 + u);
-            b[u] = (wrap_cell(cx - o.x, nc.x) * nc.y + wrap_cell(cy - o.y, nc.y)) * nc.z + wrap_cell(cz - o.z, nc.z);
-            slot[u] = a.win_woff[b[u] * kHalfWin + k0 + u] + jj;
-        }
-        ulonglong4 v[kBatch];
+    for (int u = 0; u < kPer; u++) v[u] = reinterpret_cast<const ulonglong4*>(a.win_out)[(size_t)b[u] * kHalfMaxWin + slot[u]];
+    w[0] = w[1] = w[2] = w[3] = 0;
 #pragma unroll
-        for (int u = 0; u < kBatch; u++) v[u] = reinterpret_cast<const ulonglong4*>(a.win_out)[(size_t)b[u] * kHalfMaxWin + slot[u]];
-#pragma unroll
-        for (int u = 0; u < kBatch; u++) {
-            sx += (long long)v[u].x; sy += (long long)v[u].y; sz += (long long)v[u].z; sq += (long long)v[u].w;
+    for (int u = 0; u < kPer; u++) {
+        if (part + kExclLanes * u < kHalfWin) {
+            w[0] += (long long)v[u].x; w[1] += (long long)v[u].y; w[2] += (long long)v[u].z; w[3] += (long long)v[u].w;
         }
     }
-    f = make_double3((double)sx * kFixInv, (double)sy * kFixInv, (double)sz * kFixInv);
-    dq = (double)sq * kFixInv;
 }
 
 // ---------------------------------------------------------------------------------
@@ -1471,9 +1468,14 @@ __device__ __forceinline__ void pair_rescan(const DirectArgs& a, const double* t
 // 4c: per list row (owned atom): an atom whose neighbour list overflowed (denser than
 //     planned; k_pairs skipped it) first rescans its cells, then the exclusion correction +
 //     self term (one launch for both: the overflow check costs 4 coalesced count loads)
+// kExclLanes lanes per atom: on the half-list path the 18 window reads of an atom are spread over
+// them (integer partial sums: the same bits as one lane summing all 18), so an atom waits on ~5
+// loads instead of three batches of 6; the first lane then applies the exclusion correction
+
 __global__ void __launch_bounds__(256) k_excl(DirectArgs a) {
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= a.nlr) return;
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    const int c = t / kExclLanes, part = t % kExclLanes;
+    if (c >= a.nlr) return;   // whole lane groups
     const int s = own_slot(a, c);
     const int i = a.atom_sorted[s];
     bool over = false;
@@ -1483,18 +1485,25 @@ __global__ void __launch_bounds__(256) k_excl(DirectArgs a) {
 #pragma unroll
         for (int g = 0; g < kSeg; g++) over = over || a.nl_cnt[(size_t)g * a.nlr + c] > a.nb_cap;
     }
+    if (a.half && !over && a.include_forces) {    // the partner-side sums of the half list
+        long long w[4];
+        half_window_part(a, s, part, w);
+#pragma unroll
+        for (int m = 1; m < kExclLanes; m <<= 1) {
+#pragma unroll
+            for (int k = 0; k < 4; k++) w[k] += __shfl_xor(w[k], m);
+        }
+        if (part != 0) return;
+        excl_atom(a, i, make_double3((double)w[0] * kFixInv, (double)w[1] * kFixInv, (double)w[2] * kFixInv),
+                  (double)w[3] * kFixInv);
+        return;
+    }
+    if (part != 0) return;
     if (over) {   // rare: erfcx table read from global memory
         pair_rescan(a, a.erfc_tab, s, i);
         if (!a.half && a.fallback) atomicAdd((unsigned long long*)&a.fallback[1], 1ull);
     }
-    if (a.half && !over && a.include_forces) {    // the partner-side sums of the half list
-        double3 f;
-        double dq;
-        half_window_sums(a, s, f, dq);
-        excl_atom(a, i, f, dq);
-    } else {
-        excl_atom(a, i);
-    }
+    excl_atom(a, i);
 }
 
 // ---------------------------------------------------------------------------------
@@ -1867,7 +1876,7 @@ void launch_direct(Handle& h, const double* pos, int include_forces) {
 // overflowed atoms' rescan + the exclusion correction (after launch_direct)
 void launch_direct_finish(Handle& h, const double* pos, int include_forces) {
     DirectArgs a = direct_args(h, pos, include_forces);
-    hipLaunchKernelGGL(k_excl, dim3(nblk(a.nlr, 256)), dim3(256), 0, h.stream, a);
+    hipLaunchKernelGGL(k_excl, dim3(nblk(a.nlr * kExclLanes, 256)), dim3(256), 0, h.stream, a);
 }
 
 void launch_recip_add(Handle& h) {
