@@ -1310,34 +1310,37 @@ __global__ void __launch_bounds__(kHalfBlock) k_pairs_half(DirectArgs a) {
 }
 
 // sorted slot s: the j-side sums of the 18 windows holding s (those of the cells at x offset
-// 0 and -1 from its own), as 64-bit fixed-point integers, over windows part, part + kExclLanes,
-// ... (k_excl's lanes of one atom; integer sums, so the split does not change the result).
-// Every offset load of the lane in flight, then every window load.
-constexpr int kExclLanes = 4;
-__device__ __forceinline__ void half_window_part(const DirectArgs& a, int s, int part, long long (&w)[4]) {
+// 0 and -1 from its own), converted from fixed point once (k_excl, before the exclusions)
+__device__ __forceinline__ void half_window_sums(const DirectArgs& a, int s, double3& f, double& dq) {
     const int key = a.key_s[s];
     const int3 nc = a.nc;
     const int cz = key % nc.z, cy = (key / nc.z) % nc.y, cx = key / (nc.y * nc.z);
     const int jj = s - a.cstart[key];
-    constexpr int kPer = (kHalfWin + kExclLanes - 1) / kExclLanes;
-    int b[kPer], slot[kPer];
+    long long sx = 0, sy = 0, sz = 0, sq = 0;
+    // batches of kBatch windows: every offset load of a batch in flight, then every window
+    // load (two memory latencies per batch instead of two per window; integer sums, so the
+    // order does not change the result)
+    constexpr int kBatch = 6;
+    static_assert(kHalfWin % kBatch == 0, "window batches");
 #pragma unroll
-    for (int u = 0; u < kPer; u++) {
-        const int k = min(part + kExclLanes * u, kHalfWin - 1);
-        const int3 o = half_offset(k);
-        b[u] = (wrap_cell(cx - o.x, nc.x) * nc.y + wrap_cell(cy - o.y, nc.y)) * nc.z + wrap_cell(cz - o.z, nc.z);
-        slot[u] = a.win_woff[b[u] * kHalfWin + k] + jj;
-    }
-    ulonglong4 v[kPer];
+    for (int k0 = 0; k0 < kHalfWin; k0 += kBatch) {
+        int b[kBatch], slot[kBatch];
 #pragma unroll
-    for (int u = 0; u < kPer; u++) v[u] = reinterpret_cast<const ulonglong4*>(a.win_out)[(size_t)b[u] * kHalfMaxWin + slot[u]];
-    w[0] = w[1] = w[2] = w[3] = 0;
+        for (int u = 0; u < kBatch; u++) {
+            const int3 o = half_offset(k0 + u);
+            b[u] = (wrap_cell(cx - o.x, nc.x) * nc.y + wrap_cell(cy - o.y, nc.y)) * nc.z + wrap_cell(cz - o.z, nc.z);
+            slot[u] = a.win_woff[b[u] * kHalfWin + k0 + u] + jj;
+        }
+        ulonglong4 v[kBatch];
 #pragma unroll
-    for (int u = 0; u < kPer; u++) {
-        if (part + kExclLanes * u < kHalfWin) {
-            w[0] += (long long)v[u].x; w[1] += (long long)v[u].y; w[2] += (long long)v[u].z; w[3] += (long long)v[u].w;
+        for (int u = 0; u < kBatch; u++) v[u] = reinterpret_cast<const ulonglong4*>(a.win_out)[(size_t)b[u] * kHalfMaxWin + slot[u]];
+#pragma unroll
+        for (int u = 0; u < kBatch; u++) {
+            sx += (long long)v[u].x; sy += (long long)v[u].y; sz += (long long)v[u].z; sq += (long long)v[u].w;
         }
     }
+    f = make_double3((double)sx * kFixInv, (double)sy * kFixInv, (double)sz * kFixInv);
+    dq = (double)sq * kFixInv;
 }
 
 // ---------------------------------------------------------------------------------
@@ -1468,14 +1471,9 @@ __device__ __forceinline__ void pair_rescan(const DirectArgs& a, const double* t
 // 4c: per list row (owned atom): an atom whose neighbour list overflowed (denser than
 //     planned; k_pairs skipped it) first rescans its cells, then the exclusion correction +
 //     self term (one launch for both: the overflow check costs 4 coalesced count loads)
-// kExclLanes lanes per atom: on the half-list path the 18 window reads of an atom are spread over
-// them (integer partial sums: the same bits as one lane summing all 18), so an atom waits on ~5
-// loads instead of three batches of 6; the first lane then applies the exclusion correction
-
 __global__ void __launch_bounds__(256) k_excl(DirectArgs a) {
-    const int t = blockIdx.x * blockDim.x + threadIdx.x;
-    const int c = t / kExclLanes, part = t % kExclLanes;
-    if (c >= a.nlr) return;   // whole lane groups
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= a.nlr) return;
     const int s = own_slot(a, c);
     const int i = a.atom_sorted[s];
     bool over = false;
@@ -1485,25 +1483,18 @@ __global__ void __launch_bounds__(256) k_excl(DirectArgs a) {
 #pragma unroll
         for (int g = 0; g < kSeg; g++) over = over || a.nl_cnt[(size_t)g * a.nlr + c] > a.nb_cap;
     }
-    if (a.half && !over && a.include_forces) {    // the partner-side sums of the half list
-        long long w[4];
-        half_window_part(a, s, part, w);
-#pragma unroll
-        for (int m = 1; m < kExclLanes; m <<= 1) {
-#pragma unroll
-            for (int k = 0; k < 4; k++) w[k] += __shfl_xor(w[k], m);
-        }
-        if (part != 0) return;
-        excl_atom(a, i, make_double3((double)w[0] * kFixInv, (double)w[1] * kFixInv, (double)w[2] * kFixInv),
-                  (double)w[3] * kFixInv);
-        return;
-    }
-    if (part != 0) return;
     if (over) {   // rare: erfcx table read from global memory
         pair_rescan(a, a.erfc_tab, s, i);
         if (!a.half && a.fallback) atomicAdd((unsigned long long*)&a.fallback[1], 1ull);
     }
-    excl_atom(a, i);
+    if (a.half && !over && a.include_forces) {    // the partner-side sums of the half list
+        double3 f;
+        double dq;
+        half_window_sums(a, s, f, dq);
+        excl_atom(a, i, f, dq);
+    } else {
+        excl_atom(a, i);
+    }
 }
 
 // ---------------------------------------------------------------------------------
@@ -1585,6 +1576,7 @@ __global__ void __launch_bounds__(kNopbcTile) k_nopbc(int n, int lo, int hi, int
 //    re-arms the multi-rank x-slab and (last_block_done) the ticket.
 // ---------------------------------------------------------------------------------
 constexpr int kEChunk = 256;
+constexpr int kALanes = 4;   // k_assemble_energy lanes per x-atom (cf_api.hip sizes e_part for 256 / 4 atoms per block)
 
 __device__ __forceinline__ void block_sum3(double& a0, double& a1, double& a2, double (*red)[256]) {
     red[0][threadIdx.x] = a0; red[1][threadIdx.x] = a1; red[2][threadIdx.x] = a2;
@@ -1612,25 +1604,20 @@ __global__ void __launch_bounds__(kEChunk) k_assemble_energy(int lo, int hi, con
                                                              int* __restrict__ half_flag,
                                                              long long* __restrict__ fallback) {
     __shared__ double red[3][256];
-    const int b = lo + blockIdx.x * kEChunk + threadIdx.x;
+    // kALanes lanes per x-atom: lane `sub` gathers entries cs[b] + part, + kALanes, ... (in
+    // batches of 4, every load in flight together); the lanes' partial sums are combined by an
+    // xor butterfly (the same bits in every lane: deterministic), then the first lane adds them
+    const int t = blockIdx.x * kEChunk + threadIdx.x;
+    const int b = lo + t / kALanes, sub = t % kALanes;
     double a0 = 0, a1 = 0, a2 = 0;
-    if (b < hi) {
+    if (b < hi) {   // whole lane groups
         if (out) {
-            double fx = f_part[3 * b], fy = f_part[3 * b + 1], fz = f_part[3 * b + 2];
-            if (f_rec) {   // reciprocal part from the second stream, added as k_g_interp adds it
-                const double4 r = f_rec[b];
-                fx = fma(r.w * gscale.x, r.x, fx);
-                fy = fma(r.w * gscale.y, r.y, fy);
-                fz = fma(r.w * gscale.z, r.z, fz);
-            }
-            // entries in batches of 4: the entry loads, then their dE/dq and dq/dx gathers, all
-            // in flight together (two memory latencies per batch, not per entry); the sums keep
-            // the entry order
+            double cx = 0, cy = 0, cz = 0;
             const int k1 = cs[b + 1];
-            for (int k0 = cs[b]; k0 < k1; k0 += 4) {
+            for (int k0 = cs[b] + sub; k0 < k1; k0 += 4 * kALanes) {
                 int2 en[4];
 #pragma unroll
-                for (int u = 0; u < 4; u++) en[u] = ce[min(k0 + u, k1 - 1)];
+                for (int u = 0; u < 4; u++) en[u] = ce[min(k0 + kALanes * u, k1 - 1)];
                 double g[4], d[4][3];
 #pragma unroll
                 for (int u = 0; u < 4; u++) {
@@ -1643,18 +1630,31 @@ __global__ void __launch_bounds__(kEChunk) k_assemble_energy(int lo, int hi, con
                 }
 #pragma unroll
                 for (int u = 0; u < 4; u++) {
-                    if (k0 + u < k1) {
-                        fx -= g[u] * d[u][0];
-                        fy -= g[u] * d[u][1];
-                        fz -= g[u] * d[u][2];
+                    if (k0 + kALanes * u < k1) {
+                        cx = fma(g[u], d[u][0], cx);
+                        cy = fma(g[u], d[u][1], cy);
+                        cz = fma(g[u], d[u][2], cz);
                     }
                 }
             }
-            out[3 * b] += fx;
-            out[3 * b + 1] += fy;
-            out[3 * b + 2] += fz;
+#pragma unroll
+            for (int m = 1; m < kALanes; m <<= 1) {
+                cx += __shfl_xor(cx, m); cy += __shfl_xor(cy, m); cz += __shfl_xor(cz, m);
+            }
+            if (sub == 0) {
+                double fx = f_part[3 * b], fy = f_part[3 * b + 1], fz = f_part[3 * b + 2];
+                if (f_rec) {   // reciprocal part from the second stream, added as k_g_interp adds it
+                    const double4 r = f_rec[b];
+                    fx = fma(r.w * gscale.x, r.x, fx);
+                    fy = fma(r.w * gscale.y, r.y, fy);
+                    fz = fma(r.w * gscale.z, r.z, fz);
+                }
+                out[3 * b] += fx - cx;
+                out[3 * b + 1] += fy - cy;
+                out[3 * b + 2] += fz - cz;
+            }
         }
-        a0 = e_atom[3 * b]; a1 = e_atom[3 * b + 1]; a2 = e_atom[3 * b + 2];
+        if (sub == 0) { a0 = e_atom[3 * b]; a1 = e_atom[3 * b + 1]; a2 = e_atom[3 * b + 2]; }
     }
     block_sum3(a0, a1, a2, red);
     if (threadIdx.x == 0) {   // agent-scope stores, read back by the last block (last_block_done)
@@ -1876,7 +1876,7 @@ void launch_direct(Handle& h, const double* pos, int include_forces) {
 // overflowed atoms' rescan + the exclusion correction (after launch_direct)
 void launch_direct_finish(Handle& h, const double* pos, int include_forces) {
     DirectArgs a = direct_args(h, pos, include_forces);
-    hipLaunchKernelGGL(k_excl, dim3(nblk(a.nlr * kExclLanes, 256)), dim3(256), 0, h.stream, a);
+    hipLaunchKernelGGL(k_excl, dim3(nblk(a.nlr, 256)), dim3(256), 0, h.stream, a);
 }
 
 void launch_recip_add(Handle& h) {
@@ -1896,7 +1896,7 @@ void launch_nopbc(Handle& h, const double* pos, int include_forces, int include_
 void launch_assemble_energy(Handle& h, double* forces_out, int include_energy, double* energy_out) {
     const int nown = std::max(0, h.hi - h.lo);
     int nrec = (h.pbc && include_energy && h.rank == 0) ? h.e_rec_nblk : 0;
-    const int nparts = std::max(1, nblk(nown, kEChunk));
+    const int nparts = std::max(1, nblk(nown * kALanes, kEChunk));
     hipLaunchKernelGGL(k_assemble_energy, dim3(nparts), dim3(kEChunk), 0, h.stream, h.lo, h.hi, h.ccsr_start,
                        h.ccsr_ent, h.dedq, h.dqdx, h.f_part, forces_out, h.rec_split ? h.dedq_rec : nullptr,
                        h.rec_split ? reinterpret_cast<const double4*>(h.f_rec) : nullptr,
