@@ -554,7 +554,7 @@ CF_EXPORT int cf_create(const cf_params* p, const cf_options* opt, cf_handle** o
         h.e_atom = dalloc<double>(H, (size_t)3 * n);
         h.f_part = dalloc<double>(H, (size_t)3 * n);
         h.terms_dev = dalloc<double>(H, 4);
-        h.e_part = dalloc<double>(H, 3 * ((size_t)n / 64 + 2));   // one partial per k_assemble_energy block (64 atoms)
+        h.e_part = dalloc<double>(H, 3 * ((size_t)n / 256 + 2));
         h.energy_dev = dalloc<double>(H, 1);
         h.e_ticket = dalloc<int>(H, cf::kNumTickets);
         check_hip(hipMemset(h.e_ticket, 0, sizeof(int) * cf::kNumTickets), "memset");

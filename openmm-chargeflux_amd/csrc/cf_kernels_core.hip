@@ -1576,7 +1576,6 @@ __global__ void __launch_bounds__(kNopbcTile) k_nopbc(int n, int lo, int hi, int
 //    re-arms the multi-rank x-slab and (last_block_done) the ticket.
 // ---------------------------------------------------------------------------------
 constexpr int kEChunk = 256;
-constexpr int kALanes = 4;   // k_assemble_energy lanes per x-atom (cf_api.hip sizes e_part for 256 / 4 atoms per block)
 
 __device__ __forceinline__ void block_sum3(double& a0, double& a1, double& a2, double (*red)[256]) {
     red[0][threadIdx.x] = a0; red[1][threadIdx.x] = a1; red[2][threadIdx.x] = a2;
@@ -1604,20 +1603,25 @@ __global__ void __launch_bounds__(kEChunk) k_assemble_energy(int lo, int hi, con
                                                              int* __restrict__ half_flag,
                                                              long long* __restrict__ fallback) {
     __shared__ double red[3][256];
-    // kALanes lanes per x-atom: lane `sub` gathers entries cs[b] + part, + kALanes, ... (in
-    // batches of 4, every load in flight together); the lanes' partial sums are combined by an
-    // xor butterfly (the same bits in every lane: deterministic), then the first lane adds them
-    const int t = blockIdx.x * kEChunk + threadIdx.x;
-    const int b = lo + t / kALanes, sub = t % kALanes;
+    const int b = lo + blockIdx.x * kEChunk + threadIdx.x;
     double a0 = 0, a1 = 0, a2 = 0;
-    if (b < hi) {   // whole lane groups
+    if (b < hi) {
         if (out) {
-            double cx = 0, cy = 0, cz = 0;
+            double fx = f_part[3 * b], fy = f_part[3 * b + 1], fz = f_part[3 * b + 2];
+            if (f_rec) {   // reciprocal part from the second stream, added as k_g_interp adds it
+                const double4 r = f_rec[b];
+                fx = fma(r.w * gscale.x, r.x, fx);
+                fy = fma(r.w * gscale.y, r.y, fy);
+                fz = fma(r.w * gscale.z, r.z, fz);
+            }
+            // entries in batches of 4: the entry loads, then their dE/dq and dq/dx gathers, all
+            // in flight together (two memory latencies per batch, not per entry); the sums keep
+            // the entry order
             const int k1 = cs[b + 1];
-            for (int k0 = cs[b] + sub; k0 < k1; k0 += 4 * kALanes) {
+            for (int k0 = cs[b]; k0 < k1; k0 += 4) {
                 int2 en[4];
 #pragma unroll
-                for (int u = 0; u < 4; u++) en[u] = ce[min(k0 + kALanes * u, k1 - 1)];
+                for (int u = 0; u < 4; u++) en[u] = ce[min(k0 + u, k1 - 1)];
                 double g[4], d[4][3];
 #pragma unroll
                 for (int u = 0; u < 4; u++) {
@@ -1630,31 +1634,18 @@ __global__ void __launch_bounds__(kEChunk) k_assemble_energy(int lo, int hi, con
                 }
 #pragma unroll
                 for (int u = 0; u < 4; u++) {
-                    if (k0 + kALanes * u < k1) {
-                        cx = fma(g[u], d[u][0], cx);
-                        cy = fma(g[u], d[u][1], cy);
-                        cz = fma(g[u], d[u][2], cz);
+                    if (k0 + u < k1) {
+                        fx -= g[u] * d[u][0];
+                        fy -= g[u] * d[u][1];
+                        fz -= g[u] * d[u][2];
                     }
                 }
             }
-#pragma unroll
-            for (int m = 1; m < kALanes; m <<= 1) {
-                cx += __shfl_xor(cx, m); cy += __shfl_xor(cy, m); cz += __shfl_xor(cz, m);
-            }
-            if (sub == 0) {
-                double fx = f_part[3 * b], fy = f_part[3 * b + 1], fz = f_part[3 * b + 2];
-                if (f_rec) {   // reciprocal part from the second stream, added as k_g_interp adds it
-                    const double4 r = f_rec[b];
-                    fx = fma(r.w * gscale.x, r.x, fx);
-                    fy = fma(r.w * gscale.y, r.y, fy);
-                    fz = fma(r.w * gscale.z, r.z, fz);
-                }
-                out[3 * b] += fx - cx;
-                out[3 * b + 1] += fy - cy;
-                out[3 * b + 2] += fz - cz;
-            }
+            out[3 * b] += fx;
+            out[3 * b + 1] += fy;
+            out[3 * b + 2] += fz;
         }
-        if (sub == 0) { a0 = e_atom[3 * b]; a1 = e_atom[3 * b + 1]; a2 = e_atom[3 * b + 2]; }
+        a0 = e_atom[3 * b]; a1 = e_atom[3 * b + 1]; a2 = e_atom[3 * b + 2];
     }
     block_sum3(a0, a1, a2, red);
     if (threadIdx.x == 0) {   // agent-scope stores, read back by the last block (last_block_done)
@@ -1896,7 +1887,7 @@ void launch_nopbc(Handle& h, const double* pos, int include_forces, int include_
 void launch_assemble_energy(Handle& h, double* forces_out, int include_energy, double* energy_out) {
     const int nown = std::max(0, h.hi - h.lo);
     int nrec = (h.pbc && include_energy && h.rank == 0) ? h.e_rec_nblk : 0;
-    const int nparts = std::max(1, nblk(nown * kALanes, kEChunk));
+    const int nparts = std::max(1, nblk(nown, kEChunk));
     hipLaunchKernelGGL(k_assemble_energy, dim3(nparts), dim3(kEChunk), 0, h.stream, h.lo, h.hi, h.ccsr_start,
                        h.ccsr_ent, h.dedq, h.dqdx, h.f_part, forces_out, h.rec_split ? h.dedq_rec : nullptr,
                        h.rec_split ? reinterpret_cast<const double4*>(h.f_rec) : nullptr,
