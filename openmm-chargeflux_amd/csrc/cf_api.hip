@@ -716,6 +716,7 @@ CF_EXPORT int cf_set_neighbor_skin(cf_handle* H, double skin) {
         check_hip(hipStreamSynchronize(h.stream), "stream sync");
         h.skin = skin;
         h.list_valid = false;
+        h.alloc_epoch++;   // captured graphs baked in the old list state (pos_ref, capacity): re-capture
         if (!h.pbc) return;
         alloc_nlist(H, skin);
         if (skin > 0 && !h.pos_ref) h.pos_ref = dalloc<double>(H, (size_t)3 * h.n);
@@ -772,6 +773,7 @@ CF_EXPORT int cf_update_parameters(cf_handle* H, const cf_params* p) {
             }
         }
         h.list_valid = false;   // sorted LJ / types are refreshed by the next list build
+        h.alloc_epoch++;        // lj_ntypes / typ_s are kernel arguments of captured graphs: re-capture
     });
 }
 
@@ -959,6 +961,12 @@ static bool overlap_ok(const cf::Handle& h, int flags) {
 static void launch_full(cf_handle* H, const double* pos_dev, int flags, bool reusable, double* forces_dev,
                         double* energy_dev) {
     cf::Handle& h = H->h;
+    // a launch that throws (capture or launch failure) must not leave the handle looking like a
+    // begun evaluation (every later call would fail with CF_ERR_STATE) or on the second stream
+    struct Restore {
+        cf::Handle& h; hipStream_t s;
+        ~Restore() { h.pending_flags = -1; h.stream = s; }
+    } restore{h, h.stream};
     if (!overlap_ok(h, flags)) {
         h.rec_split = false;
         h.pending_flags = flags;
@@ -1118,6 +1126,7 @@ struct GraphCache {
     hipStream_t cap = nullptr;
     hipGraphExec_t exec[SEG_COUNT] = {};
     GraphKey key[SEG_COUNT];
+    bool rec_split[SEG_COUNT] = {};   // Handle::rec_split as the captured launches leave it (restored on replay)
     int64_t captures = 0, replays = 0;
     void drop(int s) {
         if (exec[s]) (void)hipGraphExecDestroy(exec[s]);
@@ -1182,8 +1191,10 @@ static void run_segment(cf_handle* H, GraphCache* g, int seg, const GraphKey& k,
         (void)hipGraphDestroy(graph);
         check_hip(e, "hipGraphInstantiate");
         g->key[seg] = k;
+        g->rec_split[seg] = h.rec_split;
         g->captures++;
     } else {
+        h.rec_split = g->rec_split[seg];   // what the replayed launches leave in dedq / dedq_rec
         g->replays++;
     }
     check_hip(hipGraphLaunch(g->exec[seg], h.stream), "hipGraphLaunch");
@@ -1266,7 +1277,8 @@ static void run_direct(cf_handle* H) {
     cf::Handle& h = H->h;
     if (h.direct_done) return;
     h.direct_done = true;
-    run_segment(H, graph_active(H), SEG_DIRECT, make_key(h, H->pos_pending, nullptr, nullptr, h.pending_flags, false, nullptr),
+    run_segment(H, graph_active(H), SEG_DIRECT,
+                make_key(h, H->pos_pending, nullptr, nullptr, h.pending_flags, false, h.pbc ? H->box9_last : nullptr),
                 [&] { launch_direct(H); });
 }
 

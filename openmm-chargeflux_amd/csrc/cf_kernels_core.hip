@@ -1077,7 +1077,7 @@ __device__ __forceinline__ int wrap_cell(int v, int n) { return v < 0 ? v + n : 
 // point (an fp32 value times 2^34 is exact in fp64)
 // TRIC: reduced triclinic box (the box-vector minimum image, min_image); else the per-axis form
 template <bool TYPES, bool MIXED, bool TRIC>
-__global__ void __launch_bounds__(kHalfBlock) k_pairs_half(DirectArgs a) {
+__global__ void __launch_bounds__(kHalfBlock) CF_LDS_UNPAIRED k_pairs_half(DirectArgs a) {
     __shared__ double tab[MIXED ? 1 : kErfcMaxM * (kErfcDeg + 1)];
     __shared__ float tabf[MIXED ? kErfcMaxMF * (kErfcDegF + 1) : 1];
     __shared__ double2 ljt[(TYPES && !MIXED) ? kMaxLjTypes : 1];

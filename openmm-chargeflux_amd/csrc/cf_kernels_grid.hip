@@ -334,7 +334,7 @@ __device__ __forceinline__ void fma8_row_bcast(double (&acc)[8], double xv, doub
 }
 
 template <int NS, int kSpPass, bool DPP>
-__global__ void __launch_bounds__(256) k_g_spread_tile(int3 ng, int3 nb, const int* __restrict__ start,
+__global__ void __launch_bounds__(256) CF_LDS_UNPAIRED k_g_spread_tile(int3 ng, int3 nb, const int* __restrict__ start,
                                                        const double* __restrict__ taps, const int4* __restrict__ g0s,
                                                        double* __restrict__ grid, const int* __restrict__ xr, int W) {
     constexpr int NB3 = NS * NS * NS;
@@ -1423,7 +1423,7 @@ __device__ __forceinline__ double half_sum4(double pv, double px, double py, dou
 // per (j, k), then pot / gradient by y and z as in k_g_interp; the four sums per half reduced
 // in a fixed order; lanes (h, 0..3) store.
 template <int W>
-__global__ void __launch_bounds__(kInterpThreads) k_g_interp2(int3 ng, int3 nb, const int* __restrict__ start,
+__global__ void __launch_bounds__(kInterpThreads) CF_LDS_UNPAIRED k_g_interp2(int3 ng, int3 nb, const int* __restrict__ start,
                                                               const int4* __restrict__ g0s,
                                                               const double4* __restrict__ srec, double beta,
                                                               double3 gscale, const double* __restrict__ G, int lo,
@@ -1570,7 +1570,7 @@ __device__ __forceinline__ double row_sum4(double pv, double px, double py, doub
 // by 8 gives the jg = 0 lanes their z tap); y taps 2n + jg in lane (jg, n < NJ), broadcast to the
 // lanes of each half-row by row_newbcast with a bank mask.  Otherwise as k_g_interp2.
 template <int W>
-__global__ void __launch_bounds__(kInterpThreads) k_g_interp4(int3 ng, int3 nb, const int* __restrict__ start,
+__global__ void __launch_bounds__(kInterpThreads) CF_LDS_UNPAIRED k_g_interp4(int3 ng, int3 nb, const int* __restrict__ start,
                                                               const int4* __restrict__ g0s,
                                                               const double4* __restrict__ srec, double beta,
                                                               double3 gscale, const double* __restrict__ G, int lo,

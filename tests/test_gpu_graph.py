@@ -105,10 +105,11 @@ def test_graph_segments_of_a_decomposed_step_are_bitwise_eager(world):
         x = pt.clone()
         rng = np.random.default_rng(8)
         out = []
-        for _ in range(5):
+        for s in range(6):
             f.zero_()
+            b_s = box if s < 3 else box * 1.01   # the box changes partway (every segment must re-capture)
             for k in ks:
-                k.begin(x, box, True, True)
+                k.begin(x, b_s, True, True)
             total = sum(bufs[1:], bufs[0].clone())
             for b in bufs:
                 b.copy_(total)
@@ -152,3 +153,46 @@ def test_graph_recaptures_after_list_reallocation():
         assert ea == eb and np.array_equal(fa, fb)
     caps1, reps = graph.graph_stats()
     assert caps1 > caps0 and reps >= 2, (caps0, caps1, reps)
+
+
+def test_graph_recaptures_after_parameter_update():
+    """cf_update_parameters changes launch arguments baked into captured graphs (the number of LJ
+    types staged in LDS, or no types at all): the next call must re-capture, not replay."""
+    from tests.test_gpu_update import _perturb
+    system, force, pos, box = ts.water_box(2000, cutoff=1.0, ewald_tol=1e-4, every_bond_angle=5)
+    stream = torch.cuda.current_stream().cuda_stream
+    mk = lambda: HipCalcCoulForceKernel(stream=stream, kspace_algo=2).initialize(system, force)
+    eager, graph = mk(), mk()
+    for k in (eager, graph):
+        k.set_neighbor_skin(0.1)
+    graph.set_graph(True)
+    a = _traj(eager, pos, box, 3)
+    b = _traj(graph, pos, box, 3)
+    for distinct in (False, True):   # new LJ parameters; then > 64 LJ types (per-atom LJ gathers)
+        _perturb(force, np.random.default_rng(5), distinct)
+        for k in (eager, graph):
+            k.copyParametersToContext(force)
+        a += _traj(eager, pos, box, 3)
+        b += _traj(graph, pos, box, 3)
+    for (ea, fa), (eb, fb) in zip(a, b):
+        assert ea == eb and np.array_equal(fa, fb)
+
+
+def test_graph_replay_restores_reciprocal_dedq_split():
+    """A replayed forces graph leaves the reciprocal dE/dq in its own buffer (two streams): the
+    handle must know that after replaying it behind an energy-only capture (cf_get_dedq)."""
+    system, force, pos, box = ts.make("C2")
+    stream = torch.cuda.current_stream().cuda_stream
+    k = HipCalcCoulForceKernel(stream=stream, kspace_algo=2).initialize(system, force).set_graph(True)
+    ref = HipCalcCoulForceKernel(stream=stream, kspace_algo=2).initialize(system, force)
+    pt = torch.tensor(pos, dtype=torch.float64, device="cuda")
+    ref.execute_host(pos, box)
+    dq_ref = ref.dedq()
+    f = torch.zeros_like(pt)
+    e = torch.zeros(1, dtype=torch.float64, device="cuda")
+    k.execute_device(pt, box, True, True, f, e)    # capture: forces
+    k.execute_device(pt, box, False, True, None, e)  # capture: energy only
+    k.execute_device(pt, box, True, True, f, e)    # replay: forces
+    torch.cuda.synchronize()
+    assert k.graph_stats()[1] >= 1
+    assert np.array_equal(k.dedq(), dq_ref)
