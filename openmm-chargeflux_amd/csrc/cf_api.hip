@@ -201,7 +201,7 @@ void set_cells(cf_handle* H, const double L[3]) {
     // cells per axis), cells small enough for the kernel's LDS window (18 cells <= 4096 atoms,
     // with a margin for density variation: k_pairs_half flags the rare evaluation that does not
     // fit and k_excl then rescans) and sorted slots that fit the entry's 21 bits
-    const bool no_half = getenv("CF_HALF") && std::string(getenv("CF_HALF")) == "0";   // A/B and tests
+    const bool no_half = h.env_no_half;   // CF_HALF=0 at cf_create (A/B and tests)
     const double per_cell = (double)h.n / (double)ncell;
     h.half = !no_half && h.pbc && h.world == 1 && nc[0] >= 4 && nc[1] >= 4 && nc[2] >= 4 &&
              per_cell * 18.0 * 1.15 <= 4096.0 && h.n < (1 << 21);
@@ -211,6 +211,43 @@ void set_cells(cf_handle* H, const double L[3]) {
         cf::check_hip(hipMalloc(&h.win_woff, sizeof(int) * 18 * (size_t)ncell), "half-list windows");
         h.win_cells = (int)ncell;
         h.alloc_epoch++;
+    }
+    // cluster-pair half list (cf_kernels_cluster.hip): one rank, fp64 or mixed,
+    // wherever the per-atom half list applies; CF_CLUSTER=0 keeps the per-atom list (A/B and tests)
+    h.cluster = h.half && !h.env_no_cluster;
+    h.zcol = 0;
+    if (h.cluster) {
+        // within-cell z-columns of ~12 atoms (k_cell_order): clusters of 4 consecutive slots stay compact
+        h.zcol = (int)std::max(1.0, std::min(8.0, std::round(std::sqrt(per_cell / 12.0))));
+        const int need = h.n / 4 + (int)ncell + 1;
+        // entries per i-cluster: the j-clusters whose boxes come within rc + skin in a half space
+        // (cluster extent ~0.6 of the volume per cluster's edge: est = 135 at water density, rc 1,
+        // skin 0.15), x2.2 + 64 for the spread (measured off the synthetic lattice: mean 166-171,
+        // max 242-290, tools/cluster_proto.py); at most the clusters of one 18-cell window (k_cl_build)
+        const double rho = h.n / V;
+        const double ext = 0.6 * std::cbrt(4.0 / rho);
+        const double rl = h.cutoff + h.list_skin + ext;
+        const double est = 0.5 * 4.0 / 3.0 * M_PI * rl * rl * rl * rho / 4.0 + 8.0;
+        int cap = std::min(1536, ((int)(2.2 * est) + 64 + 15) / 16 * 16);
+        if (h.env_cluster_cap > 0) cap = std::max(4, std::min(cap, h.env_cluster_cap));   // tests: force overflows
+        if (need > h.ncl_cap || cap != h.cpl_cap || ncell + 1 > h.cl_cells) {
+            if (h.cl_start) { (void)hipFree(h.cl_start); (void)hipFree(h.cl_info); (void)hipFree(h.cl_bb);
+                              (void)hipFree(h.cpl); (void)hipFree(h.cpl_cnt); }
+            h.ncl_cap = std::max(need, h.ncl_cap);
+            h.cpl_cap = cap;
+            h.cl_cells = std::max((int)ncell + 1, h.cl_cells);
+            cf::check_hip(hipMalloc(&h.cl_start, sizeof(int) * h.cl_cells), "cluster table");
+            cf::check_hip(hipMalloc(&h.cl_info, sizeof(int2) * h.ncl_cap), "cluster table");
+            cf::check_hip(hipMalloc(&h.cl_bb, sizeof(float4) * 2 * h.ncl_cap), "cluster table");
+            cf::check_hip(hipMalloc(&h.cpl, sizeof(uint2) * (size_t)h.ncl_cap * h.cpl_cap), "cluster-pair list");
+            cf::check_hip(hipMalloc(&h.cpl_cnt, sizeof(int) * h.ncl_cap), "cluster-pair list");
+            h.alloc_epoch++;
+        }
+        if (!h.pos4f) {
+            cf::check_hip(hipMalloc(&h.pos4f, sizeof(float4) * h.n), "fp32 positions");
+            cf::check_hip(hipMalloc(&h.slot_of, sizeof(int) * h.n), "slot map");
+            h.alloc_epoch++;
+        }
     }
 }
 
@@ -446,6 +483,10 @@ CF_EXPORT int cf_create(const cf_params* p, const cf_options* opt, cf_handle** o
             fail(CF_ERR_INVALID, "precision must be CF_PRECISION_DOUBLE or CF_PRECISION_MIXED");
         h.mixed = o.precision == CF_PRECISION_MIXED;
         h.overlap = !(getenv("CF_OVERLAP") && std::string(getenv("CF_OVERLAP")) == "0");   // A/B
+        // list-kind switches for A/B runs and tests, latched here (set_cells runs again on every rebuild)
+        h.env_no_half = getenv("CF_HALF") && std::string(getenv("CF_HALF")) == "0";
+        h.env_no_cluster = getenv("CF_CLUSTER") && std::string(getenv("CF_CLUSTER")) == "0";
+        h.env_cluster_cap = getenv("CF_CLUSTER_CAP") ? atoi(getenv("CF_CLUSTER_CAP")) : 0;
         h.kspace_algo = o.kspace_algo;
         h.stream = (hipStream_t)o.stream;  // NULL = the null stream (orders with torch's default stream)
 
@@ -682,6 +723,9 @@ CF_EXPORT int cf_destroy(cf_handle* H) {
         for (auto& v : H->ev)
             for (hipEvent_t e : v) (void)hipEventDestroy(e);
         if (H->h.win_out) { (void)hipFree(H->h.win_out); (void)hipFree(H->h.win_woff); }
+        if (H->h.cl_start) { (void)hipFree(H->h.cl_start); (void)hipFree(H->h.cl_info); (void)hipFree(H->h.cl_bb);
+                             (void)hipFree(H->h.cpl); (void)hipFree(H->h.cpl_cnt); }
+        if (H->h.pos4f) { (void)hipFree(H->h.pos4f); (void)hipFree(H->h.slot_of); }
         if (H->h.cell_start) (void)hipFree(H->h.cell_start);
         if (H->h.cell_end) (void)hipFree(H->h.cell_end);
         if (H->h.cell_cnt) (void)hipFree(H->h.cell_cnt);
@@ -946,160 +990,6 @@ static void launch_end(cf_handle* H, int flags, double* forces_dev, double* ener
     }
 }
 
-// One single-rank evaluation.  With the grid k-space the reciprocal chain (bin sort, spread,
-// forward DFT, coefficients, inverse DFT, interpolation) depends on nothing the cell list and
-// the direct space produce -- both read the positions and k_atoms_prep's charges -- so it runs
-// on the handle's second stream while they run on the first: the small, latency-bound launches
-// of either chain (DFT stages, sorts, exclusions) fill the CUs the other leaves idle.  Joined
-// before k_assemble_energy, which adds the reciprocal dE/dq and forces (stored apart by the
-// interpolation) in the one-stream order: the same bits as launch_begin / direct / end.
-static bool overlap_ok(const cf::Handle& h, int flags) {
-    return h.overlap && h.aux && h.world == 1 && h.pbc && h.kspace_algo == 2 && h.hi > h.lo &&
-           (flags & (CF_INCLUDE_FORCES | CF_INCLUDE_ENERGY));
-}
-
-static void launch_full(cf_handle* H, const double* pos_dev, int flags, bool reusable, double* forces_dev,
-                        double* energy_dev) {
-    cf::Handle& h = H->h;
-    // a launch that throws (capture or launch failure) must not leave the handle looking like a
-    // begun evaluation (every later call would fail with CF_ERR_STATE) or on the second stream
-    struct Restore {
-        cf::Handle& h; hipStream_t s;
-        ~Restore() { h.pending_flags = -1; h.stream = s; }
-    } restore{h, h.stream};
-    if (!overlap_ok(h, flags)) {
-        h.rec_split = false;
-        h.pending_flags = flags;
-        launch_begin(H, pos_dev, flags, reusable);
-        launch_direct(H);
-        h.pending_flags = -1;
-        launch_end(H, flags, forces_dev, energy_dev);
-        return;
-    }
-    const int forces = flags & CF_INCLUDE_FORCES, energy = flags & CF_INCLUDE_ENERGY;
-    { Timed t(H, PH_FLUX); cf::launch_flux_terms(h, pos_dev); }
-    { Timed t(H, PH_PREP); cf::launch_atoms_prep(h, pos_dev, reusable); }
-    const hipStream_t main = h.stream;
-    check_hip(hipEventRecord(h.ev_fork, main), "hipEventRecord (fork)");
-    check_hip(hipStreamWaitEvent(h.aux, h.ev_fork, 0), "hipStreamWaitEvent (fork)");
-    h.stream = h.aux;
-    try {
-        { Timed t(H, PH_GSORT); cf::launch_grid_sort(h, pos_dev); }
-        { Timed t(H, PH_GSPREAD); cf::launch_grid_spread(h); }
-        { Timed t(H, PH_GDFTF); cf::launch_grid_dft_fwd(h); }
-        { Timed t(H, PH_COEFFS); cf::launch_grid_coeffs(h, energy); }
-        if (forces) {
-            { Timed t(H, PH_GDFTI); cf::launch_grid_dft_inv(h); }
-            { Timed t(H, PH_GINTERP); cf::launch_grid_interp(h, true); }
-        }
-        check_hip(hipEventRecord(h.ev_join, h.aux), "hipEventRecord (join)");
-    } catch (...) {
-        h.stream = main;
-        throw;
-    }
-    h.stream = main;
-    {
-        Timed t(H, PH_CELLS);
-        if (!reusable) cf::launch_force_rebuild(h);
-        cf::launch_cell_sort(h, pos_dev);
-    }
-    { Timed t(H, PH_NLIST); cf::launch_nlist(h, pos_dev); }
-    h.pending_flags = flags;
-    launch_direct(H);
-    h.pending_flags = -1;
-    check_hip(hipStreamWaitEvent(main, h.ev_join, 0), "hipStreamWaitEvent (join)");
-    h.rec_split = forces != 0;
-    {
-        Timed t(H, PH_ENERGY);
-        cf::launch_assemble_energy(h, (forces && forces_dev) ? forces_dev : nullptr, energy, energy_dev);
-    }
-}
-
-// Multi-rank split-phase calls with the grid k-space: the direct chain (cell sort, list, pair
-// kernels, exclusions) runs on the second stream from cf_compute_begin on, forked after
-// k_atoms_prep, while the caller's stream runs the bin sort, spread and forward DFT, the
-// caller's all-reduce of B(n) and, in cf_compute_end, the coefficients, inverse DFT and the
-// interpolation (stored apart, as in launch_full); joined before k_assemble_energy.  So the
-// latency-bound launches of a rank's small share (DFT stages over its slab, sorts) and the
-// all-reduce overlap the direct space.  Results: the bits of the one-stream split-phase order.
-// Eager calls only (a captured begin segment cannot leave its fork unjoined).
-static bool split_overlap_ok(cf_handle* H, int flags) {
-    const cf::Handle& h = H->h;
-    return h.overlap && h.aux && h.world > 1 && h.pbc && h.kspace_algo == 2 && h.hi > h.lo &&
-           (flags & (CF_INCLUDE_FORCES | CF_INCLUDE_ENERGY)) && !graph_active(H);
-}
-
-static void launch_begin_split(cf_handle* H, const double* pos_dev, int flags, bool reusable) {
-    cf::Handle& h = H->h;
-    { Timed t(H, PH_FLUX); cf::launch_flux_terms(h, pos_dev); }
-    { Timed t(H, PH_PREP); cf::launch_atoms_prep(h, pos_dev, reusable); }
-    const hipStream_t main = h.stream;
-    check_hip(hipEventRecord(h.ev_fork, main), "hipEventRecord (fork)");
-    check_hip(hipStreamWaitEvent(h.aux, h.ev_fork, 0), "hipStreamWaitEvent (fork)");
-    h.stream = h.aux;
-    try {
-        {
-            Timed t(H, PH_CELLS);
-            if (!reusable) cf::launch_force_rebuild(h);
-            cf::launch_cell_sort(h, pos_dev);
-        }
-        { Timed t(H, PH_NLIST); cf::launch_nlist(h, pos_dev); }
-        h.pending_flags = flags;
-        launch_direct(H);
-        h.pending_flags = -1;
-        check_hip(hipEventRecord(h.ev_join, h.aux), "hipEventRecord (join)");
-    } catch (...) {
-        h.stream = main;
-        h.pending_flags = -1;
-        throw;
-    }
-    h.stream = main;
-    { Timed t(H, PH_GSORT); cf::launch_grid_sort(h, pos_dev); }
-    { Timed t(H, PH_GSPREAD); cf::launch_grid_spread(h); }
-    { Timed t(H, PH_GDFTF); cf::launch_grid_dft_fwd(h); }
-}
-
-static void launch_end_split(cf_handle* H, int flags, double* forces_dev, double* energy_dev) {
-    cf::Handle& h = H->h;
-    const int forces = flags & CF_INCLUDE_FORCES, energy = flags & CF_INCLUDE_ENERGY;
-    { Timed t(H, PH_COEFFS); cf::launch_grid_coeffs(h, energy); }
-    if (forces) {
-        { Timed t(H, PH_GDFTI); cf::launch_grid_dft_inv(h); }
-        { Timed t(H, PH_GINTERP); cf::launch_grid_interp(h, true); }
-    }
-    check_hip(hipStreamWaitEvent(h.stream, h.ev_join, 0), "hipStreamWaitEvent (join)");
-    h.rec_split = forces != 0;
-    {
-        Timed t(H, PH_ENERGY);
-        cf::launch_assemble_energy(h, (forces && forces_dev) ? forces_dev : nullptr, energy, energy_dev);
-    }
-}
-
-// the second stream and its fork / join events (created outside any capture)
-static void ensure_aux(cf_handle* H) {
-    cf::Handle& h = H->h;
-    if (h.aux || !h.overlap || !h.pbc || h.kspace_algo != 2) return;
-    // CF_AUX_PRIORITY=low / high (A/B): the second stream's priority against the caller's
-    const char* pr = getenv("CF_AUX_PRIORITY");
-    if (pr && (std::string(pr) == "low" || std::string(pr) == "high")) {
-        int least = 0, greatest = 0;
-        check_hip(hipDeviceGetStreamPriorityRange(&least, &greatest), "hipDeviceGetStreamPriorityRange");
-        check_hip(hipStreamCreateWithPriority(&h.aux, hipStreamNonBlocking, std::string(pr) == "low" ? least : greatest),
-                  "hipStreamCreateWithPriority (second stream)");
-    } else {
-        check_hip(hipStreamCreateWithFlags(&h.aux, hipStreamNonBlocking), "hipStreamCreate (second stream)");
-    }
-    check_hip(hipEventCreateWithFlags(&h.ev_fork, hipEventDisableTiming), "hipEventCreate");
-    check_hip(hipEventCreateWithFlags(&h.ev_join, hipEventDisableTiming), "hipEventCreate");
-    if (!h.dedq_rec) {
-        h.dedq_rec = dalloc<double>(H, (size_t)h.n);
-        h.f_rec = dalloc<double>(H, (size_t)4 * h.n);
-        // atoms a rank does not own are never written: zero, so that cf_get_dedq adds nothing
-        check_hip(hipMemset(h.dedq_rec, 0, sizeof(double) * h.n), "memset dedq_rec");
-        check_hip(hipMemset(h.f_rec, 0, sizeof(double) * 4 * h.n), "memset f_rec");
-    }
-}
-
 // ---- hipGraph replay (cf_set_graph) ------------------------------------------------------------
 // The launches of an evaluation are captured into hipGraphs on a private stream and replayed on
 // the handle's stream while the calls look the same to the host: the same device buffers,
@@ -1107,7 +997,12 @@ static void ensure_aux(cf_handle* H) {
 // inside the graph).  Anything else re-captures.  Segments: the whole single-call evaluation
 // (cf_compute), and for the split-phase calls of a multi-rank step the begin, direct and end
 // launches separately (the caller's all-reduce runs between them on the same stream).
-enum GraphSeg { SEG_FULL, SEG_BEGIN, SEG_DIRECT, SEG_END, SEG_COUNT };
+// two-stream evaluations are captured one graph per stream chain (SEG_PRO: flux + charges,
+// SEG_REC: the reciprocal chain, SEG_DCH: cell list + direct space; split-phase SEG_RFWD / SEG_REND:
+// the reciprocal chain before / after the caller's all-reduce): the fork and join stay event
+// operations between graph launches on the two streams, so a replay keeps the overlap (one graph
+// holding both streams replayed as a single chain: 0.561 vs 0.526 ms eager at C3, round 3)
+enum GraphSeg { SEG_FULL, SEG_BEGIN, SEG_DIRECT, SEG_END, SEG_PRO, SEG_REC, SEG_DCH, SEG_RFWD, SEG_REND, SEG_COUNT };
 
 struct GraphKey {
     const void* pos = nullptr; void* frc = nullptr; void* ene = nullptr;
@@ -1210,6 +1105,182 @@ static GraphKey make_key(const cf::Handle& h, const void* pos, void* frc, void* 
     return k;
 }
 
+// One single-rank evaluation.  With the grid k-space the reciprocal chain (bin sort, spread,
+// forward DFT, coefficients, inverse DFT, interpolation) depends on nothing the cell list and
+// the direct space produce -- both read the positions and k_atoms_prep's charges -- so it runs
+// on the handle's second stream while they run on the first: the small, latency-bound launches
+// of either chain (DFT stages, sorts, exclusions) fill the CUs the other leaves idle.  Joined
+// before k_assemble_energy, which adds the reciprocal dE/dq and forces (stored apart by the
+// interpolation) in the one-stream order: the same bits as launch_begin / direct / end.
+static bool overlap_ok(const cf::Handle& h, int flags) {
+    return h.overlap && h.aux && h.world == 1 && h.pbc && h.kspace_algo == 2 && h.hi > h.lo &&
+           (flags & (CF_INCLUDE_FORCES | CF_INCLUDE_ENERGY));
+}
+
+// pieces of the two-stream evaluations (each enqueues on h.stream)
+static void launch_prologue(cf_handle* H, const double* pos_dev, bool reusable) {
+    cf::Handle& h = H->h;
+    { Timed t(H, PH_FLUX); cf::launch_flux_terms(h, pos_dev); }
+    { Timed t(H, PH_PREP); cf::launch_atoms_prep(h, pos_dev, reusable); }
+}
+// cell list + direct space + exclusions of an evaluation with these flags
+static void launch_direct_chain(cf_handle* H, const double* pos_dev, int flags, bool reusable) {
+    cf::Handle& h = H->h;
+    {
+        Timed t(H, PH_CELLS);
+        if (!reusable) cf::launch_force_rebuild(h);
+        cf::launch_cell_sort(h, pos_dev);
+    }
+    { Timed t(H, PH_NLIST); cf::launch_nlist(h, pos_dev); }
+    h.pending_flags = flags;
+    launch_direct(H);
+    h.pending_flags = -1;
+}
+// the grid reciprocal chain up to the all-reduced buffer (fwd) and from it on (end); the
+// interpolation stores into dedq_rec / f_rec (added by k_assemble_energy)
+static void launch_rec_fwd(cf_handle* H, const double* pos_dev) {
+    cf::Handle& h = H->h;
+    { Timed t(H, PH_GSORT); cf::launch_grid_sort(h, pos_dev); }
+    { Timed t(H, PH_GSPREAD); cf::launch_grid_spread(h); }
+    { Timed t(H, PH_GDFTF); cf::launch_grid_dft_fwd(h); }
+}
+static void launch_rec_end(cf_handle* H, int flags) {
+    cf::Handle& h = H->h;
+    { Timed t(H, PH_COEFFS); cf::launch_grid_coeffs(h, flags & CF_INCLUDE_ENERGY); }
+    if (flags & CF_INCLUDE_FORCES) {
+        { Timed t(H, PH_GDFTI); cf::launch_grid_dft_inv(h); }
+        { Timed t(H, PH_GINTERP); cf::launch_grid_interp(h, true); }
+    }
+}
+// run `launches` (a segment) on the second stream: eagerly, or as the segment's graph launched there
+}  // extern "C"
+template <class F>
+static void on_aux(cf_handle* H, GraphCache* g, int seg, const GraphKey& k, F&& launches) {
+    cf::Handle& h = H->h;
+    const hipStream_t main = h.stream;
+    h.stream = h.aux;
+    try {
+        run_segment(H, g, seg, k, launches);
+    } catch (...) {
+        h.stream = main;
+        throw;
+    }
+    h.stream = main;
+}
+extern "C" {
+static void fork_aux(cf::Handle& h) {
+    check_hip(hipEventRecord(h.ev_fork, h.stream), "hipEventRecord (fork)");
+    check_hip(hipStreamWaitEvent(h.aux, h.ev_fork, 0), "hipStreamWaitEvent (fork)");
+}
+
+static void launch_full(cf_handle* H, const double* pos_dev, int flags, bool reusable, double* forces_dev,
+                        double* energy_dev, GraphCache* g, const double* box9) {
+    cf::Handle& h = H->h;
+    // a launch that throws (capture or launch failure) must not leave the handle looking like a
+    // begun evaluation (every later call would fail with CF_ERR_STATE) or on the second stream
+    struct Restore {
+        cf::Handle& h; hipStream_t s;
+        ~Restore() { h.pending_flags = -1; h.stream = s; }
+    } restore{h, h.stream};
+    if (!overlap_ok(h, flags)) {
+        auto one = [&] {
+            h.rec_split = false;
+            h.pending_flags = flags;
+            launch_begin(H, pos_dev, flags, reusable);
+            launch_direct(H);
+            h.pending_flags = -1;
+            launch_end(H, flags, forces_dev, energy_dev);
+        };
+        run_segment(H, g, SEG_FULL, make_key(h, pos_dev, forces_dev, energy_dev, flags, reusable, box9), one);
+        return;
+    }
+    const int forces = flags & CF_INCLUDE_FORCES, energy = flags & CF_INCLUDE_ENERGY;
+    const GraphKey key = make_key(h, pos_dev, nullptr, nullptr, flags, reusable, box9);
+    run_segment(H, g, SEG_PRO, key, [&] { launch_prologue(H, pos_dev, reusable); });
+    fork_aux(h);
+    on_aux(H, g, SEG_REC, key, [&] {
+        launch_rec_fwd(H, pos_dev);
+        launch_rec_end(H, flags);
+    });
+    check_hip(hipEventRecord(h.ev_join, h.aux), "hipEventRecord (join)");
+    run_segment(H, g, SEG_DCH, key, [&] { launch_direct_chain(H, pos_dev, flags, reusable); });
+    check_hip(hipStreamWaitEvent(h.stream, h.ev_join, 0), "hipStreamWaitEvent (join)");
+    h.rec_split = forces != 0;
+    {
+        Timed t(H, PH_ENERGY);
+        cf::launch_assemble_energy(h, (forces && forces_dev) ? forces_dev : nullptr, energy, energy_dev);
+    }
+}
+
+// Multi-rank split-phase calls with the grid k-space: the direct chain (cell sort, list, pair
+// kernels, exclusions) runs on the second stream from cf_compute_begin on, forked after
+// k_atoms_prep, while the caller's stream runs the bin sort, spread and forward DFT, the
+// caller's all-reduce of B(n) and, in cf_compute_end, the coefficients, inverse DFT and the
+// interpolation (stored apart, as in launch_full); joined before k_assemble_energy.  So the
+// latency-bound launches of a rank's small share (DFT stages over its slab, sorts) and the
+// all-reduce overlap the direct space.  Results: the bits of the one-stream split-phase order.
+// Graph mode captures one graph per stream chain, as launch_full.
+static bool split_overlap_ok(cf_handle* H, int flags) {
+    const cf::Handle& h = H->h;
+    return h.overlap && h.aux && h.world > 1 && h.pbc && h.kspace_algo == 2 && h.hi > h.lo &&
+           (flags & (CF_INCLUDE_FORCES | CF_INCLUDE_ENERGY));
+}
+
+static void launch_begin_split(cf_handle* H, const double* pos_dev, int flags, bool reusable, GraphCache* g,
+                               const double* box9) {
+    cf::Handle& h = H->h;
+    const GraphKey key = make_key(h, pos_dev, nullptr, nullptr, flags, reusable, box9);
+    run_segment(H, g, SEG_PRO, key, [&] { launch_prologue(H, pos_dev, reusable); });
+    fork_aux(h);
+    try {
+        on_aux(H, g, SEG_DCH, key, [&] { launch_direct_chain(H, pos_dev, flags, reusable); });
+    } catch (...) {
+        h.pending_flags = -1;
+        throw;
+    }
+    check_hip(hipEventRecord(h.ev_join, h.aux), "hipEventRecord (join)");
+    run_segment(H, g, SEG_RFWD, key, [&] { launch_rec_fwd(H, pos_dev); });
+}
+
+static void launch_end_split(cf_handle* H, int flags, double* forces_dev, double* energy_dev, GraphCache* g,
+                             const double* box9) {
+    cf::Handle& h = H->h;
+    const int forces = flags & CF_INCLUDE_FORCES, energy = flags & CF_INCLUDE_ENERGY;
+    run_segment(H, g, SEG_REND, make_key(h, H->pos_pending, nullptr, nullptr, flags, false, box9),
+                [&] { launch_rec_end(H, flags); });
+    check_hip(hipStreamWaitEvent(h.stream, h.ev_join, 0), "hipStreamWaitEvent (join)");
+    h.rec_split = forces != 0;
+    {
+        Timed t(H, PH_ENERGY);
+        cf::launch_assemble_energy(h, (forces && forces_dev) ? forces_dev : nullptr, energy, energy_dev);
+    }
+}
+
+// the second stream and its fork / join events (created outside any capture)
+static void ensure_aux(cf_handle* H) {
+    cf::Handle& h = H->h;
+    if (h.aux || !h.overlap || !h.pbc || h.kspace_algo != 2) return;
+    // CF_AUX_PRIORITY=low / high (A/B): the second stream's priority against the caller's
+    const char* pr = getenv("CF_AUX_PRIORITY");
+    if (pr && (std::string(pr) == "low" || std::string(pr) == "high")) {
+        int least = 0, greatest = 0;
+        check_hip(hipDeviceGetStreamPriorityRange(&least, &greatest), "hipDeviceGetStreamPriorityRange");
+        check_hip(hipStreamCreateWithPriority(&h.aux, hipStreamNonBlocking, std::string(pr) == "low" ? least : greatest),
+                  "hipStreamCreateWithPriority (second stream)");
+    } else {
+        check_hip(hipStreamCreateWithFlags(&h.aux, hipStreamNonBlocking), "hipStreamCreate (second stream)");
+    }
+    check_hip(hipEventCreateWithFlags(&h.ev_fork, hipEventDisableTiming), "hipEventCreate");
+    check_hip(hipEventCreateWithFlags(&h.ev_join, hipEventDisableTiming), "hipEventCreate");
+    if (!h.dedq_rec) {
+        h.dedq_rec = dalloc<double>(H, (size_t)h.n);
+        h.f_rec = dalloc<double>(H, (size_t)4 * h.n);
+        // atoms a rank does not own are never written: zero, so that cf_get_dedq adds nothing
+        check_hip(hipMemset(h.dedq_rec, 0, sizeof(double) * h.n), "memset dedq_rec");
+        check_hip(hipMemset(h.f_rec, 0, sizeof(double) * 4 * h.n), "memset f_rec");
+    }
+}
+
 CF_EXPORT int cf_set_graph(cf_handle* H, int enable) {
     return guarded([&] {
         if (!H) fail(CF_ERR_INVALID, "null handle");
@@ -1254,7 +1325,7 @@ CF_EXPORT int cf_compute_begin(cf_handle* H, const double* pos_dev, const double
         H->pos_pending = pos_dev;
         h.split_overlap = split_overlap_ok(H, flags);
         if (h.split_overlap) {   // direct chain on the second stream (launch_begin_split)
-            launch_begin_split(H, pos_dev, flags, reusable);
+            launch_begin_split(H, pos_dev, flags, reusable, graph_active(H), box9);
         } else {
             run_segment(H, graph_active(H), SEG_BEGIN, make_key(h, pos_dev, nullptr, nullptr, flags, reusable, box9),
                         [&] { launch_begin(H, pos_dev, flags, reusable); });
@@ -1303,7 +1374,7 @@ CF_EXPORT int cf_compute_end(cf_handle* H, double* forces_dev, double* energy_de
         h.pending_flags = -1;
         if (h.split_overlap) {
             h.split_overlap = false;
-            launch_end_split(H, flags, forces_dev, energy_dev);
+            launch_end_split(H, flags, forces_dev, energy_dev, graph_active(H), h.pbc ? H->box9_last : nullptr);
         } else {
             run_segment(H, graph_active(H), SEG_END,
                         make_key(h, H->pos_pending, forces_dev, energy_dev, flags, false, h.pbc ? H->box9_last : nullptr),
@@ -1329,10 +1400,7 @@ CF_EXPORT int cf_compute(cf_handle* H, const double* pos_dev, const double* box9
         const bool reusable = host_prologue(H, box9);
         ensure_aux(H);
         H->pos_pending = pos_dev;
-        GraphCache* g = graph_active(H);
-        auto launches = [&] { launch_full(H, pos_dev, flags, reusable, forces_dev, energy_dev); };
-        if (g) run_segment(H, g, SEG_FULL, make_key(h, pos_dev, forces_dev, energy_dev, flags, reusable, box9), launches);
-        else launches();
+        launch_full(H, pos_dev, flags, reusable, forces_dev, energy_dev, graph_active(H), box9);
         h.pending_flags = -1;
         launch_check("compute");
     });

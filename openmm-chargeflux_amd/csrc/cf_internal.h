@@ -178,6 +178,22 @@ struct Handle {
     unsigned long long* win_out = nullptr;   // [ncell][4096][4] window partials (fixed point)
     int* win_woff = nullptr;    // [ncell][18]
     int win_cells = 0;          // cells win_out / win_woff are sized for
+    // cluster-pair half list (cf_kernels_cluster.hip): one rank, same window and
+    // fixed-point j side as the half list; clusters = runs of <= 4 consecutive sorted slots of one cell
+    bool cluster = false;
+    bool env_no_half = false, env_no_cluster = false;   // CF_HALF=0 / CF_CLUSTER=0 at cf_create
+    int env_cluster_cap = 0;    // CF_CLUSTER_CAP at cf_create (tests: a capacity that overflows)
+    int zcol = 0;               // columns per cell axis of the within-cell sort (k_cell_order; 0 = atom order)
+    int ncl_cap = 0;            // cluster capacity: N/4 + ncell
+    int cl_cells = 0;           // cells cl_start is sized for (+1)
+    int* cl_start = nullptr;    // [ncell + 1] first cluster of each cell
+    int2* cl_info = nullptr;    // [ncl_cap] (first sorted slot, atom count)
+    float4* cl_bb = nullptr;    // [ncl_cap][2] bounding box (lo, hi) at the last list build
+    int cpl_cap = 0;            // cluster-pair entries per i-cluster
+    uint2* cpl = nullptr;       // [ncl_cap][cpl_cap] (first slot of j | window cell << 21, pair mask)
+    int* cpl_cnt = nullptr;     // [ncl_cap]
+    float4* pos4f = nullptr;    // [N] sorted wrapped fp32 (x, y, z, LJ type bits)
+    int* slot_of = nullptr;     // [N] atom -> sorted slot (exclusion masks of the list build)
     // k-space (MFMA path)
     int npad = 0;               // owned rows of the phase tables, padded to the S-pass tile
     double2* tab_xq = nullptr;  // [Nown][KX]
@@ -240,6 +256,8 @@ void launch_atoms_prep(Handle& h, const double* pos, bool skin_check);   // q, s
 void launch_cell_sort(Handle& h, const double* pos);
 void launch_force_rebuild(Handle& h);                   // skin_flag = 1
 void launch_nlist(Handle& h, const double* pos);
+void launch_cluster_list(Handle& h);                   // cluster table, bounding boxes, cluster-pair list (rebuild only)
+void launch_pairs_cluster(Handle& h, const double* pos, int include_forces);   // k_pairs_cq
 void launch_direct(Handle& h, const double* pos, int include_forces);          // the pair kernel
 void launch_direct_finish(Handle& h, const double* pos, int include_forces);   // overflow rescan + exclusions
 void launch_recip_add(Handle& h);   // dedq, f_part += reciprocal partials

@@ -6,57 +6,10 @@
 #include <algorithm>
 #include <type_traits>
 
-#include "cf_internal.h"
+#include "cf_pair.h"
 
 namespace cf {
 
-// OpenMM ReferenceForce::getDeltaR[Periodic]: d = J - I, minimum image by the box vectors c,
-// b, a in that order via floor(d/L + 0.5) (used by RCK:53-55, 567, 601).  Boxes are in OpenMM's
-// reduced form a = (Lx,0,0), b = (bx,Ly,0), c = (cx,cy,Lz); T = (bx, cx, cy), zero for an
-// orthorhombic box (the per-axis form, the same bits).
-__device__ __forceinline__ double3 delta_r(double3 pi, double3 pj, double3 L, int pbc,
-                                           double3 T = make_double3(0.0, 0.0, 0.0)) {
-    double3 d = make_double3(pj.x - pi.x, pj.y - pi.y, pj.z - pi.z);
-    if (pbc) {
-        if (T.x != 0.0 || T.y != 0.0 || T.z != 0.0) {
-            const double sc = floor(d.z / L.z + 0.5);
-            d.x -= sc * T.y; d.y -= sc * T.z; d.z -= sc * L.z;
-            const double sb = floor(d.y / L.y + 0.5);
-            d.x -= sb * T.x; d.y -= sb * L.y;
-            d.x -= L.x * floor(d.x / L.x + 0.5);
-        } else {
-            d.z -= L.z * floor(d.z / L.z + 0.5);
-            d.y -= L.y * floor(d.y / L.y + 0.5);
-            d.x -= L.x * floor(d.x / L.x + 0.5);
-        }
-    }
-    return d;
-}
-
-__device__ __forceinline__ double3 ld3(const double* p, int i) {
-    return make_double3(p[3 * i], p[3 * i + 1], p[3 * i + 2]);
-}
-
-// The periodic lattice of OpenMM's reduced box: a = (L.x,0,0), b = (T.x,L.y,0), c = (T.y,T.z,L.z)
-// (T = (bx, cx, cy); all zero for an orthorhombic box, where every helper below reduces to the
-// per-axis form with the same bits: the T terms subtract exact zeros).
-// ka a + kb b + kc c
-__device__ __forceinline__ double3 lattice(double3 L, double3 T, double ka, double kb, double kc) {
-    return make_double3(ka * L.x + kb * T.x + kc * T.y, kb * L.y + kc * T.z, kc * L.z);
-}
-// fractional coordinates: x = s_a a + s_b b + s_c c
-__device__ __forceinline__ double3 fractional(double3 x, double3 L, double3 T) {
-    const double sc = x.z / L.z;
-    const double sb = (x.y - sc * T.z) / L.y;
-    const double sa = (x.x - sb * T.x - sc * T.y) / L.x;
-    return make_double3(sa, sb, sc);
-}
-// x moved by the lattice translation -(fl.x a + fl.y b + fl.z c); with fl = floor(fractional(x))
-// the result lies in the unit cell (fractional coordinates in [0, 1))
-__device__ __forceinline__ double3 wrap_by(double3 x, double3 fl, double3 L, double3 T) {
-    return make_double3(x.x - fl.x * L.x - fl.y * T.x - fl.z * T.y, x.y - fl.y * L.y - fl.z * T.z, x.z - fl.z * L.z);
-}
-__device__ __forceinline__ double3 floor3(double3 v) { return make_double3(floor(v.x), floor(v.y), floor(v.z)); }
 
 // ---------------------------------------------------------------------------------
 // 1. flux terms: one lane per term writes its charge deltas (slots) and its dq/dx
@@ -253,39 +206,87 @@ __global__ void __launch_bounds__(256) k_cell_scatter(int n, const int* __restri
     tmp[cstart[key[i]] + rank[i]] = i;
 }
 
-// one wave per cell: final position of each member = cell start + number of members with
-// a smaller atom index (members staged in LDS and read by broadcast); multi-rank: an owned
-// member's list row = the cell's first row + number of owned members with a smaller index
+// one wave per cell: final position of each member = cell start + number of members before it in
+// the cell order (members staged in LDS and read by broadcast); multi-rank: an owned member's list
+// row = the cell's first row + number of owned members before it.
+// Cell order (zcol = S > 0): the cell is cut into S x S columns along its a and b lattice
+// directions, members sorted by (column, fractional c coordinate, atom index), columns and the
+// direction along c in serpentine order -- so that runs of
+// 4 consecutive slots (the clusters of the cluster-pair list, cf_kernels_cluster.hip) are
+// spatially compact whatever the atom order of the system; zcol = 0: by atom index (the order of
+// a stable sort).  Both are total orders computed from the positions alone: deterministic.
 constexpr int kOrderLds = 1024;
 
 __global__ void __launch_bounds__(256) k_cell_order(int ncell, const int* __restrict__ flag,
                                                     const int* __restrict__ cstart, const int* __restrict__ cend,
                                                     const int* __restrict__ tmp, int* __restrict__ out, int lo, int hi,
-                                                    const int* __restrict__ own_start, int* __restrict__ own_s) {
-    __shared__ int mem[4][kOrderLds];
+                                                    const int* __restrict__ own_start, int* __restrict__ own_s,
+                                                    const double* __restrict__ pos, double3 L, double3 T, int3 nc,
+                                                    int zcol) {
+    // one 64-bit key per member: (column << 58 | quantized c coordinate << 26 | atom index), or the
+    // atom index alone -- the rank is then one unsigned compare per member pair
+    __shared__ unsigned long long memk[4][kOrderLds];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int c = blockIdx.x * 4 + w;
     if (c >= ncell || !*flag) return;
     const int b = cstart[c], m = cend[c] - b;
     const int* src = tmp + b;
-    if (m <= kOrderLds) {
-        for (int e = lane; e < m; e += 64) mem[w][e] = src[e];
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        src = mem[w];
-    }
-    for (int e = lane; e < m; e += 64) {
-        const int v = src[e];
-        int r = 0, ro = 0;
-        if (own_s) {
+    if (m > kOrderLds) {   // rare (an over-full cell): atom order, read from global memory
+        for (int e = lane; e < m; e += 64) {
+            const int v = src[e];
+            int r = 0, ro = 0;
             for (int j = 0; j < m; j++) {
                 const int u = src[j];
                 r += u < v;
-                ro += u < v && u >= lo && u < hi;
+                if (own_s) ro += u < v && u >= lo && u < hi;
             }
-        } else {
-            for (int j = 0; j < m; j++) r += src[j] < v;
+            out[b + r] = v;
+            if (own_s && v >= lo && v < hi) own_s[own_start[c] + ro] = b + r;
+        }
+        return;
+    }
+    const int cc[3] = {c / (nc.y * nc.z), (c / nc.z) % nc.y, c % nc.z};
+    for (int e = lane; e < m; e += 64) {
+        const int v = src[e];
+        unsigned long long key = (unsigned long long)v;
+        if (zcol > 0) {
+            // the member's position inside its cell in fractional cell units (as k_cell_hist bins it)
+            const double3 x = ld3(pos, v);
+            const double3 f = fractional(wrap_by(x, floor3(fractional(x, L, T)), L, T), L, T);
+            const double la = fmin(fmax(f.x * nc.x - cc[0], 0.0), 0.999999);
+            const double lb = fmin(fmax(f.y * nc.y - cc[1], 0.0), 0.999999);
+            const double lc = fmin(fmax(f.z * nc.z - cc[2], 0.0), 0.999999);
+            // columns in serpentine order, c ascending in even and descending in odd columns:
+            // consecutive slots stay neighbours across a column change (a cluster that straddles
+            // two columns is still compact)
+            const int ca = (int)(la * zcol), cb0 = (int)(lb * zcol);
+            const int col = ca * zcol + ((ca & 1) ? zcol - 1 - cb0 : cb0);
+            const unsigned zq = (unsigned)(((col & 1) ? 0.999999 - lc : lc) * 4294967296.0);
+            key |= ((unsigned long long)col << 58) | ((unsigned long long)zq << 26);
+        }
+        memk[w][e] = key;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const unsigned long long kIdx = zcol > 0 ? (1ull << 26) - 1 : ~0ull;   // (zcol > 0: n < 2^21, half lists)
+    for (int e = lane; e < m; e += 64) {
+        const unsigned long long kv = memk[w][e];
+        const int v = (int)(kv & kIdx);
+        int r = 0, ro = 0;
+        int j = 0;
+        for (; j + 2 <= m; j += 2) {   // two keys per 16-B LDS read (broadcast: every lane reads the same j)
+            const ulonglong2 u2 = *reinterpret_cast<const ulonglong2*>(&memk[w][j]);
+            r += (u2.x < kv) + (u2.y < kv);
+            if (own_s) {
+                const int ux = (int)(u2.x & kIdx), uy = (int)(u2.y & kIdx);
+                ro += (u2.x < kv && ux >= lo && ux < hi) + (u2.y < kv && uy >= lo && uy < hi);
+            }
+        }
+        if (j < m) {
+            const unsigned long long u = memk[w][j];
+            r += u < kv;
+            if (own_s) ro += u < kv && (int)(u & kIdx) >= lo && (int)(u & kIdx) < hi;
         }
         out[b + r] = v;
         if (own_s && v >= lo && v < hi) own_s[own_start[c] + ro] = b + r;
@@ -305,12 +306,15 @@ __global__ void __launch_bounds__(256) k_cell_commit(int n, const int* __restric
                                                      int* __restrict__ key_s, int* __restrict__ idx_s,
                                                      double4* __restrict__ pos4s, double2* __restrict__ ljs,
                                                      const int* __restrict__ atype, int* __restrict__ typ_s,
-                                                     double* __restrict__ pos_ref, long long* __restrict__ n_builds) {
+                                                     double* __restrict__ pos_ref, long long* __restrict__ n_builds,
+                                                     float4* __restrict__ pos4f, int* __restrict__ slot_of, int3 nc) {
     int s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= n) return;
     double4 p4;
+    int i, c;
     if (*flag) {
-        int i = idx_new[s];
+        i = idx_new[s];
+        c = key[i];
         key_s[s] = key[i];
         idx_s[s] = i;
         double3 x = ld3(pos, i);
@@ -319,14 +323,25 @@ __global__ void __launch_bounds__(256) k_cell_commit(int n, const int* __restric
         ljs[s] = lj[i];
         if (typ_s) typ_s[s] = atype[i];
         if (pos_ref) { pos_ref[3 * i] = x.x; pos_ref[3 * i + 1] = x.y; pos_ref[3 * i + 2] = x.z; }
+        if (slot_of) slot_of[i] = s;
         if (s == 0) *n_builds += 1;
     } else {
-        int i = idx_s[s];
+        i = idx_s[s];
+        c = pos4f ? key_s[s] : 0;
         double3 x = ld3(pos, i), r = ld3(pos_ref, i);
         const double3 w = wrap_by(x, floor3(fractional(r, L, T)), L, T);
         p4 = make_double4(w.x, w.y, w.z, q[i]);
     }
     pos4s[s] = p4;
+    // cluster-pair path (cf_kernels_cluster.hip): fp32 position relative to the corner of the atom's
+    // (build-time) cell -- a few nm at most, so fp32 keeps ~1e-7 nm whatever the box size -- and the
+    // LJ type in w
+    if (pos4f) {
+        const double3 o = lattice(L, T, (double)(c / (nc.y * nc.z)) / nc.x, (double)((c / nc.z) % nc.y) / nc.y,
+                                  (double)(c % nc.z) / nc.z);
+        pos4f[s] = make_float4((float)(p4.x - o.x), (float)(p4.y - o.y), (float)(p4.z - o.z),
+                               __int_as_float(typ_s ? atype[i] : 0));
+    }
 }
 
 // ---------------------------------------------------------------------------------
@@ -342,97 +357,6 @@ __global__ void __launch_bounds__(256) k_cell_commit(int n, const int* __restric
 //    4b k_pairs: lanes per owned atom walk its list with every lane busy and store the raw
 //       pair sums; k_excl applies the exclusion correction and the self term.
 // ---------------------------------------------------------------------------------
-constexpr int kMaxRegExcl = 8;
-constexpr int kErfcDeg = 7;      // erfcx polynomial degree per interval (fp64): relative error 3.6e-16
-constexpr int kErfcMaxM = 129;   // fp64 intervals of width 1/16: x = alpha r up to 8 (erfc(8) = 1e-29)
-constexpr int kErfcDegF = 6;     // the same in fp32 (mixed precision): relative error ~1e-7
-constexpr int kErfcMaxMF = 32;   // fp32 intervals of width 0.375: x = alpha r up to 11.6
-constexpr int kMaxLjTypes = 64;  // LJ types carried in the 6 high bits of a list entry
-constexpr int kSeg = 4;          // neighbour sub-lists per atom (one per scanning wave / pair lane)
-constexpr int kShiftBits = 26;
-constexpr int kJMask = (1 << kShiftBits) - 1;   // atom / slot index bits of a packed entry
-constexpr int kBruteShift = 31;  // shift code: minimum image by floor (brute-force path)
-// Half neighbour list, split by x (a half-space rule): the pair (i, j) is
-// kept by the atom of the lower x cell when their cells differ in x, and otherwise by the
-// atom with the smaller wrapped x (rounded to fp32, a per-atom key that both sides see
-// identically; ties: the lower sorted slot).  Every atom so keeps about half of its partners
-// wherever it sits in its cell (a cell-index rule -- own cell "later" partners plus 13
-// forward cells -- gives the first rows of a cell ~2x the partners of the last ones and skews
-// the sub-lists, ~0.66 lane efficiency against ~0.84).  A row's partners lie in the 18 cells
-// at x offset 0 or +1: the row cell's window.  Entry = sorted slot of j | k << 21 (window
-// cell k = ox*9 + (oy+1)*3 + (oz+1)) | LJ type << 26: the partner's address needs no table
-// lookup (the gather is not queued behind LDS work).
-constexpr int kHalfWin = 18;          // window cells per block: x offsets 0 and +1
-constexpr int kHalfBlock = 1024;      // threads per k_pairs_half block (one cell; 4 lanes per row)
-constexpr int kHalfOwn = 4;           // the row cell's own window index (0, 0, 0)
-constexpr int kHalfMaxWin = 4096;     // window atoms per block (LDS accumulators: 128 KB)
-constexpr int kHalfSlotBits = 21;     // sorted slots < 2^21 (cf_api.hip enables half lists below)
-constexpr int kHalfSlotMask = (1 << kHalfSlotBits) - 1;
-static_assert(kHalfSlotBits + 5 <= kShiftBits, "window cell bits overlap the LJ type bits");
-// j-side sums in 64-bit fixed point (integer adds: exact, so any order gives the same bits):
-// v -> round(v 2^34) via the 1.5 * 2^52 magic add (exact for |v 2^34| < 2^51); a contribution
-// with |v| >= 2^16 flags the evaluation for the fp64 rescan fallback
-constexpr double kFixScale = 17179869184.0;            // 2^34
-constexpr double kFixInv = 1.0 / 17179869184.0;
-constexpr double kFixMagic = 6755399441055744.0;       // 1.5 * 2^52
-constexpr long long kFixMagicBits = 0x4338000000000000LL;
-constexpr double kFixMax = 65536.0;
-// why half_flag was raised (bits; cf_get_fallback_stats reports their union)
-constexpr int kHalfWindowFull = 1;     // a cell's 18-cell window holds more than kHalfMaxWin atoms
-constexpr int kHalfListOverflow = 2;   // a row's sub-list overflowed, or the builder could not place it
-constexpr int kHalfFixedRange = 4;     // a partner-side term beyond the fixed-point range
-
-struct DirectArgs {
-    int n, lo, hi, include_forces;
-    double3 L; double3 invL; int3 nc; int brute;
-    double3 T; int tric;        // reduced triclinic box: off-diagonals (bx, cx, cy); tric = any nonzero
-    double rc2, alpha;
-    double rc;                  // cutoff (the half list's fixed-point range bound)
-    double ke;                  // Coulomb constant ONE_4PI_EPS0 (Handle::ke)
-    const double* erfc_tab;     // [kErfcDeg+1][kErfcMaxM] erfcx(x) on intervals of width 1/erfc_scale
-    const float* erfc_tab_f;    // [erfc_m_f][kErfcDegF+1] fp32 (mixed precision), width 1/erfc_scale_f
-    double erfc_scale; int erfc_m;
-    double erfc_scale_f; int erfc_m_f;
-    double rl2;                 // list radius^2: (rc + list skin)^2
-    int nb_cap;                 // capacity of ONE of the kSeg sub-lists
-    int nlr;                    // list rows = owned atoms; row c <-> sorted slot own_slot(c)
-    const int* own_s;           // [nlr] cell-sorted slots of the owned atoms (null: identity)
-    const int* flag;            // rebuild flag (list kernels exit when 0)
-    const int* atom_sorted; const int* key_sorted;
-    const int* cstart; const int* cend;
-    const double4* pos4s; const double2* ljs;
-    const int* typ_s;           // [N] LJ type per sorted slot (null: > kMaxLjTypes distinct types)
-    const double2* lj_tab; int lj_ntypes;   // per-type (sigma/2, 2 sqrt(eps))
-    const double* pos; const double* q;
-    const int* ex_start; const int* ex_list;
-    const double* dedq_self;
-    int* nl; int* nl_cnt;
-    double* dedq; double* f_part; double* e_atom;
-    // half list (single rank, fp64): pairs once, j-side summed in fixed point (k_pairs_half)
-    int half;
-    int* half_flag;             // device: 1 = the half-list evaluation cannot be used (k_excl rescans)
-    unsigned long long* win_out;// [ncell][kHalfMaxWin][4] per-cell window partials (fixed point)
-    int* win_woff;              // [ncell][kHalfWin] window offsets of the 18 window cells
-    const int* key_s;           // cell key per sorted slot
-    long long* fallback;        // [3] diagnostics (Handle::n_fallback_dev)
-};
-
-__device__ __forceinline__ int own_slot(const DirectArgs& a, int c) { return a.own_s ? a.own_s[c] : c; }
-
-// minimum image of a pair vector d = pos_i - pos_j: per axis d - L rint(d/L) (getDeltaRPeriodic's
-// floor(d/L + 0.5) up to exact half-box ties, which lie beyond the cutoff); a reduced triclinic
-// box subtracts c, b, a in that order (kernel-uniform branch)
-__device__ __forceinline__ void min_image(const DirectArgs& a, double& dx, double& dy, double& dz) {
-    // one branch-free sequence for both box kinds: with the off-diagonals T = 0 the shear
-    // terms subtract exact zeros, so an orthorhombic box gets the bits of the per-axis form
-    // (the two-branch version kept dx, dy, dz in scratch memory: 40 B per lane in k_pairs)
-    const double sc = rint(dz * a.invL.z);
-    dx -= sc * a.T.y; dy -= sc * a.T.z; dz -= sc * a.L.z;
-    const double sb = rint(dy * a.invL.y);
-    dx -= sb * a.T.x; dy -= sb * a.L.y;
-    dx -= a.L.x * rint(dx * a.invL.x);
-}
-
 // List layout: sub-list seg of row c holds its entries in chunks of kChunk = 4 consecutive
 // entries (16 B), chunk q of every row contiguous in row order:
 //   nl[((seg * nb_cap/4 + q) * nlr + c) * 4 + (k & 3)],  q = k / 4.
@@ -809,33 +733,6 @@ __global__ void __launch_bounds__(kWaveNL * kSeg) k_nlist_wave(DirectArgs a) {
     if (active) a.nl_cnt[(size_t)seg * a.nlr + c] = cnt;
 }
 
-struct PairAcc {
-    double fx = 0, fy = 0, fz = 0, dq = 0, e = 0;
-};
-
-struct PairAccF {   // mixed precision: fp32 forces / dE/dq, fp64 energy
-    float fx = 0, fy = 0, fz = 0, dq = 0;
-    double e = 0;
-};
-
-// erfc(x) = e^{-x^2} erfcx(x): erfcx from a piecewise degree-7 polynomial (interval table
-// in LDS, fitted at cf_create in long double, relative error ~4e-16 over [0, alpha*rc]),
-// and e^{-x^2} is shared with the force term -> one exp per pair instead of erfc + exp.
-// The table is coefficient-major, tab[j * kErfcMaxM + interval]: the 64 lanes of a read
-// fetch coefficient j of their (random) intervals from one contiguous run of doubles, so they
-// spread over the LDS banks.  (Interval-major rows of 8 doubles put every lane's read on one
-// of 4 bank groups: 6.8 conflict cycles per LDS instruction in the round-1 PMC pass.)
-__device__ __forceinline__ double erfc_exp(double x, const double* __restrict__ tab, double scale, double& e2) {
-    const double y = x * scale;
-    const int i = (int)y;
-    const double u = 2.0 * (y - (double)i) - 1.0;
-    const double* c = tab + i;
-    double p = c[kErfcDeg * kErfcMaxM];
-#pragma unroll
-    for (int j = kErfcDeg - 1; j >= 0; j--) p = fma(p, u, c[j * kErfcMaxM]);
-    e2 = exp_nonpos(-x * x);
-    return e2 * p;
-}
 
 // real-space Ewald + LJ pair (RCK:567-592), d = pos_i - pos_j (minimum image); tab = LDS
 // copy of the erfcx table (the cutoff test r <= rc guarantees alpha r lies inside it)
@@ -1057,20 +954,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))
 //     its block sets half_flag: k_excl then skips the windows and recomputes every
 //     atom's pair sums with the fp64 cell rescan.
 // ---------------------------------------------------------------------------------
-__device__ __forceinline__ unsigned long long to_fix(double v) {
-    return (unsigned long long)(__double_as_longlong(fma(v, kFixScale, kFixMagic)) - kFixMagicBits);
-}
-
-// the same for a value already scaled by 2^34: one add (literal operand) + one integer add
-__device__ __forceinline__ unsigned long long scaled_to_fix(double vs) {
-    return (unsigned long long)(__double_as_longlong(vs + kFixMagic) - kFixMagicBits);
-}
-
-__device__ __forceinline__ int3 half_offset(int k) {   // window cell k -> cell offset
-    return make_int3(k / 9, (k / 3) % 3 - 1, k % 3 - 1);
-}
-
-__device__ __forceinline__ int wrap_cell(int v, int n) { return v < 0 ? v + n : (v >= n ? v - n : v); }
 
 // MIXED: the pair term in fp32 as in k_pairs_mixed (pair vector minimum-imaged in fp64, then
 // rounded; fp32 forces and dE/dq per lane, fp64 energy), the partner side in the same fixed
@@ -1770,18 +1653,19 @@ void launch_cell_sort(Handle& h, const double* pos) {
     hipLaunchKernelGGL(k_cell_scatter, dim3(nblk(h.n, 256)), dim3(256), 0, h.stream, h.n, f, h.cell_key, h.atom_val,
                        h.cell_start, h.atom_tmp, ncell, h.cell_cnt, oc);
     hipLaunchKernelGGL(k_cell_order, dim3(nblk(ncell, 4)), dim3(256), 0, h.stream, ncell, f, h.cell_start,
-                       h.cell_end, h.atom_tmp, h.key_tmp, h.lo, h.hi, h.own_start, oc ? h.own_s : nullptr);
+                       h.cell_end, h.atom_tmp, h.key_tmp, h.lo, h.hi, h.own_start, oc ? h.own_s : nullptr, pos, L, T,
+                       nc, h.zcol);
     hipLaunchKernelGGL(k_cell_commit, dim3(nblk(h.n, 256)), dim3(256), 0, h.stream, h.n, f, h.cell_key, h.key_tmp,
                        pos, h.q, h.lj, L, T, h.cell_key_sorted, h.atom_sorted, h.pos4s, h.ljs,
                        h.atom_type, h.typ_s,
-                       h.pos_ref, h.n_builds_dev);
+                       h.pos_ref, h.n_builds_dev, h.cluster ? h.pos4f : nullptr, h.cluster ? h.slot_of : nullptr, nc);
 }
 
 void launch_force_rebuild(Handle& h) {
     check_hip(hipMemsetD32Async(h.skin_flag, 1, 1, h.stream), "set rebuild flag");
 }
 
-static DirectArgs direct_args(Handle& h, const double* pos, int include_forces) {
+DirectArgs direct_args(Handle& h, const double* pos, int include_forces) {
     DirectArgs a;
     a.n = h.n; a.lo = h.lo; a.hi = h.hi; a.include_forces = include_forces;
     a.L = make_double3(h.box_L[0], h.box_L[1], h.box_L[2]);
@@ -1813,10 +1697,19 @@ static DirectArgs direct_args(Handle& h, const double* pos, int include_forces) 
     a.win_woff = h.win_woff;
     a.key_s = h.cell_key_sorted;
     a.fallback = h.n_fallback_dev;
+    a.cl_start = h.cl_start; a.cl_info = h.cl_info; a.cpl = h.cpl; a.cpl_cnt = h.cpl_cnt; a.cpl_cap = h.cpl_cap;
+    a.pos4f = h.pos4f; a.slot_of = h.slot_of;
+    {   // fp32 prefilter: |d| from fp32 coordinates of magnitude <= ~2 L carries an error below 8 ulp(L)
+        const double Lmax = std::max(h.box_L[0], std::max(h.box_L[1], h.box_L[2])) + std::fabs(h.box_t[0]) +
+                            std::fabs(h.box_t[1]) + std::fabs(h.box_t[2]);
+        const double rcm = h.cutoff * (1.0 + 1e-5) + 8.0 * Lmax * 1.1920928955078125e-07;
+        a.rcm2f = (float)(rcm * rcm);
+    }
     return a;
 }
 
 void launch_nlist(Handle& h, const double* pos) {
+    if (h.cluster) { launch_cluster_list(h); return; }   // cf_kernels_cluster.hip
     DirectArgs a = direct_args(h, pos, 0);
     if (a.brute || h.nc[0] < 4 || h.nc[1] < 4 || h.nc[2] < 4)
         hipLaunchKernelGGL(k_nlist, dim3(nblk(a.nlr, 256)), dim3(256), 0, h.stream, a);
@@ -1825,6 +1718,7 @@ void launch_nlist(Handle& h, const double* pos) {
 }
 
 void launch_direct(Handle& h, const double* pos, int include_forces) {
+    if (h.cluster) { launch_pairs_cluster(h, pos, include_forces); return; }   // cf_kernels_cluster.hip
     DirectArgs a = direct_args(h, pos, include_forces);
     if (a.half) {
         const int ncell = h.nc[0] * h.nc[1] * h.nc[2];

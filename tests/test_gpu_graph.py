@@ -50,7 +50,10 @@ def test_graph_replay_is_bitwise_eager(algo, precision, skin):
     for (ea, fa), (eb, fb) in zip(a, b):
         assert ea == eb and np.array_equal(fa, fb)
     caps, reps = graph.graph_stats()
-    assert reps >= 4 and caps <= 4, (caps, reps)
+    # graphs per evaluation: one, or one per stream chain when the grid k-space runs on the
+    # second stream (cf_api.hip launch_full: flux + charges, reciprocal chain, direct chain)
+    segs = 3 if algo == 2 else 1
+    assert reps >= 4 * segs and caps <= 4 * segs, (caps, reps)
     assert eager.neighbor_stats() == graph.neighbor_stats()
 
 
@@ -192,6 +195,7 @@ def test_graph_replay_restores_reciprocal_dedq_split():
     e = torch.zeros(1, dtype=torch.float64, device="cuda")
     k.execute_device(pt, box, True, True, f, e)    # capture: forces
     k.execute_device(pt, box, False, True, None, e)  # capture: energy only
+    k.execute_device(pt, box, True, True, f, e)    # capture: forces
     k.execute_device(pt, box, True, True, f, e)    # replay: forces
     torch.cuda.synchronize()
     assert k.graph_stats()[1] >= 1

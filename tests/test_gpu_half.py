@@ -1,11 +1,12 @@
 """The half neighbour list (k_pairs_half, window sums in k_excl): every pair
 evaluated once (kept by the atom of the lower x cell, or within one x cell by the smaller x),
 the partner's share summed in 64-bit fixed point.  Used on one rank in fp64
-when the box has >= 4 cells per axis; CF_HALF=0 (read when a handle builds its cells) selects
+when the box has >= 4 cells per axis; CF_HALF=0 (latched by cf_create) selects
 the full two-sided list for comparison.
 
 Tolerances (written here): against the oracle forces <= 1e-8 kJ/mol/nm, energy <= 1e-9 |E| +
-1e-8; half vs full list forces <= 1e-9 (the fixed point rounds each j-side term to 2^-34).
+1e-8; half vs full list forces <= 2e-12 max|F| + 1e-9 (the fixed point rounds each j-side term to
+2^-34; the i-side sums run in another order).
 The fallbacks -- an overflowed list, a j-side term too large for the fixed point -- hand the
 evaluation to the fp64 cell rescan, which must give the same answer.
 """
@@ -29,18 +30,25 @@ def _need_gpu():
         pytest.skip("no HIP device")
 
 
-def _kernel(system, force, half, algo=0, skin=0.0, precision="double"):
-    old = os.environ.get("CF_HALF")
+def _kernel(system, force, half, algo=0, skin=0.0, precision="double", cluster=True, cap=0):
+    """half: the half list (cluster-pair form unless cluster=False: the per-atom half list,
+    CF_CLUSTER=0); else the full two-sided list (CF_HALF=0).  The variables are latched by
+    cf_create (initialize); cap: CF_CLUSTER_CAP, a cluster-pair list capacity that overflows."""
+    saved = {v: os.environ.get(v) for v in ("CF_HALF", "CF_CLUSTER", "CF_CLUSTER_CAP")}
     os.environ["CF_HALF"] = "1" if half else "0"
+    os.environ["CF_CLUSTER"] = "1" if cluster else "0"
+    if cap:
+        os.environ["CF_CLUSTER_CAP"] = str(cap)
     try:
         k = HipCalcCoulForceKernel(kspace_algo=algo, precision=precision).initialize(system, force)
         if skin:
             k.set_neighbor_skin(skin)
     finally:
-        if old is None:
-            del os.environ["CF_HALF"]
-        else:
-            os.environ["CF_HALF"] = old
+        for v, val in saved.items():
+            if val is None:
+                os.environ.pop(v, None)
+            else:
+                os.environ[v] = val
     return k
 
 
@@ -54,7 +62,7 @@ def test_half_list_matches_full_list_and_oracle(nw, algo):
     system, force, pos, box = ts.water_box(nw, cutoff=1.0, ewald_tol=1e-4, every_bond_angle=5)
     eh, fh, dh, th = _eval(_kernel(system, force, True, algo), pos, box)
     ef, ff, df, tf = _eval(_kernel(system, force, False, algo), pos, box)
-    assert np.abs(fh - ff).max() <= 1e-9, np.abs(fh - ff).max()
+    assert np.abs(fh - ff).max() <= 2e-12 * np.abs(ff).max() + 1e-9, np.abs(fh - ff).max()
     assert np.abs(dh - df).max() <= 1e-10 * np.abs(df).max()
     assert abs(th[2] - tf[2]) <= 1e-11 * abs(tf[2]) + 1e-9
     ref = Oracle(force, box).execute(pos, box)
@@ -89,11 +97,11 @@ def test_half_list_fallback_on_list_overflow():
     system.setDefaultPeriodicBoxVectors(*big)
     # (the checker is the full-list kernel on the same default box: the oracle's k-sum over the
     # 16x larger k-vector set of the wide default box takes minutes on one host core)
-    k = _kernel(system, force, True)
+    k = _kernel(system, force, True, cluster=False)   # (the cluster list sizes itself from the current box)
     ef, ff = _kernel(system, force, False).execute_host(pos, box)
     for _ in range(2):
         e, f = k.execute_host(pos, box)
-        assert np.abs(f - ff).max() <= 1e-9
+        assert np.abs(f - ff).max() <= 2e-12 * np.abs(ff).max() + 1e-9
         assert abs(e - ef) <= 1e-12 * abs(ef) + 1e-9
 
 
@@ -123,13 +131,16 @@ def _dense_overflow():
     return system, force, pos, box
 
 
-@pytest.mark.parametrize("make", [_sparse_gas, _dense_overflow], ids=["block_frame_misfit", "list_overflow"])
-def test_half_list_fallbacks_persist_over_kept_lists(make):
+@pytest.mark.parametrize("make,cluster,cap", [(_sparse_gas, False, 0), (_dense_overflow, False, 0), (_dense_overflow, True, 24)],
+                         ids=["block_frame_misfit", "list_overflow", "cluster_list_overflow"])
+def test_half_list_fallbacks_persist_over_kept_lists(make, cluster, cap):
     """A fallback raised when the list is BUILT (rows the builder could not encode, overflowed
     rows) must hold on every later evaluation that keeps that list under a skin: each step is
-    compared with the full list rebuilt from scratch (CF_HALF=0, skin 0) on the same positions."""
+    compared with the full list rebuilt from scratch (CF_HALF=0, skin 0) on the same positions.
+    (The cluster-pair list has no block frame: the sparse gas runs it without a fallback, checked
+    against the oracle below.)"""
     system, force, pos, box = make()
-    k = _kernel(system, force, True, skin=0.1)
+    k = _kernel(system, force, True, skin=0.1, cluster=cluster, cap=cap)
     ref = _kernel(system, force, False)
     rng = np.random.default_rng(11)
     x = pos.copy()
