@@ -30,14 +30,18 @@
 namespace cf {
 
 constexpr int kClSize = 4;               // atoms per cluster
-constexpr int kCqWaves = 16;             // waves per k_pairs_cq block (one cell)
+#ifndef CF_CQ_WAVES
+#define CF_CQ_WAVES 16
+#endif
+constexpr int kCqWaves = CF_CQ_WAVES;    // waves per k_pairs_cq block (one cell, one block per CU: the LDS)
 constexpr int kCqThreads = 64 * kCqWaves;
-constexpr int kCqQ = 88;                 // queue entries per i atom (a ring; what the LDS leaves: 160 KB)
+constexpr int kCqQ = kCqWaves > 12 ? 88 : 112;   // queue entries per i atom (a ring; what the 160 KB LDS leaves)
 constexpr int kCqBatch = 16;             // list entries tested per phase-A step (64 j atoms, one per lane)
 constexpr int kCqLpi = 16;               // phase-B lanes per i atom
 constexpr int kClBuildThreads = 512;
 constexpr int kClMaxCand = 1536;         // window clusters staged by k_cl_build (>= 4096 / 4 + 18 * 3)
-constexpr unsigned kClSelfMask = 0x08CEu;   // (il, jl) bits il*4 + jl with jl > il: a self pair's upper triangle
+constexpr unsigned kClSelfMask = 0x08CEu;
+typedef float v2f __attribute__((ext_vector_type(2)));   // (il, jl) bits il*4 + jl with jl > il: a self pair's upper triangle
 
 // window cell k of cell (cx, cy, cz): the wrapped cell index, and the vector from the cell's
 // corner to the window cell's (unwrapped) corner, in which frame pos4f (corner-relative fp32
@@ -342,15 +346,42 @@ __global__ void __launch_bounds__(kCqThreads) CF_LDS_UNPAIRED k_pairs_cq(DirectA
         int qh = 0;     // ring head, equal for the 4 queues (every phase-B step pops 16 from each)
 
         // phase B: lanes kk < qlen of each i atom evaluate the pair of queue entry qh + kk
+        // Prefetch: whenever every queue holds a full step, its entries and j coordinates are
+        // loaded at once (issue_pf) and used by the next phase B, which therefore does not wait
+        // for them.  Phase B runs while every queue holds 32 (keeping 16 in reserve for the next
+        // prefetch; the same lane efficiency as draining at 16: the ends of the lists decide it,
+        // tools/cluster_proto.py), so the prefetched loads complete during the next batch's tests.
+        bool pf_ok = false;   // (wave-uniform)
+        int pf_wq = 0;
+        double4 pf_pj = make_double4(0.0, 0.0, 0.0, 0.0);
+        auto all_ge = [&](int v) { return q0 >= v && q1 >= v && q2 >= v && q3 >= v; };
+        auto issue_pf = [&]() {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            pf_wq = qw[ring(qh + kk)];
+            pf_pj = a.pos4s[pf_wq & kHalfSlotMask];
+            pf_ok = true;
+        };
         auto phase_b = [&]() {
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            const int qlen = il == 0 ? q0 : (il == 1 ? q1 : (il == 2 ? q2 : q3));
+            // this lane's queue length: the four packed one byte each (lengths < 256)
+            const unsigned qpack = (unsigned)q0 | ((unsigned)q1 << 8) | ((unsigned)q2 << 16) | ((unsigned)q3 << 24);
+            const int qlen = (int)((qpack >> (8 * il)) & 255u);
             const bool act = kk < qlen;
-            const int wq = act ? qw[ring(qh + kk)] : islot;
+            int wq;
+            double4 pj;
+            if (pf_ok) {
+                wq = pf_wq;
+                pj = pf_pj;
+                pf_ok = false;
+            } else {
+                wq = act ? qw[ring(qh + kk)] : islot;
+                pj = a.pos4s[wq & kHalfSlotMask];
+            }
             const int j = wq & kHalfSlotMask;
-            const double4 pj = a.pos4s[j];
             const double3 wr = shd[(wq >> kHalfSlotBits) & 31];
             // the pair vector to j's image next to the cell: the wrap translation of j's window cell
             // (for a pair within rc < L/2 the same image, and for an orthorhombic box the same bits,
@@ -402,12 +433,17 @@ __global__ void __launch_bounds__(kCqThreads) CF_LDS_UNPAIRED k_pairs_cq(DirectA
                 }
                 qh = ring(qh + kCqLpi);
                 q0 = max(q0 - kCqLpi, 0); q1 = max(q1 - kCqLpi, 0); q2 = max(q2 - kCqLpi, 0); q3 = max(q3 - kCqLpi, 0);
+                if (all_ge(kCqLpi)) issue_pf();
                 return;
             }
             const double2 lj = TYPES ? ljt[(unsigned)wq >> kShiftBits] : a.ljs[j];
             const double dx = ddx, dy = ddy, dz = ddz;
             const double r2 = dx * dx + dy * dy + dz * dz;
+#if defined(CF_CQ_ABL) && CF_CQ_ABL == 1
+            if (act && r2 < 0.0) {   // ablation: no pair term
+#else
             if (act && r2 <= a.rc2) {   // exact voxel-hash test (RCK:567-569)
+#endif
                 const int slot = wdel[(wq >> kHalfSlotBits) & 31] + j;
                 const double ke = a.ke;
                 const double two_over_sqrtpi = 1.1283791670955126;
@@ -431,15 +467,20 @@ __global__ void __launch_bounds__(kCqThreads) CF_LDS_UNPAIRED k_pairs_cq(DirectA
                     acc.fx += nfx; acc.fy += nfy; acc.fz += nfz;
                     acc.dq += qj * ec;
                     bad |= !(fmax(fabs(ndEdRs) * a.rc, fabs(dqjs)) < kFixMax * kFixScale);
+#if !(defined(CF_CQ_ABL) && CF_CQ_ABL == 2)
                     atomicAdd(&accw[0][slot], scaled_to_fix(nfx));
                     atomicAdd(&accw[1][slot], scaled_to_fix(nfy));
                     atomicAdd(&accw[2][slot], scaled_to_fix(nfz));
                     atomicAdd(&accw[3][slot], scaled_to_fix(dqjs));
+#else
+                    acc.e += (double)slot * 1e-300;   // ablation: no partner-side atomics
+#endif
                 }
                 acc.e += qq * ec + es6 * (sig6 - 1);   // the whole pair energy: each pair once
             }
             qh = ring(qh + kCqLpi);
             q0 = max(q0 - kCqLpi, 0); q1 = max(q1 - kCqLpi, 0); q2 = max(q2 - kCqLpi, 0); q3 = max(q3 - kCqLpi, 0);
+            if (all_ge(kCqLpi)) issue_pf();
         };
 
         // phase A: a batch of 16 entries = 64 j atoms, one per lane (entry el, atom jl), each tested
@@ -461,12 +502,18 @@ __global__ void __launch_bounds__(kCqThreads) CF_LDS_UNPAIRED k_pairs_cq(DirectA
             const float xj = pj_c.x + sh.x, yj = pj_c.y + sh.y, zj = pj_c.z + sh.z;
             unsigned long long m[4];
             int cnt[4];
+            // two i atoms per packed-fp32 instruction (v_pk_add / v_pk_mul / v_pk_fma_f32)
+            const unsigned bits = (en_c.y >> jl) & 0x1111u;   // bit 4k: pair (i atom k, this j) listed
 #pragma unroll
-            for (int k = 0; k < 4; k++) {
-                const float dx = pif[k].x - xj, dy = pif[k].y - yj, dz = pif[k].z - zj;
-                const bool hit = ((en_c.y >> (4 * k + jl)) & 1u) && fmaf(dx, dx, fmaf(dy, dy, dz * dz)) <= a.rcm2f;
-                m[k] = __ballot(hit);
+            for (int k = 0; k < 4; k += 2) {
+                const v2f dx = v2f{pif[k].x, pif[k + 1].x} - v2f{xj, xj};
+                const v2f dy = v2f{pif[k].y, pif[k + 1].y} - v2f{yj, yj};
+                const v2f dz = v2f{pif[k].z, pif[k + 1].z} - v2f{zj, zj};
+                const v2f r2 = dx * dx + dy * dy + dz * dz;
+                m[k] = __ballot(((bits >> (4 * k)) & 1u) && r2.x <= a.rcm2f);
+                m[k + 1] = __ballot(((bits >> (4 * k + 4)) & 1u) && r2.y <= a.rcm2f);
                 cnt[k] = __popcll(m[k]);
+                cnt[k + 1] = __popcll(m[k + 1]);
             }
             // room for this batch's hits, then queue them
             while (q0 + cnt[0] > kCqQ || q1 + cnt[1] > kCqQ || q2 + cnt[2] > kCqQ || q3 + cnt[3] > kCqQ) phase_b();
@@ -481,7 +528,8 @@ __global__ void __launch_bounds__(kCqThreads) CF_LDS_UNPAIRED k_pairs_cq(DirectA
                 }
             }
             q0 += cnt[0]; q1 += cnt[1]; q2 += cnt[2]; q3 += cnt[3];
-            while (q0 >= kCqLpi && q1 >= kCqLpi && q2 >= kCqLpi && q3 >= kCqLpi) phase_b();   // full steps
+            if (!pf_ok && all_ge(kCqLpi)) issue_pf();
+            while (all_ge(2 * kCqLpi)) phase_b();   // full steps, one in reserve
             en_c = en_n; pj_c = pj_n; en_n = en_nn;
         }
         while (q0 > 0 || q1 > 0 || q2 > 0 || q3 > 0) phase_b();   // the rest, partly filled
