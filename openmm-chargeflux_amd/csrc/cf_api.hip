@@ -212,9 +212,12 @@ void set_cells(cf_handle* H, const double L[3]) {
         h.win_cells = (int)ncell;
         h.alloc_epoch++;
     }
-    // cluster-pair half list (cf_kernels_cluster.hip): one rank, fp64 or mixed,
-    // wherever the per-atom half list applies; CF_CLUSTER=0 keeps the per-atom list (A/B and tests)
-    h.cluster = h.half && !h.env_no_cluster;
+    // cluster-pair half list (cf_kernels_cluster.hip): one rank, fp64, wherever
+    // the per-atom half list applies.  Mixed precision keeps the per-atom list by default: its
+    // fp32 term is cheap, so the cluster kernel's phase A (the fp32 atom tests and the queueing)
+    // costs more than it saves (C5: 1.425 vs 1.235 ms, profiles/r04e_*); CF_CLUSTER=1 forces it
+    // (tests), CF_CLUSTER=0 keeps the per-atom list in fp64 (A/B and tests)
+    h.cluster = h.half && (h.env_cluster == 1 || (h.env_cluster < 0 && !h.mixed));
     h.zcol = 0;
     if (h.cluster) {
         // within-cell z-columns of ~12 atoms (k_cell_order): clusters of 4 consecutive slots stay compact
@@ -485,7 +488,8 @@ CF_EXPORT int cf_create(const cf_params* p, const cf_options* opt, cf_handle** o
         h.overlap = !(getenv("CF_OVERLAP") && std::string(getenv("CF_OVERLAP")) == "0");   // A/B
         // list-kind switches for A/B runs and tests, latched here (set_cells runs again on every rebuild)
         h.env_no_half = getenv("CF_HALF") && std::string(getenv("CF_HALF")) == "0";
-        h.env_no_cluster = getenv("CF_CLUSTER") && std::string(getenv("CF_CLUSTER")) == "0";
+        // CF_CLUSTER: "0" never the cluster-pair list, "1" also in mixed precision, unset: fp64 only
+        h.env_cluster = getenv("CF_CLUSTER") ? (std::string(getenv("CF_CLUSTER")) == "0" ? 0 : 1) : -1;
         h.env_cluster_cap = getenv("CF_CLUSTER_CAP") ? atoi(getenv("CF_CLUSTER_CAP")) : 0;
         h.kspace_algo = o.kspace_algo;
         h.stream = (hipStream_t)o.stream;  // NULL = the null stream (orders with torch's default stream)

@@ -80,6 +80,7 @@ struct GridPlan {
     bool dft8 = false;       // every axis qualifies and CF_DFT8 != 0
     bool spread_dpp = true;  // spread FMAs take the x taps by DPP row broadcast (CF_SPREAD_DPP=0: scalar loads)
     int spread_pass = 32;    // atoms per staging pass of the W > 9 spread (CF_SPREAD_PASS=64: A/B)
+    bool spread_mfma = true; // the spread on the fp64 matrix cores, 16x8x8 tiles (CF_SPREAD_MFMA=0: k_g_spread_tile)
     bool interp2 = true;     // two atoms per wave, taps by DPP row broadcast (CF_INTERP2=0: k_g_interp)
     bool interp4 = true;     // W <= 8: four atoms per wave (CF_INTERP4=0: k_g_interp2)
 };
@@ -181,7 +182,8 @@ struct Handle {
     // cluster-pair half list (cf_kernels_cluster.hip): one rank, same window and
     // fixed-point j side as the half list; clusters = runs of <= 4 consecutive sorted slots of one cell
     bool cluster = false;
-    bool env_no_half = false, env_no_cluster = false;   // CF_HALF=0 / CF_CLUSTER=0 at cf_create
+    bool env_no_half = false;   // CF_HALF=0 at cf_create
+    int env_cluster = -1;       // CF_CLUSTER at cf_create: 0, 1, or -1 (unset: fp64 only)
     int env_cluster_cap = 0;    // CF_CLUSTER_CAP at cf_create (tests: a capacity that overflows)
     int zcol = 0;               // columns per cell axis of the within-cell sort (k_cell_order; 0 = atom order)
     int ncl_cap = 0;            // cluster capacity: N/4 + ncell

@@ -526,6 +526,212 @@ __global__ void __launch_bounds__(256) CF_LDS_UNPAIRED k_g_spread_tile(int3 ng, 
     }
 }
 
+typedef double d4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ d4 mfma64(double a, double b, d4 c) {
+    return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+}
+
+// Round 4: the spread as an fp64 matrix-core contraction (`CF_SPREAD_MFMA=0`: k_g_spread_tile).
+// One 256-thread workgroup per 16 (x) x 8 (y) x 8 (z) tile, whose 1024 points are
+//     G[x][(y, z)] = sum_a X_a[x] (Y_a[y] Z_a[z])
+// over the tile's source atoms: per group of 4 atoms one v_mfma_f64_16x16x4_f64 per 16 (y, z)
+// columns, A = the 4 atoms' x windows (lane l: x = l & 15 of atom l >> 4), B = Y Z products
+// (lane l: atom l >> 4, column 16 nb + (l & 15), one multiply per lane), so the FMAs leave the
+// VALU (k_g_spread_tile: 1 mul + 8 VALU FMAs per (tile, atom) per lane plus the DPP
+// bookkeeping).  The tile is 16 wide in x so that M = 16 is the x axis with no padding; its
+// sources are the atoms whose first tap lies in the (NS + 1) x NS x NS sort bins (8^3 each, the
+// bins of k_g_bin) that can reach it: x bins 2 tx - dxb, dxb = -1 .. NS - 1, y and z bins as the
+// 8^3 tile's.  A source's x window is 16 points of its bin-aligned 24-point row starting at
+// 8 dxb (the row is zero outside [0, 24), so the two 8-point halves are row windows dxb and
+// dxb + 1, or zeros); y and z windows as before.  Passes of kP atoms staged structure-of-arrays
+// (X[kP][16], Y[kP][8], Z[kP][8]: the A reads of a wave are 512 contiguous bytes, the B reads
+// broadcast), double-buffered; the 4 waves take every 4th group of 4 atoms and keep the whole
+// tile (4 accumulators of 16 x 16 per wave), summed in fixed wave order at the end: every output
+// is the same sum in the same order on every run (bitwise reproducible), though not the VALU
+// kernel's order (equal to it to ~1e-15 relative).  When ng.x is an odd multiple of 8 (C5: 264)
+// the last x tile covers 8 planes: bin 2 tx + 1 wraps to bin 0, whose atoms reach only the
+// tile's missing half (rows < 0 are zero), and only the planes x < ng.x are written.
+template <int NS, int kP>
+__global__ void __launch_bounds__(256) k_g_spread_mfma(int3 ng, int3 nb, const int* __restrict__ start,
+                                                       const double* __restrict__ taps, const int4* __restrict__ g0s,
+                                                       double* __restrict__ grid, const int* __restrict__ xr, int W) {
+    constexpr int NBX = NS + 1;              // x bins per tile: dxb = ix - 1, ix < NBX
+    constexpr int NSRC = NBX * NS * NS;
+    static_assert(NS <= 3 && NSRC <= 256, "bin offsets are packed in 2 bits per axis");
+    static_assert(kP % 16 == 0, "groups of 4 atoms, 4 waves");
+    constexpr int kBufD = kP * 32;           // X 16 + Y 8 + Z 8 doubles per atom
+    constexpr int kStD = 2 * kBufD > 4 * 1024 ? 2 * kBufD : 4 * 1024;
+    __shared__ __attribute__((aligned(16))) double st[kStD];   // 2 staging buffers; reused by the reduction
+    __shared__ int bin_start[NSRC], bin_pre[NSRC + 1], bin_db[NSRC];
+    __shared__ int src[kSpMaxSrc];   // slot << 6 | ix << 4 | dy << 2 | dz of the kept sources
+    __shared__ int wcnt[4 * (kSpMaxSrc / 256)];
+    const int nyz = nb.y * nb.z;
+    int tile = blockIdx.x;
+    if (nyz % 8 == 0) {   // XCD-aware order, as k_g_spread_tile
+        const int per = nyz / 8, i = blockIdx.x / 8;
+        tile = (i / per) * nyz + (blockIdx.x % 8) * per + i % per;
+    }
+    const int tz = tile % nb.z, ty = (tile / nb.z) % nb.y, tx = tile / nyz;
+    const int xlim = min(16, ng.x - 16 * tx);   // 8 for the last tile when ng.x is an odd multiple of 8
+    if (!x_range_in_slab(16 * tx, 16 * tx + xlim - 1, xr, W, ng.x)) return;
+    const int t = threadIdx.x;
+    if (t < NSRC) {
+        const int ix = t / (NS * NS), dy = (t / NS) % NS, dz = t % NS;
+        const int b = (wrapb(2 * tx + 1 - ix, nb.x) * nb.y + wrapb(ty - dy, nb.y)) * nb.z + wrapb(tz - dz, nb.z);
+        const int s0 = start[b];
+        bin_start[t] = s0;
+        bin_pre[t + 1] = start[b + 1] - s0;
+        bin_db[t] = (ix << 8) | (dy << 4) | dz;
+    }
+    __syncthreads();
+    if (t == 0) {
+        bin_pre[0] = 0;
+        for (int i = 0; i < NSRC; i++) bin_pre[i + 1] += bin_pre[i];
+    }
+    __syncthreads();
+    const int total = bin_pre[NSRC];
+    const int lane = t & 63, w = wave_id();
+    const int k = lane >> 4, c = lane & 15;   // MFMA operand lane: atom k of the group, x / column c
+    d4 acc[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++) acc[q] = d4{0.0, 0.0, 0.0, 0.0};
+    for (int seg0 = 0; seg0 < total; seg0 += kSpMaxSrc) {
+        const int nall = min(kSpMaxSrc, total - seg0);
+        __syncthreads();   // previous segment's passes done with src
+        constexpr int kRounds = kSpMaxSrc / 256;
+        int2 sb[kRounds];
+        int4 g[kRounds];
+#pragma unroll
+        for (int r = 0; r < kRounds; r++) {
+            const int u = 256 * r + t;
+            sb[r] = make_int2(0, 0);
+            if (u < nall) {
+                const int a = seg0 + u;
+                int lo = 0, hi = NSRC;
+                while (hi - lo > 1) {
+                    const int mid = (lo + hi) >> 1;
+                    if (bin_pre[mid] <= a) lo = mid; else hi = mid;
+                }
+                sb[r] = make_int2(bin_start[lo] + (a - bin_pre[lo]), lo);
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < kRounds; r++) g[r] = 256 * r + t < nall ? g0s[sb[r].x] : make_int4(0, 0, 0, 0);
+        bool keep[kRounds];
+        unsigned long long m[kRounds];
+        int dbits[kRounds];
+#pragma unroll
+        for (int r = 0; r < kRounds; r++) {
+            const int db = bin_db[sb[r].y];
+            const int ix = db >> 8, dy = (db >> 4) & 15, dz = db & 15;
+            dbits[r] = (ix << 4) | (dy << 2) | dz;
+            // the x taps [rx, rx + W) of the row reach the tile's points [8 (ix - 1), 8 (ix - 1) + 16)
+            keep[r] = 256 * r + t < nall && (g[r].x & 7) + W > 8 * (ix - 1) && (g[r].y & 7) + W > 8 * dy &&
+                      (g[r].z & 7) + W > 8 * dz;
+            m[r] = __ballot(keep[r]);
+            if ((t & 63) == 0) wcnt[4 * r + (t >> 6)] = __popcll(m[r]);
+        }
+        __syncthreads();
+        int nseg = 0;
+#pragma unroll
+        for (int r = 0; r < kRounds; r++) {
+            int off = nseg;
+            for (int q = 0; q < (t >> 6); q++) off += wcnt[4 * r + q];
+            if (keep[r]) src[off + __popcll(m[r] & ((1ull << (t & 63)) - 1))] = (sb[r].x << 6) | dbits[r];
+            nseg += wcnt[4 * r] + wcnt[4 * r + 1] + wcnt[4 * r + 2] + wcnt[4 * r + 3];
+        }
+        __syncthreads();
+        if (nseg == 0) continue;
+        // staging: 16-B piece e = t & 15 of atoms a = (t >> 4) + 16 q: e < 8 x (half e >> 2),
+        // 8..11 y, 12..15 z -- the same piece kind for every q, so its axis, the bits of the
+        // source word that pick its window, the window adjustment and the LDS address pattern are
+        // per-thread constants (selects, no branches); atoms past the pass end are zero windows
+        // (the last group of 4 is read whole)
+        constexpr int kPer = kP * 16 / 256;
+        const int e = t & 15, a0 = t >> 4;
+        const int axis = e < 8 ? 0 : (e < 12 ? 1 : 2);
+        const int fsh = 4 - 2 * axis;                   // source-word bits of this axis's window
+        const int wadj = axis == 0 ? (e >> 2) - 1 : 0;  // x: window dxb + half
+        const int poff = kRow * axis + 2 * (e & 3);
+        const int dbase = axis == 0 ? 2 * e : (axis == 1 ? 16 * kP : 24 * kP) + 2 * (e & 3);
+        const int dstr = axis == 0 ? 16 : 8;            // doubles per atom in this piece's array
+        // two passes ahead: pass p + 2's loads are issued as pass p starts and have two passes of
+        // MFMAs (2 x 16 per wave at kP = 64) to land before they are staged (one pass ahead left
+        // every wave waiting on them: 33 % of wave cycles waiting, the MFMA pipe ~40 % busy)
+        v2d rva[kPer], rvb[kPer];
+        auto fetch = [&](v2d (&rv)[kPer], int p) {
+            const int base = p * kP, n = min(kP, nseg - base);
+#pragma unroll
+            for (int q = 0; q < kPer; q++) {
+                const int a = a0 + 16 * q;
+                const int s = src[base + min(a, n - 1)];
+                const int wi = ((s >> fsh) & 3) + wadj;
+#if defined(CF_SPM_ABL) && CF_SPM_ABL == 2   // ablation: no tap loads (timing only)
+                const v2d v = v2d{(double)s, (double)(wi + poff)};
+#else
+                const v2d v = *reinterpret_cast<const v2d*>(taps + (size_t)(s >> 6) * kTapStride + poff + 8 * max(wi, 0));
+#endif
+                rv[q] = a < n && (unsigned)wi <= 2u ? v : v2d{0.0, 0.0};
+            }
+        };
+        auto stage = [&](const v2d (&rv)[kPer], int p) {
+            double* buf = st + (p & 1) * kBufD;
+#pragma unroll
+            for (int q = 0; q < kPer; q++)
+                *reinterpret_cast<v2d*>(buf + dbase + dstr * (a0 + 16 * q)) = rv[q];
+        };
+        const int npass = (nseg + kP - 1) / kP;
+        // pass p: `nxt` holds pass p + 1 (loaded during pass p - 1), `fre` receives pass p + 2
+        auto pass = [&](int p, v2d (&fre)[kPer], const v2d (&nxt)[kPer]) {
+            if (p + 2 < npass) fetch(fre, p + 2);
+            const int n = min(kP, nseg - p * kP);
+            const double* buf = st + (p & 1) * kBufD;
+            const double* xb = buf + c;
+            const double* yb = buf + 16 * kP + (c >> 3);
+            const double* zb = buf + 24 * kP + (c & 7);
+            const int ngr = (n + 3) >> 2;
+            for (int gi = w; gi < ngr; gi += 4) {
+                const int a = 4 * gi + k;
+                const double xa = xb[16 * a];
+                const double za = zb[8 * a];
+                const double* ya = yb + 8 * a;
+#if defined(CF_SPM_ABL) && CF_SPM_ABL == 1   // ablation: no MFMAs (timing only)
+                acc[0][0] += xa * ya[0] * za;
+#else
+#pragma unroll
+                for (int q = 0; q < 4; q++) acc[q] = mfma64(xa, ya[2 * q] * za, acc[q]);
+#endif
+            }
+            if (p + 1 < npass) stage(nxt, p + 1);
+            __syncthreads();
+        };
+        fetch(rva, 0);
+        if (npass > 1) fetch(rvb, 1);
+        stage(rva, 0);
+        __syncthreads();
+        for (int p = 0; p < npass; p += 2) {
+            pass(p, rva, rvb);
+            if (p + 1 < npass) pass(p + 1, rvb, rva);
+        }
+    }
+    // the 4 waves' partial tiles, summed in fixed wave order; acc[q][i] of lane l is the point
+    // x = (l >> 4) + 4 i, (y, z) column 16 q + (l & 15)
+    __syncthreads();
+    double* red = st;   // [4][16 x][64 (y, z)]
+#pragma unroll
+    for (int q = 0; q < 4; q++)
+#pragma unroll
+        for (int i = 0; i < 4; i++) red[w * 1024 + (k + 4 * i) * 64 + 16 * q + c] = acc[q][i];
+    __syncthreads();
+#pragma unroll
+    for (int h = 0; h < 4; h++) {
+        const int pt = t + 256 * h, x = pt >> 6, l = pt & 63;
+        const double v = ((red[pt] + red[1024 + pt]) + red[2048 + pt]) + red[3072 + pt];
+        if (x < xlim) grid[((size_t)(16 * tx + x) * ng.y + 8 * ty + (l >> 3)) * ng.z + 8 * tz + (l & 7)] = v;
+    }
+}
+
 // ---------------------------------------------------------------------------------
 // 3. pruned DFT stages
 // ---------------------------------------------------------------------------------
@@ -559,12 +765,6 @@ struct CGemm {
     const int* xr = nullptr;
     int W = 0, ngx = 0;
 };
-
-typedef double d4 __attribute__((ext_vector_type(4)));
-
-__device__ __forceinline__ d4 mfma64(double a, double b, d4 c) {
-    return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
-}
 
 constexpr int kGBK = 16;   // k per LDS chunk (4 MFMA k-steps)
 
@@ -1741,6 +1941,8 @@ void grid_plan(Handle& h, int width, double sigma) {
     p.spread_dpp = !(sd && sd[0] == '0');
     const char* sp = getenv("CF_SPREAD_PASS");
     p.spread_pass = sp ? std::atoi(sp) : 32;
+    const char* sm = getenv("CF_SPREAD_MFMA");
+    p.spread_mfma = !(sm && sm[0] == '0');
     const char* i2 = getenv("CF_INTERP2");
     p.interp2 = !(i2 && i2[0] == '0');
     const char* i4 = getenv("CF_INTERP4");
@@ -1854,6 +2056,22 @@ void launch_grid_spread(Handle& h) {
     const int3 ng = make_int3(p.ng[0], p.ng[1], p.ng[2]), nb = make_int3(p.nb[0], p.nb[1], p.nb[2]);
 #define CF_SPT(NS_, P_, D_) hipLaunchKernelGGL((k_g_spread_tile<NS_, P_, D_>), dim3(p.nbins), dim3(256), 0, h.stream, \
                                                ng, nb, h.g_start, h.g_taps, h.g_g0s, h.g_grid, h.g_xrange, p.W)
+    if (p.spread_mfma && nb.x >= 4) {   // the matrix-core form: 16 x 8 x 8 tiles (4 distinct x bins)
+        const dim3 g((unsigned)((ng.x + 15) / 16 * nb.y * nb.z));
+        if (p.W <= 9)
+            hipLaunchKernelGGL((k_g_spread_mfma<2, 64>), g, dim3(256), 0, h.stream, ng, nb, h.g_start, h.g_taps,
+                               h.g_g0s, h.g_grid, h.g_xrange, p.W);
+        else if (p.spread_pass == 128)   // A/B (CF_SPREAD_PASS=128 / 32)
+            hipLaunchKernelGGL((k_g_spread_mfma<3, 128>), g, dim3(256), 0, h.stream, ng, nb, h.g_start, h.g_taps,
+                               h.g_g0s, h.g_grid, h.g_xrange, p.W);
+        else if (p.spread_pass == 32)
+            hipLaunchKernelGGL((k_g_spread_mfma<3, 32>), g, dim3(256), 0, h.stream, ng, nb, h.g_start, h.g_taps,
+                               h.g_g0s, h.g_grid, h.g_xrange, p.W);
+        else
+            hipLaunchKernelGGL((k_g_spread_mfma<3, 64>), g, dim3(256), 0, h.stream, ng, nb, h.g_start, h.g_taps,
+                               h.g_g0s, h.g_grid, h.g_xrange, p.W);
+        return;
+    }
     // a first tap in bin B reaches tiles B .. B + NS - 1: NS = 2 when W <= 9 (8 source bins per
     // tile instead of 27).  Passes of 32 atoms at W = 14 (64 / 128 measured slower at C3)
     if (p.W <= 9) {

@@ -302,3 +302,55 @@ def test_grid_interp4_matches_interp(monkeypatch, case, width):
         assert e1 == e0
         assert np.abs(f1 - f0).max() <= 1e-12 * np.abs(f0).max(), np.abs(f1 - f0).max()
         assert np.abs(d1 - d0).max() <= 1e-12 * np.abs(d0).max(), np.abs(d1 - d0).max()
+
+
+def _odd_tile_box():
+    """A water box whose grid has an odd number of 8-point bins along x (ng = round8(2 (2K - 1)),
+    cf_kernels_grid.hip grid_plan), so the matrix-core spread's last 16-wide x tile is a half tile."""
+    for n in (700, 900, 1100, 1300, 1500, 1800, 2100):
+        system, force, pos, box = ts.water_box(n, cutoff=0.9, ewald_tol=1e-4)
+        k = HipCalcCoulForceKernel(kspace_algo=GRID).initialize(system, force)
+        kx = k.ewald_params()[1][0]
+        k.destroy()
+        if ((-(-2 * (2 * kx - 1) // 8)) % 2) == 1:
+            return system, force, pos, box
+    pytest.skip("no odd-bin box among the sizes tried")
+
+
+@pytest.mark.parametrize("case,width", [("C2", 14), ("w4k", 14), ("w4k", 13), ("w4k", 11), ("w4k", 8), ("w4k", 5),
+                                        ("small", 14), ("tric", 12), ("odd", 14), ("odd", 8)])
+def test_grid_spread_mfma_matches_vector_spread(monkeypatch, case, width):
+    """The matrix-core spread (k_g_spread_mfma: 16x8x8 tiles, v_mfma_f64_16x16x4 over groups of
+    4 source atoms) against the vector spread (CF_SPREAD_MFMA=0, k_g_spread_tile): the same
+    grid sums in another order, so energy, forces and dE/dq equal to <= 1e-12 relative, and the
+    matrix form bitwise reproducible run to run.  'small' has a small grid (few x-bins per
+    16-wide tile), 'tric' a reduced triclinic box, 'odd' an odd number of x-bins (a half tile
+    at the end of every x row, as C5's 264-point grid)."""
+    if case == "C2":
+        system, force, pos, box = ts.make("C2")
+    elif case == "small":
+        system, force, pos, box = ts.water_box(300, cutoff=0.9, ewald_tol=1e-4)
+    elif case == "tric":
+        system, force, pos, box = ts.water_box(2000, cutoff=0.9, ewald_tol=1e-4)
+        box = box.copy()
+        box[1, 0] = 0.3 * box[0, 0]
+        box[2, 0] = -0.2 * box[0, 0]
+        box[2, 1] = 0.25 * box[1, 1]
+        system.setDefaultPeriodicBoxVectors(*box)
+    elif case == "odd":
+        system, force, pos, box = _odd_tile_box()
+    else:
+        system, force, pos, box = ts.water_box(4000, cutoff=1.0, ewald_tol=1e-4, every_bond_angle=5)
+    out = []
+    for flag in ("0", "1", "1"):
+        monkeypatch.setenv("CF_SPREAD_MFMA", flag)
+        k = HipCalcCoulForceKernel(kspace_algo=GRID, grid_width=width).initialize(system, force)
+        e, f = k.execute_host(pos, box)
+        out.append((e, f, k.dedq(), k.energy_terms()))
+        k.destroy()
+    (e0, f0, d0, t0), (e1, f1, d1, _), (e2, f2, d2, _) = out
+    scale = sum(abs(t) for t in t0)
+    assert abs(e1 - e0) <= 1e-12 * scale, (e0, e1)
+    assert np.abs(f1 - f0).max() <= 1e-12 * np.abs(f0).max(), np.abs(f1 - f0).max()
+    assert np.abs(d1 - d0).max() <= 1e-12 * np.abs(d0).max(), np.abs(d1 - d0).max()
+    assert e2 == e1 and np.array_equal(f2, f1) and np.array_equal(d2, d1)

@@ -172,10 +172,12 @@ def test_half_list_sparse_gas_matches_oracle_with_skin():
         x = x + rng.normal(scale=0.002, size=x.shape)
 
 
-def test_half_list_mixed_precision():
-    # the fp32 half-list kernel against the fp32 full list and the fp64 half list (same k-space)
+@pytest.mark.parametrize("cluster", [False, True], ids=["atom_list", "cluster_list"])
+def test_half_list_mixed_precision(cluster):
+    # the fp32 half-list kernel (the per-atom list, the mixed default, and the cluster-pair list,
+    # CF_CLUSTER=1) against the fp32 full list and the fp64 half list (same k-space)
     system, force, pos, box = ts.water_box(4000, cutoff=1.0, ewald_tol=1e-4, every_bond_angle=5)
-    em, fm, dm, tm = _eval(_kernel(system, force, True, 0, precision="mixed"), pos, box)
+    em, fm, dm, tm = _eval(_kernel(system, force, True, 0, precision="mixed", cluster=cluster), pos, box)
     ef, ff, df, tf = _eval(_kernel(system, force, False, 0, precision="mixed"), pos, box)
     ed, fd, dd, td = _eval(_kernel(system, force, True, 0), pos, box)
     rms = lambda a, b: np.sqrt(((a - b) ** 2).sum(1).mean() / (b ** 2).sum(1).mean())

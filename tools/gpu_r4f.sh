@@ -5,8 +5,8 @@ out=gpurun_out/r4f
 mkdir -p $out
 step() { local rc=$1 name=$2; echo "$name rc=$rc"; [ $rc -eq 0 ] || exit $rc; }
 L=openmm-chargeflux_amd/libchargeflux_hip.so
-cp $L tmp_ab/libchargeflux_hip_intree.so
-use() { cp tmp_ab/libchargeflux_hip_$1.so $L; }
+cp $L tmp_ab/libchargeflux_hip_intree.so || exit 3
+use() { cp tmp_ab/libchargeflux_hip_$1.so $L || exit 3; }
 for v in w16 w12; do
     use $v
     timeout -k 10 300 python -u -m pytest tests/test_gpu_cluster.py -x -q --timeout 150 --timeout-method thread > $out/tests_$v.log 2>&1; rc=$?; tail -1 $out/tests_$v.log; step $rc tests_$v

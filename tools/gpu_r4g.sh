@@ -5,10 +5,10 @@ out=gpurun_out/r4g
 mkdir -p $out
 step() { local rc=$1 name=$2; echo "$name rc=$rc"; [ $rc -eq 0 ] || exit $rc; }
 L=openmm-chargeflux_amd/libchargeflux_hip.so
-cp $L tmp_ab/libchargeflux_hip_intree.so
+cp $L tmp_ab/libchargeflux_hip_intree.so || exit 3
 R=$GRAFT_REPO_ROOT
 for v in w16 abl1 abl2 atom; do
-    if [ $v = atom ]; then cp tmp_ab/libchargeflux_hip_w16.so $L; export CF_CLUSTER=0; else cp tmp_ab/libchargeflux_hip_$v.so $L; unset CF_CLUSTER; fi
+    if [ $v = atom ]; then cp tmp_ab/libchargeflux_hip_w16.so $L || exit 3; export CF_CLUSTER=0; else cp tmp_ab/libchargeflux_hip_$v.so $L || exit 3; unset CF_CLUSTER; fi
     (cd /tmp && export TMPDIR=/tmp && CF_OVERLAP=0 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/$out/tr_$v -o run --output-format csv -- python3 $R/tools/pair_ablation.py --evals 20 > $R/$out/tr_$v.log 2>&1); step $? tr_$v
 done
 unset CF_CLUSTER
