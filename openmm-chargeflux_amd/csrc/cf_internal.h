@@ -80,7 +80,8 @@ struct GridPlan {
     bool dft8 = false;       // every axis qualifies and CF_DFT8 != 0
     bool spread_dpp = true;  // spread FMAs take the x taps by DPP row broadcast (CF_SPREAD_DPP=0: scalar loads)
     int spread_pass = 32;    // atoms per staging pass of the W > 9 spread (CF_SPREAD_PASS=64: A/B)
-    bool spread_mfma = true; // the spread on the fp64 matrix cores, 16x8x8 tiles (CF_SPREAD_MFMA=0: k_g_spread_tile)
+    bool spread_mfma = true; // W > 9: the spread on the fp64 matrix cores, 16x8x8 tiles (CF_SPREAD_MFMA=0: k_g_spread_tile)
+    bool spread_mfma_all = false;   // CF_SPREAD_MFMA=2: the matrix form at every width (tests)
     bool interp2 = true;     // two atoms per wave, taps by DPP row broadcast (CF_INTERP2=0: k_g_interp)
     bool interp4 = true;     // W <= 8: four atoms per wave (CF_INTERP4=0: k_g_interp2)
 };

@@ -552,17 +552,22 @@ __device__ __forceinline__ d4 mfma64(double a, double b, d4 c) {
 // kernel's order (equal to it to ~1e-15 relative).  When ng.x is an odd multiple of 8 (C5: 264)
 // the last x tile covers 8 planes: bin 2 tx + 1 wraps to bin 0, whose atoms reach only the
 // tile's missing half (rows < 0 are zero), and only the planes x < ng.x are written.
-template <int NS, int kP>
-__global__ void __launch_bounds__(256) k_g_spread_mfma(int3 ng, int3 nb, const int* __restrict__ start,
+#ifdef CF_SPM_WPE   // A/B builds: a waves-per-SIMD floor (VGPR cap) for k_g_spread_mfma
+#define CF_SPM_ATTR __attribute__((amdgpu_waves_per_eu(CF_SPM_WPE, 8)))
+#else
+#define CF_SPM_ATTR
+#endif
+template <int NS>
+__global__ void __launch_bounds__(256) CF_SPM_ATTR k_g_spread_mfma(int3 ng, int3 nb, const int* __restrict__ start,
                                                        const double* __restrict__ taps, const int4* __restrict__ g0s,
                                                        double* __restrict__ grid, const int* __restrict__ xr, int W) {
     constexpr int NBX = NS + 1;              // x bins per tile: dxb = ix - 1, ix < NBX
     constexpr int NSRC = NBX * NS * NS;
-    static_assert(NS <= 3 && NSRC <= 256, "bin offsets are packed in 2 bits per axis");
-    static_assert(kP % 16 == 0, "groups of 4 atoms, 4 waves");
-    constexpr int kBufD = kP * 32;           // X 16 + Y 8 + Z 8 doubles per atom
-    constexpr int kStD = 2 * kBufD > 4 * 1024 ? 2 * kBufD : 4 * 1024;
-    __shared__ __attribute__((aligned(16))) double st[kStD];   // 2 staging buffers; reused by the reduction
+    static_assert(NS <= 3 && NSRC <= 64, "bin offsets are packed in 2 bits per axis; one wave scans the bins");
+    constexpr int kBA = 16;                  // atoms per wave block (4 groups of 4: 16 MFMAs)
+    constexpr int kBufD = kBA * 32;          // X 16 + Y 8 + Z 8 doubles per atom
+    __shared__ __attribute__((aligned(16))) double st[4 * kBufD];   // one buffer per wave; [0, 1024) reused by the reduction
+    static_assert(4 * kBufD >= 1024, "the reduction buffer fits");
     __shared__ int bin_start[NSRC], bin_pre[NSRC + 1], bin_db[NSRC];
     __shared__ int src[kSpMaxSrc];   // slot << 6 | ix << 4 | dy << 2 | dz of the kept sources
     __shared__ int wcnt[4 * (kSpMaxSrc / 256)];
@@ -576,29 +581,46 @@ __global__ void __launch_bounds__(256) k_g_spread_mfma(int3 ng, int3 nb, const i
     const int xlim = min(16, ng.x - 16 * tx);   // 8 for the last tile when ng.x is an odd multiple of 8
     if (!x_range_in_slab(16 * tx, 16 * tx + xlim - 1, xr, W, ng.x)) return;
     const int t = threadIdx.x;
-    if (t < NSRC) {
-        const int ix = t / (NS * NS), dy = (t / NS) % NS, dz = t % NS;
-        const int b = (wrapb(2 * tx + 1 - ix, nb.x) * nb.y + wrapb(ty - dy, nb.y)) * nb.z + wrapb(tz - dz, nb.z);
-        const int s0 = start[b];
-        bin_start[t] = s0;
-        bin_pre[t + 1] = start[b + 1] - s0;
-        bin_db[t] = (ix << 8) | (dy << 4) | dz;
-    }
-    __syncthreads();
-    if (t == 0) {
-        bin_pre[0] = 0;
-        for (int i = 0; i < NSRC; i++) bin_pre[i + 1] += bin_pre[i];
+    const int lane = t & 63, w = wave_id();
+    if (w == 0) {   // the source bins, their counts scanned across the lanes (was a serial loop)
+        int s0 = 0, cnt = 0;
+        if (lane < NSRC) {
+            const int ix = lane / (NS * NS), dy = (lane / NS) % NS, dz = lane % NS;
+            const int b = (wrapb(2 * tx + 1 - ix, nb.x) * nb.y + wrapb(ty - dy, nb.y)) * nb.z + wrapb(tz - dz, nb.z);
+            s0 = start[b];
+            cnt = start[b + 1] - s0;
+            bin_start[lane] = s0;
+            bin_db[lane] = (ix << 8) | (dy << 4) | dz;
+        }
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int v = __shfl_up(cnt, o);
+            if (lane >= o) cnt += v;
+        }
+        if (lane < NSRC) bin_pre[lane + 1] = cnt;
+        if (lane == 0) bin_pre[0] = 0;
     }
     __syncthreads();
     const int total = bin_pre[NSRC];
-    const int lane = t & 63, w = wave_id();
     const int k = lane >> 4, c = lane & 15;   // MFMA operand lane: atom k of the group, x / column c
     d4 acc[4];
 #pragma unroll
     for (int q = 0; q < 4; q++) acc[q] = d4{0.0, 0.0, 0.0, 0.0};
+    // staging: piece e = lane & 15 (16 B) of atoms (lane >> 4) + 4 q, q < 4, of a wave block: e < 8
+    // x (half e >> 2), 8..11 y, 12..15 z -- per-lane constants: the axis, the source-word bits
+    // that pick its window, the window adjustment and the LDS address pattern (selects, no
+    // branches); atoms past the end are zero windows (the last group of 4 is read whole)
+    const int e = lane & 15, a0 = lane >> 4;
+    const int axis = e < 8 ? 0 : (e < 12 ? 1 : 2);
+    const int fsh = 4 - 2 * axis;                   // source-word bits of this axis's window
+    const int wadj = axis == 0 ? (e >> 2) - 1 : 0;  // x: window dxb + half
+    const int poff = kRow * axis + 2 * (e & 3);
+    const int dbase = axis == 0 ? 2 * e : (axis == 1 ? 16 * kBA : 24 * kBA) + 2 * (e & 3);
+    const int dstr = axis == 0 ? 16 : 8;            // doubles per atom in this piece's array
+    double* const wbuf = st + w * kBufD;            // this wave's buffer
     for (int seg0 = 0; seg0 < total; seg0 += kSpMaxSrc) {
         const int nall = min(kSpMaxSrc, total - seg0);
-        __syncthreads();   // previous segment's passes done with src
+        __syncthreads();   // previous segment's blocks done with src
         constexpr int kRounds = kSpMaxSrc / 256;
         int2 sb[kRounds];
         int4 g[kRounds];
@@ -642,29 +664,23 @@ __global__ void __launch_bounds__(256) k_g_spread_mfma(int3 ng, int3 nb, const i
             nseg += wcnt[4 * r] + wcnt[4 * r + 1] + wcnt[4 * r + 2] + wcnt[4 * r + 3];
         }
         __syncthreads();
-        if (nseg == 0) continue;
-        // staging: 16-B piece e = t & 15 of atoms a = (t >> 4) + 16 q: e < 8 x (half e >> 2),
-        // 8..11 y, 12..15 z -- the same piece kind for every q, so its axis, the bits of the
-        // source word that pick its window, the window adjustment and the LDS address pattern are
-        // per-thread constants (selects, no branches); atoms past the pass end are zero windows
-        // (the last group of 4 is read whole)
-        constexpr int kPer = kP * 16 / 256;
-        const int e = t & 15, a0 = t >> 4;
-        const int axis = e < 8 ? 0 : (e < 12 ? 1 : 2);
-        const int fsh = 4 - 2 * axis;                   // source-word bits of this axis's window
-        const int wadj = axis == 0 ? (e >> 2) - 1 : 0;  // x: window dxb + half
-        const int poff = kRow * axis + 2 * (e & 3);
-        const int dbase = axis == 0 ? 2 * e : (axis == 1 ? 16 * kP : 24 * kP) + 2 * (e & 3);
-        const int dstr = axis == 0 ? 16 : 8;            // doubles per atom in this piece's array
-        // two passes ahead: pass p + 2's loads are issued as pass p starts and have two passes of
-        // MFMAs (2 x 16 per wave at kP = 64) to land before they are staged (one pass ahead left
-        // every wave waiting on them: 33 % of wave cycles waiting, the MFMA pipe ~40 % busy)
-        v2d rva[kPer], rvb[kPer];
-        auto fetch = [&](v2d (&rv)[kPer], int p) {
-            const int base = p * kP, n = min(kP, nseg - base);
+        // Wave w takes the blocks of 16 kept sources w, w + 4, w + 8, ... through its own LDS
+        // double buffer, with no block barrier until the segment ends: the waves drift apart, so
+        // one wave's MFMAs overlap another's staging (the block-wide passes of 32 or 64 atoms had
+        // every wave meet at each pass barrier: 51 of 81 us with the MFMAs removed).  Block bi + 2's
+        // tap loads are issued as block bi starts, two blocks (32 MFMAs) before they are staged.
+        const int nwb = (nseg + kBA - 1) / kBA;
+#if defined(CF_SPM_ABL) && CF_SPM_ABL == 3   // ablation: source lists only (timing only)
+        const int nb_w = 0 * nwb;
+#else
+        const int nb_w = nwb > w ? (nwb - w + 3) / 4 : 0;   // this wave's blocks
+#endif
+        v2d rva[4], rvb[4];
+        auto fetch = [&](v2d (&rv)[4], int bi) {
+            const int base = (w + 4 * bi) * kBA, n = min(kBA, nseg - base);
 #pragma unroll
-            for (int q = 0; q < kPer; q++) {
-                const int a = a0 + 16 * q;
+            for (int q = 0; q < 4; q++) {
+                const int a = a0 + 4 * q;
                 const int s = src[base + min(a, n - 1)];
                 const int wi = ((s >> fsh) & 3) + wadj;
 #if defined(CF_SPM_ABL) && CF_SPM_ABL == 2   // ablation: no tap loads (timing only)
@@ -675,23 +691,22 @@ __global__ void __launch_bounds__(256) k_g_spread_mfma(int3 ng, int3 nb, const i
                 rv[q] = a < n && (unsigned)wi <= 2u ? v : v2d{0.0, 0.0};
             }
         };
-        auto stage = [&](const v2d (&rv)[kPer], int p) {
-            double* buf = st + (p & 1) * kBufD;
+        // one buffer per wave: a wave's LDS accesses execute in order, so block bi + 1 is staged
+        // over block bi right after the wave's own reads of it (16 KB per workgroup instead of 32:
+        // more workgroups per CU)
+        auto stage = [&](const v2d (&rv)[4]) {
 #pragma unroll
-            for (int q = 0; q < kPer; q++)
-                *reinterpret_cast<v2d*>(buf + dbase + dstr * (a0 + 16 * q)) = rv[q];
+            for (int q = 0; q < 4; q++) *reinterpret_cast<v2d*>(wbuf + dbase + dstr * (a0 + 4 * q)) = rv[q];
         };
-        const int npass = (nseg + kP - 1) / kP;
-        // pass p: `nxt` holds pass p + 1 (loaded during pass p - 1), `fre` receives pass p + 2
-        auto pass = [&](int p, v2d (&fre)[kPer], const v2d (&nxt)[kPer]) {
-            if (p + 2 < npass) fetch(fre, p + 2);
-            const int n = min(kP, nseg - p * kP);
-            const double* buf = st + (p & 1) * kBufD;
-            const double* xb = buf + c;
-            const double* yb = buf + 16 * kP + (c >> 3);
-            const double* zb = buf + 24 * kP + (c & 7);
+        // block bi: `nxt` holds block bi + 1 (loaded during block bi - 1), `fre` receives bi + 2
+        auto block = [&](int bi, v2d (&fre)[4], const v2d (&nxt)[4]) {
+            if (bi + 2 < nb_w) fetch(fre, bi + 2);
+            const int n = min(kBA, nseg - (w + 4 * bi) * kBA);
+            const double* xb = wbuf + c;
+            const double* yb = wbuf + 16 * kBA + (c >> 3);
+            const double* zb = wbuf + 24 * kBA + (c & 7);
             const int ngr = (n + 3) >> 2;
-            for (int gi = w; gi < ngr; gi += 4) {
+            for (int gi = 0; gi < ngr; gi++) {
                 const int a = 4 * gi + k;
                 const double xa = xb[16 * a];
                 const double za = zb[8 * a];
@@ -703,32 +718,41 @@ __global__ void __launch_bounds__(256) k_g_spread_mfma(int3 ng, int3 nb, const i
                 for (int q = 0; q < 4; q++) acc[q] = mfma64(xa, ya[2 * q] * za, acc[q]);
 #endif
             }
-            if (p + 1 < npass) stage(nxt, p + 1);
-            __syncthreads();
+            wave_sync();   // (keeps the compiler from moving the stores above the reads)
+            if (bi + 1 < nb_w) stage(nxt);
+            wave_sync();   // this wave's stores before its next block's reads
         };
-        fetch(rva, 0);
-        if (npass > 1) fetch(rvb, 1);
-        stage(rva, 0);
-        __syncthreads();
-        for (int p = 0; p < npass; p += 2) {
-            pass(p, rva, rvb);
-            if (p + 1 < npass) pass(p + 1, rvb, rva);
+        if (nb_w > 0) {
+            fetch(rva, 0);
+            if (nb_w > 1) fetch(rvb, 1);
+            stage(rva);
+            wave_sync();
+            for (int bi = 0; bi < nb_w; bi += 2) {
+                block(bi, rva, rvb);
+                if (bi + 1 < nb_w) block(bi + 1, rvb, rva);
+            }
         }
     }
-    // the 4 waves' partial tiles, summed in fixed wave order; acc[q][i] of lane l is the point
-    // x = (l >> 4) + 4 i, (y, z) column 16 q + (l & 15)
-    __syncthreads();
-    double* red = st;   // [4][16 x][64 (y, z)]
+    // the 4 waves' partial tiles, summed in fixed wave order ((w0 + w1) + w2) + w3 through one
+    // 8-KB tile; acc[q][i] of lane l is the point x = (l >> 4) + 4 i, (y, z) column 16 q + (l & 15)
+    double* red = st;   // [16 x][64 (y, z)]
+    for (int ww = 0; ww < 4; ww++) {
+        __syncthreads();
+        if (w == ww) {
 #pragma unroll
-    for (int q = 0; q < 4; q++)
+            for (int q = 0; q < 4; q++)
 #pragma unroll
-        for (int i = 0; i < 4; i++) red[w * 1024 + (k + 4 * i) * 64 + 16 * q + c] = acc[q][i];
+                for (int i = 0; i < 4; i++) {
+                    double& r = red[(k + 4 * i) * 64 + 16 * q + c];
+                    r = ww == 0 ? acc[q][i] : r + acc[q][i];
+                }
+        }
+    }
     __syncthreads();
 #pragma unroll
     for (int h = 0; h < 4; h++) {
         const int pt = t + 256 * h, x = pt >> 6, l = pt & 63;
-        const double v = ((red[pt] + red[1024 + pt]) + red[2048 + pt]) + red[3072 + pt];
-        if (x < xlim) grid[((size_t)(16 * tx + x) * ng.y + 8 * ty + (l >> 3)) * ng.z + 8 * tz + (l & 7)] = v;
+        if (x < xlim) grid[((size_t)(16 * tx + x) * ng.y + 8 * ty + (l >> 3)) * ng.z + 8 * tz + (l & 7)] = red[pt];
     }
 }
 
@@ -1439,7 +1463,11 @@ __device__ __forceinline__ void interp_stage(int3 ng, const double* __restrict__
             y -= y >= ng.y ? ng.y : 0;
             // 32-bit byte offset from the uniform base: one global_load with an SGPR base
             const unsigned off = (unsigned)(x * zy + y * ng.z + z) * 8u;
+#if defined(CF_IN_ABL) && CF_IN_ABL == 2   // ablation: no halo loads (timing only)
+            gv[q] = (double)off;
+#else
             gv[q] = *reinterpret_cast<const double*>(reinterpret_cast<const char*>(G) + off);
+#endif
             a += kDA; b += kDB;
             if (b >= R) { b -= R; a += 1; }
         }
@@ -1645,6 +1673,10 @@ __global__ void __launch_bounds__(kInterpThreads) CF_LDS_UNPAIRED k_g_interp2(in
     const int tz = tile % nb.z, ty = (tile / nb.z) % nb.y, tx = tile / (nb.z * nb.y);
     interp_stage<W>(ng, G, tx, ty, tz, sg);
     __syncthreads();
+#if defined(CF_IN_ABL) && CF_IN_ABL == 1   // ablation: staging only (timing only)
+    if (sg[threadIdx.x] == 1.2345e300) dedq[threadIdx.x] = 0.0;
+    return;
+#endif
     const int lane = threadIdx.x & 63, w = wave_id();
     const int h = lane >> 5, jg = (lane >> 4) & 1, k = lane & 15;
     const double hw_inv = 2.0 / W;
@@ -1943,6 +1975,7 @@ void grid_plan(Handle& h, int width, double sigma) {
     p.spread_pass = sp ? std::atoi(sp) : 32;
     const char* sm = getenv("CF_SPREAD_MFMA");
     p.spread_mfma = !(sm && sm[0] == '0');
+    p.spread_mfma_all = sm && sm[0] == '2';
     const char* i2 = getenv("CF_INTERP2");
     p.interp2 = !(i2 && i2[0] == '0');
     const char* i4 = getenv("CF_INTERP4");
@@ -2056,20 +2089,18 @@ void launch_grid_spread(Handle& h) {
     const int3 ng = make_int3(p.ng[0], p.ng[1], p.ng[2]), nb = make_int3(p.nb[0], p.nb[1], p.nb[2]);
 #define CF_SPT(NS_, P_, D_) hipLaunchKernelGGL((k_g_spread_tile<NS_, P_, D_>), dim3(p.nbins), dim3(256), 0, h.stream, \
                                                ng, nb, h.g_start, h.g_taps, h.g_g0s, h.g_grid, h.g_xrange, p.W)
-    if (p.spread_mfma && nb.x >= 4) {   // the matrix-core form: 16 x 8 x 8 tiles (4 distinct x bins)
+    // the matrix-core form (16 x 8 x 8 tiles, 4 distinct x bins) for W > 9; at W <= 9 (the mixed
+    // C5 grid) the vector form with its 8^3 tiles and 8 source bins measured faster (322 against
+    // 330 us at C5: the 16-wide x tile doubles the zero-tap share of a narrow kernel)
+    // (CF_SPREAD_MFMA=2 selects the matrix form at any width, for the tests; 0 never)
+    if (p.spread_mfma && nb.x >= 4 && (p.W > 9 || p.spread_mfma_all)) {
         const dim3 g((unsigned)((ng.x + 15) / 16 * nb.y * nb.z));
         if (p.W <= 9)
-            hipLaunchKernelGGL((k_g_spread_mfma<2, 64>), g, dim3(256), 0, h.stream, ng, nb, h.g_start, h.g_taps,
-                               h.g_g0s, h.g_grid, h.g_xrange, p.W);
-        else if (p.spread_pass == 128)   // A/B (CF_SPREAD_PASS=128 / 32)
-            hipLaunchKernelGGL((k_g_spread_mfma<3, 128>), g, dim3(256), 0, h.stream, ng, nb, h.g_start, h.g_taps,
-                               h.g_g0s, h.g_grid, h.g_xrange, p.W);
-        else if (p.spread_pass == 32)
-            hipLaunchKernelGGL((k_g_spread_mfma<3, 32>), g, dim3(256), 0, h.stream, ng, nb, h.g_start, h.g_taps,
-                               h.g_g0s, h.g_grid, h.g_xrange, p.W);
+            hipLaunchKernelGGL((k_g_spread_mfma<2>), g, dim3(256), 0, h.stream, ng, nb, h.g_start, h.g_taps, h.g_g0s,
+                               h.g_grid, h.g_xrange, p.W);
         else
-            hipLaunchKernelGGL((k_g_spread_mfma<3, 64>), g, dim3(256), 0, h.stream, ng, nb, h.g_start, h.g_taps,
-                               h.g_g0s, h.g_grid, h.g_xrange, p.W);
+            hipLaunchKernelGGL((k_g_spread_mfma<3>), g, dim3(256), 0, h.stream, ng, nb, h.g_start, h.g_taps, h.g_g0s,
+                               h.g_grid, h.g_xrange, p.W);
         return;
     }
     // a first tap in bin B reaches tiles B .. B + NS - 1: NS = 2 when W <= 9 (8 source bins per

@@ -342,7 +342,7 @@ def test_grid_spread_mfma_matches_vector_spread(monkeypatch, case, width):
     else:
         system, force, pos, box = ts.water_box(4000, cutoff=1.0, ewald_tol=1e-4, every_bond_angle=5)
     out = []
-    for flag in ("0", "1", "1"):
+    for flag in ("0", "2", "2"):   # 2: the matrix form at every width (the default uses it for W > 9)
         monkeypatch.setenv("CF_SPREAD_MFMA", flag)
         k = HipCalcCoulForceKernel(kspace_algo=GRID, grid_width=width).initialize(system, force)
         e, f = k.execute_host(pos, box)

@@ -4,7 +4,7 @@ collectives (the S(k) buffer is not reduced, so energies are not meaningful here
 per-step wall time, the library's per-phase GPU time and the host time to enqueue a step,
 i.e. what each rank does at N = W minus RCCL.  Analysis tool, not the benchmark.
 
-usage: python tools/scaling_probe.py [--worlds 1 2 4 8] [--steps 40]
+usage: python tools/scaling_probe.py [--worlds 1 2 4 8] [--steps 40] [--config C5 --precision mixed]
 """
 import argparse
 import json
@@ -24,10 +24,11 @@ from openmmcoul import testsystems as ts  # noqa: E402
 from openmmcoul.distributed import ShardedCoulKernel  # noqa: E402
 
 
-def probe(system, force, pos_np, box, world, steps, skin, algo=2, timing=True, graph=False):
+def probe(system, force, pos_np, box, world, steps, skin, algo=2, timing=True, graph=False, precision="double"):
     dev = torch.device("cuda", 0)
     stream = torch.cuda.current_stream(dev).cuda_stream
-    k = HipCalcCoulForceKernel(device=0, stream=stream, rank=0, world_size=world, kspace_algo=algo).initialize(system, force)
+    k = HipCalcCoulForceKernel(device=0, stream=stream, rank=0, world_size=world, kspace_algo=algo,
+                               precision=precision).initialize(system, force)
     if skin > 0:
         k.set_neighbor_skin(skin)
     if graph:
@@ -81,13 +82,14 @@ def main():
     ap.add_argument("--config", default="C3")
     ap.add_argument("--neighbor-skin", type=float, default=0.1)
     ap.add_argument("--kspace-algo", type=int, default=2)
+    ap.add_argument("--precision", default="double", help="double | mixed (C5)")
     ap.add_argument("--no-timing", action="store_true", help="no per-phase events (clean wall time)")
     ap.add_argument("--graph", action="store_true", help="replay the launches as hipGraphs (implies --no-timing)")
     args = ap.parse_args()
     system, force, pos_np, box = ts.make(args.config)
     for w in args.worlds:
         print(json.dumps(probe(system, force, pos_np, box, w, args.steps, args.neighbor_skin, args.kspace_algo,
-                               not (args.no_timing or args.graph), args.graph)), flush=True)
+                               not (args.no_timing or args.graph), args.graph, args.precision)), flush=True)
 
 
 if __name__ == "__main__":
