@@ -491,6 +491,8 @@ CF_EXPORT int cf_create(const cf_params* p, const cf_options* opt, cf_handle** o
         // CF_CLUSTER: "0" never the cluster-pair list, "1" also in mixed precision, unset: fp64 only
         h.env_cluster = getenv("CF_CLUSTER") ? (std::string(getenv("CF_CLUSTER")) == "0" ? 0 : 1) : -1;
         h.env_cluster_cap = getenv("CF_CLUSTER_CAP") ? atoi(getenv("CF_CLUSTER_CAP")) : 0;
+        h.env_direct_aux = !(getenv("CF_DIRECT_ON_AUX") && std::string(getenv("CF_DIRECT_ON_AUX")) == "0");
+        h.env_sync_events = getenv("CF_SYNC") && std::string(getenv("CF_SYNC")) == "event";
         h.kspace_algo = o.kspace_algo;
         h.stream = (hipStream_t)o.stream;  // NULL = the null stream (orders with torch's default stream)
 
@@ -1172,9 +1174,35 @@ static void on_aux(cf_handle* H, GraphCache* g, int seg, const GraphKey& k, F&& 
     h.stream = main;
 }
 extern "C" {
+// Fork / join between the caller's stream and the second stream.  Both are enqueued between
+// graph segments (never inside a capture), so the same calls serve eager and graph mode.  The
+// producer's write is enqueued before the consumer's wait, so a failed enqueue can never leave a
+// wait for a value nobody writes.
 static void fork_aux(cf::Handle& h) {
-    check_hip(hipEventRecord(h.ev_fork, h.stream), "hipEventRecord (fork)");
-    check_hip(hipStreamWaitEvent(h.aux, h.ev_fork, 0), "hipStreamWaitEvent (fork)");
+    if (h.env_sync_events) {
+        check_hip(hipEventRecord(h.ev_fork, h.stream), "hipEventRecord (fork)");
+        check_hip(hipStreamWaitEvent(h.aux, h.ev_fork, 0), "hipStreamWaitEvent (fork)");
+        return;
+    }
+    const unsigned long long v = ++h.sync_seq;
+    check_hip(hipStreamWriteValue64(h.stream, h.sync_flag, v, 0), "hipStreamWriteValue64 (fork)");
+    check_hip(hipStreamWaitValue64(h.aux, h.sync_flag, v, hipStreamWaitValueGte, ~0ull), "hipStreamWaitValue64 (fork)");
+}
+// the join's producer side (after the second stream's chain) and consumer side (the caller's stream)
+static void join_post(cf::Handle& h) {
+    if (h.env_sync_events) {
+        check_hip(hipEventRecord(h.ev_join, h.aux), "hipEventRecord (join)");
+        return;
+    }
+    check_hip(hipStreamWriteValue64(h.aux, h.sync_flag + 1, h.sync_seq, 0), "hipStreamWriteValue64 (join)");
+}
+static void join_wait(cf::Handle& h) {
+    if (h.env_sync_events) {
+        check_hip(hipStreamWaitEvent(h.stream, h.ev_join, 0), "hipStreamWaitEvent (join)");
+        return;
+    }
+    check_hip(hipStreamWaitValue64(h.stream, h.sync_flag + 1, h.sync_seq, hipStreamWaitValueGte, ~0ull),
+              "hipStreamWaitValue64 (join)");
 }
 
 static void launch_full(cf_handle* H, const double* pos_dev, int flags, bool reusable, double* forces_dev,
@@ -1202,13 +1230,26 @@ static void launch_full(cf_handle* H, const double* pos_dev, int flags, bool reu
     const GraphKey key = make_key(h, pos_dev, nullptr, nullptr, flags, reusable, box9);
     run_segment(H, g, SEG_PRO, key, [&] { launch_prologue(H, pos_dev, reusable); });
     fork_aux(h);
-    on_aux(H, g, SEG_REC, key, [&] {
+    auto rec = [&] {
         launch_rec_fwd(H, pos_dev);
         launch_rec_end(H, flags);
-    });
-    check_hip(hipEventRecord(h.ev_join, h.aux), "hipEventRecord (join)");
-    run_segment(H, g, SEG_DCH, key, [&] { launch_direct_chain(H, pos_dev, flags, reusable); });
-    check_hip(hipStreamWaitEvent(h.stream, h.ev_join, 0), "hipStreamWaitEvent (join)");
+    };
+    auto dch = [&] { launch_direct_chain(H, pos_dev, flags, reusable); };
+    // The direct chain goes to the second stream and the reciprocal chain stays on the caller's
+    // (CF_DIRECT_ON_AUX=0: the other way round).  Each hand-over costs the waiting queue ~5-15 us
+    // (tools/sync_probe.hip); this way the join's wait sits behind the reciprocal chain, which
+    // ends last, so the direct chain's end is long signalled when the caller's queue reaches it:
+    // C3 0.4607-0.4642 -> 0.4486-0.4504 ms/step (profiles/r04q_*)
+    if (h.env_direct_aux) {
+        on_aux(H, g, SEG_DCH, key, dch);
+        join_post(h);
+        run_segment(H, g, SEG_REC, key, rec);
+    } else {
+        on_aux(H, g, SEG_REC, key, rec);
+        join_post(h);
+        run_segment(H, g, SEG_DCH, key, dch);
+    }
+    join_wait(h);
     h.rec_split = forces != 0;
     {
         Timed t(H, PH_ENERGY);
@@ -1242,7 +1283,7 @@ static void launch_begin_split(cf_handle* H, const double* pos_dev, int flags, b
         h.pending_flags = -1;
         throw;
     }
-    check_hip(hipEventRecord(h.ev_join, h.aux), "hipEventRecord (join)");
+    join_post(h);
     run_segment(H, g, SEG_RFWD, key, [&] { launch_rec_fwd(H, pos_dev); });
 }
 
@@ -1252,7 +1293,7 @@ static void launch_end_split(cf_handle* H, int flags, double* forces_dev, double
     const int forces = flags & CF_INCLUDE_FORCES, energy = flags & CF_INCLUDE_ENERGY;
     run_segment(H, g, SEG_REND, make_key(h, H->pos_pending, nullptr, nullptr, flags, false, box9),
                 [&] { launch_rec_end(H, flags); });
-    check_hip(hipStreamWaitEvent(h.stream, h.ev_join, 0), "hipStreamWaitEvent (join)");
+    join_wait(h);
     h.rec_split = forces != 0;
     {
         Timed t(H, PH_ENERGY);
@@ -1274,8 +1315,19 @@ static void ensure_aux(cf_handle* H) {
     } else {
         check_hip(hipStreamCreateWithFlags(&h.aux, hipStreamNonBlocking), "hipStreamCreate (second stream)");
     }
-    check_hip(hipEventCreateWithFlags(&h.ev_fork, hipEventDisableTiming), "hipEventCreate");
-    check_hip(hipEventCreateWithFlags(&h.ev_join, hipEventDisableTiming), "hipEventCreate");
+    // fork / join order two streams of this device only: an agent-scope release is enough (kernel
+    // ends already release to the device; the default system-scope fence of an event record
+    // writes the L2s back for host visibility, ~15-20 us per fork and per join on the timeline,
+    // profiles/r04e_c3_timeline_eager_vs_graph.txt).  CF_EVENT_FENCE=system: the default fence (A/B)
+    const char* ef = getenv("CF_EVENT_FENCE");
+    const unsigned evf = hipEventDisableTiming | (ef && std::string(ef) == "system" ? 0u : hipEventDisableSystemFence);
+    check_hip(hipEventCreateWithFlags(&h.ev_fork, evf), "hipEventCreate");
+    check_hip(hipEventCreateWithFlags(&h.ev_join, evf), "hipEventCreate");
+    if (!h.sync_flag) {
+        h.sync_flag = dalloc<unsigned long long>(H, 2);
+        check_hip(hipMemset(h.sync_flag, 0, 2 * sizeof(unsigned long long)), "sync flag init");
+        h.sync_seq = 0;
+    }
     if (!h.dedq_rec) {
         h.dedq_rec = dalloc<double>(H, (size_t)h.n);
         h.f_rec = dalloc<double>(H, (size_t)4 * h.n);

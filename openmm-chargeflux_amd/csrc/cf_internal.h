@@ -135,6 +135,12 @@ struct Handle {
     bool split_overlap = false; // a begun multi-rank evaluation runs its direct chain on aux (cf_api.hip)
     hipStream_t aux = nullptr;
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    // fork / join by stream memory operations (hipStreamWriteValue64 / hipStreamWaitValue64 on
+    // sync_flag[0] / [1], value = the evaluation's sequence number): ~5.5 us per hand-over
+    // against ~11 (system-fence event) / ~8.5 (agent-fence event), tools/sync_probe.hip
+    unsigned long long* sync_flag = nullptr;
+    unsigned long long sync_seq = 0;
+    bool env_sync_events = false;   // CF_SYNC=event at cf_create: fork / join by events (A/B)
     double* dedq_rec = nullptr; // [N]
     double* f_rec = nullptr;    // [N][4]: the interpolated gradient p and -q (force = -q (ng/L) p)
     // cell list
@@ -185,6 +191,7 @@ struct Handle {
     bool cluster = false;
     bool env_no_half = false;   // CF_HALF=0 at cf_create
     int env_cluster = -1;       // CF_CLUSTER at cf_create: 0, 1, or -1 (unset: fp64 only)
+    bool env_direct_aux = true;    // one rank's direct chain on the second stream (CF_DIRECT_ON_AUX=0 at cf_create: the reciprocal chain)
     int env_cluster_cap = 0;    // CF_CLUSTER_CAP at cf_create (tests: a capacity that overflows)
     int zcol = 0;               // columns per cell axis of the within-cell sort (k_cell_order; 0 = atom order)
     int ncl_cap = 0;            // cluster capacity: N/4 + ncell
