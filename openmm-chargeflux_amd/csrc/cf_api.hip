@@ -12,6 +12,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <exception>
 #include <numeric>
 #include <stdexcept>
 #include <string>
@@ -1174,34 +1175,51 @@ static void on_aux(cf_handle* H, GraphCache* g, int seg, const GraphKey& k, F&& 
     h.stream = main;
 }
 extern "C" {
-// Fork / join between the caller's stream and the second stream.  Both are enqueued between
-// graph segments (never inside a capture), so the same calls serve eager and graph mode.  The
-// producer's write is enqueued before the consumer's wait, so a failed enqueue can never leave a
-// wait for a value nobody writes.
-static void fork_aux(cf::Handle& h) {
-    if (h.env_sync_events) {
-        check_hip(hipEventRecord(h.ev_fork, h.stream), "hipEventRecord (fork)");
-        check_hip(hipStreamWaitEvent(h.aux, h.ev_fork, 0), "hipStreamWaitEvent (fork)");
-        return;
-    }
-    const unsigned long long v = ++h.sync_seq;
-    check_hip(hipStreamWriteValue64(h.stream, h.sync_flag, v, 0), "hipStreamWriteValue64 (fork)");
-    check_hip(hipStreamWaitValue64(h.aux, h.sync_flag, v, hipStreamWaitValueGte, ~0ull), "hipStreamWaitValue64 (fork)");
+// Fork / join between the caller's stream and the second stream.  Events (CF_SYNC=event, A/B)
+// are recorded and waited between graph segments.  The default hands over by memory: the
+// producer's segment ends with k_signal (flag += 1, captured with the segment in graph mode),
+// the consumer's stream waits with hipStreamWaitValue64 for the count this evaluation reaches
+// (enqueued after the producer's launches, so a failed enqueue never leaves a wait for a signal
+// nobody sends).
+static void fork_aux(cf::Handle& h) {   // event form: record on the caller's stream, wait on the second
+    check_hip(hipEventRecord(h.ev_fork, h.stream), "hipEventRecord (fork)");
+    check_hip(hipStreamWaitEvent(h.aux, h.ev_fork, 0), "hipStreamWaitEvent (fork)");
 }
-// the join's producer side (after the second stream's chain) and consumer side (the caller's stream)
-static void join_post(cf::Handle& h) {
-    if (h.env_sync_events) {
-        check_hip(hipEventRecord(h.ev_join, h.aux), "hipEventRecord (join)");
-        return;
-    }
-    check_hip(hipStreamWriteValue64(h.aux, h.sync_flag + 1, h.sync_seq, 0), "hipStreamWriteValue64 (join)");
+static void wait_fork(cf::Handle& h) {   // memory form, consumer side (the producer: k_signal(sync_flag))
+    check_hip(hipStreamWaitValue64(h.aux, h.sync_flag, ++h.sync_seq, hipStreamWaitValueGte, ~0ull),
+              "hipStreamWaitValue64 (fork)");
 }
+static void join_post(cf::Handle& h) {   // event form only (the memory form: k_signal(sync_flag + 1) on aux)
+    check_hip(hipEventRecord(h.ev_join, h.aux), "hipEventRecord (join)");
+}
+// After a failed evaluation: the hand-over counts may be off by one (a signal enqueued whose wait
+// was not, or the reverse never happens: a wait is enqueued only after its signal).  Every wait
+// already enqueued has its signal enqueued before it, so draining both streams terminates; the
+// counts are then read back.
+static void resync_flags(cf::Handle& h) {
+    if (!h.sync_flag) return;
+    (void)hipStreamSynchronize(h.stream);
+    if (h.aux) (void)hipStreamSynchronize(h.aux);
+    unsigned long long v[2] = {0, 0};
+    if (hipMemcpy(v, h.sync_flag, sizeof(v), hipMemcpyDeviceToHost) == hipSuccess) {
+        h.sync_seq = v[0];
+        h.join_seq = v[1];
+    }
+}
+// resyncs the hand-over counts when the scope is left by an exception
+struct SyncGuard {
+    cf::Handle& h;
+    int n = std::uncaught_exceptions();
+    ~SyncGuard() {
+        if (std::uncaught_exceptions() > n) resync_flags(h);
+    }
+};
 static void join_wait(cf::Handle& h) {
     if (h.env_sync_events) {
         check_hip(hipStreamWaitEvent(h.stream, h.ev_join, 0), "hipStreamWaitEvent (join)");
         return;
     }
-    check_hip(hipStreamWaitValue64(h.stream, h.sync_flag + 1, h.sync_seq, hipStreamWaitValueGte, ~0ull),
+    check_hip(hipStreamWaitValue64(h.stream, h.sync_flag + 1, ++h.join_seq, hipStreamWaitValueGte, ~0ull),
               "hipStreamWaitValue64 (join)");
 }
 
@@ -1228,13 +1246,33 @@ static void launch_full(cf_handle* H, const double* pos_dev, int flags, bool reu
     }
     const int forces = flags & CF_INCLUDE_FORCES, energy = flags & CF_INCLUDE_ENERGY;
     const GraphKey key = make_key(h, pos_dev, nullptr, nullptr, flags, reusable, box9);
-    run_segment(H, g, SEG_PRO, key, [&] { launch_prologue(H, pos_dev, reusable); });
-    fork_aux(h);
     auto rec = [&] {
         launch_rec_fwd(H, pos_dev);
         launch_rec_end(H, flags);
     };
     auto dch = [&] { launch_direct_chain(H, pos_dev, flags, reusable); };
+    if (!h.env_sync_events) {
+        // memory hand-overs: two segments per evaluation (one graph per stream in graph mode)
+        SyncGuard sync_guard{h};
+        const bool dax = h.env_direct_aux;   // the reciprocal chain stays on the caller's stream
+        run_segment(H, g, SEG_PRO, key, [&] {
+            launch_prologue(H, pos_dev, reusable);
+            cf::launch_signal(h, h.sync_flag);
+            if (dax) rec(); else dch();
+        });
+        wait_fork(h);
+        on_aux(H, g, dax ? SEG_DCH : SEG_REC, key, [&] {
+            if (dax) dch(); else rec();
+            cf::launch_signal(h, h.sync_flag + 1);
+        });
+        join_wait(h);
+        h.rec_split = forces != 0;
+        Timed t(H, PH_ENERGY);
+        cf::launch_assemble_energy(h, (forces && forces_dev) ? forces_dev : nullptr, energy, energy_dev);
+        return;
+    }
+    run_segment(H, g, SEG_PRO, key, [&] { launch_prologue(H, pos_dev, reusable); });
+    fork_aux(h);
     // The direct chain goes to the second stream and the reciprocal chain stays on the caller's
     // (CF_DIRECT_ON_AUX=0: the other way round).  Each hand-over costs the waiting queue ~5-15 us
     // (tools/sync_probe.hip); this way the join's wait sits behind the reciprocal chain, which
@@ -1275,6 +1313,25 @@ static void launch_begin_split(cf_handle* H, const double* pos_dev, int flags, b
                                const double* box9) {
     cf::Handle& h = H->h;
     const GraphKey key = make_key(h, pos_dev, nullptr, nullptr, flags, reusable, box9);
+    if (!h.env_sync_events) {   // memory hand-overs (see fork_aux)
+        SyncGuard sync_guard{h};
+        run_segment(H, g, SEG_PRO, key, [&] {
+            launch_prologue(H, pos_dev, reusable);
+            cf::launch_signal(h, h.sync_flag);
+            launch_rec_fwd(H, pos_dev);
+        });
+        wait_fork(h);
+        try {
+            on_aux(H, g, SEG_DCH, key, [&] {
+                launch_direct_chain(H, pos_dev, flags, reusable);
+                cf::launch_signal(h, h.sync_flag + 1);
+            });
+        } catch (...) {
+            h.pending_flags = -1;
+            throw;
+        }
+        return;
+    }
     run_segment(H, g, SEG_PRO, key, [&] { launch_prologue(H, pos_dev, reusable); });
     fork_aux(h);
     try {
@@ -1291,6 +1348,7 @@ static void launch_end_split(cf_handle* H, int flags, double* forces_dev, double
                              const double* box9) {
     cf::Handle& h = H->h;
     const int forces = flags & CF_INCLUDE_FORCES, energy = flags & CF_INCLUDE_ENERGY;
+    SyncGuard sync_guard{h};
     run_segment(H, g, SEG_REND, make_key(h, H->pos_pending, nullptr, nullptr, flags, false, box9),
                 [&] { launch_rec_end(H, flags); });
     join_wait(h);

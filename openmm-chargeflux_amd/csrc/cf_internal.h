@@ -139,7 +139,7 @@ struct Handle {
     // sync_flag[0] / [1], value = the evaluation's sequence number): ~5.5 us per hand-over
     // against ~11 (system-fence event) / ~8.5 (agent-fence event), tools/sync_probe.hip
     unsigned long long* sync_flag = nullptr;
-    unsigned long long sync_seq = 0;
+    unsigned long long sync_seq = 0, join_seq = 0;   // the values sync_flag[0] / [1] reach this evaluation
     bool env_sync_events = false;   // CF_SYNC=event at cf_create: fork / join by events (A/B)
     double* dedq_rec = nullptr; // [N]
     double* f_rec = nullptr;    // [N][4]: the interpolated gradient p and -q (force = -q (ng/L) p)
@@ -272,6 +272,7 @@ void launch_direct(Handle& h, const double* pos, int include_forces);          /
 void launch_direct_finish(Handle& h, const double* pos, int include_forces);   // overflow rescan + exclusions
 void launch_recip_add(Handle& h);   // dedq, f_part += reciprocal partials
 void launch_nopbc(Handle& h, const double* pos, int include_forces, int include_energy);
+void launch_signal(Handle& h, unsigned long long* flag);   // one-thread kernel: *flag += 1 (system-scope release)
 void launch_assemble_energy(Handle& h, double* forces_out, int include_energy, double* energy_out);   // chain rule (forces_out != null) + energy
 
 void kspace_plan(Handle& h);

@@ -1778,6 +1778,20 @@ void launch_nopbc(Handle& h, const double* pos, int include_forces, int include_
                        h.e_atom);
 }
 
+// The producer side of a fork / join hand-over: one thread adds 1 to the flag with a system-scope
+// release (the consumer is the runtime's hipStreamWaitValue64 poller, which reads memory).  An
+// increment rather than a stored value, so that a captured graph replays it unchanged; the host
+// counts the evaluations (Handle::sync_seq / join_seq).  This kernel replaces
+// hipStreamWriteValue64, whose runtime kernel started ~13 us after its predecessor on the
+// producer's queue (the runtime's fences; profiles/r04q_stream_sync.txt).
+__global__ void k_signal(unsigned long long* __restrict__ flag) {
+    if (threadIdx.x == 0) __hip_atomic_fetch_add(flag, 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+void launch_signal(Handle& h, unsigned long long* flag) {
+    hipLaunchKernelGGL(k_signal, dim3(1), dim3(64), 0, h.stream, flag);
+}
+
 void launch_assemble_energy(Handle& h, double* forces_out, int include_energy, double* energy_out) {
     const int nown = std::max(0, h.hi - h.lo);
     int nrec = (h.pbc && include_energy && h.rank == 0) ? h.e_rec_nblk : 0;

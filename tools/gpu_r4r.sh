@@ -1,0 +1,24 @@
+#!/bin/bash
+# round 4: memory hand-overs produced by k_signal inside the segments (2 segments / graphs per
+# evaluation): overlap / graph / multi-rank tests, timelines, benches, rank-0 probes.
+out=gpurun_out/r4r
+mkdir -p $out
+step() { local rc=$1 name=$2; echo "$name rc=$rc"; [ $rc -eq 0 ] || exit $rc; }
+R=$GRAFT_REPO_ROOT
+timeout -k 10 500 python -u -m pytest tests/test_gpu_overlap.py tests/test_gpu_graph.py tests/test_gpu_parity.py tests/test_gpu_skin.py -x -q --timeout 150 --timeout-method thread > $out/tests.log 2>&1; rc=$?; tail -2 $out/tests.log; step $rc tests
+CF_SYNC=event timeout -k 10 300 python -u -m pytest tests/test_gpu_overlap.py tests/test_gpu_graph.py -x -q --timeout 150 --timeout-method thread > $out/tests_ev.log 2>&1; rc=$?; tail -1 $out/tests_ev.log; step $rc tests_ev
+for g in 0 1; do
+    (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace -d $R/$out/tl_g$g -o run --output-format csv -- python3 $R/bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-exact-compare --no-kernel-timing --graph $g > $R/$out/tl_g$g.log 2>&1); step $? tl_g$g
+    echo "graph=$g: $(python3 tools/trace_gaps.py $out/tl_g$g/run_kernel_trace.csv --steps 8)"
+    python3 tools/step_timeline.py $out/tl_g$g > $out/step_g$g.txt
+done
+for n in sig1 ev1 sig2 ev2; do
+    unset CF_SYNC
+    case $n in ev*) export CF_SYNC=event;; esac
+    timeout -k 10 300 python -u bench.py --steps 40 --warmup 5 --no-cpu-baseline --no-exact-compare > $out/bench_$n.json 2> $out/bench_$n.err; step $? bench_$n
+    python3 -c "import json; d = json.loads(open('$out/bench_$n.json').read().strip().splitlines()[-1]); print('$n', d['ms_per_step'], d.get('graph_replay_ms_per_step'))"
+done
+unset CF_SYNC
+timeout -k 10 300 python -u tools/scaling_probe.py --worlds 1 8 --steps 40 --no-timing > $out/probe_eager.jsonl 2> $out/probe_eager.err; step $? probe_eager
+timeout -k 10 300 python -u tools/scaling_probe.py --worlds 1 8 --steps 40 --graph > $out/probe_graph.jsonl 2> $out/probe_graph.err; step $? probe_graph
+cat $out/probe_eager.jsonl $out/probe_graph.jsonl | cut -c1-150
