@@ -127,8 +127,8 @@ def cpu_baseline(force, pos, box, k_sample):
 # (the instantiation that runs in the profiled command; a phase timed as one bracket may be
 # several launches: their bytes are summed)
 PMC_KERNEL = {"kspace_force": ["cf::k_force<"], "kspace_sfac": ["cf::k_sfac<"],
-              "direct_pairs": ["cf::k_pairs_half<"],
-              "grid_spread": ["cf::k_g_spread_tile<"], "grid_interp": ["cf::k_g_interp<"]}
+              "direct_pairs": ["cf::k_pairs_cq<"],          # the cluster-pair kernel (fp64, one rank)
+              "grid_spread": ["cf::k_g_spread_mfma<"], "grid_interp": ["cf::k_g_interp2<"]}
 
 
 def pair_count(force, pos, box):
@@ -335,11 +335,13 @@ def main():
     n_own = hi - lo
     # algorithmic work per launch of each hot phase: (HBM bytes,
     # flops, compute pipe, its peak)
-    #  direct_pairs  (k_pairs_half on one fp64 rank, k_pairs otherwise) bytes 4 P_c + 80 N
-    #                (int32 half list + per-atom in/out), flops 80 P_c on the fp64 VALU (fp32 VALU for
-    #                the mixed-precision kernel); P_c counts each pair once
-    #  grid_spread   2 N W^3 fp64 VALU flops (one FMA per atom x grid point of its support), bytes 24 N W
-    #                (the atom's three tap rows) + 8 ng^3 (grid out)
+    #  direct_pairs  (k_pairs_cq on one fp64 rank, k_pairs_half in mixed precision, k_pairs on
+    #                several ranks) bytes 4 P_c + 80 N (a 4-B list entry per pair + per-atom in/out),
+    #                flops 80 P_c on the fp64 VALU (fp32 VALU for the mixed-precision kernel); P_c
+    #                counts each pair once
+    #  grid_spread   2 N W^3 fp64 flops (one FMA per atom x grid point of its support; on the matrix
+    #                cores for W > 9, k_g_spread_mfma: the fp64 MFMA and VALU peaks are both 78.6
+    #                TF/s), bytes 24 N W (the atom's three tap rows) + 8 ng^3 (grid out)
     #  grid_interp   4 N W^3 fp64 VALU flops (two FMAs per grid value), bytes 8 ng^3 + 24 N W + 32 N
     #  kspace_sfac / kspace_force (exact path)  4 / 8 fp64 MFMA flops per atom x half-space k-vector
     # fraction of the roof = max(B / BW, F / P) / t; "bound" names the larger term
@@ -351,7 +353,9 @@ def main():
         ng3 = float(np.prod(kern.kernel.grid_shape())) if args.kspace_algo == 2 else 0.0
         pair_pipe = ("valu", FP64_PEAK_TFLOPS) if args.precision == "double" else ("valu_fp32", FP32_PEAK_TFLOPS)
         alg = {"direct_pairs": (4.0 * p_c + 80.0 * n_own, 80.0 * p_c) + pair_pipe,
-               "grid_spread": (24.0 * n_own * w_grid + 8.0 * ng3, 2.0 * n_own * w_grid ** 3, "valu", FP64_PEAK_TFLOPS),
+               "grid_spread": (24.0 * n_own * w_grid + 8.0 * ng3, 2.0 * n_own * w_grid ** 3,
+                               "mfma" if w_grid > 9 and os.environ.get("CF_SPREAD_MFMA", "1") != "0" else "valu",
+                               FP64_PEAK_TFLOPS),
                "grid_interp": (8.0 * ng3 + 24.0 * n_own * w_grid + 32.0 * n_own, 4.0 * n_own * w_grid ** 3, "valu",
                                FP64_PEAK_TFLOPS),
                "kspace_sfac": (64.0 * n_own, 4.0 * units, "mfma", FP64_PEAK_TFLOPS),

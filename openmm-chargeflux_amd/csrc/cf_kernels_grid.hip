@@ -1437,6 +1437,52 @@ __device__ __forceinline__ double wave_sum4(double pv, double px, double py, dou
 
 // the potential grid over tile (tx, ty, tz) plus the W - 1 halo, wrapped, into sg[R][R][R]:
 // rows of R consecutive z; thread t covers column c = t % R of rows t / R, t / R + RPP, ...
+// The same halo, 16 B per load: thread t takes the z pair (2 c, 2 c + 1), c = t % ceil(R / 2), of
+// rows t / ceil(R / 2), + RPP, ... (an even z and an even ng.z keep every pair inside one wrapped
+// row and 16-B aligned; the odd R's last pair reads one point past the halo, not stored).  Half
+// the loads and address computations of interp_stage (its VALU work was a third of
+// k_g_interp2's, profiles/r04i_*)
+template <int W>
+__device__ __forceinline__ void interp_stage16(int3 ng, const double* __restrict__ G, int tx, int ty, int tz,
+                                               double* __restrict__ sg) {
+    constexpr int R = 7 + W;
+    constexpr int RC = (R + 1) / 2;            // z pairs per row
+    constexpr int RPP = kInterpThreads / RC;   // rows per pass
+    const int c = threadIdx.x % RC, r0 = threadIdx.x / RC;
+    int z = 8 * tz + 2 * c;
+    z -= z >= ng.z ? ng.z : 0;
+    constexpr int kRows = (R * R + RPP - 1) / RPP;
+    constexpr int kDA = RPP / R, kDB = RPP % R;
+    if (r0 < RPP) {
+        v2d gv[kRows];
+        int a = r0 / R, b = r0 - (r0 / R) * R;
+        const int zy = ng.y * ng.z;
+#pragma unroll
+        for (int q = 0; q < kRows; q++) {
+            const bool in = r0 + q * RPP < R * R;
+            int x = 8 * tx + (in ? a : 0), y = 8 * ty + (in ? b : 0);
+            x -= x >= ng.x ? ng.x : 0;
+            y -= y >= ng.y ? ng.y : 0;
+            const unsigned off = (unsigned)(x * zy + y * ng.z + z) * 8u;
+#if defined(CF_IN_ABL) && CF_IN_ABL == 2   // ablation: no halo loads (timing only)
+            gv[q] = v2d{(double)off, 0.0};
+#else
+            gv[q] = *reinterpret_cast<const v2d*>(reinterpret_cast<const char*>(G) + off);
+#endif
+            a += kDA; b += kDB;
+            if (b >= R) { b -= R; a += 1; }
+        }
+#pragma unroll
+        for (int q = 0; q < kRows; q++) {
+            const int row = r0 + q * RPP;
+            if (row < R * R) {
+                sg[row * R + 2 * c] = gv[q].x;
+                if (2 * c + 1 < R) sg[row * R + 2 * c + 1] = gv[q].y;
+            }
+        }
+    }
+}
+
 template <int W>
 __device__ __forceinline__ void interp_stage(int3 ng, const double* __restrict__ G, int tx, int ty, int tz,
                                              double* __restrict__ sg) {
@@ -1671,7 +1717,7 @@ __global__ void __launch_bounds__(kInterpThreads) CF_LDS_UNPAIRED k_g_interp2(in
     const int s0 = start[tile], s1 = start[tile + 1];
     if (s0 == s1) return;
     const int tz = tile % nb.z, ty = (tile / nb.z) % nb.y, tx = tile / (nb.z * nb.y);
-    interp_stage<W>(ng, G, tx, ty, tz, sg);
+    interp_stage16<W>(ng, G, tx, ty, tz, sg);
     __syncthreads();
 #if defined(CF_IN_ABL) && CF_IN_ABL == 1   // ablation: staging only (timing only)
     if (sg[threadIdx.x] == 1.2345e300) dedq[threadIdx.x] = 0.0;
@@ -1822,7 +1868,7 @@ __global__ void __launch_bounds__(kInterpThreads) CF_LDS_UNPAIRED k_g_interp4(in
     const int s0 = start[tile], s1 = start[tile + 1];
     if (s0 == s1) return;
     const int tz = tile % nb.z, ty = (tile / nb.z) % nb.y, tx = tile / (nb.z * nb.y);
-    interp_stage<W>(ng, G, tx, ty, tz, sg);
+    interp_stage16<W>(ng, G, tx, ty, tz, sg);
     __syncthreads();
     const int lane = threadIdx.x & 63, w = wave_id();
     const int q = lane >> 4, jg = (lane >> 3) & 1, k = lane & 7;

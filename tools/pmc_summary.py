@@ -20,6 +20,7 @@ FETCH_FACTOR = {
     "cf::k_pairs<": 2.0,
     "cf::k_pairs_cq": 2.0,         # the cluster-pair list: 16 consecutive 8-B entries per wave (streaming; upper estimate)
     "cf::k_g_spread_tile": 1.0,    # 64-B window pieces + wave-uniform 64-B x windows (c_seg64, c_scalar64)
+    "cf::k_g_spread_mfma": 1.0,    # 64-B window pieces read as 16-B lanes (c_seg64)
     "cf::k_excl": 1.0,             # 32-B window-sum gathers (c_gather32: 64-B granules = real traffic)
     "cf::k_g_interp": 1.17,        # 168-B halo row runs (c_rows168: FETCH = 0.853 of the bytes)
 }
