@@ -493,7 +493,12 @@ CF_EXPORT int cf_create(const cf_params* p, const cf_options* opt, cf_handle** o
         h.env_cluster = getenv("CF_CLUSTER") ? (std::string(getenv("CF_CLUSTER")) == "0" ? 0 : 1) : -1;
         h.env_cluster_cap = getenv("CF_CLUSTER_CAP") ? atoi(getenv("CF_CLUSTER_CAP")) : 0;
         h.env_direct_aux = !(getenv("CF_DIRECT_ON_AUX") && std::string(getenv("CF_DIRECT_ON_AUX")) == "0");
-        h.env_sync_events = getenv("CF_SYNC") && std::string(getenv("CF_SYNC")) == "event";
+        // fork / join by events with CF_SYNC=event, and whenever rocprofv3 collects counters
+        // (ROCPROF_COUNTER_COLLECTION in the environment): counter collection serializes the
+        // dispatches, and the runtime's hipStreamWaitValue64 is a polling kernel, which then holds
+        // the device while its producer waits behind it (a C3 --pmc pass hung, round 4)
+        const char* sy = getenv("CF_SYNC");
+        h.env_sync_events = sy ? std::string(sy) == "event" : getenv("ROCPROF_COUNTER_COLLECTION") != nullptr;
         h.kspace_algo = o.kspace_algo;
         h.stream = (hipStream_t)o.stream;  // NULL = the null stream (orders with torch's default stream)
 
