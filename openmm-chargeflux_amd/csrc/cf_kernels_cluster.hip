@@ -510,8 +510,10 @@ __global__ void __launch_bounds__(kCqThreads) CF_LDS_UNPAIRED k_pairs_cq(DirectA
                 const v2f dy = v2f{pif[k].y, pif[k + 1].y} - v2f{yj, yj};
                 const v2f dz = v2f{pif[k].z, pif[k + 1].z} - v2f{zj, zj};
                 const v2f r2 = dx * dx + dy * dy + dz * dz;
-                m[k] = __ballot(((bits >> (4 * k)) & 1u) && r2.x <= a.rcm2f);
-                m[k + 1] = __ballot(((bits >> (4 * k + 4)) & 1u) && r2.y <= a.rcm2f);
+                // two ballots ANDed on the scalar unit (a ballot of `listed && in range` was
+                // compiled as compare, s_and, select, compare: two VALU instructions more per atom)
+                m[k] = __ballot(r2.x <= a.rcm2f) & __ballot((bits >> (4 * k)) & 1u);
+                m[k + 1] = __ballot(r2.y <= a.rcm2f) & __ballot((bits >> (4 * k + 4)) & 1u);
                 cnt[k] = __popcll(m[k]);
                 cnt[k + 1] = __popcll(m[k + 1]);
             }
