@@ -422,7 +422,9 @@ struct Timed {
         size_t need = 2 * (size_t)(H->nrec[ph] + 1);
         while (v.size() < need) {
             hipEvent_t e;
-            cf::check_hip(hipEventCreate(&e), "hipEventCreate");
+            // device-scope release: the default system-scope fence of a record writes the L2s
+            // back and delays the next launch by ~10 us, which the interval then includes
+            cf::check_hip(hipEventCreateWithFlags(&e, hipEventReleaseToDevice), "hipEventCreate");
             v.push_back(e);
         }
         cf::check_hip(hipEventRecord(v[2 * H->nrec[ph]], H->h.stream), "hipEventRecord");
