@@ -968,15 +968,27 @@ __global__ void __launch_bounds__(kHalfBlock) CF_LDS_UNPAIRED k_pairs_half(Direc
     __shared__ int2 win[kHalfWin];                     // (first sorted slot, window offset) per window cell
     __shared__ int wdel[kHalfWin];                     // window offset - first sorted slot
     __shared__ unsigned long long accw[4][kHalfMaxWin];   // j-side fx, fy, fz, dE/dq (fixed point)
+    // MIXED, orthorhombic: the translation that brings a window cell's (wrapped) atoms next to
+    // this cell, so the pair vector is x_i - (x_j + t) -- three adds instead of the per-pair
+    // minimum image (multiply, rint, fma per axis; round-3 review).  For a pair within rc <
+    // L/2 it is the minimum image.
+    constexpr bool kWrapTab = MIXED && !TRIC;
+    __shared__ double3 wrt[kWrapTab ? kHalfWin : 1];
     __shared__ int wtot;
     const int cell = xcd_block();
     const int3 nc = a.nc;
     const int cz = cell % nc.z, cy = (cell / nc.z) % nc.y, cx = cell / (nc.y * nc.z);
     if (threadIdx.x < kHalfWin) {
         const int3 o = half_offset(threadIdx.x);
-        const int w = (wrap_cell(cx + o.x, nc.x) * nc.y + wrap_cell(cy + o.y, nc.y)) * nc.z + wrap_cell(cz + o.z, nc.z);
+        const int ux = cx + o.x, uy = cy + o.y, uz = cz + o.z;
+        const int wx = wrap_cell(ux, nc.x), wy = wrap_cell(uy, nc.y), wz = wrap_cell(uz, nc.z);
+        const int w = (wx * nc.y + wy) * nc.z + wz;
         const int b = a.cstart[w];
         win[threadIdx.x] = make_int2(b, a.cend[w] - b);
+        if constexpr (kWrapTab)
+            wrt[threadIdx.x] = make_double3(ux == wx ? 0.0 : (ux > wx ? a.L.x : -a.L.x),
+                                            uy == wy ? 0.0 : (uy > wy ? a.L.y : -a.L.y),
+                                            uz == wz ? 0.0 : (uz > wz ? a.L.z : -a.L.z));
     }
     if constexpr (TYPES) {
         for (int e = threadIdx.x; e < a.lj_ntypes; e += kHalfBlock) {
@@ -1026,9 +1038,10 @@ __global__ void __launch_bounds__(kHalfBlock) CF_LDS_UNPAIRED k_pairs_half(Direc
             const float qi = (float)pi.w, ke = (float)a.ke, keqi = ke * qi;
             const float rc2 = (float)a.rc2, alpha = (float)a.alpha, escale = (float)a.erfc_scale_f;
             const v4i* nl4 = reinterpret_cast<const v4i*>(a.nl) + (size_t)g * (a.nb_cap / kChunk) * a.nlr + row;
-            struct Cand { double4 p; float2 lj; int slot; };
+            struct Cand { double4 p; float2 lj; int slot; double3 wr; };
             auto gather = [&](int e, bool ok) {
                 const int t = ok ? (e & kHalfSlotMask) : 0;
+                const int wc = ok ? (e >> kHalfSlotBits) & 31 : 0;
                 Cand cd;
                 cd.p = a.pos4s[t];
                 if constexpr (TYPES) {
@@ -1037,17 +1050,19 @@ __global__ void __launch_bounds__(kHalfBlock) CF_LDS_UNPAIRED k_pairs_half(Direc
                     const double2 d = a.ljs[t];
                     cd.lj = make_float2((float)d.x, (float)d.y);
                 }
-                cd.slot = wdel[ok ? (e >> kHalfSlotBits) & 31 : 0] + t;
+                cd.slot = wdel[wc] + t;
+                if constexpr (kWrapTab) cd.wr = wrt[wc];
                 return cd;
             };
             auto eval = [&](const Cand& cd) {
-                double dxd = pi.x - cd.p.x, dyd = pi.y - cd.p.y, dzd = pi.z - cd.p.z;
+                double dxd, dyd, dzd;
                 if constexpr (TRIC) {
+                    dxd = pi.x - cd.p.x; dyd = pi.y - cd.p.y; dzd = pi.z - cd.p.z;
                     min_image(a, dxd, dyd, dzd);
                 } else {
-                    dxd -= a.L.x * rint(dxd * a.invL.x);
-                    dyd -= a.L.y * rint(dyd * a.invL.y);
-                    dzd -= a.L.z * rint(dzd * a.invL.z);
+                    dxd = pi.x - (cd.p.x + cd.wr.x);
+                    dyd = pi.y - (cd.p.y + cd.wr.y);
+                    dzd = pi.z - (cd.p.z + cd.wr.z);
                 }
                 const float dx = (float)dxd, dy = (float)dyd, dz = (float)dzd;
                 const float r2 = fmaf(dx, dx, fmaf(dy, dy, dz * dz));
