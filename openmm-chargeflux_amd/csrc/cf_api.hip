@@ -1389,9 +1389,15 @@ static void ensure_aux(cf_handle* H) {
     check_hip(hipEventCreateWithFlags(&h.ev_fork, evf), "hipEventCreate");
     check_hip(hipEventCreateWithFlags(&h.ev_join, evf), "hipEventCreate");
     if (!h.sync_flag) {
+        // zeroed and drained before any wait is enqueued: the allocation may reuse a destroyed
+        // handle's flags, whose old counts would satisfy this handle's first waits at once (the
+        // second stream would start before its producer -- a C5 test saw wrong forces), and
+        // hipMemset runs on the null stream, which the non-blocking second stream does not follow
         h.sync_flag = dalloc<unsigned long long>(H, 2);
         check_hip(hipMemset(h.sync_flag, 0, 2 * sizeof(unsigned long long)), "sync flag init");
+        check_hip(hipDeviceSynchronize(), "sync flag init");
         h.sync_seq = 0;
+        h.join_seq = 0;
     }
     if (!h.dedq_rec) {
         h.dedq_rec = dalloc<double>(H, (size_t)h.n);

@@ -135,3 +135,19 @@ def test_set_overlap_at_run_time_is_bitwise(monkeypatch):
     k.destroy()
     for e, f, d in res[1:]:
         assert e == res[0][0] and np.array_equal(f, res[0][1]) and np.array_equal(d, res[0][2])
+
+
+def test_successive_handles_hand_over_from_zero(monkeypatch):
+    """The fork / join counters of a new handle start from zero even when its allocation reuses a
+    destroyed handle's counters (cf_api.hip ensure_aux): otherwise the old counts satisfy the new
+    handle's first waits at once and the second stream starts before its producer.  Each of
+    several handles, created after the previous one ran and was destroyed, gives on its first
+    evaluations the one-stream bits."""
+    system, force, pos, box = ts.water_box(4000, cutoff=1.0, ewald_tol=1e-4, every_bond_angle=5)
+    ref = _run(monkeypatch, False, system, force, pos, box, 0.0, steps=2)
+    for _ in range(4):
+        got = _run(monkeypatch, True, system, force, pos, box, 0.0, steps=2)
+        for (ea, fa, da, ta), (eb, fb, db, tb) in zip(ref, got):
+            assert ea == eb and np.array_equal(fa, fb) and np.array_equal(ta, tb)
+            if da is not None:
+                assert np.array_equal(da, db)
