@@ -204,8 +204,15 @@ void set_cells(cf_handle* H, const double L[3]) {
     // fit and k_excl then rescans) and sorted slots that fit the entry's 21 bits
     const bool no_half = h.env_no_half;   // CF_HALF=0 at cf_create (A/B and tests)
     const double per_cell = (double)h.n / (double)ncell;
-    h.half = !no_half && h.pbc && h.world == 1 && nc[0] >= 4 && nc[1] >= 4 && nc[2] >= 4 &&
-             per_cell * 18.0 * 1.15 <= 4096.0 && h.n < (1 << 21);
+    // several ranks (CF_CLUSTER_MR=1, off by default): the cluster-pair form (fp64), with the
+    // builder keeping the cluster pairs that touch this rank's atoms (each rank evaluates those
+    // once, both sides; k_excl gathers the partner-side sums of its own atoms).  Correct (the
+    // multi-rank GPU tests pass with it) but slower than the full per-atom list at W = 4 / 8:
+    // 0.336 / 0.304 against 0.255 / 0.197 ms rank-0 (profiles/r04ag_*): a thin slab's cells and
+    // their window neighbours run whole 1024-thread blocks with the 128-KB window for few owned atoms
+    const bool want_cluster = h.env_cluster == 1 || (h.env_cluster < 0 && !h.mixed);
+    h.half = !no_half && h.pbc && (h.world == 1 || (want_cluster && h.env_cluster_mr)) && nc[0] >= 4 &&
+             nc[1] >= 4 && nc[2] >= 4 && per_cell * 18.0 * 1.15 <= 4096.0 && h.n < (1 << 21);
     if (h.half && ncell > h.win_cells) {
         if (h.win_out) { (void)hipFree(h.win_out); (void)hipFree(h.win_woff); }
         cf::check_hip(hipMalloc(&h.win_out, sizeof(unsigned long long) * 4 * 4096 * (size_t)ncell), "half-list windows");
@@ -218,7 +225,7 @@ void set_cells(cf_handle* H, const double L[3]) {
     // fp32 term is cheap, so the cluster kernel's phase A (the fp32 atom tests and the queueing)
     // costs more than it saves (C5: 1.425 vs 1.235 ms, profiles/r04e_*); CF_CLUSTER=1 forces it
     // (tests), CF_CLUSTER=0 keeps the per-atom list in fp64 (A/B and tests)
-    h.cluster = h.half && (h.env_cluster == 1 || (h.env_cluster < 0 && !h.mixed));
+    h.cluster = h.half && want_cluster;
     h.zcol = 0;
     if (h.cluster) {
         // within-cell z-columns of ~12 atoms (k_cell_order): clusters of 4 consecutive slots stay compact
@@ -501,6 +508,7 @@ CF_EXPORT int cf_create(const cf_params* p, const cf_options* opt, cf_handle** o
         // the device while its producer waits behind it (a C3 --pmc pass hung, round 4)
         const char* sy = getenv("CF_SYNC");
         h.env_sync_events = sy ? std::string(sy) == "event" : getenv("ROCPROF_COUNTER_COLLECTION") != nullptr;
+        h.env_cluster_mr = getenv("CF_CLUSTER_MR") && std::string(getenv("CF_CLUSTER_MR")) == "1";
         h.kspace_algo = o.kspace_algo;
         h.stream = (hipStream_t)o.stream;  // NULL = the null stream (orders with torch's default stream)
 

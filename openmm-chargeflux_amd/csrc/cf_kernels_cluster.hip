@@ -89,7 +89,8 @@ __global__ void __launch_bounds__(1024) k_cl_scan(int ncell, const int* __restri
 __global__ void __launch_bounds__(256) k_cl_bbox(int ncell, const int* __restrict__ flag, const int* __restrict__ cstart,
                                                  const int* __restrict__ cend, const int* __restrict__ cl_start,
                                                  const float4* __restrict__ pos4f, int2* __restrict__ cl_info,
-                                                 float4* __restrict__ cl_bb, int3 nc, double3 L, double3 T) {
+                                                 float4* __restrict__ cl_bb, int3 nc, double3 L, double3 T,
+                                                 const int* __restrict__ atom_sorted, int lo, int hi, int n) {
     const int lane = threadIdx.x & 63;
     const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (c >= ncell || !*flag) return;
@@ -98,16 +99,20 @@ __global__ void __launch_bounds__(256) k_cl_bbox(int ncell, const int* __restric
                               (double)(c % nc.z) / nc.z).x;
     for (int k = lane; k * kClSize < e - b; k += 64) {
         const int first = b + k * kClSize, cnt = min(kClSize, e - first);
-        float4 lo = pos4f[first], hi = lo;
-        for (int u = 1; u < cnt; u++) {
+        float4 bl = pos4f[first], bh = bl;
+        bool own = lo == 0 && hi == n;   // one rank: every cluster is owned
+        for (int u = 0; u < cnt; u++) {
             const float4 p = pos4f[first + u];
-            lo.x = fminf(lo.x, p.x); lo.y = fminf(lo.y, p.y); lo.z = fminf(lo.z, p.z);
-            hi.x = fmaxf(hi.x, p.x); hi.y = fmaxf(hi.y, p.y); hi.z = fmaxf(hi.z, p.z);
+            bl.x = fminf(bl.x, p.x); bl.y = fminf(bl.y, p.y); bl.z = fminf(bl.z, p.z);
+            bh.x = fmaxf(bh.x, p.x); bh.y = fmaxf(bh.y, p.y); bh.z = fmaxf(bh.z, p.z);
+            const int ai = atom_sorted[first + u];
+            own = own || (ai >= lo && ai < hi);
         }
         cl_info[k0 + k] = make_int2(first, cnt);
-        lo.w = (float)(ox + 0.5 * ((double)lo.x + (double)hi.x));
-        cl_bb[2 * (k0 + k)] = lo;
-        cl_bb[2 * (k0 + k) + 1] = hi;
+        bl.w = (float)(ox + 0.5 * ((double)bl.x + (double)bh.x));
+        bh.w = own ? 1.f : 0.f;   // the cluster holds an atom this rank owns (k_cl_build's filter)
+        cl_bb[2 * (k0 + k)] = bl;
+        cl_bb[2 * (k0 + k) + 1] = bh;
     }
 }
 
@@ -166,7 +171,9 @@ __global__ void __launch_bounds__(kClBuildThreads) k_cl_build(DirectArgs a, cons
         const float4 sh = wsh[k];
         const float4 lo = cl_bb[2 * cj], hi = cl_bb[2 * cj + 1];
         const int first = a.cl_info[cj].x;
-        cand_lo[t] = make_float4(lo.x + sh.x, lo.y + sh.y, lo.z + sh.z, __int_as_float(cj | ((a.cl_info[cj].y - 1) << 29)));
+        const unsigned ownj = hi.w != 0.f ? 0x80000000u : 0u;
+        cand_lo[t] = make_float4(lo.x + sh.x, lo.y + sh.y, lo.z + sh.z,
+                                 __int_as_float((int)((unsigned)cj | ((unsigned)(a.cl_info[cj].y - 1) << 29) | ownj)));
         cand_hi[t] = make_float4(hi.x + sh.x, hi.y + sh.y, hi.z + sh.z, __int_as_float(first | (k << kHalfSlotBits)));
         cand_x[t] = lo.w;
     }
@@ -176,6 +183,7 @@ __global__ void __launch_bounds__(kClBuildThreads) k_cl_build(DirectArgs a, cons
     for (int ci = c0 + wv; ci < c1; ci += kClBuildThreads / 64) {
         const float4 ilo = cl_bb[2 * ci], ihi = cl_bb[2 * ci + 1];
         const float xki = ilo.w;
+        const bool owni = ihi.w != 0.f;   // several ranks: a pair is listed when either cluster holds an owned atom
         const int2 ii = a.cl_info[ci];
         const unsigned rows = (1u << (4 * ii.y)) - 1u;   // bits of the valid i atoms (il < count)
         uint2* out = cpl + (size_t)ci * a.cpl_cap;
@@ -216,8 +224,10 @@ __global__ void __launch_bounds__(kClBuildThreads) k_cl_build(DirectArgs a, cons
                 ent = __float_as_int(hi.w);
                 const int k = ent >> kHalfSlotBits;
                 const float xkj = cand_x[t];
-                if (dx * dx + dy * dy + dz * dz <= rlm2 && (k >= 9 || xkj > xki || (xkj == xki && cj >= ci))) {
-                    const int jcnt = ((unsigned)__float_as_int(lo.w) >> 29) + 1;
+                const bool ownj = (unsigned)__float_as_int(lo.w) >> 31;
+                if (dx * dx + dy * dy + dz * dz <= rlm2 && (k >= 9 || xkj > xki || (xkj == xki && cj >= ci)) &&
+                    (owni || ownj)) {
+                    const int jcnt = (((unsigned)__float_as_int(lo.w) >> 29) & 3u) + 1;
                     const unsigned cols = 0x1111u * ((1u << jcnt) - 1u);   // bits of the valid j atoms
                     mask = rows & cols & (cj == ci ? kClSelfMask : 0xFFFFu);
                     hit = true;
@@ -270,10 +280,12 @@ __global__ void __launch_bounds__(kCqThreads) CF_LDS_UNPAIRED k_pairs_cq(DirectA
     __shared__ double3 shd[kHalfWin];       // wrap translation of each window cell (phase B, window_cell)
     __shared__ unsigned long long accw[4][kHalfMaxWin];   // j-side fx, fy, fz, dE/dq (fixed point)
     __shared__ int qbuf[kCqWaves][4][kCqQ];  // per wave, per i atom: ring of hit entries
-    __shared__ int wtot, next_ci;
+    __shared__ int wtot, next_ci, nown;
     const int cell = xcd_block();
     const int3 nc = a.nc;
     const int cz = cell % nc.z, cy = (cell / nc.z) % nc.y, cx = cell / (nc.y * nc.z);
+    if (threadIdx.x == 0) nown = 0;
+    __syncthreads();
     if (threadIdx.x < kHalfWin) {
         float4 off;
         double3 wr;
@@ -282,6 +294,8 @@ __global__ void __launch_bounds__(kCqThreads) CF_LDS_UNPAIRED k_pairs_cq(DirectA
         win[threadIdx.x] = make_int2(b, a.cend[w] - b);
         shf[threadIdx.x] = off;
         shd[threadIdx.x] = wr;
+        // several ranks: owned atoms in the window (its own cell is window cell 0)
+        if (a.own_start && a.own_start[w + 1] > a.own_start[w]) atomicAdd(&nown, 1);
     }
     if constexpr (TYPES)
         for (int e = threadIdx.x; e < a.lj_ntypes; e += kCqThreads) ljt[e] = a.lj_tab[e];
@@ -306,6 +320,9 @@ __global__ void __launch_bounds__(kCqThreads) CF_LDS_UNPAIRED k_pairs_cq(DirectA
     __syncthreads();
     const int nw = wtot;
     if (nw > kHalfMaxWin) return;   // block-uniform; k_excl recomputes everything
+    // several ranks: no owned atom in the cell or its window -- no pair this rank keeps has an atom
+    // here, and k_excl reads this window only for owned atoms of the window's cells (none): skip
+    if (a.own_start && nown == 0) return;   // block-uniform
     if (threadIdx.x < kHalfWin) a.win_woff[cell * kHalfWin + threadIdx.x] = win[threadIdx.x].y;
     for (int e = threadIdx.x; e < nw; e += kCqThreads) {
         accw[0][e] = 0; accw[1][e] = 0; accw[2][e] = 0; accw[3][e] = 0;
@@ -540,8 +557,8 @@ __global__ void __launch_bounds__(kCqThreads) CF_LDS_UNPAIRED k_pairs_cq(DirectA
             acc.fx += __shfl_xor(acc.fx, m); acc.fy += __shfl_xor(acc.fy, m); acc.fz += __shfl_xor(acc.fz, m);
             acc.dq += __shfl_xor(acc.dq, m); acc.e += __shfl_xor(acc.e, m);
         }
-        if (kk == 0 && il < inf.y) {
-            const int i = a.atom_sorted[islot];
+        const int i = a.atom_sorted[islot];
+        if (kk == 0 && il < inf.y && i >= a.lo && i < a.hi) {   // this rank's atoms only
             a.e_atom[3 * i + 1] = acc.e;
             if (a.include_forces) {
                 a.dedq[i] = acc.dq;
@@ -578,7 +595,8 @@ void launch_cluster_list(Handle& h) {
                        h.cl_start);
     hipLaunchKernelGGL(k_cl_bbox, dim3((ncell + 3) / 4), dim3(256), 0, h.stream, ncell, h.skin_flag, h.cell_start,
                        h.cell_end, h.cl_start, h.pos4f, h.cl_info, h.cl_bb, make_int3(h.nc[0], h.nc[1], h.nc[2]),
-                       make_double3(h.box_L[0], h.box_L[1], h.box_L[2]), make_double3(h.box_t[0], h.box_t[1], h.box_t[2]));
+                       make_double3(h.box_L[0], h.box_L[1], h.box_L[2]), make_double3(h.box_t[0], h.box_t[1], h.box_t[2]),
+                       a.atom_sorted, a.lo, a.hi, a.n);
     const double rl = (h.cutoff + h.list_skin) * (1.0 + 1e-5) + 1e-5;
     hipLaunchKernelGGL(k_cl_build, dim3(ncell), dim3(kClBuildThreads), 0, h.stream, a, h.cl_bb, h.cpl, h.cpl_cnt,
                        (float)(rl * rl));

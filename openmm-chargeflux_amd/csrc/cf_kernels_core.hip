@@ -1696,6 +1696,7 @@ DirectArgs direct_args(Handle& h, const double* pos, int include_forces) {
     a.nb_cap = h.nb_cap;
     a.nlr = h.hi - h.lo;
     a.own_s = h.own_s;
+    a.own_start = h.world > 1 ? h.own_start : nullptr;
     a.flag = h.skin_flag;
     a.atom_sorted = h.atom_sorted; a.key_sorted = h.cell_key_sorted;
     a.cstart = h.cell_start; a.cend = h.cell_end;

@@ -111,6 +111,7 @@ struct DirectArgs {
     int nb_cap;                 // capacity of ONE of the kSeg sub-lists
     int nlr;                    // list rows = owned atoms; row c <-> sorted slot own_slot(c)
     const int* own_s;           // [nlr] cell-sorted slots of the owned atoms (null: identity)
+    const int* own_start;       // [ncell + 1] owned atoms per cell, scanned (null on one rank)
     const int* flag;            // rebuild flag (list kernels exit when 0)
     const int* atom_sorted; const int* key_sorted;
     const int* cstart; const int* cend;
