@@ -86,3 +86,23 @@ def test_cluster_list_odd_cells_and_exclusions():
     assert np.abs(fc - ref["forces"]).max() <= 1e-8
     assert np.abs(dc - ref["dedq"]).max() <= 1e-9 * np.abs(ref["dedq"]).max()
     assert abs(ec - ref["energy"]) <= 1e-9 * np.abs(ref["terms"]).sum() + 1e-8
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_cluster_list_on_several_ranks_opt_in(monkeypatch, world):
+    """The ownership-filtered cluster-pair list on several ranks (CF_CLUSTER_MR=1, opt-in: slower
+    than the full per-atom list at W = 4/8): `world` handles on this GPU, the k-space
+    buffers summed by hand, against one rank -- each rank evaluates the cluster pairs that touch
+    its atoms, k_excl gathers its atoms' partner-side sums."""
+    from openmmcoul import HipCalcCoulForceKernel
+    from tests.test_gpu_configs import _decomposed
+    system, force, pos, box = ts.water_box(4000, cutoff=1.0, ewald_tol=1e-4, every_bond_angle=5)
+    k = HipCalcCoulForceKernel(kspace_algo=2).initialize(system, force)
+    e1, f1 = k.execute_host(pos, box)
+    d1, t1 = k.dedq(), k.energy_terms()
+    k.destroy()
+    monkeypatch.setenv("CF_CLUSTER_MR", "1")
+    ew, fw, dw, _ = _decomposed(system, force, pos, box, world, 2)
+    assert abs(ew - e1) <= 1e-11 * np.abs(t1).sum()
+    assert np.abs(fw - f1).max() <= 2e-12 * np.abs(f1).max() + 1e-9
+    assert np.abs(dw - d1).max() <= 2e-12 * np.abs(d1).max() + 1e-9
