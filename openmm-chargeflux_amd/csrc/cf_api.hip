@@ -708,6 +708,8 @@ CF_EXPORT int cf_create(const cf_params* p, const cf_options* opt, cf_handle** o
                 h.g_order = dalloc<int>(H, no);
                 h.g_g0s = dalloc<int4>(H, no);
                 h.g_taps = dalloc<double>(H, no * 72);
+                // W <= 9: k_g_order_taps stores points 0..15 of each row only; 16..23 stay zero
+                check_hip(hipMemset(h.g_taps, 0, sizeof(double) * no * 72), "memset taps");
                 if (h.world > 1) {
                     h.g_xrange = dalloc<int>(H, 3);
                     const int init[3] = {INT_MAX, INT_MIN, 0};

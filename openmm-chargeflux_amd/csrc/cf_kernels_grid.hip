@@ -285,8 +285,16 @@ __global__ void __launch_bounds__(256) k_g_order_taps(int nbins, const int* __re
         }
         wave_sync();
         const size_t s0 = (size_t)b0 + c0;
-        for (int e = lane; e < mc * kPairs; e += 64)
-            reinterpret_cast<v2d*>(taps)[s0 * kPairs + e] = reinterpret_cast<const v2d*>(rw)[e];
+        if (W <= 9) {   // taps end at point (g0 mod 8) + W - 1 <= 15: points 16..23 stay the zeros
+                        // written at allocation (cf_create), so a row is 8 pairs of its 12
+            for (int e = lane; e < mc * 24; e += 64) {
+                const int pr = (e / 8) * 12 + (e & 7);   // (atom, axis) = e / 8
+                reinterpret_cast<v2d*>(taps)[s0 * kPairs + pr] = reinterpret_cast<const v2d*>(rw)[pr];
+            }
+        } else {
+            for (int e = lane; e < mc * kPairs; e += 64)
+                reinterpret_cast<v2d*>(taps)[s0 * kPairs + e] = reinterpret_cast<const v2d*>(rw)[e];
+        }
         if (!fast && lane < mc) {
             const int io = so[c0 + lane];
             const int4 g = g0u[io];
