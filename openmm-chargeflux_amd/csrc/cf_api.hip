@@ -509,6 +509,7 @@ CF_EXPORT int cf_create(const cf_params* p, const cf_options* opt, cf_handle** o
         const char* sy = getenv("CF_SYNC");
         h.env_sync_events = sy ? std::string(sy) == "event" : getenv("ROCPROF_COUNTER_COLLECTION") != nullptr;
         h.env_cluster_mr = getenv("CF_CLUSTER_MR") && std::string(getenv("CF_CLUSTER_MR")) == "1";
+        h.env_bin_rounds = getenv("CF_BIN_ROUNDS") ? std::max(0, std::min(8, atoi(getenv("CF_BIN_ROUNDS")))) : 0;
         h.kspace_algo = o.kspace_algo;
         h.stream = (hipStream_t)o.stream;  // NULL = the null stream (orders with torch's default stream)
 

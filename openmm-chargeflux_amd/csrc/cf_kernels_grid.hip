@@ -101,9 +101,12 @@ __global__ void __launch_bounds__(256) k_g_bin(int lo, int nown, const double* _
                                                const double* __restrict__ q, double3 L, int3 ng, int W, int3 nb,
                                                double4* __restrict__ srec, int4* __restrict__ g0u,
                                                int* __restrict__ rank, int* __restrict__ cnt, int* __restrict__ xr,
-                                               int* __restrict__ ticket, int* __restrict__ start) {
+                                               int* __restrict__ ticket, int* __restrict__ start, int per) {
     __shared__ int sh[256];
-    const int io = blockIdx.x * blockDim.x + threadIdx.x;
+    // `per` rounds of 256 atoms per block: the ticket of last_block_done is one address that
+    // every block increments, so fewer, longer blocks at large N (launch_grid_sort)
+    for (int it = 0; it < per; it++) {
+    const int io = (blockIdx.x * per + it) * blockDim.x + threadIdx.x;
     const bool valid = io < nown;
     if (xr) {   // x-slab of the owned atoms' first taps, relative to the first owned atom's
         double u0 = pos[3 * lo] / L.x;
@@ -156,6 +159,7 @@ __global__ void __launch_bounds__(256) k_g_bin(int lo, int nown, const double* _
     }
     const int r = wave_agg_inc(cnt, bin, valid);
     if (valid) rank[io] = r;
+    }
     if (!last_block_done(ticket)) return;
     block_counts_to_bounds<256>(nb.x * nb.y * nb.z, cnt, start, nullptr, true, sh);
 }
@@ -2107,8 +2111,10 @@ void launch_grid_sort(Handle& h, const double* pos) {
     const int3 ng = make_int3(p.ng[0], p.ng[1], p.ng[2]), nb = make_int3(p.nb[0], p.nb[1], p.nb[2]);
     const double3 L = make_double3(h.box_L[0], h.box_L[1], h.box_L[2]);
     // g_cnt is zero here: cleared at cf_create and by k_g_scatter of the previous evaluation
-    hipLaunchKernelGGL(k_g_bin, dim3(nblk(nown, 256)), dim3(256), 0, h.stream, h.lo, nown, pos, h.q, L, ng, p.W,
-                       nb, h.g_srec, h.g_g0u, h.g_rank, h.g_cnt, h.g_xrange, h.e_ticket + kTicketGrid, h.g_start);
+    // at least ~512 blocks of 256 atoms each round; up to 8 rounds per block (C5: 5, C3: 1)
+    const int per = h.env_bin_rounds > 0 ? h.env_bin_rounds : std::max(1, std::min(8, nown / (256 * 512)));
+    hipLaunchKernelGGL(k_g_bin, dim3(nblk(nown, 256 * per)), dim3(256), 0, h.stream, h.lo, nown, pos, h.q, L, ng, p.W,
+                       nb, h.g_srec, h.g_g0u, h.g_rank, h.g_cnt, h.g_xrange, h.e_ticket + kTicketGrid, h.g_start, per);
     hipLaunchKernelGGL(k_g_scatter, dim3(nblk(nown, 256)), dim3(256), 0, h.stream, nown, h.g_g0u, h.g_rank, h.g_start,
                        h.g_tmp, p.nbins, h.g_cnt);
     if (p.W == 14) hipLaunchKernelGGL(k_g_order_taps<14>, dim3(nblk(p.nbins, kOtWaves)), dim3(256), 0, h.stream, p.nbins, h.g_start, h.g_tmp,

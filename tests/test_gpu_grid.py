@@ -354,3 +354,23 @@ def test_grid_spread_mfma_matches_vector_spread(monkeypatch, case, width):
     assert np.abs(f1 - f0).max() <= 1e-12 * np.abs(f0).max(), np.abs(f1 - f0).max()
     assert np.abs(d1 - d0).max() <= 1e-12 * np.abs(d0).max(), np.abs(d1 - d0).max()
     assert e2 == e1 and np.array_equal(f2, f1) and np.array_equal(d2, d1)
+
+
+@pytest.mark.parametrize("rounds", ["3", "8"])
+def test_grid_bin_rounds_bitwise(monkeypatch, rounds):
+    """k_g_bin with several 256-atom rounds per block (the default from 262144 owned atoms up;
+    CF_BIN_ROUNDS forces it at a small size): the provisional ranks come from atomics in any
+    order, k_g_order_taps restores the stable order, so energy, forces and dE/dq are bitwise
+    equal to the one-round launch -- including a ragged last block."""
+    system, force, pos, box = ts.water_box(4000, cutoff=1.0, ewald_tol=1e-4, every_bond_angle=5)
+    out = []
+    for r in ("1", rounds):
+        monkeypatch.setenv("CF_BIN_ROUNDS", r)
+        k = HipCalcCoulForceKernel(kspace_algo=GRID).initialize(system, force)
+        e, f = k.execute_host(pos, box)
+        e2, f2 = k.execute_host(pos, box)   # the ticket re-armed by the last block
+        out.append((e, f, k.dedq()))
+        assert e2 == e and np.array_equal(f2, f)
+        k.destroy()
+    (e0, f0, d0), (e1, f1, d1) = out
+    assert e1 == e0 and np.array_equal(f1, f0) and np.array_equal(d1, d0)
