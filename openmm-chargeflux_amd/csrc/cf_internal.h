@@ -191,7 +191,7 @@ struct Handle {
     bool cluster = false;
     bool env_no_half = false;   // CF_HALF=0 at cf_create
     int env_cluster = -1;       // CF_CLUSTER at cf_create: 0, 1, or -1 (unset: fp64 only)
-    int env_bin_rounds = 0;        // k_g_bin rounds of 256 atoms per block (CF_BIN_ROUNDS; 0: by N)
+    int env_bin_rounds = 0;        // k_g_bin / k_assemble_energy rounds of 256 atoms per block (CF_BIN_ROUNDS; 0: by N)
     bool env_cluster_mr = false;   // several ranks: the cluster-pair list (CF_CLUSTER_MR=1; default: the full per-atom list)
     bool env_direct_aux = true;    // one rank's direct chain on the second stream (CF_DIRECT_ON_AUX=0 at cf_create: the reciprocal chain)
     int env_cluster_cap = 0;    // CF_CLUSTER_CAP at cf_create (tests: a capacity that overflows)

@@ -1499,10 +1499,13 @@ __global__ void __launch_bounds__(kEChunk) k_assemble_energy(int lo, int hi, con
                                                              double* __restrict__ energy_int, int* __restrict__ ticket,
                                                              int* __restrict__ flag, int* __restrict__ xrange,
                                                              int* __restrict__ half_flag,
-                                                             long long* __restrict__ fallback) {
+                                                             long long* __restrict__ fallback, int per) {
     __shared__ double red[3][256];
-    const int b = lo + blockIdx.x * kEChunk + threadIdx.x;
     double a0 = 0, a1 = 0, a2 = 0;
+    // `per` chunks of kEChunk atoms per block at large N: fewer partials and fewer increments
+    // of the one ticket address (as k_g_bin); each thread's energies are summed in chunk order
+    for (int it = 0; it < per; it++) {
+    const int b = lo + (blockIdx.x * per + it) * kEChunk + threadIdx.x;
     if (b < hi) {
         if (out) {
             double fx = f_part[3 * b], fy = f_part[3 * b + 1], fz = f_part[3 * b + 2];
@@ -1543,7 +1546,8 @@ __global__ void __launch_bounds__(kEChunk) k_assemble_energy(int lo, int hi, con
             out[3 * b + 1] += fy;
             out[3 * b + 2] += fz;
         }
-        a0 = e_atom[3 * b]; a1 = e_atom[3 * b + 1]; a2 = e_atom[3 * b + 2];
+        a0 += e_atom[3 * b]; a1 += e_atom[3 * b + 1]; a2 += e_atom[3 * b + 2];
+    }
     }
     block_sum3(a0, a1, a2, red);
     if (threadIdx.x == 0) {   // agent-scope stores, read back by the last block (last_block_done)
@@ -1811,13 +1815,14 @@ void launch_signal(Handle& h, unsigned long long* flag) {
 void launch_assemble_energy(Handle& h, double* forces_out, int include_energy, double* energy_out) {
     const int nown = std::max(0, h.hi - h.lo);
     int nrec = (h.pbc && include_energy && h.rank == 0) ? h.e_rec_nblk : 0;
-    const int nparts = std::max(1, nblk(nown, kEChunk));
+    const int per = h.env_bin_rounds > 0 ? h.env_bin_rounds : std::max(1, std::min(8, nown / (kEChunk * 512)));   // as launch_grid_sort
+    const int nparts = std::max(1, nblk(nown, kEChunk * per));
     hipLaunchKernelGGL(k_assemble_energy, dim3(nparts), dim3(kEChunk), 0, h.stream, h.lo, h.hi, h.ccsr_start,
                        h.ccsr_ent, h.dedq, h.dqdx, h.f_part, forces_out, h.rec_split ? h.dedq_rec : nullptr,
                        h.rec_split ? reinterpret_cast<const double4*>(h.f_rec) : nullptr,
                        make_double3(h.gp.ng[0] / h.box_L[0], h.gp.ng[1] / h.box_L[1], h.gp.ng[2] / h.box_L[2]), h.e_atom, h.e_part, h.e_rec_part, nrec, h.pbc,
                        h.terms_dev, energy_out, h.energy_dev, h.e_ticket + kTicketEnergy, h.skin_flag, h.g_xrange,
-                       h.half ? h.half_flag : nullptr, h.n_fallback_dev);
+                       h.half ? h.half_flag : nullptr, h.n_fallback_dev, per);
 }
 
 }  // namespace cf
