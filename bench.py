@@ -194,6 +194,8 @@ def main():
     ap.add_argument("--graph", type=int, default=0,
                     help="1: replay each step's CoulForce launches as a captured hipGraph (cf_set_graph) in the "
                          "timed region")
+    ap.add_argument("--handover", default="event", choices=["event", "memory"],
+                    help="fork / join of the library's second stream (cf_options.handover; memory: opt-in)")
     ap.add_argument("--dt", type=float, default=0.001, help="ps")
     ap.add_argument("--neighbor-skin", type=float, default=None,
                     help="nm; persistent list rebuilt when an atom moved > skin/2 (0 = every step); default "
@@ -220,7 +222,7 @@ def main():
     n = len(pos_np)
     n_waters = force.getNumFluxWaters() + force.getNumFluxAngles()
     kern = ShardedCoulKernel(system, force, local, kspace_algo=args.kspace_algo, neighbor_skin=args.neighbor_skin,
-                             grid_width=args.grid_width, precision=args.precision)
+                             grid_width=args.grid_width, precision=args.precision, handover=args.handover)
     lo, hi = kern.lo, kern.hi
     alpha, kmax = kern.kernel.ewald_params()
     k_half = (kmax[2] - 1) + (kmax[1] - 1) * (2 * kmax[2] - 1) + (kmax[0] - 1) * (2 * kmax[1] - 1) * (2 * kmax[2] - 1)
@@ -264,7 +266,6 @@ def main():
     # its own, not stretched by kernels of the other chain sharing the CUs.  Those event records
     # cost ~10% of a step, so the timed region below brackets only the dominant kernel.
     HOT = ("direct_pairs", "grid_spread", "grid_interp", "kspace_sfac", "kspace_force")
-    overlap = os.environ.get("CF_OVERLAP", "1") != "0"   # the library's setting at create
     kern.kernel.set_overlap(False)
     kern.kernel.set_timing(True)
     for _ in range(args.steps):
@@ -272,7 +273,7 @@ def main():
     torch.cuda.synchronize()
     timing_all = kern.kernel.timing()
     kern.kernel.set_timing(False)
-    kern.kernel.set_overlap(overlap)
+    kern.kernel.set_overlap(True)   # the library's default
     ms_eval = float(np.mean([a.elapsed_time(b) for a, b in ev])) if ev else float("nan")
     per_step = {k: v[0] / args.steps for k, v in timing_all.items()}   # amortized (list phases are not every step)
     dom = max((k for k in HOT if per_step.get(k, 0.0) > 0), key=lambda k: per_step[k], default=None)
@@ -354,7 +355,7 @@ def main():
         pair_pipe = ("valu", FP64_PEAK_TFLOPS) if args.precision == "double" else ("valu_fp32", FP32_PEAK_TFLOPS)
         alg = {"direct_pairs": (4.0 * p_c + 80.0 * n_own, 80.0 * p_c) + pair_pipe,
                "grid_spread": (24.0 * n_own * w_grid + 8.0 * ng3, 2.0 * n_own * w_grid ** 3,
-                               "mfma" if w_grid > 9 and os.environ.get("CF_SPREAD_MFMA", "1") != "0" else "valu",
+                               "mfma" if w_grid > 9 else "valu",
                                FP64_PEAK_TFLOPS),
                "grid_interp": (8.0 * ng3 + 24.0 * n_own * w_grid + 32.0 * n_own, 4.0 * n_own * w_grid ** 3, "valu",
                                FP64_PEAK_TFLOPS),
@@ -457,7 +458,7 @@ def main():
                                    f"{dt * 1000:g} fs, " + ("fp64" if args.precision == "double" else
                                                             "mixed precision (fp32 pair kernel)"),
                        "atoms": n, "kmax": list(kmax), "k_half": k_half,
-                       "neighbor_skin_nm": args.neighbor_skin,
+                       "neighbor_skin_nm": args.neighbor_skin, "handover": args.handover,
                        "kspace": {0: "exact k-sum, fp64 MFMA", 1: "exact k-sum, VALU",
                                   2: f"grid (ES kernel W={w_grid}, pruned DFT), same k-set"}[args.kspace_algo],
                        "nlist_builds_in_timed_steps": f"{builds1 - builds0}/{evals1 - evals0}",

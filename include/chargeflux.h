@@ -27,7 +27,7 @@ extern "C" {
 #define CF_EXPORT __attribute__((visibility("default")))
 #endif
 
-#define CF_API_VERSION 2   /* 2: cf_params.one_4pi_eps0 */
+#define CF_API_VERSION 3   /* 2: cf_params.one_4pi_eps0; 3: cf_options.handover, pair_list, variants, list_capacity */
 
 /* Error codes (negative).  cf_last_error() returns the message of the last failure
  * on the calling thread.  Mirrors the reference's OpenMMException paths. */
@@ -96,11 +96,48 @@ typedef struct cf_options {
                             accumulates forces in fp32 and energies in fp64 per atom; every
                             other term stays fp64.  Accuracy target: RMS
                             relative force error <= 1e-4 against the fp64 build. */
-    int32_t reserved[5];
+    int32_t handover;    /* fork / join of the handle's second stream (grid k-space, see cf_set_overlap):
+                            CF_HANDOVER_EVENT (0, default): hipEvents, waited on by the command
+                            processor -- safe under any dispatch order;
+                            CF_HANDOVER_MEMORY (1): a one-thread counter kernel + hipStreamWaitValue64,
+                            ~5 us per hand-over cheaper, but the runtime executes the wait as a
+                            polling kernel, so a tool that serializes dispatches (rocprofv3 counter
+                            collection) can deadlock it.  Same results either way. */
+    int32_t pair_list;   /* direct-space neighbour list (periodic):
+                            CF_PAIR_LIST_AUTO (0): cluster-pair half list on one rank in fp64, per-atom
+                              half list on one rank in mixed precision, per-atom full list on several ranks;
+                            CF_PAIR_LIST_CLUSTER (1): the cluster-pair half list wherever its cell window
+                              fits (also mixed precision, and several ranks with an ownership filter);
+                            CF_PAIR_LIST_ATOM_HALF (2): the per-atom half list on one rank (full on several);
+                            CF_PAIR_LIST_FULL (3): the per-atom full (two-sided) list.
+                            Same pair set and the same results up to the fp64 summation order. */
+    int32_t variants;    /* CF_VARIANT_* bits: alternative kernels of the same sums, kept for A/B
+                            verification (0 = the production kernels) */
+    int32_t list_capacity;   /* cluster-pair list entries per i-cluster; 0 = automatic.  A list that
+                            overflows it is evaluated by the fp64 rescan (slow, same results). */
+    int32_t reserved[1];
 } cf_options;
 
 #define CF_PRECISION_DOUBLE 0
 #define CF_PRECISION_MIXED 1
+
+#define CF_HANDOVER_EVENT 0
+#define CF_HANDOVER_MEMORY 1
+
+#define CF_PAIR_LIST_AUTO 0
+#define CF_PAIR_LIST_CLUSTER 1
+#define CF_PAIR_LIST_ATOM_HALF 2
+#define CF_PAIR_LIST_FULL 3
+
+/* cf_options.variants (grid k-space; each equal to the production kernel to <= 1e-12 relative) */
+#define CF_VARIANT_GEMM_DFT 1        /* the DFT stages as fp64-MFMA complex GEMMs (k_g_cgemm), not the
+                                        8 x Q factorized stages (also used when a grid exceeds those) */
+#define CF_VARIANT_VECTOR_SPREAD 2   /* W > 9: the VALU spread (k_g_spread_tile), not the matrix cores */
+#define CF_VARIANT_MFMA_SPREAD 4     /* W <= 9: the matrix-core spread (k_g_spread_mfma) */
+#define CF_VARIANT_INTERP1 8         /* one atom per wave interpolation (k_g_interp) */
+#define CF_VARIANT_INTERP2 16        /* W <= 8: two atoms per wave (k_g_interp2), not four */
+#define CF_VARIANT_BLOCK_ROUNDS(r) (((r) & 15) << 8)   /* grid bin sort and energy kernels: r rounds of
+                                        256 atoms per block (1..8; 0 = by N) */
 
 /* compute flags */
 #define CF_INCLUDE_FORCES 1
@@ -197,7 +234,7 @@ CF_EXPORT int cf_set_graph(cf_handle* h, int enable);
 /* Number of graph captures and replays since cf_set_graph(h, 1). */
 CF_EXPORT int cf_get_graph_stats(const cf_handle* h, int64_t* captures, int64_t* replays);
 
-/* Second stream (default on; CF_OVERLAP=0 in the environment at cf_create turns it off): with the
+/* Second stream (default on; cf_options.handover selects its fork / join): with the
  * grid k-space a single-rank cf_compute runs the reciprocal chain, and the split-phase calls of
  * a multi-rank step run the direct-space chain, on a second stream of the handle, joined before
  * the chain rule.  Results are bitwise those of the one-stream order.  enable = 0 launches

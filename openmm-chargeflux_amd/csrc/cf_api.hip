@@ -202,16 +202,16 @@ void set_cells(cf_handle* H, const double L[3]) {
     // cells per axis), cells small enough for the kernel's LDS window (18 cells <= 4096 atoms,
     // with a margin for density variation: k_pairs_half flags the rare evaluation that does not
     // fit and k_excl then rescans) and sorted slots that fit the entry's 21 bits
-    const bool no_half = h.env_no_half;   // CF_HALF=0 at cf_create (A/B and tests)
-    const double per_cell = (double)h.n / (double)ncell;
-    // several ranks (CF_CLUSTER_MR=1, off by default): the cluster-pair form (fp64), with the
-    // builder keeping the cluster pairs that touch this rank's atoms (each rank evaluates those
+    // cf_options.pair_list.  Several ranks with CF_PAIR_LIST_CLUSTER: the cluster-pair form, with
+    // the builder keeping the cluster pairs that touch this rank's atoms (each rank evaluates those
     // once, both sides; k_excl gathers the partner-side sums of its own atoms).  Correct (the
     // multi-rank GPU tests pass with it) but slower than the full per-atom list at W = 4 / 8:
     // 0.336 / 0.304 against 0.255 / 0.197 ms rank-0 (profiles/r04ag_*): a thin slab's cells and
     // their window neighbours run whole 1024-thread blocks with the 128-KB window for few owned atoms
-    const bool want_cluster = h.env_cluster == 1 || (h.env_cluster < 0 && !h.mixed);
-    h.half = !no_half && h.pbc && (h.world == 1 || (want_cluster && h.env_cluster_mr)) && nc[0] >= 4 &&
+    const double per_cell = (double)h.n / (double)ncell;
+    const bool want_cluster = h.pair_list == CF_PAIR_LIST_CLUSTER || (h.pair_list == CF_PAIR_LIST_AUTO && !h.mixed);
+    h.half = h.pair_list != CF_PAIR_LIST_FULL && h.pbc &&
+             (h.world == 1 || (want_cluster && h.pair_list == CF_PAIR_LIST_CLUSTER)) && nc[0] >= 4 &&
              nc[1] >= 4 && nc[2] >= 4 && per_cell * 18.0 * 1.15 <= 4096.0 && h.n < (1 << 21);
     if (h.half && ncell > h.win_cells) {
         if (h.win_out) { (void)hipFree(h.win_out); (void)hipFree(h.win_woff); }
@@ -223,8 +223,8 @@ void set_cells(cf_handle* H, const double L[3]) {
     // cluster-pair half list (cf_kernels_cluster.hip): one rank, fp64, wherever
     // the per-atom half list applies.  Mixed precision keeps the per-atom list by default: its
     // fp32 term is cheap, so the cluster kernel's phase A (the fp32 atom tests and the queueing)
-    // costs more than it saves (C5: 1.425 vs 1.235 ms, profiles/r04e_*); CF_CLUSTER=1 forces it
-    // (tests), CF_CLUSTER=0 keeps the per-atom list in fp64 (A/B and tests)
+    // costs more than it saves (C5: 1.425 vs 1.235 ms, profiles/r04e_*); CF_PAIR_LIST_CLUSTER forces
+    // it, CF_PAIR_LIST_ATOM_HALF keeps the per-atom list in fp64
     h.cluster = h.half && want_cluster;
     h.zcol = 0;
     if (h.cluster) {
@@ -240,7 +240,7 @@ void set_cells(cf_handle* H, const double L[3]) {
         const double rl = h.cutoff + h.list_skin + ext;
         const double est = 0.5 * 4.0 / 3.0 * M_PI * rl * rl * rl * rho / 4.0 + 8.0;
         int cap = std::min(1536, ((int)(2.2 * est) + 64 + 15) / 16 * 16);
-        if (h.env_cluster_cap > 0) cap = std::max(4, std::min(cap, h.env_cluster_cap));   // tests: force overflows
+        if (h.list_capacity > 0) cap = std::max(4, std::min(cap, h.list_capacity));   // cf_options.list_capacity
         if (need > h.ncl_cap || cap != h.cpl_cap || ncell + 1 > h.cl_cells) {
             if (h.cl_start) { (void)hipFree(h.cl_start); (void)hipFree(h.cl_info); (void)hipFree(h.cl_bb);
                               (void)hipFree(h.cpl); (void)hipFree(h.cpl_cnt); }
@@ -443,11 +443,6 @@ struct Timed {
     }
 };
 
-void launch_check(const char* what) {
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) fail(CF_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
-}
-
 }  // namespace
 
 namespace cf {
@@ -495,21 +490,20 @@ CF_EXPORT int cf_create(const cf_params* p, const cf_options* opt, cf_handle** o
         if (o.precision != CF_PRECISION_DOUBLE && o.precision != CF_PRECISION_MIXED)
             fail(CF_ERR_INVALID, "precision must be CF_PRECISION_DOUBLE or CF_PRECISION_MIXED");
         h.mixed = o.precision == CF_PRECISION_MIXED;
-        h.overlap = !(getenv("CF_OVERLAP") && std::string(getenv("CF_OVERLAP")) == "0");   // A/B
-        // list-kind switches for A/B runs and tests, latched here (set_cells runs again on every rebuild)
-        h.env_no_half = getenv("CF_HALF") && std::string(getenv("CF_HALF")) == "0";
-        // CF_CLUSTER: "0" never the cluster-pair list, "1" also in mixed precision, unset: fp64 only
-        h.env_cluster = getenv("CF_CLUSTER") ? (std::string(getenv("CF_CLUSTER")) == "0" ? 0 : 1) : -1;
-        h.env_cluster_cap = getenv("CF_CLUSTER_CAP") ? atoi(getenv("CF_CLUSTER_CAP")) : 0;
-        h.env_direct_aux = !(getenv("CF_DIRECT_ON_AUX") && std::string(getenv("CF_DIRECT_ON_AUX")) == "0");
-        // fork / join by events with CF_SYNC=event, and whenever rocprofv3 collects counters
-        // (ROCPROF_COUNTER_COLLECTION in the environment): counter collection serializes the
-        // dispatches, and the runtime's hipStreamWaitValue64 is a polling kernel, which then holds
-        // the device while its producer waits behind it (a C3 --pmc pass hung, round 4)
-        const char* sy = getenv("CF_SYNC");
-        h.env_sync_events = sy ? std::string(sy) == "event" : getenv("ROCPROF_COUNTER_COLLECTION") != nullptr;
-        h.env_cluster_mr = getenv("CF_CLUSTER_MR") && std::string(getenv("CF_CLUSTER_MR")) == "1";
-        h.env_bin_rounds = getenv("CF_BIN_ROUNDS") ? std::max(0, std::min(8, atoi(getenv("CF_BIN_ROUNDS")))) : 0;
+        if (o.handover != CF_HANDOVER_EVENT && o.handover != CF_HANDOVER_MEMORY)
+            fail(CF_ERR_INVALID, "handover must be CF_HANDOVER_EVENT or CF_HANDOVER_MEMORY");
+        if (o.pair_list < CF_PAIR_LIST_AUTO || o.pair_list > CF_PAIR_LIST_FULL)
+            fail(CF_ERR_INVALID, "pair_list must be one of CF_PAIR_LIST_AUTO, _CLUSTER, _ATOM_HALF, _FULL");
+        if (o.variants & ~(0x1F | (15 << 8))) fail(CF_ERR_INVALID, "unknown bits in variants");
+        if (o.list_capacity < 0) fail(CF_ERR_INVALID, "list_capacity must be >= 0");
+        // the memory hand-over is opt-in: hipStreamWaitValue64 runs as a polling kernel on this
+        // runtime, so a dispatcher that serializes kernels (rocprofv3 counter collection) can run
+        // the wait ahead of its producer and hold the device (a C3 --pmc pass hung, round 4); the
+        // event waits are executed by the command processor and cannot starve anything
+        h.handover_memory = o.handover == CF_HANDOVER_MEMORY;
+        h.pair_list = o.pair_list;
+        h.variants = o.variants;
+        h.list_capacity = o.list_capacity;
         h.kspace_algo = o.kspace_algo;
         h.stream = (hipStream_t)o.stream;  // NULL = the null stream (orders with torch's default stream)
 
@@ -1193,12 +1187,14 @@ static void on_aux(cf_handle* H, GraphCache* g, int seg, const GraphKey& k, F&& 
     h.stream = main;
 }
 extern "C" {
-// Fork / join between the caller's stream and the second stream.  Events (CF_SYNC=event, A/B)
-// are recorded and waited between graph segments.  The default hands over by memory: the
-// producer's segment ends with k_signal (flag += 1, captured with the segment in graph mode),
-// the consumer's stream waits with hipStreamWaitValue64 for the count this evaluation reaches
-// (enqueued after the producer's launches, so a failed enqueue never leaves a wait for a signal
-// nobody sends).
+// Fork / join between the caller's stream and the second stream.  Default (CF_HANDOVER_EVENT):
+// agent-scope events, recorded after the producer's launches and waited on by the command
+// processor (barrier packets), so no dispatch order can let a wait hold the device.
+// CF_HANDOVER_MEMORY (opt-in): the producer's segment ends with k_signal (flag += 1, captured with
+// the segment in graph mode) and the consumer's stream waits with hipStreamWaitValue64 for the
+// count this evaluation reaches -- ~5 us cheaper per hand-over, but this runtime executes that wait
+// as a polling kernel (cf_create).  Every wait is enqueued after its producer's launches, so a
+// failed enqueue never leaves a wait for a signal nobody sends.
 static void fork_aux(cf::Handle& h) {   // event form: record on the caller's stream, wait on the second
     check_hip(hipEventRecord(h.ev_fork, h.stream), "hipEventRecord (fork)");
     check_hip(hipStreamWaitEvent(h.aux, h.ev_fork, 0), "hipStreamWaitEvent (fork)");
@@ -1210,12 +1206,12 @@ static void wait_fork(cf::Handle& h) {   // memory form, consumer side (the prod
 static void join_post(cf::Handle& h) {   // event form only (the memory form: k_signal(sync_flag + 1) on aux)
     check_hip(hipEventRecord(h.ev_join, h.aux), "hipEventRecord (join)");
 }
-// After a failed evaluation: the hand-over counts may be off by one (a signal enqueued whose wait
-// was not, or the reverse never happens: a wait is enqueued only after its signal).  Every wait
-// already enqueued has its signal enqueued before it, so draining both streams terminates; the
-// counts are then read back.
+// After a failed evaluation in the memory form: the hand-over counts may be off by one (a signal
+// enqueued whose wait was not, or the reverse never happens: a wait is enqueued only after its
+// signal).  Every wait already enqueued has its signal enqueued before it, so draining both
+// streams terminates; the counts are then read back.
 static void resync_flags(cf::Handle& h) {
-    if (!h.sync_flag) return;
+    if (!h.sync_flag || !h.handover_memory) return;
     (void)hipStreamSynchronize(h.stream);
     if (h.aux) (void)hipStreamSynchronize(h.aux);
     unsigned long long v[2] = {0, 0};
@@ -1232,8 +1228,18 @@ struct SyncGuard {
         if (std::uncaught_exceptions() > n) resync_flags(h);
     }
 };
+// a launch error reported after the launches of an entry point: the memory hand-over counts are
+// resynchronised before the error is returned (a begin that queued its signal but failed later
+// must not leave the next evaluation's wait satisfied by a stale count)
+static void launch_check(cf::Handle& h, const char* what) {
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        resync_flags(h);
+        fail(CF_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
+    }
+}
 static void join_wait(cf::Handle& h) {
-    if (h.env_sync_events) {
+    if (!h.handover_memory) {
         check_hip(hipStreamWaitEvent(h.stream, h.ev_join, 0), "hipStreamWaitEvent (join)");
         return;
     }
@@ -1269,48 +1275,35 @@ static void launch_full(cf_handle* H, const double* pos_dev, int flags, bool reu
         launch_rec_end(H, flags);
     };
     auto dch = [&] { launch_direct_chain(H, pos_dev, flags, reusable); };
-    if (!h.env_sync_events) {
-        // memory hand-overs: two segments per evaluation (one graph per stream in graph mode)
+    // The direct chain goes to the second stream and the reciprocal chain stays on the caller's.
+    // Each hand-over costs the waiting queue ~5-15 us (tools/sync_probe.hip); this way the join's
+    // wait sits behind the reciprocal chain, which ends last, so the direct chain's end is long
+    // signalled when the caller's queue reaches it: C3 0.4607-0.4642 -> 0.4486-0.4504 ms/step
+    // (profiles/r04q_*, the other way round)
+    if (h.handover_memory) {   // two segments per evaluation (one graph per stream in graph mode)
         SyncGuard sync_guard{h};
-        const bool dax = h.env_direct_aux;   // the reciprocal chain stays on the caller's stream
         run_segment(H, g, SEG_PRO, key, [&] {
             launch_prologue(H, pos_dev, reusable);
             cf::launch_signal(h, h.sync_flag);
-            if (dax) rec(); else dch();
+            rec();
         });
         wait_fork(h);
-        on_aux(H, g, dax ? SEG_DCH : SEG_REC, key, [&] {
-            if (dax) dch(); else rec();
+        on_aux(H, g, SEG_DCH, key, [&] {
+            dch();
             cf::launch_signal(h, h.sync_flag + 1);
         });
         join_wait(h);
-        h.rec_split = forces != 0;
-        Timed t(H, PH_ENERGY);
-        cf::launch_assemble_energy(h, (forces && forces_dev) ? forces_dev : nullptr, energy, energy_dev);
-        return;
-    }
-    run_segment(H, g, SEG_PRO, key, [&] { launch_prologue(H, pos_dev, reusable); });
-    fork_aux(h);
-    // The direct chain goes to the second stream and the reciprocal chain stays on the caller's
-    // (CF_DIRECT_ON_AUX=0: the other way round).  Each hand-over costs the waiting queue ~5-15 us
-    // (tools/sync_probe.hip); this way the join's wait sits behind the reciprocal chain, which
-    // ends last, so the direct chain's end is long signalled when the caller's queue reaches it:
-    // C3 0.4607-0.4642 -> 0.4486-0.4504 ms/step (profiles/r04q_*)
-    if (h.env_direct_aux) {
+    } else {
+        run_segment(H, g, SEG_PRO, key, [&] { launch_prologue(H, pos_dev, reusable); });
+        fork_aux(h);
         on_aux(H, g, SEG_DCH, key, dch);
         join_post(h);
         run_segment(H, g, SEG_REC, key, rec);
-    } else {
-        on_aux(H, g, SEG_REC, key, rec);
-        join_post(h);
-        run_segment(H, g, SEG_DCH, key, dch);
+        join_wait(h);
     }
-    join_wait(h);
     h.rec_split = forces != 0;
-    {
-        Timed t(H, PH_ENERGY);
-        cf::launch_assemble_energy(h, (forces && forces_dev) ? forces_dev : nullptr, energy, energy_dev);
-    }
+    Timed t(H, PH_ENERGY);
+    cf::launch_assemble_energy(h, (forces && forces_dev) ? forces_dev : nullptr, energy, energy_dev);
 }
 
 // Multi-rank split-phase calls with the grid k-space: the direct chain (cell sort, list, pair
@@ -1331,7 +1324,7 @@ static void launch_begin_split(cf_handle* H, const double* pos_dev, int flags, b
                                const double* box9) {
     cf::Handle& h = H->h;
     const GraphKey key = make_key(h, pos_dev, nullptr, nullptr, flags, reusable, box9);
-    if (!h.env_sync_events) {   // memory hand-overs (see fork_aux)
+    if (h.handover_memory) {   // memory hand-overs (see fork_aux)
         SyncGuard sync_guard{h};
         run_segment(H, g, SEG_PRO, key, [&] {
             launch_prologue(H, pos_dev, reusable);
@@ -1381,34 +1374,29 @@ static void launch_end_split(cf_handle* H, int flags, double* forces_dev, double
 static void ensure_aux(cf_handle* H) {
     cf::Handle& h = H->h;
     if (h.aux || !h.overlap || !h.pbc || h.kspace_algo != 2) return;
-    // CF_AUX_PRIORITY=low / high (A/B): the second stream's priority against the caller's
-    const char* pr = getenv("CF_AUX_PRIORITY");
-    if (pr && (std::string(pr) == "low" || std::string(pr) == "high")) {
-        int least = 0, greatest = 0;
-        check_hip(hipDeviceGetStreamPriorityRange(&least, &greatest), "hipDeviceGetStreamPriorityRange");
-        check_hip(hipStreamCreateWithPriority(&h.aux, hipStreamNonBlocking, std::string(pr) == "low" ? least : greatest),
-                  "hipStreamCreateWithPriority (second stream)");
-    } else {
-        check_hip(hipStreamCreateWithFlags(&h.aux, hipStreamNonBlocking), "hipStreamCreate (second stream)");
-    }
+    check_hip(hipStreamCreateWithFlags(&h.aux, hipStreamNonBlocking), "hipStreamCreate (second stream)");
     // fork / join order two streams of this device only: an agent-scope release is enough (kernel
     // ends already release to the device; the default system-scope fence of an event record
     // writes the L2s back for host visibility, ~15-20 us per fork and per join on the timeline,
-    // profiles/r04e_c3_timeline_eager_vs_graph.txt).  CF_EVENT_FENCE=system: the default fence (A/B)
-    const char* ef = getenv("CF_EVENT_FENCE");
-    const unsigned evf = hipEventDisableTiming | (ef && std::string(ef) == "system" ? 0u : hipEventDisableSystemFence);
+    // profiles/r04e_c3_timeline_eager_vs_graph.txt)
+    const unsigned evf = hipEventDisableTiming | hipEventDisableSystemFence;
     check_hip(hipEventCreateWithFlags(&h.ev_fork, evf), "hipEventCreate");
     check_hip(hipEventCreateWithFlags(&h.ev_join, evf), "hipEventCreate");
-    if (!h.sync_flag) {
-        // zeroed and drained before any wait is enqueued: the allocation may reuse a destroyed
-        // handle's flags, whose old counts would satisfy this handle's first waits at once (the
-        // second stream would start before its producer -- a C5 test saw wrong forces), and
-        // hipMemset runs on the null stream, which the non-blocking second stream does not follow
-        h.sync_flag = dalloc<unsigned long long>(H, 2);
-        check_hip(hipMemset(h.sync_flag, 0, 2 * sizeof(unsigned long long)), "sync flag init");
-        check_hip(hipDeviceSynchronize(), "sync flag init");
-        h.sync_seq = 0;
-        h.join_seq = 0;
+    if (h.handover_memory && !h.sync_flag) {
+        int can_wait = 0;
+        if (hipDeviceGetAttribute(&can_wait, hipDeviceAttributeCanUseStreamWaitValue, h.device) != hipSuccess ||
+            !can_wait) {
+            h.handover_memory = false;   // the runtime cannot wait on memory: events
+        } else {
+            // zeroed and drained before any wait is enqueued: the allocation may reuse a destroyed
+            // handle's flags, whose old counts would satisfy this handle's first waits at once (the
+            // second stream would start before its producer -- a C5 test saw wrong forces, round 4)
+            h.sync_flag = dalloc<unsigned long long>(H, 2);
+            check_hip(hipMemsetAsync(h.sync_flag, 0, 2 * sizeof(unsigned long long), h.aux), "sync flag init");
+            check_hip(hipStreamSynchronize(h.aux), "sync flag init");
+            h.sync_seq = 0;
+            h.join_seq = 0;
+        }
     }
     if (!h.dedq_rec) {
         h.dedq_rec = dalloc<double>(H, (size_t)h.n);
@@ -1468,7 +1456,7 @@ CF_EXPORT int cf_compute_begin(cf_handle* H, const double* pos_dev, const double
             run_segment(H, graph_active(H), SEG_BEGIN, make_key(h, pos_dev, nullptr, nullptr, flags, reusable, box9),
                         [&] { launch_begin(H, pos_dev, flags, reusable); });
         }
-        launch_check("compute_begin");
+        launch_check(h, "compute_begin");
         h.pending_flags = flags;
         h.direct_done = h.split_overlap;
     });
@@ -1497,7 +1485,7 @@ CF_EXPORT int cf_compute_direct(cf_handle* H) {
         if (H->h.pending_flags < 0) fail(CF_ERR_STATE, "cf_compute_direct without cf_compute_begin");
         check_hip(hipSetDevice(H->h.device), "hipSetDevice");
         run_direct(H);
-        launch_check("compute_direct");
+        launch_check(H->h, "compute_direct");
     });
 }
 
@@ -1518,7 +1506,7 @@ CF_EXPORT int cf_compute_end(cf_handle* H, double* forces_dev, double* energy_de
                         make_key(h, H->pos_pending, forces_dev, energy_dev, flags, false, h.pbc ? H->box9_last : nullptr),
                         [&] { launch_end(H, flags, forces_dev, energy_dev); });
         }
-        launch_check("compute_end");
+        launch_check(h, "compute_end");
     });
 }
 
@@ -1540,7 +1528,7 @@ CF_EXPORT int cf_compute(cf_handle* H, const double* pos_dev, const double* box9
         H->pos_pending = pos_dev;
         launch_full(H, pos_dev, flags, reusable, forces_dev, energy_dev, graph_active(H), box9);
         h.pending_flags = -1;
-        launch_check("compute");
+        launch_check(h, "compute");
     });
 }
 

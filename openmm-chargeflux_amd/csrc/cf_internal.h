@@ -77,13 +77,11 @@ struct GridPlan {
     // first mode of class r and the class size
     int mt[3] = {0, 0, 0};
     int rj[3][8] = {}, rc[3][8] = {};
-    bool dft8 = false;       // every axis qualifies and CF_DFT8 != 0
-    bool spread_dpp = true;  // spread FMAs take the x taps by DPP row broadcast (CF_SPREAD_DPP=0: scalar loads)
-    int spread_pass = 32;    // atoms per staging pass of the W > 9 spread (CF_SPREAD_PASS=64: A/B)
-    bool spread_mfma = true; // W > 9: the spread on the fp64 matrix cores, 16x8x8 tiles (CF_SPREAD_MFMA=0: k_g_spread_tile)
-    bool spread_mfma_all = false;   // CF_SPREAD_MFMA=2: the matrix form at every width (tests)
-    bool interp2 = true;     // two atoms per wave, taps by DPP row broadcast (CF_INTERP2=0: k_g_interp)
-    bool interp4 = true;     // W <= 8: four atoms per wave (CF_INTERP4=0: k_g_interp2)
+    bool dft8 = false;       // every axis qualifies and not CF_VARIANT_GEMM_DFT
+    bool spread_mfma = true; // W > 9: the spread on the fp64 matrix cores, 16x8x8 tiles (CF_VARIANT_VECTOR_SPREAD: k_g_spread_tile)
+    bool spread_mfma_all = false;   // CF_VARIANT_MFMA_SPREAD: the matrix form at every width
+    bool interp2 = true;     // two atoms per wave, taps by DPP row broadcast (CF_VARIANT_INTERP1: k_g_interp)
+    bool interp4 = true;     // W <= 8: four atoms per wave (CF_VARIANT_INTERP2: k_g_interp2)
 };
 
 struct Handle {
@@ -128,19 +126,19 @@ struct Handle {
     double* e_atom = nullptr;   // [N*3] per-atom (self, direct, exclusion) energy
     double* f_part = nullptr;   // [N*3] non-chain forces (recip + direct + excl)
     // single rank, grid k-space: the reciprocal chain runs on a second stream beside the cell
-    // list and direct space (CF_OVERLAP=0: one stream); its interpolation then stores into
+    // list and direct space (cf_set_overlap(h, 0): one stream); its interpolation then stores into
     // dedq_rec / f_rec, added by k_assemble_energy in the one-stream order ((direct + excl) + rec)
     bool overlap = true;
     bool rec_split = false;     // the last evaluation left the reciprocal dE/dq in dedq_rec
     bool split_overlap = false; // a begun multi-rank evaluation runs its direct chain on aux (cf_api.hip)
     hipStream_t aux = nullptr;
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
-    // fork / join by stream memory operations (hipStreamWriteValue64 / hipStreamWaitValue64 on
-    // sync_flag[0] / [1], value = the evaluation's sequence number): ~5.5 us per hand-over
-    // against ~11 (system-fence event) / ~8.5 (agent-fence event), tools/sync_probe.hip
+    // fork / join: agent-scope events (default), or with CF_HANDOVER_MEMORY by stream memory
+    // operations (k_signal / hipStreamWaitValue64 on sync_flag[0] / [1], value = the evaluation's
+    // sequence number): ~5.5 us per hand-over against ~8.5 (agent-fence event), tools/sync_probe.hip
     unsigned long long* sync_flag = nullptr;
     unsigned long long sync_seq = 0, join_seq = 0;   // the values sync_flag[0] / [1] reach this evaluation
-    bool env_sync_events = false;   // CF_SYNC=event at cf_create: fork / join by events (A/B)
+    bool handover_memory = false;   // cf_options.handover == CF_HANDOVER_MEMORY
     double* dedq_rec = nullptr; // [N]
     double* f_rec = nullptr;    // [N][4]: the interpolated gradient p and -q (force = -q (ng/L) p)
     // cell list
@@ -189,12 +187,10 @@ struct Handle {
     // cluster-pair half list (cf_kernels_cluster.hip): one rank, same window and
     // fixed-point j side as the half list; clusters = runs of <= 4 consecutive sorted slots of one cell
     bool cluster = false;
-    bool env_no_half = false;   // CF_HALF=0 at cf_create
-    int env_cluster = -1;       // CF_CLUSTER at cf_create: 0, 1, or -1 (unset: fp64 only)
-    int env_bin_rounds = 0;        // k_g_bin / k_assemble_energy rounds of 256 atoms per block (CF_BIN_ROUNDS; 0: by N)
-    bool env_cluster_mr = false;   // several ranks: the cluster-pair list (CF_CLUSTER_MR=1; default: the full per-atom list)
-    bool env_direct_aux = true;    // one rank's direct chain on the second stream (CF_DIRECT_ON_AUX=0 at cf_create: the reciprocal chain)
-    int env_cluster_cap = 0;    // CF_CLUSTER_CAP at cf_create (tests: a capacity that overflows)
+    int pair_list = CF_PAIR_LIST_AUTO;   // cf_options.pair_list
+    int list_capacity = 0;      // cf_options.list_capacity (0: automatic)
+    int variants = 0;           // cf_options.variants (CF_VARIANT_*)
+    int block_rounds() const { return (variants >> 8) & 15; }   // k_g_bin / k_assemble_energy rounds (0: by N)
     int zcol = 0;               // columns per cell axis of the within-cell sort (k_cell_order; 0 = atom order)
     int ncl_cap = 0;            // cluster capacity: N/4 + ncell
     int cl_cells = 0;           // cells cl_start is sized for (+1)

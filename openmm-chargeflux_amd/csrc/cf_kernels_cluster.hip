@@ -30,10 +30,7 @@
 namespace cf {
 
 constexpr int kClSize = 4;               // atoms per cluster
-#ifndef CF_CQ_WAVES
-#define CF_CQ_WAVES 16
-#endif
-constexpr int kCqWaves = CF_CQ_WAVES;    // waves per k_pairs_cq block (one cell, one block per CU: the LDS)
+constexpr int kCqWaves = 16;             // waves per k_pairs_cq block (one cell, one block per CU: the LDS)
 constexpr int kCqThreads = 64 * kCqWaves;
 constexpr int kCqQ = kCqWaves > 12 ? 88 : 112;   // queue entries per i atom (a ring; what the 160 KB LDS leaves)
 constexpr int kCqBatch = 16;             // list entries tested per phase-A step (64 j atoms, one per lane)
@@ -456,11 +453,7 @@ __global__ void __launch_bounds__(kCqThreads) CF_LDS_UNPAIRED k_pairs_cq(DirectA
             const double2 lj = TYPES ? ljt[(unsigned)wq >> kShiftBits] : a.ljs[j];
             const double dx = ddx, dy = ddy, dz = ddz;
             const double r2 = dx * dx + dy * dy + dz * dz;
-#if defined(CF_CQ_ABL) && CF_CQ_ABL == 1
-            if (act && r2 < 0.0) {   // ablation: no pair term
-#else
             if (act && r2 <= a.rc2) {   // exact voxel-hash test (RCK:567-569)
-#endif
                 const int slot = wdel[(wq >> kHalfSlotBits) & 31] + j;
                 const double ke = a.ke;
                 const double two_over_sqrtpi = 1.1283791670955126;
@@ -484,14 +477,10 @@ __global__ void __launch_bounds__(kCqThreads) CF_LDS_UNPAIRED k_pairs_cq(DirectA
                     acc.fx += nfx; acc.fy += nfy; acc.fz += nfz;
                     acc.dq += qj * ec;
                     bad |= !(fmax(fabs(ndEdRs) * a.rc, fabs(dqjs)) < kFixMax * kFixScale);
-#if !(defined(CF_CQ_ABL) && CF_CQ_ABL == 2)
                     atomicAdd(&accw[0][slot], scaled_to_fix(nfx));
                     atomicAdd(&accw[1][slot], scaled_to_fix(nfy));
                     atomicAdd(&accw[2][slot], scaled_to_fix(nfz));
                     atomicAdd(&accw[3][slot], scaled_to_fix(dqjs));
-#else
-                    acc.e += (double)slot * 1e-300;   // ablation: no partner-side atomics
-#endif
                 }
                 acc.e += qq * ec + es6 * (sig6 - 1);   // the whole pair energy: each pair once
             }

@@ -1810,12 +1810,15 @@ __global__ void k_signal(unsigned long long* __restrict__ flag) {
 
 void launch_signal(Handle& h, unsigned long long* flag) {
     hipLaunchKernelGGL(k_signal, dim3(1), dim3(64), 0, h.stream, flag);
+    // a signal that was not enqueued would leave its consumer's wait pending forever: fail inside
+    // the hand-over's scope (SyncGuard, cf_api.hip), which resynchronises the counts
+    check_hip(hipPeekAtLastError(), "k_signal launch");
 }
 
 void launch_assemble_energy(Handle& h, double* forces_out, int include_energy, double* energy_out) {
     const int nown = std::max(0, h.hi - h.lo);
     int nrec = (h.pbc && include_energy && h.rank == 0) ? h.e_rec_nblk : 0;
-    const int per = h.env_bin_rounds > 0 ? h.env_bin_rounds : std::max(1, std::min(8, nown / (kEChunk * 512)));   // as launch_grid_sort
+    const int per = h.block_rounds() > 0 ? std::min(8, h.block_rounds()) : std::max(1, std::min(8, nown / (kEChunk * 512)));   // as launch_grid_sort
     const int nparts = std::max(1, nblk(nown, kEChunk * per));
     hipLaunchKernelGGL(k_assemble_energy, dim3(nparts), dim3(kEChunk), 0, h.stream, h.lo, h.hi, h.ccsr_start,
                        h.ccsr_ent, h.dedq, h.dqdx, h.f_part, forces_out, h.rec_split ? h.dedq_rec : nullptr,

@@ -182,10 +182,7 @@ constexpr int kRow = 24;
 constexpr int kTapStride = 3 * kRow;
 constexpr int kOtWaves = 4;     // bins per 256-thread block: one wave per bin, no block barriers
 constexpr int kOtLds = 128;     // members per bin staged in LDS (denser bins read global memory)
-#ifndef CF_OT_CHUNK
-#define CF_OT_CHUNK 8   // build-time knob for A/B builds (-DCF_OT_CHUNK=16)
-#endif
-constexpr int kOtChunk = CF_OT_CHUNK;   // atoms whose tap rows are assembled in LDS at a time
+constexpr int kOtChunk = 8;     // atoms whose tap rows are assembled in LDS at a time (16, 24 slower)
 
 // LDS written by some lanes of a wave, then read by others of the same wave
 __device__ __forceinline__ void wave_sync() {
@@ -345,7 +342,7 @@ __device__ __forceinline__ void fma8_row_bcast(double (&acc)[8], double xv, doub
         : "v"(xv), "v"(yz));
 }
 
-template <int NS, int kSpPass, bool DPP>
+template <int NS, int kSpPass>
 __global__ void __launch_bounds__(256) CF_LDS_UNPAIRED k_g_spread_tile(int3 ng, int3 nb, const int* __restrict__ start,
                                                        const double* __restrict__ taps, const int4* __restrict__ g0s,
                                                        double* __restrict__ grid, const int* __restrict__ xr, int W) {
@@ -356,7 +353,6 @@ __global__ void __launch_bounds__(256) CF_LDS_UNPAIRED k_g_spread_tile(int3 ng, 
     __shared__ int bin_start[NB3], bin_pre[NB3 + 1], bin_db[NB3];
     __shared__ int src[kSpMaxSrc];   // slot << 6 | (dx, dy, dz) 2 bits each, of the segment's atoms that reach this tile
     __shared__ int wcnt[4 * (kSpMaxSrc / 256)];
-    __shared__ int xoff[2][kSpPass];   // offset in taps of each staged atom's x window
     // XCD-aware tile order (as in k_g_interp)
     const int nyz = nb.y * nb.z;
     int tile = blockIdx.x;
@@ -383,7 +379,7 @@ __global__ void __launch_bounds__(256) CF_LDS_UNPAIRED k_g_spread_tile(int3 ng, 
     __syncthreads();
     const int total = bin_pre[NB3];
     const int lane = t & 63, w = wave_id();
-    const int y = lane >> 3, z = lane & 7;
+    const int y = lane >> 3;   // this lane's (y, z) column: y = lane >> 3, z = lane & 7
     double acc[8];
 #pragma unroll
     for (int i = 0; i < 8; i++) acc[i] = 0.0;
@@ -437,12 +433,9 @@ __global__ void __launch_bounds__(256) CF_LDS_UNPAIRED k_g_spread_tile(int3 ng, 
         __syncthreads();
         if (nseg == 0) continue;
         // staging: 16-B piece e of the pass = atom e / 12, axis (e % 12) / 4, quarter e % 4 of the window
-        // (the x window is staged too although the FMAs read it from memory with scalar loads: those
-        // vector loads bring it into L2 ahead of them, 0.110 -> 0.100 ms at C3)
         constexpr int kPieces = kSpPass * kSpWin / 2;          // 768 at 64 atoms per pass
         constexpr int kPer = (kPieces + 255) / 256;             // 3 per thread at 64
         v2d r[kPer];
-        int xo_r[kPer];
         auto fetch = [&](int base, int n) {
 #pragma unroll
             for (int q = 0; q < kPer; q++) {
@@ -452,37 +445,33 @@ __global__ void __launch_bounds__(256) CF_LDS_UNPAIRED k_g_spread_tile(int3 ng, 
                 const int sb = src[u];
                 const int db = (sb >> (4 - 2 * d)) & 3;
                 const int off = (sb >> 6) * kTapStride + d * kRow + 8 * db;
-                xo_r[q] = off;
                 r[q] = *reinterpret_cast<const v2d*>(taps + off + 2 * h);
-                // DPP form: atoms past the pass end are staged as zero windows, so that the
-                // compute loop reads whole groups of four without bounds checks (adds exact zeros)
-                if (DPP && a >= n) r[q] = v2d{0.0, 0.0};
+                // atoms past the pass end are staged as zero windows, so that the compute loop
+                // reads whole groups of four without bounds checks (adds exact zeros)
+                if (a >= n) r[q] = v2d{0.0, 0.0};
             }
         };
-        auto stage = [&](double* buf, int* xb) {
+        auto stage = [&](double* buf) {
 #pragma unroll
             for (int q = 0; q < kPer; q++) {
                 const int e = t + 256 * q;
-                if (kPieces % 256 == 0 || e < kPieces) {
-                    reinterpret_cast<v2d*>(buf)[e] = r[q];
-                    if (e % 12 == 0) xb[e / 12] = xo_r[q];
-                }
+                if (kPieces % 256 == 0 || e < kPieces) reinterpret_cast<v2d*>(buf)[e] = r[q];
             }
         };
         const int npass = (nseg + kSpPass - 1) / kSpPass;
         fetch(0, min(kSpPass, nseg));
-        stage(st, xoff[0]);
+        stage(st);
         __syncthreads();
         for (int p = 0; p < npass; p++) {
             const int base = p * kSpPass, n = min(kSpPass, nseg - base);
             if (p + 1 < npass) fetch(base + kSpPass, min(kSpPass, nseg - base - kSpPass));
             const double* buf = st + (p & 1) * kSpPass * kSpWin;
-            const int* xb = xoff[p & 1];
-            if constexpr (DPP) {
+            {
                 // lane l reads x tap (l & 7) of the staged window, so lane i of every 16-lane row
                 // holds tap i, and each FMA takes tap i by a row broadcast of its operand
                 // (row_newbcast:i, 64-bit DPP): every operand comes from the LDS with 8-B per-lane
-                // reads, no scalar-load latency.  Same products and order as the scalar form.
+                // reads, no scalar-load latency (round 2 read the x window with wave-uniform scalar
+                // loads, whose latency every wave waited on).
                 // Four atoms per iteration: their twelve reads in flight together, one wait (a
                 // branch-free body at fixed offsets; the windows of atoms past the pass end are
                 // staged as zeros, kSpPass is a multiple of 16, so every read is in the buffer).
@@ -499,28 +488,8 @@ __global__ void __launch_bounds__(256) CF_LDS_UNPAIRED k_g_spread_tile(int3 ng, 
 #pragma unroll
                     for (int u = 0; u < 4; u++) fma8_row_bcast(acc, xv[u], yv[u] * zv[u]);
                 }
-            } else
-            // the x window is the same for every lane: scalar loads (SGPR operands of the FMAs),
-            // so the LDS serves only the per-lane y and z taps (2 of the 6 reads per atom)
-            // (two atoms per iteration: one wait covers both windows' scalar loads; four measured
-            // slower, 0.100 -> 0.110 ms at C3)
-            for (int a = w; a < n; a += 8) {
-                const bool two = a + 4 < n;
-                const double* rw0 = buf + a * kSpWin;
-                const double* rw1 = buf + (two ? a + 4 : a) * kSpWin;
-                const double* xw0 = taps + __builtin_amdgcn_readfirstlane(xb[a]);
-                const double* xw1 = taps + __builtin_amdgcn_readfirstlane(xb[two ? a + 4 : a]);
-                const double yz0 = rw0[8 + y] * rw0[16 + z];
-                const double yz1 = two ? rw1[8 + y] * rw1[16 + z] : 0.0;   // + 0 x: the same sums
-                double x0[8], x1[8];
-#pragma unroll
-                for (int i = 0; i < 8; i++) { x0[i] = xw0[i]; x1[i] = xw1[i]; }
-#pragma unroll
-                for (int i = 0; i < 8; i++) acc[i] = fma(x0[i], yz0, acc[i]);
-#pragma unroll
-                for (int i = 0; i < 8; i++) acc[i] = fma(x1[i], yz1, acc[i]);
             }
-            if (p + 1 < npass) stage(st + ((p + 1) & 1) * kSpPass * kSpWin, xoff[(p + 1) & 1]);
+            if (p + 1 < npass) stage(st + ((p + 1) & 1) * kSpPass * kSpWin);
             __syncthreads();
         }
     }
@@ -544,7 +513,7 @@ __device__ __forceinline__ d4 mfma64(double a, double b, d4 c) {
     return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
 }
 
-// Round 4: the spread as an fp64 matrix-core contraction (`CF_SPREAD_MFMA=0`: k_g_spread_tile).
+// Round 4: the spread as an fp64 matrix-core contraction (CF_VARIANT_VECTOR_SPREAD: k_g_spread_tile).
 // One 256-thread workgroup per 16 (x) x 8 (y) x 8 (z) tile, whose 1024 points are
 //     G[x][(y, z)] = sum_a X_a[x] (Y_a[y] Z_a[z])
 // over the tile's source atoms: per group of 4 atoms one v_mfma_f64_16x16x4_f64 per 16 (y, z)
@@ -564,13 +533,8 @@ __device__ __forceinline__ d4 mfma64(double a, double b, d4 c) {
 // kernel's order (equal to it to ~1e-15 relative).  When ng.x is an odd multiple of 8 (C5: 264)
 // the last x tile covers 8 planes: bin 2 tx + 1 wraps to bin 0, whose atoms reach only the
 // tile's missing half (rows < 0 are zero), and only the planes x < ng.x are written.
-#ifdef CF_SPM_WPE   // A/B builds: a waves-per-SIMD floor (VGPR cap) for k_g_spread_mfma
-#define CF_SPM_ATTR __attribute__((amdgpu_waves_per_eu(CF_SPM_WPE, 8)))
-#else
-#define CF_SPM_ATTR
-#endif
 template <int NS>
-__global__ void __launch_bounds__(256) CF_SPM_ATTR k_g_spread_mfma(int3 ng, int3 nb, const int* __restrict__ start,
+__global__ void __launch_bounds__(256) k_g_spread_mfma(int3 ng, int3 nb, const int* __restrict__ start,
                                                        const double* __restrict__ taps, const int4* __restrict__ g0s,
                                                        double* __restrict__ grid, const int* __restrict__ xr, int W) {
     constexpr int NBX = NS + 1;              // x bins per tile: dxb = ix - 1, ix < NBX
@@ -682,11 +646,7 @@ __global__ void __launch_bounds__(256) CF_SPM_ATTR k_g_spread_mfma(int3 ng, int3
         // every wave meet at each pass barrier: 51 of 81 us with the MFMAs removed).  Block bi + 2's
         // tap loads are issued as block bi starts, two blocks (32 MFMAs) before they are staged.
         const int nwb = (nseg + kBA - 1) / kBA;
-#if defined(CF_SPM_ABL) && CF_SPM_ABL == 3   // ablation: source lists only (timing only)
-        const int nb_w = 0 * nwb;
-#else
         const int nb_w = nwb > w ? (nwb - w + 3) / 4 : 0;   // this wave's blocks
-#endif
         v2d rva[4], rvb[4];
         auto fetch = [&](v2d (&rv)[4], int bi) {
             const int base = (w + 4 * bi) * kBA, n = min(kBA, nseg - base);
@@ -695,11 +655,7 @@ __global__ void __launch_bounds__(256) CF_SPM_ATTR k_g_spread_mfma(int3 ng, int3
                 const int a = a0 + 4 * q;
                 const int s = src[base + min(a, n - 1)];
                 const int wi = ((s >> fsh) & 3) + wadj;
-#if defined(CF_SPM_ABL) && CF_SPM_ABL == 2   // ablation: no tap loads (timing only)
-                const v2d v = v2d{(double)s, (double)(wi + poff)};
-#else
                 const v2d v = *reinterpret_cast<const v2d*>(taps + (size_t)(s >> 6) * kTapStride + poff + 8 * max(wi, 0));
-#endif
                 rv[q] = a < n && (unsigned)wi <= 2u ? v : v2d{0.0, 0.0};
             }
         };
@@ -723,12 +679,8 @@ __global__ void __launch_bounds__(256) CF_SPM_ATTR k_g_spread_mfma(int3 ng, int3
                 const double xa = xb[16 * a];
                 const double za = zb[8 * a];
                 const double* ya = yb + 8 * a;
-#if defined(CF_SPM_ABL) && CF_SPM_ABL == 1   // ablation: no MFMAs (timing only)
-                acc[0][0] += xa * ya[0] * za;
-#else
 #pragma unroll
                 for (int q = 0; q < 4; q++) acc[q] = mfma64(xa, ya[2 * q] * za, acc[q]);
-#endif
             }
             wave_sync();   // (keeps the compiler from moving the stores above the reads)
             if (bi + 1 < nb_w) stage(nxt);
@@ -1454,7 +1406,18 @@ __device__ __forceinline__ double wave_sum4(double pv, double px, double py, dou
 // row and 16-B aligned; the odd R's last pair reads one point past the halo, not stored).  Half
 // the loads and address computations of interp_stage (its VALU work was a third of
 // k_g_interp2's, profiles/r04i_*)
+// x-plane stride of k_g_interp2's halo (doubles): the smallest >= R^2 that is W..32-W modulo 32,
+// so that the two 16-lane rows of a half-wave -- x rows 2ii and 2ii + 1, W z points each --
+// fall on disjoint LDS banks (a ds_read_b64 group is 32 lanes over 64 four-byte banks, i.e.
+// 32 doubles: the rows' residues b..b+W-1 and b+SX..b+SX+W-1 mod 32 must not meet)
 template <int W>
+constexpr int interp_plane_stride() {
+    int s = (7 + W) * (7 + W);
+    while (s % 32 < W || s % 32 > 32 - W) s++;
+    return s;
+}
+
+template <int W, int SX = (7 + W) * (7 + W)>
 __device__ __forceinline__ void interp_stage16(int3 ng, const double* __restrict__ G, int tx, int ty, int tz,
                                                double* __restrict__ sg) {
     constexpr int R = 7 + W;
@@ -1467,20 +1430,18 @@ __device__ __forceinline__ void interp_stage16(int3 ng, const double* __restrict
     constexpr int kDA = RPP / R, kDB = RPP % R;
     if (r0 < RPP) {
         v2d gv[kRows];
+        int so[kRows];   // LDS row offset a * SX + b * R of halo row (a, b) = (x, y)
         int a = r0 / R, b = r0 - (r0 / R) * R;
         const int zy = ng.y * ng.z;
 #pragma unroll
         for (int q = 0; q < kRows; q++) {
             const bool in = r0 + q * RPP < R * R;
+            so[q] = a * SX + b * R;
             int x = 8 * tx + (in ? a : 0), y = 8 * ty + (in ? b : 0);
             x -= x >= ng.x ? ng.x : 0;
             y -= y >= ng.y ? ng.y : 0;
             const unsigned off = (unsigned)(x * zy + y * ng.z + z) * 8u;
-#if defined(CF_IN_ABL) && CF_IN_ABL == 2   // ablation: no halo loads (timing only)
-            gv[q] = v2d{(double)off, 0.0};
-#else
             gv[q] = *reinterpret_cast<const v2d*>(reinterpret_cast<const char*>(G) + off);
-#endif
             a += kDA; b += kDB;
             if (b >= R) { b -= R; a += 1; }
         }
@@ -1488,8 +1449,8 @@ __device__ __forceinline__ void interp_stage16(int3 ng, const double* __restrict
         for (int q = 0; q < kRows; q++) {
             const int row = r0 + q * RPP;
             if (row < R * R) {
-                sg[row * R + 2 * c] = gv[q].x;
-                if (2 * c + 1 < R) sg[row * R + 2 * c + 1] = gv[q].y;
+                sg[so[q] + 2 * c] = gv[q].x;
+                if (2 * c + 1 < R) sg[so[q] + 2 * c + 1] = gv[q].y;
             }
         }
     }
@@ -1521,11 +1482,7 @@ __device__ __forceinline__ void interp_stage(int3 ng, const double* __restrict__
             y -= y >= ng.y ? ng.y : 0;
             // 32-bit byte offset from the uniform base: one global_load with an SGPR base
             const unsigned off = (unsigned)(x * zy + y * ng.z + z) * 8u;
-#if defined(CF_IN_ABL) && CF_IN_ABL == 2   // ablation: no halo loads (timing only)
-            gv[q] = (double)off;
-#else
             gv[q] = *reinterpret_cast<const double*>(reinterpret_cast<const char*>(G) + off);
-#endif
             a += kDA; b += kDB;
             if (b >= R) { b -= R; a += 1; }
         }
@@ -1700,14 +1657,17 @@ __device__ __forceinline__ double half_sum4(double pv, double px, double py, dou
 }
 
 // Two atoms per wave, one per 32-lane half h.  Lane (h, jg, k): z column k of the tile's halo,
-// rows j = 2jj + jg (jj < NJ = ceil(W/2): no padded j rows at even W, 14 = 2 x 7).  Every tap
-// lives in a register: each lane evaluates x tap k, z tap k and y tap 2k + jg (k < NJ) of its
-// half's atom, and the contractions take the x and y taps they need from the lane that holds
-// them by DPP row broadcast (x tap i is in lane i of every row, y tap 2jj + jg in lane jj of
-// row jg), so the LDS serves only the potential halo (49 reads per atom instead of 56 plus 14
-// broadcast tap reads, no tap stores, no wave barriers).  t0 = sum_i G X_i, t1 = sum_i G dX_i
-// per (j, k), then pot / gradient by y and z as in k_g_interp; the four sums per half reduced
-// in a fixed order; lanes (h, 0..3) store.
+// x rows i = 2ii + jg (ii < NX2 = ceil(W/2)), every y row j < W, taken in two halves of NJH rows
+// (the accumulators of one half stay in registers).  Every tap lives in a register: each lane
+// evaluates x tap 2k + jg (k < NX2), y tap k and z tap k of its half's atom, and the contractions
+// take the x and y taps they need from the lane that holds them by DPP row broadcast (x tap 2ii +
+// jg in lane ii of row jg, y tap j in lane j of both rows), so the LDS serves only the potential
+// halo (49 reads per atom at W = 14).  A halo read of the two rows of a half hits x planes 2ii and
+// 2ii + 1, whose z runs lie on disjoint LDS banks with the plane stride SX (interp_plane_stride;
+// round 4 split the rows by y parity, 21 doubles apart: 3 of the 14 banks pairs met, 1.69
+// conflict cycles per LDS instruction).  t0 = sum_i G X_i, t1 = sum_i G dX_i per (j, k) over the
+// lane's x rows, then pot / gradient by y and z as in k_g_interp; the four sums of a half over
+// its 32 lanes (both x parities) reduced in a fixed order; lanes (h, 0..3) store.
 template <int W>
 __global__ void __launch_bounds__(kInterpThreads) CF_LDS_UNPAIRED k_g_interp2(int3 ng, int3 nb, const int* __restrict__ start,
                                                               const int4* __restrict__ g0s,
@@ -1716,10 +1676,13 @@ __global__ void __launch_bounds__(kInterpThreads) CF_LDS_UNPAIRED k_g_interp2(in
                                                               double* __restrict__ dedq, double* __restrict__ f_part,
                                                               int store) {
     constexpr int R = 7 + W;
-    constexpr int NJ = (W + 1) / 2;
+    constexpr int SX = interp_plane_stride<W>();
+    constexpr int NX2 = (W + 1) / 2;              // x rows per lane (the lane's parity)
+    constexpr int NJH = (W + 1) / 2;              // y rows per half
+    constexpr int NQ = 2 * NX2;                   // (y half, x row) steps
     constexpr int NW = kInterpThreads / 64;
     static_assert(W <= 16, "row broadcast reaches lanes 0..15");
-    extern __shared__ double sg[];   // [R][R][R]
+    extern __shared__ double sg[];   // [R][SX]: x planes of R rows of R z points
     const int nyz = nb.y * nb.z;
     int tile = blockIdx.x;
     if (nyz % 8 == 0) {
@@ -1729,12 +1692,8 @@ __global__ void __launch_bounds__(kInterpThreads) CF_LDS_UNPAIRED k_g_interp2(in
     const int s0 = start[tile], s1 = start[tile + 1];
     if (s0 == s1) return;
     const int tz = tile % nb.z, ty = (tile / nb.z) % nb.y, tx = tile / (nb.z * nb.y);
-    interp_stage16<W>(ng, G, tx, ty, tz, sg);
+    interp_stage16<W, SX>(ng, G, tx, ty, tz, sg);
     __syncthreads();
-#if defined(CF_IN_ABL) && CF_IN_ABL == 1   // ablation: staging only (timing only)
-    if (sg[threadIdx.x] == 1.2345e300) dedq[threadIdx.x] = 0.0;
-    return;
-#endif
     const int lane = threadIdx.x & 63, w = wave_id();
     const int h = lane >> 5, jg = (lane >> 4) & 1, k = lane & 15;
     const double hw_inv = 2.0 / W;
@@ -1750,61 +1709,72 @@ __global__ void __launch_bounds__(kInterpThreads) CF_LDS_UNPAIRED k_g_interp2(in
             g_n = g0s[sb + 2 * NW + h];
             sr_n = srec[g_n.w];
         }
-        // taps (t = g0 + m - s, g0 = ceil(s - W/2)): x tap k, y tap 2k + jg, z tap k; zero
+        // taps (t = g0 + m - s, g0 = ceil(s - W/2)): y tap k, z tap k, x tap 2k + jg; zero
         // beyond the support
-        // (one pass for x and z: row jg = 0 of each half evaluates x tap k, row 1 z tap k, and a
+        // (one pass for y and z: row jg = 0 of each half evaluates y tap k, row 1 z tap k, and a
         // v_permlane16_swap copies each row's values into the other, so every lane ends with both)
         double xv = 0, xd = 0, yv = 0, yd = 0, zv = 0, zd = 0;
         {
-            const double sd = jg ? sr.z : sr.x;
+            const double sd = jg ? sr.z : sr.y;
             double v = 0, dv = 0;
             if (k < W) es_tap(ceil(sd - 0.5 * W) + k - sd, hw_inv, beta, v, dv);
-            rows_even_odd(v, xv, zv);
-            rows_even_odd(dv, xd, zd);
+            rows_even_odd(v, yv, zv);
+            rows_even_odd(dv, yd, zd);
         }
-        if (k < NJ && 2 * k + jg < W) es_tap(ceil(sr.y - 0.5 * W) + (2 * k + jg) - sr.y, hw_inv, beta, yv, yd);
+        if (k < NX2 && 2 * k + jg < W) es_tap(ceil(sr.x - 0.5 * W) + (2 * k + jg) - sr.x, hw_inv, beta, xv, xd);
         xv = dpp_ready(xv); xd = dpp_ready(xd); yv = dpp_ready(yv); yd = dpp_ready(yd);
         const int rx = g.x & 7, ry = g.y & 7, rz = g.z & 7;
-        const double* base = sg + (rx * R + ry) * R + rz + (k < W ? k : 0);
-        double t0[NJ], t1[NJ];   // row 0 initialises them (products: no zero fill)
-        // x rows i in order; the NJ halo reads of row i + 1 are issued before row i's FMAs (the
-        // scheduling barriers keep them there: the compiler otherwise sinks each read to its
-        // first use, behind the inline asm, one LDS latency per read)
-        double gv[2][NJ];
-        auto load_row = [&](int i, double (&g)[NJ]) {
+        const double* base = sg + (rx + jg) * SX + ry * R + rz + (k < W ? k : 0);
+        double t0[NJH], t1[NJH];   // the first x row of a y half initialises them (products)
+        double pv = 0, px = 0, py = 0;
+        // steps q = (y half, x row ii) in order; the NJH halo reads of step q + 1 are issued
+        // before step q's FMAs (the scheduling barriers keep them there: the compiler otherwise
+        // sinks each read to its first use, behind the inline asm, one LDS latency per read)
+        double gv[2][NJH];
+        // odd W: x row W of the jg = 1 lanes lies past the halo (its tap is zero); they re-read row
+        // W - 1 of the jg = 0 lanes (the same addresses: a broadcast)
+        const int xlast = (W % 2 == 1 && jg) ? -SX : 0;
+        auto load_step = [&](int q, double (&gq)[NJH]) {
+            const int yh = q / NX2, ii = q % NX2;
+            const int xo = 2 * ii * SX + (ii == NX2 - 1 ? xlast : 0);
 #pragma unroll
-            for (int jj = 0; jj < NJ; jj++) {
-                const int j = 2 * jj + jg;
-                g[jj] = base[(i * R + (j < W ? j : 0)) * R];
+            for (int jj = 0; jj < NJH; jj++) {
+                const int j = yh * NJH + jj;
+                gq[jj] = base[xo + (j < W ? j : 0) * R];
             }
         };
-        load_row(0, gv[0]);
-        static_for<W>([&](auto I) {
-            constexpr int i = decltype(I)::value;
-            if constexpr (i + 1 < W) load_row(i + 1, gv[(i + 1) & 1]);
+        load_step(0, gv[0]);
+        static_for<NQ>([&](auto Q) {
+            constexpr int q = decltype(Q)::value;
+            constexpr int yh = q / NX2, ii = q % NX2;
+            if constexpr (q + 1 < NQ) load_step(q + 1, gv[(q + 1) & 1]);
             __builtin_amdgcn_sched_barrier(0);
-            if constexpr (i == 0) {
+            if constexpr (ii == 0) {
                 const double x0 = row_bcast0(xv), d0 = row_bcast0(xd);
 #pragma unroll
-                for (int jj = 0; jj < NJ; jj++) {
-                    t0[jj] = x0 * gv[0][jj];
-                    t1[jj] = d0 * gv[0][jj];
+                for (int jj = 0; jj < NJH; jj++) {
+                    t0[jj] = x0 * gv[q & 1][jj];
+                    t1[jj] = d0 * gv[q & 1][jj];
                 }
             } else {
 #pragma unroll
-                for (int jj = 0; jj < NJ; jj++) {
-                    fmac_row_bcast<i>(t0[jj], xv, gv[i & 1][jj]);
-                    fmac_row_bcast<i>(t1[jj], xd, gv[i & 1][jj]);
+                for (int jj = 0; jj < NJH; jj++) {
+                    fmac_row_bcast<ii>(t0[jj], xv, gv[q & 1][jj]);
+                    fmac_row_bcast<ii>(t1[jj], xd, gv[q & 1][jj]);
                 }
             }
             __builtin_amdgcn_sched_barrier(0);
-        });
-        double pv = 0, px = 0, py = 0;
-        static_for<NJ>([&](auto J) {
-            constexpr int jj = decltype(J)::value;
-            fmac_row_bcast<jj>(pv, yv, t0[jj]);
-            fmac_row_bcast<jj>(px, yv, t1[jj]);
-            fmac_row_bcast<jj>(py, yd, t0[jj]);
+            if constexpr (ii == NX2 - 1) {   // this y half done: contract with its y taps
+                static_for<NJH>([&](auto J) {
+                    constexpr int jj = decltype(J)::value;
+                    constexpr int j = yh * NJH + jj;
+                    if constexpr (j < W) {
+                        fmac_row_bcast<j>(pv, yv, t0[jj]);
+                        fmac_row_bcast<j>(px, yv, t1[jj]);
+                        fmac_row_bcast<j>(py, yd, t0[jj]);
+                    }
+                });
+            }
         });
         const double pz = pv * zd;
         pv *= zv; px *= zv; py *= zv;
@@ -2025,19 +1995,12 @@ void grid_plan(Handle& h, int width, double sigma) {
     p.KX = h.kmax[0]; p.KY = h.kmax[1]; p.KZ = h.kmax[2];
     p.NX = 2 * p.KX - 1; p.NY = 2 * p.KY - 1;
     // factorized stages: mode set k0 + j, j < J per axis (x, y: |n| < K; z: 0 <= nz < K)
-    const char* env = getenv("CF_DFT8");
-    p.dft8 = !(env && env[0] == '0');
-    const char* sd = getenv("CF_SPREAD_DPP");
-    p.spread_dpp = !(sd && sd[0] == '0');
-    const char* sp = getenv("CF_SPREAD_PASS");
-    p.spread_pass = sp ? std::atoi(sp) : 32;
-    const char* sm = getenv("CF_SPREAD_MFMA");
-    p.spread_mfma = !(sm && sm[0] == '0');
-    p.spread_mfma_all = sm && sm[0] == '2';
-    const char* i2 = getenv("CF_INTERP2");
-    p.interp2 = !(i2 && i2[0] == '0');
-    const char* i4 = getenv("CF_INTERP4");
-    p.interp4 = !(i4 && i4[0] == '0');
+    // alternative kernels of the same sums (cf_options.variants, A/B verification)
+    p.dft8 = !(h.variants & CF_VARIANT_GEMM_DFT);
+    p.spread_mfma = !(h.variants & CF_VARIANT_VECTOR_SPREAD);
+    p.spread_mfma_all = (h.variants & CF_VARIANT_MFMA_SPREAD) != 0;
+    p.interp2 = !(h.variants & CF_VARIANT_INTERP1);
+    p.interp4 = !(h.variants & CF_VARIANT_INTERP2);
     for (int d = 0; d < 3; d++) {
         const int K = h.kmax[d], J = d == 2 ? K : 2 * K - 1, k0 = d == 2 ? 0 : -(K - 1);
         int mx = 0;
@@ -2112,7 +2075,7 @@ void launch_grid_sort(Handle& h, const double* pos) {
     const double3 L = make_double3(h.box_L[0], h.box_L[1], h.box_L[2]);
     // g_cnt is zero here: cleared at cf_create and by k_g_scatter of the previous evaluation
     // at least ~512 blocks of 256 atoms each round; up to 8 rounds per block (C5: 5, C3: 1)
-    const int per = h.env_bin_rounds > 0 ? h.env_bin_rounds : std::max(1, std::min(8, nown / (256 * 512)));
+    const int per = h.block_rounds() > 0 ? std::min(8, h.block_rounds()) : std::max(1, std::min(8, nown / (256 * 512)));
     hipLaunchKernelGGL(k_g_bin, dim3(nblk(nown, 256 * per)), dim3(256), 0, h.stream, h.lo, nown, pos, h.q, L, ng, p.W,
                        nb, h.g_srec, h.g_g0u, h.g_rank, h.g_cnt, h.g_xrange, h.e_ticket + kTicketGrid, h.g_start, per);
     hipLaunchKernelGGL(k_g_scatter, dim3(nblk(nown, 256)), dim3(256), 0, h.stream, nown, h.g_g0u, h.g_rank, h.g_start,
@@ -2147,12 +2110,12 @@ void launch_grid_sort(Handle& h, const double* pos) {
 void launch_grid_spread(Handle& h) {
     const GridPlan& p = h.gp;
     const int3 ng = make_int3(p.ng[0], p.ng[1], p.ng[2]), nb = make_int3(p.nb[0], p.nb[1], p.nb[2]);
-#define CF_SPT(NS_, P_, D_) hipLaunchKernelGGL((k_g_spread_tile<NS_, P_, D_>), dim3(p.nbins), dim3(256), 0, h.stream, \
+#define CF_SPT(NS_, P_) hipLaunchKernelGGL((k_g_spread_tile<NS_, P_>), dim3(p.nbins), dim3(256), 0, h.stream, \
                                                ng, nb, h.g_start, h.g_taps, h.g_g0s, h.g_grid, h.g_xrange, p.W)
     // the matrix-core form (16 x 8 x 8 tiles, 4 distinct x bins) for W > 9; at W <= 9 (the mixed
     // C5 grid) the vector form with its 8^3 tiles and 8 source bins measured faster (322 against
     // 330 us at C5: the 16-wide x tile doubles the zero-tap share of a narrow kernel)
-    // (CF_SPREAD_MFMA=2 selects the matrix form at any width, for the tests; 0 never)
+    // (CF_VARIANT_MFMA_SPREAD selects the matrix form at any width, CF_VARIANT_VECTOR_SPREAD never)
     if (p.spread_mfma && nb.x >= 4 && (p.W > 9 || p.spread_mfma_all)) {
         const dim3 g((unsigned)((ng.x + 15) / 16 * nb.y * nb.z));
         if (p.W <= 9)
@@ -2165,13 +2128,8 @@ void launch_grid_spread(Handle& h) {
     }
     // a first tap in bin B reaches tiles B .. B + NS - 1: NS = 2 when W <= 9 (8 source bins per
     // tile instead of 27).  Passes of 32 atoms at W = 14 (64 / 128 measured slower at C3)
-    if (p.W <= 9) {
-        if (p.spread_dpp) { CF_SPT(2, 64, true); } else { CF_SPT(2, 64, false); }
-    } else if (p.spread_dpp && p.spread_pass == 64) {   // A/B (CF_SPREAD_PASS=64)
-        CF_SPT(3, 64, true);
-    } else {
-        if (p.spread_dpp) { CF_SPT(3, 32, true); } else { CF_SPT(3, 32, false); }
-    }
+    if (p.W <= 9) CF_SPT(2, 64);
+    else CF_SPT(3, 32);
 #undef CF_SPT
 }
 
@@ -2372,12 +2330,13 @@ void launch_grid_interp(Handle& h, bool split) {
     const int3 ng = make_int3(p.ng[0], p.ng[1], p.ng[2]), nb = make_int3(p.nb[0], p.nb[1], p.nb[2]);
     const double3 gs = make_double3(p.ng[0] / h.box_L[0], p.ng[1] / h.box_L[1], p.ng[2] / h.box_L[2]);
     const size_t R = 7 + p.W;
-    const size_t lds = R * R * R * sizeof(double);
-    // W <= 8: four atoms per wave (k_g_interp4); else two (k_g_interp2); CF_INTERP2=0: one (k_g_interp)
+    // W <= 8: four atoms per wave (k_g_interp4); else two (k_g_interp2); CF_VARIANT_INTERP1: one (k_g_interp)
 #define CF_INTERP(W_)                                                                                               \
     hipLaunchKernelGGL(!p.interp2 ? k_g_interp<W_> : (W_ <= 8 && p.interp4) ? k_g_interp4<(W_ <= 8 ? W_ : 8)>      \
                                                                            : k_g_interp2<W_>,                          \
-                       dim3(p.nbins), dim3(kInterpThreads), lds,                                                    \
+                       dim3(p.nbins), dim3(kInterpThreads),                                                         \
+                       (!p.interp2 || (W_ <= 8 && p.interp4) ? R * R : (size_t)interp_plane_stride<W_>()) * R *     \
+                           sizeof(double),                                                                          \
                        h.stream, ng, nb, h.g_start, h.g_g0s, h.g_srec, p.beta, gs, h.g_grid, h.lo,                   \
                        split ? h.dedq_rec : h.dedq, split ? h.f_rec : h.f_part, split ? 1 : 0)
     CF_GRID_W_DISPATCH(p.W, CF_INTERP)

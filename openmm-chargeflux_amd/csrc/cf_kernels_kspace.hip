@@ -593,13 +593,9 @@ void kspace_plan(Handle& h) {
     sp.nchunks = std::max(1, (nown + sp.chunk_atoms - 1) / sp.chunk_atoms);
     // ---- force pass
     FPassPlan& fp = h.fp;
-    // variant (NA, waves): (2, 8) default; CF_FORCE_VARIANT=1 -> (4, 4), 2 -> (2, 4)
+    // (NA, waves) = (2, 8): 16-atom tiles per wave, waves per workgroup ((4, 4) and (2, 4) measured slower)
     fp.na = 2;
     fp.waves = 8;
-    if (const char* v = getenv("CF_FORCE_VARIANT")) {
-        if (atoi(v) == 1) { fp.na = 4; fp.waves = 4; }
-        if (atoi(v) == 2) { fp.na = 2; fp.waves = 4; }
-    }
     int atoms_per_wg = fp.na * 16 * fp.waves;
     fp.natom_groups = std::max(1, (nown + atoms_per_wg - 1) / atoms_per_wg);
     fp.kchunks = g.NB;
@@ -690,12 +686,7 @@ void launch_kspace_force(Handle& h, const double* pos) {
     a.lo = h.lo; a.nown = h.hi - h.lo; a.npad = h.npad; a.msplit = h.fp.msplit;
     a.cs = h.tab_cs; a.coef = h.coef_a; a.pos = pos; a.q = h.q; a.t_part = h.t_part;
     dim3 grid(h.fp.natom_groups, h.fp.kchunks * h.fp.msplit);
-    if (h.fp.na == 4 && h.fp.waves == 4)
-        hipLaunchKernelGGL((k_force<4, 4>), grid, dim3(256), 0, h.stream, a);
-    else if (h.fp.na == 2 && h.fp.waves == 4)
-        hipLaunchKernelGGL((k_force<2, 4>), grid, dim3(256), 0, h.stream, a);
-    else
-        hipLaunchKernelGGL((k_force<2, 8>), grid, dim3(512), 0, h.stream, a);
+    hipLaunchKernelGGL((k_force<2, 8>), grid, dim3(512), 0, h.stream, a);
 }
 
 // =================================================================================

@@ -21,6 +21,23 @@ CF_ERR_STATE = -3
 CF_ERR_NOMEM = -4
 CF_PRECISION_DOUBLE = 0
 CF_PRECISION_MIXED = 1
+CF_HANDOVER_EVENT = 0
+CF_HANDOVER_MEMORY = 1
+CF_PAIR_LIST_AUTO = 0
+CF_PAIR_LIST_CLUSTER = 1
+CF_PAIR_LIST_ATOM_HALF = 2
+CF_PAIR_LIST_FULL = 3
+CF_VARIANT_GEMM_DFT = 1
+CF_VARIANT_VECTOR_SPREAD = 2
+CF_VARIANT_MFMA_SPREAD = 4
+CF_VARIANT_INTERP1 = 8
+CF_VARIANT_INTERP2 = 16
+
+
+def CF_VARIANT_BLOCK_ROUNDS(r: int) -> int:
+    return (int(r) & 15) << 8
+
+
 CF_INCLUDE_FORCES = 1
 CF_INCLUDE_ENERGY = 2
 ONE_4PI_EPS0 = 138.935456                    # OpenMM 7.x headers: cf_params.one_4pi_eps0 = 0
@@ -61,7 +78,11 @@ class cf_options(C.Structure):
         ("kspace_algo", C.c_int32),
         ("grid_width", C.c_int32),
         ("precision", C.c_int32),
-        ("reserved", C.c_int32 * 5),
+        ("handover", C.c_int32),
+        ("pair_list", C.c_int32),
+        ("variants", C.c_int32),
+        ("list_capacity", C.c_int32),
+        ("reserved", C.c_int32 * 1),
     ]
 
 

@@ -33,7 +33,8 @@ class ShardedCoulKernel:
     (device scalar) and adds forces for this rank's owned atoms into `forces`."""
 
     def __init__(self, system, force, device: int, group=None, kspace_algo: int = 0, kernel=None,
-                 neighbor_skin: float = 0.0, grid_width: int = 0, precision: str = "double"):
+                 neighbor_skin: float = 0.0, grid_width: int = 0, precision: str = "double", **options):
+        """options: further HipCalcCoulForceKernel options (pair_list, handover, variants, ...)."""
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
@@ -42,7 +43,7 @@ class ShardedCoulKernel:
             stream = torch.cuda.current_stream(self.device).cuda_stream
             kernel = HipCalcCoulForceKernel(device=device, stream=stream, rank=self.rank, world_size=self.world,
                                             kspace_algo=kspace_algo, grid_width=grid_width,
-                                            precision=precision).initialize(system, force)
+                                            precision=precision, **options).initialize(system, force)
             if neighbor_skin > 0:
                 kernel.set_neighbor_skin(neighbor_skin)
         else:  # any object with the split-phase kernel interface (tests drive this on CPU/gloo)

@@ -75,11 +75,28 @@ class HipCalcCoulForceKernel:
     KSPACE_EXACT_VALU = 1   # exact k-sum, direct sincos (check path)
     KSPACE_GRID = 2         # same k-sum via ES-kernel grid (spread, pruned DFT, interpolate)
 
+    PAIR_LISTS = {"auto": _cabi.CF_PAIR_LIST_AUTO, "cluster": _cabi.CF_PAIR_LIST_CLUSTER,
+                  "atom_half": _cabi.CF_PAIR_LIST_ATOM_HALF, "full": _cabi.CF_PAIR_LIST_FULL}
+    HANDOVERS = {"event": _cabi.CF_HANDOVER_EVENT, "memory": _cabi.CF_HANDOVER_MEMORY}
+
     def __init__(self, device: int = 0, stream=None, rank: int = 0, world_size: int = 1, kspace_algo: int = 0,
-                 grid_width: int = 0, precision: str = "double", one_4pi_eps0: float = 0.0):
+                 grid_width: int = 0, precision: str = "double", one_4pi_eps0: float = 0.0,
+                 pair_list: str = "auto", handover: str = "event", variants: int = 0, list_capacity: int = 0):
         """one_4pi_eps0: ONE_4PI_EPS0 of the OpenMM the force is evaluated for (the reference
         takes it from openmm/reference/SimTKOpenMMRealType.h, ReferenceCoulKernels.cpp:7);
-        0 = 138.935456 (OpenMM 7.x), _cabi.ONE_4PI_EPS0_CODATA2018 for OpenMM 8.x."""
+        0 = 138.935456 (OpenMM 7.x), _cabi.ONE_4PI_EPS0_CODATA2018 for OpenMM 8.x.
+        pair_list, handover, variants, list_capacity: cf_options fields (include/chargeflux.h):
+        the neighbour-list kind ("auto", "cluster", "atom_half", "full"), the second stream's
+        fork / join ("event" or the opt-in "memory"), CF_VARIANT_* bits (alternative kernels of the
+        same sums) and the cluster-pair list capacity (0 = automatic)."""
+        if pair_list not in self.PAIR_LISTS:
+            raise ValueError(f"pair_list must be one of {sorted(self.PAIR_LISTS)}")
+        if handover not in self.HANDOVERS:
+            raise ValueError(f"handover must be one of {sorted(self.HANDOVERS)}")
+        self._pair_list = self.PAIR_LISTS[pair_list]
+        self._handover = self.HANDOVERS[handover]
+        self._variants = int(variants)
+        self._list_capacity = int(list_capacity)
         self._lib = _cabi.load_library()
         self._ke = float(one_4pi_eps0)
         self._grid_width = grid_width
@@ -108,6 +125,8 @@ class HipCalcCoulForceKernel:
         opt.rank, opt.world_size, opt.kspace_algo = self._rank, self._world, self._algo
         opt.grid_width = self._grid_width
         opt.precision = self._precision
+        opt.handover, opt.pair_list = self._handover, self._pair_list
+        opt.variants, opt.list_capacity = self._variants, self._list_capacity
         self.destroy()
         _cabi.check(self._lib.cf_create(C.byref(params), C.byref(opt), C.byref(self._h)), self._lib)
         del keep

@@ -3,7 +3,7 @@ clusters of <= 4 cell-sorted atoms, one list entry per cluster pair with a 16-bi
 (exclusions, the self pair's triangle, partial clusters), an fp32 cutoff prefilter whose hits are
 compacted into per-atom queues, and the fp64 pair term with the exact r <= rc test.  It must
 evaluate exactly the reference's pair set (RCK:559-593): checked against the per-atom half list
-(CF_CLUSTER=0), the full two-sided list (CF_HALF=0) and the oracle.
+(pair_list "atom_half"), the full two-sided list (pair_list "full") and the oracle.
 
 Tolerances (written here): cluster vs per-atom half list forces <= 2e-12 max|F| + 1e-9 kJ/mol/nm
 (the same pairs; the partner side in 2^-34 fixed point, the i side summed in another order:
@@ -89,8 +89,8 @@ def test_cluster_list_odd_cells_and_exclusions():
 
 
 @pytest.mark.parametrize("world", [2, 4])
-def test_cluster_list_on_several_ranks_opt_in(monkeypatch, world):
-    """The ownership-filtered cluster-pair list on several ranks (CF_CLUSTER_MR=1, opt-in: slower
+def test_cluster_list_on_several_ranks_opt_in(world):
+    """The ownership-filtered cluster-pair list on several ranks (pair_list "cluster", opt-in: slower
     than the full per-atom list at W = 4/8): `world` handles on this GPU, the k-space
     buffers summed by hand, against one rank -- each rank evaluates the cluster pairs that touch
     its atoms, k_excl gathers its atoms' partner-side sums."""
@@ -101,8 +101,7 @@ def test_cluster_list_on_several_ranks_opt_in(monkeypatch, world):
     e1, f1 = k.execute_host(pos, box)
     d1, t1 = k.dedq(), k.energy_terms()
     k.destroy()
-    monkeypatch.setenv("CF_CLUSTER_MR", "1")
-    ew, fw, dw, _ = _decomposed(system, force, pos, box, world, 2)
+    ew, fw, dw, _ = _decomposed(system, force, pos, box, world, 2, pair_list="cluster")
     assert abs(ew - e1) <= 1e-11 * np.abs(t1).sum()
     assert np.abs(fw - f1).max() <= 2e-12 * np.abs(f1).max() + 1e-9
     assert np.abs(dw - d1).max() <= 2e-12 * np.abs(d1).max() + 1e-9

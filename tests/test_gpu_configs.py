@@ -28,7 +28,7 @@ pytestmark = pytest.mark.gpu
 
 torch = pytest.importorskip("torch")
 
-from openmmcoul import HipCalcCoulForceKernel  # noqa: E402
+from openmmcoul import HipCalcCoulForceKernel, _cabi  # noqa: E402
 from openmmcoul import testsystems as ts  # noqa: E402
 from openmmcoul.distributed import device_buffer_as_tensor  # noqa: E402
 
@@ -58,13 +58,14 @@ def c3_golden(c3):
     return d
 
 
-def _decomposed(system, force, pos, box, world, algo, precision="double", width=0):
+def _decomposed(system, force, pos, box, world, algo, precision="double", width=0, **opts):
     """One evaluation split over `world` handles on this GPU: begin on every rank, sum the
-    k-space buffers (the all-reduce), end on every rank.  Returns (energy, forces, dedq)."""
+    k-space buffers (the all-reduce), end on every rank.  Returns (energy, forces, dedq);
+    opts: further HipCalcCoulForceKernel options (pair_list, handover, ...)."""
     stream = torch.cuda.current_stream().cuda_stream
     pt = torch.tensor(pos, dtype=torch.float64, device="cuda")
     ks = [HipCalcCoulForceKernel(stream=stream, rank=r, world_size=world, kspace_algo=algo, precision=precision,
-                                 grid_width=width).initialize(system, force) for r in range(world)]
+                                 grid_width=width, **opts).initialize(system, force) for r in range(world)]
     for k in ks:
         k.begin(pt, box, True, True)
     bufs = [device_buffer_as_tensor(*k.kspace_buffer(), "cuda") for k in ks]
@@ -170,11 +171,11 @@ def c5():
     return ts.make("C5")
 
 
-def _c5_eval(system, force, pos, box, prec, width):
+def _c5_eval(system, force, pos, box, prec, width, variants=0):
     stream = torch.cuda.current_stream().cuda_stream
     pt = torch.tensor(pos, dtype=torch.float64, device="cuda")
-    k = HipCalcCoulForceKernel(stream=stream, kspace_algo=GRID, precision=prec, grid_width=width).initialize(system,
-                                                                                                            force)
+    k = HipCalcCoulForceKernel(stream=stream, kspace_algo=GRID, precision=prec, grid_width=width,
+                               variants=variants).initialize(system, force)
     assert k.ewald_params()[1] == (65, 65, 65)
     f = torch.zeros_like(pt)
     e = torch.zeros(1, dtype=torch.float64, device="cuda")
@@ -223,14 +224,12 @@ def test_c5_mixed_rank_split(c5, world):
     assert np.abs(f4 - f1).max() <= 1e-6 * np.abs(f1).max()
 
 
-def test_c5_dft8_matches_gemm_stages(c5, monkeypatch):
+def test_c5_dft8_matches_gemm_stages(c5):
     """C5 (kmax 65, ng 264 = 8 x 33): the factorized DFT stages (default) against the fp64-MFMA
-    GEMM stages (CF_DFT8=0, read when the handle is created) on the same positions, fp64 W = 14:
-    only the summation order differs -> energy and forces equal to <= 1e-12 relative."""
+    GEMM stages (CF_VARIANT_GEMM_DFT) on the same positions, fp64 W = 14: only the summation order
+    differs -> energy and forces equal to <= 1e-12 relative."""
     system, force, pos, box = c5
-    monkeypatch.setenv("CF_DFT8", "0")
-    eg, fg, tg = _c5_eval(system, force, pos, box, "double", 14)
-    monkeypatch.setenv("CF_DFT8", "1")
+    eg, fg, tg = _c5_eval(system, force, pos, box, "double", 14, variants=_cabi.CF_VARIANT_GEMM_DFT)
     e8, f8, t8 = _c5_eval(system, force, pos, box, "double", 14)
     assert abs(e8 - eg) <= 1e-12 * np.abs(tg).sum(), (e8, eg)
     assert np.abs(f8 - fg).max() <= 1e-12 * np.abs(fg).max(), np.abs(f8 - fg).max()

@@ -2,7 +2,6 @@
 the same bits as eager calls -- over a trajectory with a kept neighbour list (rebuilds decided
 on the device inside the graph), after a box change (re-capture) and with other output buffers
 (re-capture) -- and the cache must actually replay.  Bar: bitwise equality."""
-import os
 
 import numpy as np
 import pytest
@@ -52,10 +51,9 @@ def test_graph_replay_is_bitwise_eager(algo, precision, skin):
     for (ea, fa), (eb, fb) in zip(a, b):
         assert ea == eb and np.array_equal(fa, fb)
     caps, reps = graph.graph_stats()
-    # graphs per evaluation: one, or one per stream when the grid k-space uses the second stream
-    # (cf_api.hip launch_full: flux + charges + reciprocal chain, direct chain; 3 with the
-    # event hand-overs of CF_SYNC=event: flux + charges, reciprocal chain, direct chain)
-    segs = (3 if os.environ.get("CF_SYNC") == "event" else 2) if algo == 2 else 1
+    # graphs per evaluation: one, or with the grid k-space on two streams 3 with the event
+    # hand-overs (cf_api.hip launch_full: flux + charges, direct chain, reciprocal chain)
+    segs = 3 if algo == 2 else 1
     assert reps >= 4 * segs and caps <= 4 * segs, (caps, reps)
     assert eager.neighbor_stats() == graph.neighbor_stats()
 

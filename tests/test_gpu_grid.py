@@ -18,7 +18,7 @@ pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
 
 from oracle import Oracle  # noqa: E402
-from openmmcoul import HipCalcCoulForceKernel, ChargeFluxError  # noqa: E402
+from openmmcoul import HipCalcCoulForceKernel, ChargeFluxError, _cabi  # noqa: E402
 from openmmcoul import testsystems as ts  # noqa: E402
 from openmmcoul.distributed import device_buffer_as_tensor  # noqa: E402
 
@@ -211,17 +211,9 @@ def test_grid_options_validation():
 
 
 def _with_dft8(flag, system, force, **kw):
-    # CF_DFT8 is read when the handle is created (grid plan): "0" selects the GEMM stages
-    import os
-    old = os.environ.get("CF_DFT8")
-    os.environ["CF_DFT8"] = flag
-    try:
-        return HipCalcCoulForceKernel(kspace_algo=GRID, **kw).initialize(system, force)
-    finally:
-        if old is None:
-            del os.environ["CF_DFT8"]
-        else:
-            os.environ["CF_DFT8"] = old
+    # flag "0": the GEMM stages (CF_VARIANT_GEMM_DFT), "1": the factorized stages (default)
+    v = _cabi.CF_VARIANT_GEMM_DFT if flag == "0" else 0
+    return HipCalcCoulForceKernel(kspace_algo=GRID, variants=v, **kw).initialize(system, force)
 
 
 @pytest.mark.parametrize("case", ["C2", "noncubic", "odd_kmax_12k", "C3"])
@@ -254,22 +246,23 @@ def test_grid_dft8_matches_gemm_stages(case):
     assert np.abs(d1 - d0).max() <= 1e-12 * np.abs(d0).max(), np.abs(d1 - d0).max()
 
 
-@pytest.mark.parametrize("case,width,spread_dpp", [("C2", 14, "1"), ("C2", 13, "1"), ("w4k", 14, "1"), ("w4k", 14, "0"),
-                                                   ("w4k", 8, "1"), ("w4k", 11, "1")])
-def test_grid_interp2_matches_interp(monkeypatch, case, width, spread_dpp):
-    """The two-atoms-per-wave interpolation (k_g_interp2: taps in registers, DPP row broadcasts)
-    against the one-atom form (CF_INTERP2=0), even and odd kernel widths, with either spread
-    form (CF_SPREAD_DPP; the spread forms are bitwise equal): the same sums in another order,
-    forces and dE/dq equal to <= 1e-12 relative, energy unchanged (not interpolated)."""
+@pytest.mark.parametrize("case,width,spread", [("C2", 14, 0), ("C2", 13, 0), ("w4k", 14, 0), ("w4k", 14, 2),
+                                               ("w4k", 8, 0), ("w4k", 11, 0), ("w4k", 16, 0), ("w4k", 12, 0),
+                                               ("w4k", 9, 0)])
+def test_grid_interp2_matches_interp(case, width, spread):
+    """The two-atoms-per-wave interpolation (k_g_interp2: taps in registers, DPP row broadcasts,
+    x rows split by parity over the two rows of a half-wave) against the one-atom form
+    (CF_VARIANT_INTERP1), even and odd kernel widths, with either spread (spread = 2:
+    CF_VARIANT_VECTOR_SPREAD): the same sums in another order, forces and dE/dq equal to <= 1e-12
+    relative, energy unchanged (not interpolated)."""
     if case == "C2":
         system, force, pos, box = ts.make("C2")
     else:
         system, force, pos, box = ts.water_box(4000, cutoff=1.0, ewald_tol=1e-4, every_bond_angle=5)
-    monkeypatch.setenv("CF_SPREAD_DPP", spread_dpp)
     out = []
-    for flag in ("0", "1"):
-        monkeypatch.setenv("CF_INTERP2", flag)
-        k = HipCalcCoulForceKernel(kspace_algo=GRID, grid_width=width).initialize(system, force)
+    for v in (_cabi.CF_VARIANT_INTERP1, 0):
+        k = HipCalcCoulForceKernel(kspace_algo=GRID, grid_width=width, variants=v | spread | (
+            _cabi.CF_VARIANT_INTERP2 if width <= 8 else 0)).initialize(system, force)
         e, f = k.execute_host(pos, box)
         out.append((e, f, k.dedq()))
         k.destroy()
@@ -280,20 +273,18 @@ def test_grid_interp2_matches_interp(monkeypatch, case, width, spread_dpp):
 
 
 @pytest.mark.parametrize("case,width", [("C2", 8), ("w4k", 8), ("w4k", 7), ("w4k", 6), ("w4k", 5), ("w4k", 4)])
-def test_grid_interp4_matches_interp(monkeypatch, case, width):
+def test_grid_interp4_matches_interp(case, width):
     """The four-atoms-per-wave interpolation (k_g_interp4, W <= 8: one atom per 16-lane row, y
-    taps by bank-masked row broadcasts) against the one-atom form (CF_INTERP2=0) and the
-    two-atom form (CF_INTERP4=0), even and odd widths: forces and dE/dq equal to <= 1e-12
+    taps by bank-masked row broadcasts) against the one-atom form (CF_VARIANT_INTERP1) and the
+    two-atom form (CF_VARIANT_INTERP2), even and odd widths: forces and dE/dq equal to <= 1e-12
     relative, energy unchanged (not interpolated)."""
     if case == "C2":
         system, force, pos, box = ts.make("C2")
     else:
         system, force, pos, box = ts.water_box(4000, cutoff=1.0, ewald_tol=1e-4, every_bond_angle=5)
     out = []
-    for i2, i4 in (("0", "1"), ("1", "0"), ("1", "1")):
-        monkeypatch.setenv("CF_INTERP2", i2)
-        monkeypatch.setenv("CF_INTERP4", i4)
-        k = HipCalcCoulForceKernel(kspace_algo=GRID, grid_width=width).initialize(system, force)
+    for v in (_cabi.CF_VARIANT_INTERP1, _cabi.CF_VARIANT_INTERP2, 0):
+        k = HipCalcCoulForceKernel(kspace_algo=GRID, grid_width=width, variants=v).initialize(system, force)
         e, f = k.execute_host(pos, box)
         out.append((e, f, k.dedq()))
         k.destroy()
@@ -319,9 +310,9 @@ def _odd_tile_box():
 
 @pytest.mark.parametrize("case,width", [("C2", 14), ("w4k", 14), ("w4k", 13), ("w4k", 11), ("w4k", 8), ("w4k", 5),
                                         ("small", 14), ("tric", 12), ("odd", 14), ("odd", 8)])
-def test_grid_spread_mfma_matches_vector_spread(monkeypatch, case, width):
+def test_grid_spread_mfma_matches_vector_spread(case, width):
     """The matrix-core spread (k_g_spread_mfma: 16x8x8 tiles, v_mfma_f64_16x16x4 over groups of
-    4 source atoms) against the vector spread (CF_SPREAD_MFMA=0, k_g_spread_tile): the same
+    4 source atoms) against the vector spread (CF_VARIANT_VECTOR_SPREAD, k_g_spread_tile): the same
     grid sums in another order, so energy, forces and dE/dq equal to <= 1e-12 relative, and the
     matrix form bitwise reproducible run to run.  'small' has a small grid (few x-bins per
     16-wide tile), 'tric' a reduced triclinic box, 'odd' an odd number of x-bins (a half tile
@@ -342,9 +333,9 @@ def test_grid_spread_mfma_matches_vector_spread(monkeypatch, case, width):
     else:
         system, force, pos, box = ts.water_box(4000, cutoff=1.0, ewald_tol=1e-4, every_bond_angle=5)
     out = []
-    for flag in ("0", "2", "2"):   # 2: the matrix form at every width (the default uses it for W > 9)
-        monkeypatch.setenv("CF_SPREAD_MFMA", flag)
-        k = HipCalcCoulForceKernel(kspace_algo=GRID, grid_width=width).initialize(system, force)
+    # the vector form, then the matrix form at every width twice (the default uses it for W > 9)
+    for v in (_cabi.CF_VARIANT_VECTOR_SPREAD, _cabi.CF_VARIANT_MFMA_SPREAD, _cabi.CF_VARIANT_MFMA_SPREAD):
+        k = HipCalcCoulForceKernel(kspace_algo=GRID, grid_width=width, variants=v).initialize(system, force)
         e, f = k.execute_host(pos, box)
         out.append((e, f, k.dedq(), k.energy_terms()))
         k.destroy()
@@ -356,19 +347,19 @@ def test_grid_spread_mfma_matches_vector_spread(monkeypatch, case, width):
     assert e2 == e1 and np.array_equal(f2, f1) and np.array_equal(d2, d1)
 
 
-@pytest.mark.parametrize("rounds", ["3", "8"])
-def test_grid_bin_rounds_bitwise(monkeypatch, rounds):
+@pytest.mark.parametrize("rounds", [3, 8])
+def test_grid_bin_rounds_bitwise(rounds):
     """k_g_bin and k_assemble_energy with several 256-atom rounds per block (the default from
-    262144 owned atoms up; CF_BIN_ROUNDS forces it at a small size): the provisional ranks come
+    262144 owned atoms up; CF_VARIANT_BLOCK_ROUNDS forces it at a small size): the provisional ranks come
     from atomics in any order and k_g_order_taps restores the stable order, so forces and dE/dq
     are bitwise equal to the one-round launch -- including a ragged last block; the energy is
     the same fixed-order sum regrouped (per-thread chunk sums, fewer block partials): <= 1e-13
     relative, and bitwise reproducible run to run."""
     system, force, pos, box = ts.water_box(4000, cutoff=1.0, ewald_tol=1e-4, every_bond_angle=5)
     out = []
-    for r in ("1", rounds):
-        monkeypatch.setenv("CF_BIN_ROUNDS", r)
-        k = HipCalcCoulForceKernel(kspace_algo=GRID).initialize(system, force)
+    for r in (1, rounds):
+        k = HipCalcCoulForceKernel(kspace_algo=GRID, variants=_cabi.CF_VARIANT_BLOCK_ROUNDS(r)).initialize(system,
+                                                                                                          force)
         e, f = k.execute_host(pos, box)
         e2, f2 = k.execute_host(pos, box)   # the ticket re-armed by the last block
         out.append((e, f, k.dedq()))

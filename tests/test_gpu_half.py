@@ -1,17 +1,16 @@
 """The half neighbour list (k_pairs_half, window sums in k_excl): every pair
 evaluated once (kept by the atom of the lower x cell, or within one x cell by the smaller x),
 the partner's share summed in 64-bit fixed point.  Used on one rank in fp64
-when the box has >= 4 cells per axis; CF_HALF=0 (latched by cf_create) selects
+when the box has >= 4 cells per axis; cf_options.pair_list = CF_PAIR_LIST_FULL selects
 the full two-sided list for comparison.
 
 Tolerances (written here): against the oracle forces <= 1e-8 kJ/mol/nm, energy <= 1e-9 |E| +
-1e-8; half vs full list forces <= 2e-12 max|F| + 1e-9 (the fixed point rounds each j-side term to
-2^-34; the i-side sums run in another order).
+1e-8; half vs full list forces <= 1e-9 for the per-atom half list, <= 2e-12 max|F| + 1e-9 for the
+cluster-pair list (the fixed point rounds each j-side term to 2^-34; the i-side sums run in another
+order).
 The fallbacks -- an overflowed list, a j-side term too large for the fixed point -- hand the
 evaluation to the fp64 cell rescan, which must give the same answer.
 """
-import os
-
 import numpy as np
 import pytest
 
@@ -31,24 +30,14 @@ def _need_gpu():
 
 
 def _kernel(system, force, half, algo=0, skin=0.0, precision="double", cluster=True, cap=0):
-    """half: the half list (cluster-pair form unless cluster=False: the per-atom half list,
-    CF_CLUSTER=0); else the full two-sided list (CF_HALF=0).  The variables are latched by
-    cf_create (initialize); cap: CF_CLUSTER_CAP, a cluster-pair list capacity that overflows."""
-    saved = {v: os.environ.get(v) for v in ("CF_HALF", "CF_CLUSTER", "CF_CLUSTER_CAP")}
-    os.environ["CF_HALF"] = "1" if half else "0"
-    os.environ["CF_CLUSTER"] = "1" if cluster else "0"
-    if cap:
-        os.environ["CF_CLUSTER_CAP"] = str(cap)
-    try:
-        k = HipCalcCoulForceKernel(kspace_algo=algo, precision=precision).initialize(system, force)
-        if skin:
-            k.set_neighbor_skin(skin)
-    finally:
-        for v, val in saved.items():
-            if val is None:
-                os.environ.pop(v, None)
-            else:
-                os.environ[v] = val
+    """half: the half list (the cluster-pair form unless cluster=False: the per-atom half list);
+    else the full two-sided list (cf_options.pair_list); cap: a cluster-pair list capacity that
+    overflows (cf_options.list_capacity)."""
+    pl = ("cluster" if cluster else "atom_half") if half else "full"
+    k = HipCalcCoulForceKernel(kspace_algo=algo, precision=precision, pair_list=pl,
+                               list_capacity=cap).initialize(system, force)
+    if skin:
+        k.set_neighbor_skin(skin)
     return k
 
 
@@ -57,12 +46,14 @@ def _eval(k, pos, box):
     return e, f, k.dedq(), k.energy_terms()
 
 
+@pytest.mark.parametrize("cluster", [False, True], ids=["atom_list", "cluster_list"])
 @pytest.mark.parametrize("nw,algo", [(4000, 0), (7000, 2)])
-def test_half_list_matches_full_list_and_oracle(nw, algo):
+def test_half_list_matches_full_list_and_oracle(nw, algo, cluster):
     system, force, pos, box = ts.water_box(nw, cutoff=1.0, ewald_tol=1e-4, every_bond_angle=5)
-    eh, fh, dh, th = _eval(_kernel(system, force, True, algo), pos, box)
+    eh, fh, dh, th = _eval(_kernel(system, force, True, algo, cluster=cluster), pos, box)
     ef, ff, df, tf = _eval(_kernel(system, force, False, algo), pos, box)
-    assert np.abs(fh - ff).max() <= 2e-12 * np.abs(ff).max() + 1e-9, np.abs(fh - ff).max()
+    bar = 2e-12 * np.abs(ff).max() + 1e-9 if cluster else 1e-9
+    assert np.abs(fh - ff).max() <= bar, np.abs(fh - ff).max()
     assert np.abs(dh - df).max() <= 1e-10 * np.abs(df).max()
     assert abs(th[2] - tf[2]) <= 1e-11 * abs(tf[2]) + 1e-9
     ref = Oracle(force, box).execute(pos, box)
@@ -136,7 +127,7 @@ def _dense_overflow():
 def test_half_list_fallbacks_persist_over_kept_lists(make, cluster, cap):
     """A fallback raised when the list is BUILT (rows the builder could not encode, overflowed
     rows) must hold on every later evaluation that keeps that list under a skin: each step is
-    compared with the full list rebuilt from scratch (CF_HALF=0, skin 0) on the same positions.
+    compared with the full list rebuilt from scratch (pair_list "full", skin 0) on the same positions.
     (The cluster-pair list has no block frame: the sparse gas runs it without a fallback, checked
     against the oracle below.)"""
     system, force, pos, box = make()
@@ -175,7 +166,7 @@ def test_half_list_sparse_gas_matches_oracle_with_skin():
 @pytest.mark.parametrize("cluster", [False, True], ids=["atom_list", "cluster_list"])
 def test_half_list_mixed_precision(cluster):
     # the fp32 half-list kernel (the per-atom list, the mixed default, and the cluster-pair list,
-    # CF_CLUSTER=1) against the fp32 full list and the fp64 half list (same k-space)
+    # pair_list "cluster") against the fp32 full list and the fp64 half list (same k-space)
     system, force, pos, box = ts.water_box(4000, cutoff=1.0, ewald_tol=1e-4, every_bond_angle=5)
     em, fm, dm, tm = _eval(_kernel(system, force, True, 0, precision="mixed", cluster=cluster), pos, box)
     ef, ff, df, tf = _eval(_kernel(system, force, False, 0, precision="mixed"), pos, box)

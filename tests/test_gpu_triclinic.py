@@ -146,18 +146,10 @@ def _big(shear=(0.3, -0.25, 0.2), n=4000):
 
 
 def _kernel(system, force, algo, half=True, skin=0.0, precision="double"):
-    import os
-    old = os.environ.get("CF_HALF")
-    os.environ["CF_HALF"] = "1" if half else "0"
-    try:
-        k = HipCalcCoulForceKernel(kspace_algo=algo, precision=precision).initialize(system, force)
-        if skin:
-            k.set_neighbor_skin(skin)
-    finally:
-        if old is None:
-            del os.environ["CF_HALF"]
-        else:
-            os.environ["CF_HALF"] = old
+    k = HipCalcCoulForceKernel(kspace_algo=algo, precision=precision,
+                               pair_list="auto" if half else "full").initialize(system, force)
+    if skin:
+        k.set_neighbor_skin(skin)
     return k
 
 
