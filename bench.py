@@ -123,12 +123,12 @@ def cpu_baseline(force, pos, box, k_sample):
     }
 
 
-# rocprofv3 kernel names of the library's timing phases at C3, up to their template arguments
-# (the instantiation that runs in the profiled command; a phase timed as one bracket may be
-# several launches: their bytes are summed)
+# rocprofv3 kernel names of the library's timing phases, up to their template arguments (the
+# instantiation that runs in the profiled command; a phase timed as one bracket may be several
+# launches: their bytes are summed).  The pair kernel follows the list kind (cf_get_pair_list).
 PMC_KERNEL = {"kspace_force": ["cf::k_force<"], "kspace_sfac": ["cf::k_sfac<"],
-              "direct_pairs": ["cf::k_pairs_cq<"],          # the cluster-pair kernel (fp64, one rank)
               "grid_spread": ["cf::k_g_spread_mfma<"], "grid_interp": ["cf::k_g_interp2<"]}
+PAIR_KERNEL = {"cluster": "cf::k_pairs_cq<", "atom_half": "cf::k_pairs_half<", "full": "cf::k_pairs<"}
 
 
 def pair_count(force, pos, box):
@@ -149,21 +149,31 @@ def pair_count(force, pos, box):
     return int(n_all - n_ex)
 
 
-def pmc_traffic(config, world, phase, precision):
-    """HBM bytes per launch of the dominant kernel from the newest committed PMC summary
-    (profiles/r*_c3_pmc_summary_*.json, written by tools/profile_round.sh from separate
-    rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this same bench command, with the
-    gfx950 FETCH_SIZE x2 correction).  None when no profile matches this workload (the
-    profiles are of the default fp64 C3 command; mixed precision runs other kernels)."""
-    if config != "C3" or world != 1 or precision != "double":
+def pmc_traffic(config, world, phase, precision, pair_list):
+    """HBM bytes per launch of the dominant kernel from the newest committed PMC summary of this
+    workload -- profiles/r*_c3_pmc_summary*.json (fp64 C3) or r*_c5_pmc_summary*.json (mixed C5),
+    written by tools/profile_round.sh / the session scripts from separate rocprofv3 --pmc
+    FETCH_SIZE / WRITE_SIZE passes of this same bench command, with the gfx950 FETCH_SIZE
+    correction -- newest = highest round, a "final" summary first.  None when no profile matches."""
+    wl = {("C3", "double"): "c3", ("C5", "mixed"): "c5"}.get((config, precision))
+    if wl is None or world != 1:
         return None, None
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_c3_pmc_summary_*.json")))
+    import re
+
+    def newest(f):
+        m = re.match(r"r(\d+)", os.path.basename(f))
+        return (int(m.group(1)) if m else -1, "final" in os.path.basename(f), os.path.basename(f))
+
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{wl}_pmc_summary*.json")), key=newest)
     if not files:
         return None, None
     summary = json.load(open(files[-1]))
     total = 0
-    for prefix in PMC_KERNEL[phase]:
+    prefixes = [PAIR_KERNEL.get(pair_list, "?")] if phase == "direct_pairs" else PMC_KERNEL[phase]
+    if phase == "direct_pairs" and pair_list == "full" and precision == "mixed":
+        prefixes = ["cf::k_pairs_mixed<"]
+    for prefix in prefixes:
         hits = [e for name, e in summary.items() if isinstance(e, dict) and name.startswith(prefix)
                 and "hbm_read_bytes_est" in e and "hbm_write_bytes" in e]
         if len(hits) != 1:   # none, or several instantiations profiled: no unambiguous figure
@@ -194,6 +204,8 @@ def main():
     ap.add_argument("--graph", type=int, default=0,
                     help="1: replay each step's CoulForce launches as a captured hipGraph (cf_set_graph) in the "
                          "timed region")
+    ap.add_argument("--pair-list", default="auto", choices=["auto", "cluster", "atom_half", "full"],
+                    help="direct-space list (cf_options.pair_list; auto: cluster-pair list on one fp64 rank)")
     ap.add_argument("--handover", default="event", choices=["event", "memory"],
                     help="fork / join of the library's second stream (cf_options.handover; memory: opt-in)")
     ap.add_argument("--dt", type=float, default=0.001, help="ps")
@@ -222,7 +234,8 @@ def main():
     n = len(pos_np)
     n_waters = force.getNumFluxWaters() + force.getNumFluxAngles()
     kern = ShardedCoulKernel(system, force, local, kspace_algo=args.kspace_algo, neighbor_skin=args.neighbor_skin,
-                             grid_width=args.grid_width, precision=args.precision, handover=args.handover)
+                             grid_width=args.grid_width, precision=args.precision, handover=args.handover,
+                             pair_list=args.pair_list)
     lo, hi = kern.lo, kern.hi
     alpha, kmax = kern.kernel.ewald_params()
     k_half = (kmax[2] - 1) + (kmax[1] - 1) * (2 * kmax[2] - 1) + (kmax[0] - 1) * (2 * kmax[1] - 1) * (2 * kmax[2] - 1)
@@ -308,7 +321,21 @@ def main():
     for _ in range(args.steps):
         energy = step(True)
     torch.cuda.synchronize()
-    ms_eval_clean = float(np.mean([a.elapsed_time(b) for a, b in ev])) if ev else float("nan")
+    ms_eval_events = float(np.mean([a.elapsed_time(b) for a, b in ev])) if ev else float("nan")
+    # harness pass: K steps of the MD harness alone (restraints, integrator, position all-gather;
+    # no CoulForce call), wall clock.  ms_per_force_eval = ms_per_step - this: what the force
+    # evaluation adds to a step.  (The event-bracketed figure above reads longer than a whole
+    # step at C5 -- 2.82 against 2.69 ms in round 4: two extra event records per step on the
+    # library's stream delay the launches they sit between -- so it is reported beside it only.)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t_h0 = time.perf_counter()
+    for _ in range(args.steps):
+        md.restrain_kick_drift(pos, vel, frc, False)
+        kern.replicate_positions(pos)
+    torch.cuda.synchronize()
+    ms_harness = (time.perf_counter() - t_h0) / args.steps * 1e3
     # graph pass (after the timed region, not part of it): K steps with the CoulForce launches
     # replayed as a captured hipGraph, wall clock; measures what graph replay would give `value`
     graph_ms = None
@@ -327,6 +354,7 @@ def main():
     kern.synchronize()   # energy all-reduce still in flight (multi-rank)
     e_final = energy.item()
     ms_step = elapsed / args.steps * 1e3
+    ms_eval_clean = ms_step - ms_harness
     ns_day = 86.4 / ms_step * (dt / 0.001)
 
     per_launch = {k: (v[0] / v[1] if v[1] else 0.0) for k, v in timing_all.items()}   # isolated (breakdown pass)
@@ -371,7 +399,7 @@ def main():
 
         present = [k for k in alg if per_step.get(k, 0.0) > 0]
         r = roof(dom, per_launch[dom])
-        traffic, traffic_src = pmc_traffic(args.config, world, dom, args.precision)
+        traffic, traffic_src = pmc_traffic(args.config, world, dom, args.precision, kern.kernel.pair_list())
         if r["bound"] == "hbm":
             achieved, peak, unit = r["gbs"], HBM_PEAK_GBS, "GB/s"
         else:
@@ -464,13 +492,16 @@ def main():
                        "nlist_builds_in_timed_steps": f"{builds1 - builds0}/{evals1 - evals0}",
                        "parallelism": f"atom-decomposition x{world}" + (" (RCCL all-reduce of S(k))" if world > 1 else "")},
             "ms_per_force_eval": round(ms_eval_clean, 4),
+            "ms_per_harness_step": round(ms_harness, 4),
+            "ms_per_force_eval_events": round(ms_eval_events, 4),
             "ms_per_force_eval_instrumented": round(ms_eval, 4),
             "graph_replay_ms_per_step": None if graph_ms is None else round(graph_ms, 4),
             "graph_stats": None if graph_ms is None else list(gstats),
             "energy_kj_mol": e_final,
             "kernels_ms_per_step": {k: round(v, 4) for k, v in per_step.items()},
-            "timing_note": (f"value: K steps with HIP events around {dom} launches only; ms_per_force_eval: a "
-                            f"separate K-step pass with two events around each execute and no library timing; "
+            "timing_note": (f"value: K steps with HIP events around {dom} launches only; ms_per_force_eval: "
+                            f"ms_per_step minus ms_per_harness_step (K steps of the MD harness alone, wall clock); "
+                            f"ms_per_force_eval_events: a K-step pass with two torch events around each execute; "
                             f"kernels_ms_per_step and ms_per_force_eval_instrumented: a K-step pass with every "
                             f"phase bracketed by events and the second stream off (one stream: each phase's "
                             f"own time; kernels_roofline is from that pass)"),

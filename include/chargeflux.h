@@ -180,6 +180,10 @@ CF_EXPORT int cf_set_neighbor_skin(cf_handle* h, double skin);
  * tolerance (alpha and kmax stay those of cf_create); otherwise CF_ERR_INVALID.  The next
  * evaluation rebuilds the neighbour list.  Not allowed between cf_compute_begin and _end. */
 CF_EXPORT int cf_update_parameters(cf_handle* h, const cf_params* params);
+/* The direct-space list the handle evaluates with (cf_options.pair_list resolved for this system and
+ * box: CF_PAIR_LIST_CLUSTER, CF_PAIR_LIST_ATOM_HALF or CF_PAIR_LIST_FULL; CF_PAIR_LIST_AUTO before the
+ * first periodic evaluation and without periodic boundaries). */
+CF_EXPORT int cf_get_pair_list(const cf_handle* h, int32_t* kind);
 /* Number of neighbour-list builds and evaluations since cf_create. */
 CF_EXPORT int cf_get_neighbor_stats(const cf_handle* h, int64_t* builds, int64_t* evaluations);
 /* Slow-path diagnostics since cf_create (synchronises the stream): evaluations whose half-list

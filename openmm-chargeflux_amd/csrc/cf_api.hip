@@ -857,6 +857,14 @@ CF_EXPORT int cf_get_neighbor_stats(const cf_handle* H, int64_t* builds, int64_t
     return CF_OK;
 }
 
+CF_EXPORT int cf_get_pair_list(const cf_handle* H, int32_t* kind) {
+    if (!H || !kind) { g_err = "null argument"; return CF_ERR_INVALID; }
+    const cf::Handle& h = H->h;
+    *kind = !h.pbc || h.nc[0] == 0 ? CF_PAIR_LIST_AUTO
+                                   : (h.cluster ? CF_PAIR_LIST_CLUSTER : (h.half ? CF_PAIR_LIST_ATOM_HALF : CF_PAIR_LIST_FULL));
+    return CF_OK;
+}
+
 CF_EXPORT int cf_get_fallback_stats(const cf_handle* H, int64_t* half_list_fallbacks, int64_t* rows_rescanned,
                                     int32_t* reasons) {
     if (!H) { g_err = "null handle"; return CF_ERR_INVALID; }

@@ -121,6 +121,7 @@ SIGNATURES = [
     ("cf_get_fallback_stats", C.c_int, [C.c_void_p, C.POINTER(C.c_int64), C.POINTER(C.c_int64),
                                         C.POINTER(C.c_int32)]),
     ("cf_get_graph_stats", C.c_int, [C.c_void_p, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
+    ("cf_get_pair_list", C.c_int, [C.c_void_p, C.POINTER(C.c_int32)]),
 ]
 
 _lib = None

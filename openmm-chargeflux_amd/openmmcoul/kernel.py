@@ -192,6 +192,13 @@ class HipCalcCoulForceKernel:
         _cabi.check(self._lib.cf_get_graph_stats(self._h, C.byref(c), C.byref(r)), self._lib)
         return c.value, r.value
 
+    def pair_list(self):
+        """The direct-space list in use: "cluster", "atom_half" or "full" ("auto" before the first
+        periodic evaluation and without PBC) -- cf_get_pair_list."""
+        k = C.c_int32()
+        _cabi.check(self._lib.cf_get_pair_list(self._h, C.byref(k)), self._lib)
+        return {v: n for n, v in self.PAIR_LISTS.items()}[k.value]
+
     def neighbor_stats(self):
         """(list builds, evaluations) since initialize."""
         b, e = C.c_int64(), C.c_int64()
