@@ -32,9 +32,9 @@ namespace cf {
 constexpr int kClSize = 4;               // atoms per cluster
 constexpr int kCqWaves = 16;             // waves per k_pairs_cq block (one cell, one block per CU: the LDS)
 constexpr int kCqThreads = 64 * kCqWaves;
-constexpr int kCqQ = 76;                 // queue entries per i atom (a ring; what the 160 KB LDS leaves)
+constexpr int kCqQ = kCqWaves > 12 ? 88 : 112;   // queue entries per i atom (a ring; what the 160 KB LDS leaves)
 constexpr int kCqBatch = 16;             // list entries tested per phase-A step (64 j atoms, one per lane)
-constexpr int kCqLpi = 16;               // phase-B lanes per row (one i atom per row and step)
+constexpr int kCqLpi = 16;               // phase-B lanes per i atom
 constexpr int kClBuildThreads = 512;
 constexpr int kClMaxCand = 1536;         // window clusters staged by k_cl_build (>= 4096 / 4 + 18 * 3)
 constexpr unsigned kClSelfMask = 0x08CEu;
@@ -261,38 +261,12 @@ __global__ void __launch_bounds__(kClBuildThreads) k_cl_build(DirectArgs a, cons
 // ---------------------------------------------------------------------------------
 // k_pairs_cq: the pair loop over the cluster-pair list (see the top of this file)
 // ---------------------------------------------------------------------------------
-// Phase B rows.  Round 4 tied each 16-lane row of a phase-B step to one i atom of the cluster
-// (row k pops queue k), so a step ran with the rows of the shorter queues partly idle: ~75 % of
-// the lanes evaluated a pair.  Here a step's four rows are dealt to the queues greedily -- each
-// row takes 16 entries of the currently fullest queue, two rows may take the same one -- so the
-// rows are full except at the end of a cluster.  A row's i atom therefore changes from step to
-// step: its i side (forces, dE/dq and the pair energies) is summed over the row's 16 lanes in a
-// fixed order (DPP) and added in the window's 64-bit fixed point to the i atom's own-cell slot
-// (forces, dE/dq: accw, the i atoms lie in window cell kHalfOwn) and to eown (energy).  Integer
-// adds of deterministic row sums: the results do not depend on which wave took which cluster.
-// The queues are emptied at the end of every cluster, so each cluster's steps -- and with them
-// the row sums -- are a function of that cluster's list alone.
-constexpr int kCqOwnMax = 256;   // own-cell atoms whose pair energies eown holds (a denser cell falls back)
-
-// the row's 16-lane total of v in every lane of the row (row rotations by 8, 4, 2, 1)
-__device__ __forceinline__ double row_total(double v) {
-    auto ror = [](double x, auto ctrl) {
-        const long long b = __double_as_longlong(x);
-        const int lo = __builtin_amdgcn_mov_dpp((int)b, decltype(ctrl)::value, 0xF, 0xF, false);
-        const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), decltype(ctrl)::value, 0xF, 0xF, false);
-        return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
-    };
-    v += ror(v, std::integral_constant<int, 0x128>{});   // row_ror:8
-    v += ror(v, std::integral_constant<int, 0x124>{});   // row_ror:4
-    v += ror(v, std::integral_constant<int, 0x122>{});   // row_ror:2
-    v += ror(v, std::integral_constant<int, 0x121>{});   // row_ror:1
-    return v;
-}
-
-// MIXED (CF_PRECISION_MIXED, C5): phase B in fp32 -- the pair vector formed in fp64 and rounded
-// (its error is ~ulp(r)), erfc from the degree-6 fp32 table, fp32 pair terms; the sums (row
-// totals in fp64 of the fp32 terms, the fixed-point window) as in fp64
-template <bool TYPES, bool MIXED>
+// MIXED (CF_PRECISION_MIXED, C5): phase B in fp32 -- the pair vector from the corner-relative
+// fp32 positions and the window cell's offset (no fp64 minimum image: the corner frame keeps the
+// coordinates small, so fp32 carries ~1e-7 nm whatever the box size), erfc from the degree-6 fp32
+// table, fp32 i-side sums, fp64 energy, the j side in the same fixed point (an fp32 value times
+// 2^34 is exact in fp64)
+template <bool TYPES, bool TRIC, bool MIXED>
 __global__ void __launch_bounds__(kCqThreads) CF_LDS_UNPAIRED k_pairs_cq(DirectArgs a) {
     __shared__ double tab[MIXED ? 1 : kErfcMaxM * (kErfcDeg + 1)];
     __shared__ float tabf[MIXED ? kErfcMaxMF * (kErfcDegF + 1) : 1];
@@ -301,8 +275,7 @@ __global__ void __launch_bounds__(kCqThreads) CF_LDS_UNPAIRED k_pairs_cq(DirectA
     __shared__ int wdel[kHalfWin];          // window offset - first sorted slot
     __shared__ float4 shf[kHalfWin];        // corner offset of each window cell (phase A, window_cell)
     __shared__ double3 shd[kHalfWin];       // wrap translation of each window cell (phase B, window_cell)
-    __shared__ unsigned long long accw[4][kHalfMaxWin];   // fx, fy, fz, dE/dq of the window's atoms (fixed point)
-    __shared__ unsigned long long eown[kCqOwnMax];        // pair energies of the cell's own atoms (fixed point)
+    __shared__ unsigned long long accw[4][kHalfMaxWin];   // j-side fx, fy, fz, dE/dq (fixed point)
     __shared__ int qbuf[kCqWaves][4][kCqQ];  // per wave, per i atom: ring of hit entries
     __shared__ int wtot, next_ci, nown;
     const int cell = xcd_block();
@@ -318,7 +291,7 @@ __global__ void __launch_bounds__(kCqThreads) CF_LDS_UNPAIRED k_pairs_cq(DirectA
         win[threadIdx.x] = make_int2(b, a.cend[w] - b);
         shf[threadIdx.x] = off;
         shd[threadIdx.x] = wr;
-        // several ranks: owned atoms in the window (its own cell is window cell kHalfOwn)
+        // several ranks: owned atoms in the window (its own cell is window cell 0)
         if (a.own_start && a.own_start[w + 1] > a.own_start[w]) atomicAdd(&nown, 1);
     }
     if constexpr (TYPES)
@@ -339,12 +312,11 @@ __global__ void __launch_bounds__(kCqThreads) CF_LDS_UNPAIRED k_pairs_cq(DirectA
         }
         wtot = off;
         next_ci = 0;
-        if (off > kHalfMaxWin || win[kHalfOwn + 1].y - win[kHalfOwn].y > kCqOwnMax) atomicOr(a.half_flag, kHalfWindowFull);
+        if (off > kHalfMaxWin) atomicOr(a.half_flag, kHalfWindowFull);
     }
     __syncthreads();
     const int nw = wtot;
-    const int cs0 = win[kHalfOwn].x, own0 = win[kHalfOwn].y, ncs = win[kHalfOwn + 1].y - own0;
-    if (nw > kHalfMaxWin || ncs > kCqOwnMax) return;   // block-uniform; k_excl recomputes everything
+    if (nw > kHalfMaxWin) return;   // block-uniform; k_excl recomputes everything
     // several ranks: no owned atom in the cell or its window -- no pair this rank keeps has an atom
     // here, and k_excl reads this window only for owned atoms of the window's cells (none): skip
     if (a.own_start && nown == 0) return;   // block-uniform
@@ -352,12 +324,12 @@ __global__ void __launch_bounds__(kCqThreads) CF_LDS_UNPAIRED k_pairs_cq(DirectA
     for (int e = threadIdx.x; e < nw; e += kCqThreads) {
         accw[0][e] = 0; accw[1][e] = 0; accw[2][e] = 0; accw[3][e] = 0;
     }
-    for (int e = threadIdx.x; e < ncs; e += kCqThreads) eown[e] = 0;
     __syncthreads();
 
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int row = lane >> 4, kk = lane & 15;         // phase B: row (its i atom varies), lane kk of its 16
+    const int il = lane >> 4, kk = lane & 15;          // phase B: i atom il, lane kk of its 16
     const int jl = lane & 3, el = lane >> 2;           // phase A: entry el of the batch, j atom jl
+    int* const qw = qbuf[wv][il];
     const int c0 = a.cl_start[cell], ncl = a.cl_start[cell + 1] - c0;
     bool bad = false, bad_list = false;
     auto ring = [](int x) { return x >= kCqQ ? x - kCqQ : x; };   // x < 2 kCqQ
@@ -368,7 +340,10 @@ __global__ void __launch_bounds__(kCqThreads) CF_LDS_UNPAIRED k_pairs_cq(DirectA
         if (ci >= ncl) break;
         ci += c0;
         const int2 inf = a.cl_info[ci];
-        const int iloc0 = inf.x - cs0;   // own-cell index of the cluster's first atom
+        const int islot = inf.x + min(il, inf.y - 1);
+        const double4 pi = a.pos4s[islot];
+        const double2 li = TYPES ? ljt[__float_as_int(a.pos4f[islot].w)] : a.ljs[islot];
+        const double kqis = a.ke * pi.w * kFixScale;   // k_e q_i in fixed-point units
         // the 4 i atoms' fp32 positions, wave-uniform (phase A tests every lane's j against all 4)
         float4 pif[4];   // (readfirstlane: kept in SGPRs, VOP2 operands of the tests)
         auto sgpr = [](float v) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v))); };
@@ -380,104 +355,60 @@ __global__ void __launch_bounds__(kCqThreads) CF_LDS_UNPAIRED k_pairs_cq(DirectA
         int ne = a.cpl_cnt[ci];
         if (ne > a.cpl_cap) { bad_list = true; ne = 0; }   // the evaluation falls back (k_excl rescans)
         const uint2* lst = a.cpl + (size_t)ci * a.cpl_cap;
-        int q[4] = {0, 0, 0, 0}, qh[4] = {0, 0, 0, 0};   // queue lengths and heads (wave-uniform)
-        auto qtot = [&]() { return q[0] + q[1] + q[2] + q[3]; };
+        std::conditional_t<MIXED, PairAccF, PairAcc> acc;
+        int q0 = 0, q1 = 0, q2 = 0, q3 = 0;   // queue lengths (wave-uniform)
+        int qh = 0;     // ring head, equal for the 4 queues (every phase-B step pops 16 from each)
 
-        // a phase-B step: rows dealt greedily to the fullest queues (take[r] entries of queue
-        // src[r] from ring position pos[r]); decided when the step's loads are issued
-        struct Step { unsigned src, pos, take; };   // 4 rows packed: 2, 8, 8 bits per row
-        auto plan = [&]() {
-            int avail[4] = {q[0], q[1], q[2], q[3]}, used[4] = {0, 0, 0, 0};
-            Step s{0u, 0u, 0u};
-#pragma unroll
-            for (int r = 0; r < 4; r++) {
-                int k = 0;
-#pragma unroll
-                for (int u = 1; u < 4; u++) k = avail[u] > avail[k] ? u : k;   // ties: the lower queue
-                const int t = min(avail[k], kCqLpi);
-                s.src |= (unsigned)k << (2 * r);
-                s.pos |= (unsigned)ring(qh[k] + used[k]) << (8 * r);
-                s.take |= (unsigned)t << (8 * r);
-                avail[k] -= t;
-                used[k] += t;
-            }
-            return s;
-        };
-        auto retire = [&](const Step& s) {   // the step's entries leave their queues
-#pragma unroll
-            for (int r = 0; r < 4; r++) {
-                const int k = (s.src >> (2 * r)) & 3, t = (s.take >> (8 * r)) & 255;
-#pragma unroll
-                for (int u = 0; u < 4; u++)
-                    if (u == k) { q[u] -= t; qh[u] = ring(qh[u] + t); }
-            }
-        };
-        // this lane's entry of a planned step: queue, ring position, active
-        auto lane_entry = [&](const Step& s, int& k, int& pos) {
-            k = (s.src >> (2 * row)) & 3;
-            pos = ring((int)((s.pos >> (8 * row)) & 255) + kk);
-            return kk < (int)((s.take >> (8 * row)) & 255);
-        };
-
-        // Prefetch: whenever the queues hold a full step, its plan, entries, j and i coordinates are
-        // loaded at once (issue_pf) and used by the next phase B, which therefore does not wait for
-        // them.  Phase B runs while the queues hold two steps (keeping one in reserve for the next
-        // prefetch), so the prefetched loads complete during the next batch's tests.
-        bool pf_ok = false, drain = false;   // (wave-uniform)
-        Step pf_s{0u, 0u, 0u};
+        // phase B: lanes kk < qlen of each i atom evaluate the pair of queue entry qh + kk
+        // Prefetch: whenever every queue holds a full step, its entries and j coordinates are
+        // loaded at once (issue_pf) and used by the next phase B, which therefore does not wait
+        // for them.  Phase B runs while every queue holds 32 (keeping 16 in reserve for the next
+        // prefetch; the same lane efficiency as draining at 16: the ends of the lists decide it,
+        // tools/cluster_proto.py), so the prefetched loads complete during the next batch's tests.
+        bool pf_ok = false;   // (wave-uniform)
         int pf_wq = 0;
-        double4 pf_pj = make_double4(0.0, 0.0, 0.0, 0.0), pf_pi = make_double4(0.0, 0.0, 0.0, 0.0);
-        auto fence_lds = []() {
+        double4 pf_pj = make_double4(0.0, 0.0, 0.0, 0.0);
+        auto all_ge = [&](int v) { return q0 >= v && q1 >= v && q2 >= v && q3 >= v; };
+        auto issue_pf = [&]() {
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        };
-        auto issue_pf = [&]() {
-            fence_lds();
-            pf_s = plan();
-            int k, pos;
-            const bool act = lane_entry(pf_s, k, pos);
-            pf_wq = act ? qbuf[wv][k][pos] : 0;
-            pf_pj = a.pos4s[act ? (pf_wq & kHalfSlotMask) : inf.x];
-            pf_pi = a.pos4s[inf.x + min(k, inf.y - 1)];
+            pf_wq = qw[ring(qh + kk)];
+            pf_pj = a.pos4s[pf_wq & kHalfSlotMask];
             pf_ok = true;
         };
         auto phase_b = [&]() {
-            fence_lds();
-            Step s;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            // this lane's queue length: the four packed one byte each (lengths < 256)
+            const unsigned qpack = (unsigned)q0 | ((unsigned)q1 << 8) | ((unsigned)q2 << 16) | ((unsigned)q3 << 24);
+            const int qlen = (int)((qpack >> (8 * il)) & 255u);
+            const bool act = kk < qlen;
             int wq;
-            double4 pj, pi;
-            int k, pos;
-            bool act;
+            double4 pj;
             if (pf_ok) {
-                s = pf_s;
-                act = lane_entry(s, k, pos);
-                wq = pf_wq; pj = pf_pj; pi = pf_pi;
+                wq = pf_wq;
+                pj = pf_pj;
                 pf_ok = false;
             } else {
-                s = plan();
-                act = lane_entry(s, k, pos);
-                wq = act ? qbuf[wv][k][pos] : 0;
-                pj = a.pos4s[act ? (wq & kHalfSlotMask) : inf.x];
-                pi = a.pos4s[inf.x + min(k, inf.y - 1)];
+                wq = act ? qw[ring(qh + kk)] : islot;
+                pj = a.pos4s[wq & kHalfSlotMask];
             }
-            retire(s);
-            const int islot = inf.x + min(k, inf.y - 1);
-            const double2 li = TYPES ? ljt[__float_as_int(a.pos4f[islot].w)] : a.ljs[islot];
-            const int j = wq & kHalfSlotMask, wc = (wq >> kHalfSlotBits) & 31;
-            const double3 wr = shd[wc];
+            const int j = wq & kHalfSlotMask;
+            const double3 wr = shd[(wq >> kHalfSlotBits) & 31];
             // the pair vector to j's image next to the cell: the wrap translation of j's window cell
             // (for a pair within rc < L/2 the same image, and for an orthorhombic box the same bits,
             // as the minimum image d - L rint(d / L))
             const double ddx = pi.x - (pj.x + wr.x), ddy = pi.y - (pj.y + wr.y), ddz = pi.z - (pj.z + wr.z);
-            // this lane's i-side contributions (in fixed-point units) and pair energy
-            double vx = 0.0, vy = 0.0, vz = 0.0, vq = 0.0, ve = 0.0;
             if constexpr (MIXED) {
+                // formed in fp64 from the wrapped coordinates, then rounded: its error is ~ulp(r),
+                // not ulp of a coordinate
                 const float qjv = (float)pj.w;
                 const float dx = (float)ddx, dy = (float)ddy, dz = (float)ddz;
                 const float r2 = fmaf(dx, dx, fmaf(dy, dy, dz * dz));
                 if (act && r2 <= (float)a.rc2) {
-                    const int slot = wdel[wc] + j;
+                    const int slot = wdel[(wq >> kHalfSlotBits) & 31] + j;
                     const double2 ljd = TYPES ? ljt[(unsigned)wq >> kShiftBits] : a.ljs[j];
                     const float ke = (float)a.ke, qi = (float)pi.w;
                     const float inv_r = rsqrtf(r2);
@@ -488,7 +419,7 @@ __global__ void __launch_bounds__(kCqThreads) CF_LDS_UNPAIRED k_pairs_cq(DirectA
                     const float* c = tabf + it * (kErfcDegF + 1);
                     float pc = c[kErfcDegF];
 #pragma unroll
-                    for (int m = kErfcDegF - 1; m >= 0; m--) pc = fmaf(pc, u, c[m]);
+                    for (int q = kErfcDegF - 1; q >= 0; q--) pc = fmaf(pc, u, c[q]);
                     const float e2 = __expf(-ar * ar);
                     const float ec = e2 * pc;
                     const float sig = (float)li.x + (float)ljd.x;
@@ -504,74 +435,58 @@ __global__ void __launch_bounds__(kCqThreads) CF_LDS_UNPAIRED k_pairs_cq(DirectA
                                            es6 * (12.0f * sig6 - 6.0f) * inv_r2;
                         const float fx = dEdR * dx, fy = dEdR * dy, fz = dEdR * dz;
                         const float dqj = ke * qi * inv_r * ec;
-                        vx = (double)fx * kFixScale; vy = (double)fy * kFixScale; vz = (double)fz * kFixScale;
-                        vq = (double)(qj * ec) * kFixScale;
+                        acc.fx += fx; acc.fy += fy; acc.fz += fz;
+                        acc.dq = fmaf(qj, ec, acc.dq);
                         bad |= !(fmaxf(fmaxf(fabsf(fx), fabsf(fy)), fmaxf(fabsf(fz), fabsf(dqj))) < (float)kFixMax);
                         atomicAdd(&accw[0][slot], to_fix(-(double)fx));
                         atomicAdd(&accw[1][slot], to_fix(-(double)fy));
                         atomicAdd(&accw[2][slot], to_fix(-(double)fz));
                         atomicAdd(&accw[3][slot], to_fix((double)dqj));
                     }
-                    ve = (double)fmaf(qq, ec, es6 * (sig6 - 1.0f));   // the whole pair energy
+                    acc.e += (double)fmaf(qq, ec, es6 * (sig6 - 1.0f));   // the whole pair energy
                 }
-            } else {
-                const double2 lj = TYPES ? ljt[(unsigned)wq >> kShiftBits] : a.ljs[j];
-                const double dx = ddx, dy = ddy, dz = ddz;
-                const double r2 = dx * dx + dy * dy + dz * dz;
-                if (act && r2 <= a.rc2) {   // exact voxel-hash test (RCK:567-569)
-                    const int slot = wdel[wc] + j;
-                    const double ke = a.ke;
-                    const double two_over_sqrtpi = 1.1283791670955126;
-                    const double inv_r = rsqrt_fp64(r2);
-                    const double ar = a.alpha * (r2 * inv_r);
-                    double e2;
-                    const double ec = erfc_exp(ar, tab, a.erfc_scale, e2);
-                    const double qj = ke * pj.w * inv_r;
-                    const double qq = pi.w * qj;
-                    const double sig = li.x + lj.x;
-                    double s2 = inv_r * sig;
-                    s2 *= s2;
-                    const double sig6 = s2 * s2 * s2;
-                    const double es6 = sig6 * li.y * lj.y;
-                    if (a.include_forces) {
-                        // -F_ij in fixed-point units (x -2^34: exact): the j side adds it, the i side
-                        // its negation
-                        const double ndEdRs = fma(qq, ec + ar * e2 * two_over_sqrtpi, es6 * (12 * sig6 - 6)) *
-                                              ((inv_r * inv_r) * -kFixScale);
-                        const double nfx = ndEdRs * dx, nfy = ndEdRs * dy, nfz = ndEdRs * dz;
-                        const double ecr = inv_r * ec * kFixScale;
-                        const double dqjs = (ke * pi.w) * ecr;
-                        vx = -nfx; vy = -nfy; vz = -nfz;
-                        vq = (ke * pj.w) * ecr;
-                        // (|nf_c| <= |ndEdRs| r <= |ndEdRs| rc; the comparisons take the magnitudes as
-                        // source modifiers; an infinite or NaN term fails them)
-                        bad |= !(fabs(ndEdRs) * a.rc < kFixMax * kFixScale && fabs(dqjs) < kFixMax * kFixScale);
-                        atomicAdd(&accw[0][slot], scaled_to_fix(nfx));
-                        atomicAdd(&accw[1][slot], scaled_to_fix(nfy));
-                        atomicAdd(&accw[2][slot], scaled_to_fix(nfz));
-                        atomicAdd(&accw[3][slot], scaled_to_fix(dqjs));
-                    }
-                    ve = qq * ec + es6 * (sig6 - 1);   // the whole pair energy: each pair once
-                }
+                qh = ring(qh + kCqLpi);
+                q0 = max(q0 - kCqLpi, 0); q1 = max(q1 - kCqLpi, 0); q2 = max(q2 - kCqLpi, 0); q3 = max(q3 - kCqLpi, 0);
+                if (all_ge(kCqLpi)) issue_pf();
+                return;
             }
-            // the i side: each row's sums over its 16 lanes (one i atom per row), added in fixed point
-            // to the atom's slots by lanes 0..4 of the row (a row with no entries adds zeros)
-            vx = row_total(vx); vy = row_total(vy); vz = row_total(vz); ve = row_total(ve);
-            if (a.include_forces) vq = row_total(vq);
-            if (kk < 5 && (int)((s.take >> (8 * row)) & 255) > 0) {
-                const int iloc = iloc0 + k;
-                const double v = kk == 0 ? vx : kk == 1 ? vy : kk == 2 ? vz : kk == 3 ? vq : ve;
-                if (kk < 4) {
-                    if (a.include_forces) {
-                        bad |= !(fabs(v) < kFixMax * kFixScale);
-                        atomicAdd(&accw[kk][own0 + iloc], scaled_to_fix(v));
-                    }
-                } else {
-                    bad |= !(fabs(v) < kFixMax);
-                    atomicAdd(&eown[iloc], to_fix(v));
+            const double2 lj = TYPES ? ljt[(unsigned)wq >> kShiftBits] : a.ljs[j];
+            const double dx = ddx, dy = ddy, dz = ddz;
+            const double r2 = dx * dx + dy * dy + dz * dz;
+            if (act && r2 <= a.rc2) {   // exact voxel-hash test (RCK:567-569)
+                const int slot = wdel[(wq >> kHalfSlotBits) & 31] + j;
+                const double ke = a.ke;
+                const double two_over_sqrtpi = 1.1283791670955126;
+                const double inv_r = rsqrt_fp64(r2);
+                const double ar = a.alpha * (r2 * inv_r);
+                double e2;
+                const double ec = erfc_exp(ar, tab, a.erfc_scale, e2);
+                const double qj = ke * pj.w * inv_r;
+                const double qq = pi.w * qj;
+                const double sig = li.x + lj.x;
+                double s2 = inv_r * sig;
+                s2 *= s2;
+                const double sig6 = s2 * s2 * s2;
+                const double es6 = sig6 * li.y * lj.y;
+                if (a.include_forces) {
+                    // -F_ij in fixed-point units (x -2^34: exact), accumulated on both sides
+                    const double ndEdRs = fma(qq, ec + ar * e2 * two_over_sqrtpi, es6 * (12 * sig6 - 6)) *
+                                          ((inv_r * inv_r) * -kFixScale);
+                    const double nfx = ndEdRs * dx, nfy = ndEdRs * dy, nfz = ndEdRs * dz;
+                    const double dqjs = kqis * inv_r * ec;
+                    acc.fx += nfx; acc.fy += nfy; acc.fz += nfz;
+                    acc.dq += qj * ec;
+                    bad |= !(fmax(fabs(ndEdRs) * a.rc, fabs(dqjs)) < kFixMax * kFixScale);
+                    atomicAdd(&accw[0][slot], scaled_to_fix(nfx));
+                    atomicAdd(&accw[1][slot], scaled_to_fix(nfy));
+                    atomicAdd(&accw[2][slot], scaled_to_fix(nfz));
+                    atomicAdd(&accw[3][slot], scaled_to_fix(dqjs));
                 }
+                acc.e += qq * ec + es6 * (sig6 - 1);   // the whole pair energy: each pair once
             }
-            if (qtot() >= 4 * kCqLpi || (drain && qtot() > 0)) issue_pf();
+            qh = ring(qh + kCqLpi);
+            q0 = max(q0 - kCqLpi, 0); q1 = max(q1 - kCqLpi, 0); q2 = max(q2 - kCqLpi, 0); q3 = max(q3 - kCqLpi, 0);
+            if (all_ge(kCqLpi)) issue_pf();
         };
 
         // phase A: a batch of 16 entries = 64 j atoms, one per lane (entry el, atom jl), each tested
@@ -609,36 +524,51 @@ __global__ void __launch_bounds__(kCqThreads) CF_LDS_UNPAIRED k_pairs_cq(DirectA
                 cnt[k + 1] = __popcll(m[k + 1]);
             }
             // room for this batch's hits, then queue them
-            while (q[0] + cnt[0] > kCqQ || q[1] + cnt[1] > kCqQ || q[2] + cnt[2] > kCqQ || q[3] + cnt[3] > kCqQ) phase_b();
+            while (q0 + cnt[0] > kCqQ || q1 + cnt[1] > kCqQ || q2 + cnt[2] > kCqQ || q3 + cnt[3] > kCqQ) phase_b();
             const int word = (int)((en_c.x & kHalfSlotMask) + jl) | (wc << kHalfSlotBits) |
                              (__float_as_int(pj_c.w) << kShiftBits);
+            const int qs[4] = {q0, q1, q2, q3};
 #pragma unroll
             for (int k = 0; k < 4; k++) {
                 if ((m[k] >> lane) & 1ull) {
                     const int r = __builtin_amdgcn_mbcnt_hi((unsigned)(m[k] >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m[k], 0u));
-                    qbuf[wv][k][ring(qh[k] + q[k] + r)] = word;
+                    qbuf[wv][k][ring(qh + qs[k] + r)] = word;
                 }
             }
-            q[0] += cnt[0]; q[1] += cnt[1]; q[2] += cnt[2]; q[3] += cnt[3];
-            if (!pf_ok && qtot() >= 4 * kCqLpi) issue_pf();
-            while (qtot() >= 8 * kCqLpi) phase_b();   // full steps, one in reserve
+            q0 += cnt[0]; q1 += cnt[1]; q2 += cnt[2]; q3 += cnt[3];
+            if (!pf_ok && all_ge(kCqLpi)) issue_pf();
+            while (all_ge(2 * kCqLpi)) phase_b();   // full steps, one in reserve
             en_c = en_n; pj_c = pj_n; en_n = en_nn;
         }
-        drain = true;
-        if (!pf_ok && qtot() > 0) issue_pf();
-        while (qtot() > 0) phase_b();   // the rest, partly filled
+        while (q0 > 0 || q1 > 0 || q2 > 0 || q3 > 0) phase_b();   // the rest, partly filled
+#pragma unroll
+        for (int m = 1; m < kCqLpi; m <<= 1) {
+            acc.fx += __shfl_xor(acc.fx, m); acc.fy += __shfl_xor(acc.fy, m); acc.fz += __shfl_xor(acc.fz, m);
+            acc.dq += __shfl_xor(acc.dq, m); acc.e += __shfl_xor(acc.e, m);
+        }
+        const int i = a.atom_sorted[islot];
+        if (kk == 0 && il < inf.y && i >= a.lo && i < a.hi) {   // this rank's atoms only
+            a.e_atom[3 * i + 1] = acc.e;
+            if (a.include_forces) {
+                a.dedq[i] = acc.dq;
+                if constexpr (MIXED) {
+                    a.f_part[3 * i] = acc.fx;
+                    a.f_part[3 * i + 1] = acc.fy;
+                    a.f_part[3 * i + 2] = acc.fz;
+                } else {   // accumulated as -F in fixed-point units
+                    a.f_part[3 * i] = acc.fx * -kFixInv;
+                    a.f_part[3 * i + 1] = acc.fy * -kFixInv;
+                    a.f_part[3 * i + 2] = acc.fz * -kFixInv;
+                }
+            }
+        }
     }
     {
         const int why = (__ballot(bad_list) ? kHalfListOverflow : 0) | (__ballot(bad) ? kHalfFixedRange : 0);
         if (why && lane == 0) atomicOr(a.half_flag, why);
     }
-    __syncthreads();
-    // the own atoms' pair energies (this rank's atoms only)
-    for (int e = threadIdx.x; e < ncs; e += kCqThreads) {
-        const int i = a.atom_sorted[cs0 + e];
-        if (i >= a.lo && i < a.hi) a.e_atom[3 * i + 1] = (double)(long long)eown[e] * kFixInv;
-    }
     if (!a.include_forces) return;
+    __syncthreads();
     unsigned long long* out = a.win_out + (size_t)cell * kHalfMaxWin * 4;
     for (int e = threadIdx.x; e < nw; e += kCqThreads)
         reinterpret_cast<ulonglong4*>(out)[e] = make_ulonglong4(accw[0][e], accw[1][e], accw[2][e], accw[3][e]);
@@ -664,16 +594,16 @@ void launch_cluster_list(Handle& h) {
 void launch_pairs_cluster(Handle& h, const double* pos, int include_forces) {
     DirectArgs a = direct_args(h, pos, include_forces);
     const int ncell = h.nc[0] * h.nc[1] * h.nc[2];
-// (any reduced box: the pair vector comes from the window cell's lattice translation, the same image
-// as the reference's c, b, a minimum image for a pair within rc when rc <= half of each perpendicular
-// width -- set_box checks rc <= L/2, and the cells are at least rc + skin wide)
-#define CF_PAIRS_CQ(TY_, MX_) hipLaunchKernelGGL((k_pairs_cq<TY_, MX_>), dim3(ncell), dim3(kCqThreads), 0, h.stream, a)
-    if (h.mixed) {
-        if (a.typ_s) CF_PAIRS_CQ(true, true);
-        else CF_PAIRS_CQ(false, true);
+#define CF_PAIRS_CQ(TY_, TR_, MX_) hipLaunchKernelGGL((k_pairs_cq<TY_, TR_, MX_>), dim3(ncell), dim3(kCqThreads), 0, h.stream, a)
+    if (h.mixed) {   // (the fp32 pair vector needs no minimum image: TRIC only matters in fp64)
+        if (a.typ_s) CF_PAIRS_CQ(true, false, true);
+        else CF_PAIRS_CQ(false, false, true);
+    } else if (a.typ_s) {
+        if (a.tric) CF_PAIRS_CQ(true, true, false);
+        else CF_PAIRS_CQ(true, false, false);
     } else {
-        if (a.typ_s) CF_PAIRS_CQ(true, false);
-        else CF_PAIRS_CQ(false, false);
+        if (a.tric) CF_PAIRS_CQ(false, true, false);
+        else CF_PAIRS_CQ(false, false, false);
     }
 #undef CF_PAIRS_CQ
 }

@@ -787,21 +787,15 @@ __device__ __forceinline__ void store_pairs(const PairAcc& acc, const DirectArgs
 // operation order per atom is that of one fused loop: pair sums, then exclusions in list
 // order, then dE/dq_self + sum.
 // (add_f, add_dq: the half list's partner-side sums of the atom, added to the stored pair sums)
-// base_part: the pair sums so far are in f_part / dedq (false: add_f / add_dq are the whole pair sums)
 __device__ __forceinline__ void excl_atom(const DirectArgs& a, int i, double3 add_f = make_double3(0.0, 0.0, 0.0),
-                                          double add_dq = 0.0, bool base_part = true) {
+                                          double add_dq = 0.0) {
     const double ke = a.ke;
     const double two_over_sqrtpi = 1.1283791670955126;
     const int ex0 = a.ex_start[i], exc = a.ex_start[i + 1] - ex0;
     double fx = 0, fy = 0, fz = 0, dq = 0, ex_e = 0;
     if (a.include_forces) {
-        if (base_part) {
-            fx = a.f_part[3 * i] + add_f.x; fy = a.f_part[3 * i + 1] + add_f.y; fz = a.f_part[3 * i + 2] + add_f.z;
-            dq = a.dedq[i] + add_dq;
-        } else {
-            fx = add_f.x; fy = add_f.y; fz = add_f.z;
-            dq = add_dq;
-        }
+        fx = a.f_part[3 * i] + add_f.x; fy = a.f_part[3 * i + 1] + add_f.y; fz = a.f_part[3 * i + 2] + add_f.z;
+        dq = a.dedq[i] + add_dq;
     }
     if (exc) {
         double3 xi = ld3(a.pos, i);
@@ -1395,7 +1389,7 @@ __global__ void __launch_bounds__(256) k_excl(DirectArgs a) {
         double3 f;
         double dq;
         half_window_sums(a, s, f, dq);
-        excl_atom(a, i, f, dq, !a.iside_win);   // (k_pairs_cq: the windows hold the i side too)
+        excl_atom(a, i, f, dq);
     } else {
         excl_atom(a, i);
     }
@@ -1725,7 +1719,6 @@ DirectArgs direct_args(Handle& h, const double* pos, int include_forces) {
     a.fallback = h.n_fallback_dev;
     a.cl_start = h.cl_start; a.cl_info = h.cl_info; a.cpl = h.cpl; a.cpl_cnt = h.cpl_cnt; a.cpl_cap = h.cpl_cap;
     a.pos4f = h.pos4f; a.slot_of = h.slot_of;
-    a.iside_win = h.cluster ? 1 : 0;
     {   // fp32 prefilter: |d| from fp32 coordinates of magnitude <= ~2 L carries an error below 8 ulp(L)
         const double Lmax = std::max(h.box_L[0], std::max(h.box_L[1], h.box_L[2])) + std::fabs(h.box_t[0]) +
                             std::fabs(h.box_t[1]) + std::fabs(h.box_t[2]);

@@ -139,8 +139,6 @@ struct DirectArgs {
     const float4* pos4f;        // [N] fp32 (x, y, z, LJ type bits)
     const int* slot_of;         // [N] atom -> sorted slot
     float rcm2f;                // prefilter radius^2: rc with a margin above the fp32 rounding of |d|
-    int iside_win;              // the pair kernel adds the i side into the window too (k_pairs_cq): k_excl
-                                // takes both sides from the windows, not from f_part / dedq
 };
 
 __device__ __forceinline__ int own_slot(const DirectArgs& a, int c) { return a.own_s ? a.own_s[c] : c; }
