@@ -109,7 +109,10 @@ typedef struct cf_options {
                             CF_PAIR_LIST_CLUSTER (1): the cluster-pair half list wherever its cell window
                               fits (also mixed precision, and several ranks with an ownership filter);
                             CF_PAIR_LIST_ATOM_HALF (2): the per-atom half list on one rank (full on several);
-                            CF_PAIR_LIST_FULL (3): the per-atom full (two-sided) list.
+                            CF_PAIR_LIST_FULL (3): the per-atom full (two-sided) list;
+                            CF_PAIR_LIST_OCTANT (4): the octant (eighth-shell) cluster-pair list on one
+                              rank (fp64 or mixed): an 8-cell window per block, both sides of every pair
+                              in fixed point.
                             Same pair set and the same results up to the fp64 summation order. */
     int32_t variants;    /* CF_VARIANT_* bits: alternative kernels of the same sums, kept for A/B
                             verification (0 = the production kernels) */
@@ -128,6 +131,7 @@ typedef struct cf_options {
 #define CF_PAIR_LIST_CLUSTER 1
 #define CF_PAIR_LIST_ATOM_HALF 2
 #define CF_PAIR_LIST_FULL 3
+#define CF_PAIR_LIST_OCTANT 4
 
 /* cf_options.variants (grid k-space; each equal to the production kernel to <= 1e-12 relative) */
 #define CF_VARIANT_GEMM_DFT 1        /* the DFT stages as fp64-MFMA complex GEMMs (k_g_cgemm), not the

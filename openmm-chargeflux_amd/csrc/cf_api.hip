@@ -209,7 +209,12 @@ void set_cells(cf_handle* H, const double L[3]) {
     // 0.336 / 0.304 against 0.255 / 0.197 ms rank-0 (profiles/r04ag_*): a thin slab's cells and
     // their window neighbours run whole 1024-thread blocks with the 128-KB window for few owned atoms
     const double per_cell = (double)h.n / (double)ncell;
-    const bool want_cluster = h.pair_list == CF_PAIR_LIST_CLUSTER || (h.pair_list == CF_PAIR_LIST_AUTO && !h.mixed);
+    // octant list (cf_kernels_es.hip): one rank, an 8-cell window that two 512-thread
+    // blocks per CU hold in LDS (water density: 1 500 atoms, cap ~1 900)
+    const int es_wcap = ((2 * 40960 - cf::es_static_lds_bytes(h.mixed, true) - 256) / 32) & ~15;
+    const bool want_es = h.world == 1 && h.pair_list == CF_PAIR_LIST_OCTANT &&
+                         per_cell * 8.0 * 1.15 <= es_wcap;
+    const bool want_cluster = want_es || h.pair_list == CF_PAIR_LIST_CLUSTER || (h.pair_list == CF_PAIR_LIST_AUTO && !h.mixed);
     h.half = h.pair_list != CF_PAIR_LIST_FULL && h.pbc &&
              (h.world == 1 || (want_cluster && h.pair_list == CF_PAIR_LIST_CLUSTER)) && nc[0] >= 4 &&
              nc[1] >= 4 && nc[2] >= 4 && per_cell * 18.0 * 1.15 <= 4096.0 && h.n < (1 << 21);
@@ -226,6 +231,7 @@ void set_cells(cf_handle* H, const double L[3]) {
     // costs more than it saves (C5: 1.425 vs 1.235 ms, profiles/r04e_*); CF_PAIR_LIST_CLUSTER forces
     // it, CF_PAIR_LIST_ATOM_HALF keeps the per-atom list in fp64
     h.cluster = h.half && want_cluster;
+    h.es = h.cluster && want_es;
     h.zcol = 0;
     if (h.cluster) {
         // within-cell z-columns of ~12 atoms (k_cell_order): clusters of 4 consecutive slots stay compact
@@ -240,6 +246,7 @@ void set_cells(cf_handle* H, const double L[3]) {
         const double rl = h.cutoff + h.list_skin + ext;
         const double est = 0.5 * 4.0 / 3.0 * M_PI * rl * rl * rl * rho / 4.0 + 8.0;
         int cap = std::min(1536, ((int)(2.2 * est) + 64 + 15) / 16 * 16);
+        if (h.es) cap = 384;   // the octant builder's row stage (k_es_build); the pool is per block
         if (h.list_capacity > 0) cap = std::max(4, std::min(cap, h.list_capacity));   // cf_options.list_capacity
         if (need > h.ncl_cap || cap != h.cpl_cap || ncell + 1 > h.cl_cells) {
             if (h.cl_start) { (void)hipFree(h.cl_start); (void)hipFree(h.cl_info); (void)hipFree(h.cl_bb);
@@ -250,9 +257,33 @@ void set_cells(cf_handle* H, const double L[3]) {
             cf::check_hip(hipMalloc(&h.cl_start, sizeof(int) * h.cl_cells), "cluster table");
             cf::check_hip(hipMalloc(&h.cl_info, sizeof(int2) * h.ncl_cap), "cluster table");
             cf::check_hip(hipMalloc(&h.cl_bb, sizeof(float4) * 2 * h.ncl_cap), "cluster table");
-            cf::check_hip(hipMalloc(&h.cpl, sizeof(uint2) * (size_t)h.ncl_cap * h.cpl_cap), "cluster-pair list");
+            cf::check_hip(hipMalloc(&h.cpl, sizeof(uint2) * (size_t)h.ncl_cap * (h.es ? 1 : h.cpl_cap)), "cluster-pair list");
             cf::check_hip(hipMalloc(&h.cpl_cnt, sizeof(int) * h.ncl_cap), "cluster-pair list");
             h.alloc_epoch++;
+        }
+        if (h.es) {
+            // rows: the clusters of 4 octant cells; pool: the block's entries, ~89 % of its cell's
+            // clusters' half-space partners plus the short cross-pair rows, x1.6 + 256
+            const int rows_max = std::min(1024, (int)(4.0 * std::ceil(per_cell / 4.0) * 1.6) + 64);
+            const int pool_cap = (int)(1.6 * 1.15 * (per_cell / 4.0) * est) + 256;
+            if (ncell > h.es_cells || rows_max > h.es_rows_max || pool_cap > h.es_pool_cap) {
+                if (h.es_row) { (void)hipFree(h.es_row); (void)hipFree(h.es_pool); (void)hipFree(h.e_blk); }
+                h.es_cells = std::max((int)ncell, h.es_cells);
+                h.es_rows_max = std::max(rows_max, h.es_rows_max);
+                h.es_pool_cap = std::max(pool_cap, h.es_pool_cap);
+                cf::check_hip(hipMalloc(&h.es_row, sizeof(int2) * (size_t)h.es_cells * h.es_rows_max), "octant list");
+                cf::check_hip(hipMalloc(&h.es_pool, sizeof(uint2) * (size_t)h.es_cells * h.es_pool_cap), "octant list");
+                cf::check_hip(hipMalloc(&h.e_blk, sizeof(double) * (size_t)h.es_cells), "octant list");
+                h.alloc_epoch++;
+            }
+            if (!h.es_part) {
+                cf::check_hip(hipMalloc(&h.es_part, sizeof(ulonglong4) * 8 * (size_t)h.n), "octant window sums");
+                h.alloc_epoch++;
+            }
+            if (h.es_wcap != es_wcap) {
+                h.es_wcap = es_wcap;
+                cf::es_set_lds_limit(32 * es_wcap);
+            }
         }
         if (!h.pos4f) {
             cf::check_hip(hipMalloc(&h.pos4f, sizeof(float4) * h.n), "fp32 positions");
@@ -492,8 +523,8 @@ CF_EXPORT int cf_create(const cf_params* p, const cf_options* opt, cf_handle** o
         h.mixed = o.precision == CF_PRECISION_MIXED;
         if (o.handover != CF_HANDOVER_EVENT && o.handover != CF_HANDOVER_MEMORY)
             fail(CF_ERR_INVALID, "handover must be CF_HANDOVER_EVENT or CF_HANDOVER_MEMORY");
-        if (o.pair_list < CF_PAIR_LIST_AUTO || o.pair_list > CF_PAIR_LIST_FULL)
-            fail(CF_ERR_INVALID, "pair_list must be one of CF_PAIR_LIST_AUTO, _CLUSTER, _ATOM_HALF, _FULL");
+        if (o.pair_list < CF_PAIR_LIST_AUTO || o.pair_list > CF_PAIR_LIST_OCTANT)
+            fail(CF_ERR_INVALID, "pair_list must be one of CF_PAIR_LIST_AUTO, _CLUSTER, _ATOM_HALF, _FULL, _OCTANT");
         if (o.variants & ~(0x1F | (15 << 8))) fail(CF_ERR_INVALID, "unknown bits in variants");
         if (o.list_capacity < 0) fail(CF_ERR_INVALID, "list_capacity must be >= 0");
         // the memory hand-over is opt-in: hipStreamWaitValue64 runs as a polling kernel on this
@@ -745,6 +776,8 @@ CF_EXPORT int cf_destroy(cf_handle* H) {
         if (H->h.cl_start) { (void)hipFree(H->h.cl_start); (void)hipFree(H->h.cl_info); (void)hipFree(H->h.cl_bb);
                              (void)hipFree(H->h.cpl); (void)hipFree(H->h.cpl_cnt); }
         if (H->h.pos4f) { (void)hipFree(H->h.pos4f); (void)hipFree(H->h.slot_of); }
+        if (H->h.es_row) { (void)hipFree(H->h.es_row); (void)hipFree(H->h.es_pool); (void)hipFree(H->h.e_blk); }
+        if (H->h.es_part) (void)hipFree(H->h.es_part);
         if (H->h.cell_start) (void)hipFree(H->h.cell_start);
         if (H->h.cell_end) (void)hipFree(H->h.cell_end);
         if (H->h.cell_cnt) (void)hipFree(H->h.cell_cnt);
@@ -861,7 +894,8 @@ CF_EXPORT int cf_get_pair_list(const cf_handle* H, int32_t* kind) {
     if (!H || !kind) { g_err = "null argument"; return CF_ERR_INVALID; }
     const cf::Handle& h = H->h;
     *kind = !h.pbc || h.nc[0] == 0 ? CF_PAIR_LIST_AUTO
-                                   : (h.cluster ? CF_PAIR_LIST_CLUSTER : (h.half ? CF_PAIR_LIST_ATOM_HALF : CF_PAIR_LIST_FULL));
+                                   : (h.es ? CF_PAIR_LIST_OCTANT
+                                      : (h.cluster ? CF_PAIR_LIST_CLUSTER : (h.half ? CF_PAIR_LIST_ATOM_HALF : CF_PAIR_LIST_FULL)));
     return CF_OK;
 }
 

@@ -201,6 +201,17 @@ struct Handle {
     uint2* cpl = nullptr;       // [ncl_cap][cpl_cap] (first slot of j | window cell << 21, pair mask)
     int* cpl_cnt = nullptr;     // [ncl_cap]
     float4* pos4f = nullptr;    // [N] sorted wrapped fp32 (x, y, z, LJ type bits)
+    // octant (eighth-shell) cluster-pair list (cf_kernels_es.hip): one rank, the
+    // cluster table above, an 8-cell window per block, both sides summed in the window
+    bool es = false;
+    int es_wcap = 0;            // window atoms per k_pairs_es block (dynamic LDS: 32 B each)
+    int es_rows_max = 0;        // rows (clusters of octant positions 0..3) per block
+    int es_pool_cap = 0;        // list entries per block
+    int es_cells = 0;           // cells es_row / es_pool / e_blk are sized for
+    int2* es_row = nullptr;     // [ncell][es_rows_max] (offset in the block's pool, count; -1 = overflowed)
+    uint2* es_pool = nullptr;   // [ncell][es_pool_cap] (first slot of j | octant position << 21, pair mask)
+    ulonglong4* es_part = nullptr;   // [8][N] each atom's window sums from the 8 octants holding it
+    double* e_blk = nullptr;    // [ncell] pair energy per octant block
     int* slot_of = nullptr;     // [N] atom -> sorted slot (exclusion masks of the list build)
     // k-space (MFMA path)
     int npad = 0;               // owned rows of the phase tables, padded to the S-pass tile
@@ -266,6 +277,11 @@ void launch_force_rebuild(Handle& h);                   // skin_flag = 1
 void launch_nlist(Handle& h, const double* pos);
 void launch_cluster_list(Handle& h);                   // cluster table, bounding boxes, cluster-pair list (rebuild only)
 void launch_pairs_cluster(Handle& h, const double* pos, int include_forces);   // k_pairs_cq
+void launch_cluster_table(Handle& h);                  // k_cl_scan + k_cl_bbox (rebuild only)
+void launch_es_list(Handle& h);                        // cluster table + k_es_build (rebuild only)
+void launch_pairs_es(Handle& h, const double* pos, int include_forces);        // k_pairs_es
+int es_static_lds_bytes(bool mixed, bool types);
+void es_set_lds_limit(int bytes);
 void launch_direct(Handle& h, const double* pos, int include_forces);          // the pair kernel
 void launch_direct_finish(Handle& h, const double* pos, int include_forces);   // overflow rescan + exclusions
 void launch_recip_add(Handle& h);   // dedq, f_part += reciprocal partials

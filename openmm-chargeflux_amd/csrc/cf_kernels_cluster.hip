@@ -266,7 +266,7 @@ __global__ void __launch_bounds__(kClBuildThreads) k_cl_build(DirectArgs a, cons
 // coordinates small, so fp32 carries ~1e-7 nm whatever the box size), erfc from the degree-6 fp32
 // table, fp32 i-side sums, fp64 energy, the j side in the same fixed point (an fp32 value times
 // 2^34 is exact in fp64)
-template <bool TYPES, bool TRIC, bool MIXED>
+template <bool TYPES, bool MIXED>
 __global__ void __launch_bounds__(kCqThreads) CF_LDS_UNPAIRED k_pairs_cq(DirectArgs a) {
     __shared__ double tab[MIXED ? 1 : kErfcMaxM * (kErfcDeg + 1)];
     __shared__ float tabf[MIXED ? kErfcMaxMF * (kErfcDegF + 1) : 1];
@@ -577,7 +577,7 @@ __global__ void __launch_bounds__(kCqThreads) CF_LDS_UNPAIRED k_pairs_cq(DirectA
 // ---------------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------------
-void launch_cluster_list(Handle& h) {
+void launch_cluster_table(Handle& h) {
     DirectArgs a = direct_args(h, nullptr, 0);
     const int ncell = h.nc[0] * h.nc[1] * h.nc[2];
     hipLaunchKernelGGL(k_cl_scan, dim3(1), dim3(1024), 0, h.stream, ncell, h.skin_flag, h.cell_start, h.cell_end,
@@ -586,6 +586,12 @@ void launch_cluster_list(Handle& h) {
                        h.cell_end, h.cl_start, h.pos4f, h.cl_info, h.cl_bb, make_int3(h.nc[0], h.nc[1], h.nc[2]),
                        make_double3(h.box_L[0], h.box_L[1], h.box_L[2]), make_double3(h.box_t[0], h.box_t[1], h.box_t[2]),
                        a.atom_sorted, a.lo, a.hi, a.n);
+}
+
+void launch_cluster_list(Handle& h) {
+    DirectArgs a = direct_args(h, nullptr, 0);
+    const int ncell = h.nc[0] * h.nc[1] * h.nc[2];
+    launch_cluster_table(h);
     const double rl = (h.cutoff + h.list_skin) * (1.0 + 1e-5) + 1e-5;
     hipLaunchKernelGGL(k_cl_build, dim3(ncell), dim3(kClBuildThreads), 0, h.stream, a, h.cl_bb, h.cpl, h.cpl_cnt,
                        (float)(rl * rl));
@@ -594,16 +600,16 @@ void launch_cluster_list(Handle& h) {
 void launch_pairs_cluster(Handle& h, const double* pos, int include_forces) {
     DirectArgs a = direct_args(h, pos, include_forces);
     const int ncell = h.nc[0] * h.nc[1] * h.nc[2];
-#define CF_PAIRS_CQ(TY_, TR_, MX_) hipLaunchKernelGGL((k_pairs_cq<TY_, TR_, MX_>), dim3(ncell), dim3(kCqThreads), 0, h.stream, a)
-    if (h.mixed) {   // (the fp32 pair vector needs no minimum image: TRIC only matters in fp64)
-        if (a.typ_s) CF_PAIRS_CQ(true, false, true);
-        else CF_PAIRS_CQ(false, false, true);
-    } else if (a.typ_s) {
-        if (a.tric) CF_PAIRS_CQ(true, true, false);
-        else CF_PAIRS_CQ(true, false, false);
+// (any reduced box: the pair vector comes from the window cell's lattice translation, which for a
+// pair within rc is the image of the reference's c, b, a minimum image when rc is at most half of
+// each perpendicular width -- set_box checks rc <= L/2, and the cells are at least rc + skin wide)
+#define CF_PAIRS_CQ(TY_, MX_) hipLaunchKernelGGL((k_pairs_cq<TY_, MX_>), dim3(ncell), dim3(kCqThreads), 0, h.stream, a)
+    if (h.mixed) {
+        if (a.typ_s) CF_PAIRS_CQ(true, true);
+        else CF_PAIRS_CQ(false, true);
     } else {
-        if (a.tric) CF_PAIRS_CQ(false, true, false);
-        else CF_PAIRS_CQ(false, false, false);
+        if (a.typ_s) CF_PAIRS_CQ(true, false);
+        else CF_PAIRS_CQ(false, false);
     }
 #undef CF_PAIRS_CQ
 }

@@ -786,16 +786,22 @@ __device__ __forceinline__ void store_pairs(const PairAcc& acc, const DirectArgs
 // (VGPRs -> occupancy).  The
 // operation order per atom is that of one fused loop: pair sums, then exclusions in list
 // order, then dE/dq_self + sum.
-// (add_f, add_dq: the half list's partner-side sums of the atom, added to the stored pair sums)
+// (add_f, add_dq: the half list's partner-side sums of the atom, added to the stored pair sums;
+// base_part false: they are the whole pair sums -- the octant list sums both sides in its windows)
 __device__ __forceinline__ void excl_atom(const DirectArgs& a, int i, double3 add_f = make_double3(0.0, 0.0, 0.0),
-                                          double add_dq = 0.0) {
+                                          double add_dq = 0.0, bool base_part = true) {
     const double ke = a.ke;
     const double two_over_sqrtpi = 1.1283791670955126;
     const int ex0 = a.ex_start[i], exc = a.ex_start[i + 1] - ex0;
     double fx = 0, fy = 0, fz = 0, dq = 0, ex_e = 0;
     if (a.include_forces) {
-        fx = a.f_part[3 * i] + add_f.x; fy = a.f_part[3 * i + 1] + add_f.y; fz = a.f_part[3 * i + 2] + add_f.z;
-        dq = a.dedq[i] + add_dq;
+        if (base_part) {
+            fx = a.f_part[3 * i] + add_f.x; fy = a.f_part[3 * i + 1] + add_f.y; fz = a.f_part[3 * i + 2] + add_f.z;
+            dq = a.dedq[i] + add_dq;
+        } else {
+            fx = add_f.x; fy = add_f.y; fz = add_f.z;
+            dq = add_dq;
+        }
     }
     if (exc) {
         double3 xi = ld3(a.pos, i);
@@ -1385,7 +1391,25 @@ __global__ void __launch_bounds__(256) k_excl(DirectArgs a) {
         pair_rescan(a, a.erfc_tab, s, i);
         if (!a.half && a.fallback) atomicAdd((unsigned long long*)&a.fallback[1], 1ull);
     }
-    if (a.half && !over && a.include_forces) {    // the partner-side sums of the half list
+    if (a.es && !over) {   // octant list: both sides from the 8 octant windows holding s; the pair
+                           // energy per block, carried by atoms 0..ncell-1 into the fixed-order sum
+        const int ncell = a.nc.x * a.nc.y * a.nc.z;
+        a.e_atom[3 * i + 1] = i < ncell ? a.e_blk[i] : 0.0;
+        if (a.include_forces) {
+            ulonglong4 v[8];
+#pragma unroll
+            for (int p = 0; p < 8; p++) v[p] = a.es_part[(size_t)p * a.n + s];
+            long long sx = 0, sy = 0, sz = 0, sq = 0;
+#pragma unroll
+            for (int p = 0; p < 8; p++) {
+                sx += (long long)v[p].x; sy += (long long)v[p].y; sz += (long long)v[p].z; sq += (long long)v[p].w;
+            }
+            excl_atom(a, i, make_double3((double)sx * kFixInv, (double)sy * kFixInv, (double)sz * kFixInv),
+                      (double)sq * kFixInv, false);
+        } else {
+            excl_atom(a, i);
+        }
+    } else if (a.half && !over && a.include_forces) {    // the partner-side sums of the half list
         double3 f;
         double dq;
         half_window_sums(a, s, f, dq);
@@ -1719,6 +1743,9 @@ DirectArgs direct_args(Handle& h, const double* pos, int include_forces) {
     a.fallback = h.n_fallback_dev;
     a.cl_start = h.cl_start; a.cl_info = h.cl_info; a.cpl = h.cpl; a.cpl_cnt = h.cpl_cnt; a.cpl_cap = h.cpl_cap;
     a.pos4f = h.pos4f; a.slot_of = h.slot_of;
+    a.es = h.es ? 1 : 0;
+    a.es_row = h.es_row; a.es_pool = h.es_pool; a.es_rows_max = h.es_rows_max; a.es_pool_cap = h.es_pool_cap;
+    a.es_part = h.es_part; a.e_blk = h.e_blk;
     {   // fp32 prefilter: |d| from fp32 coordinates of magnitude <= ~2 L carries an error below 8 ulp(L)
         const double Lmax = std::max(h.box_L[0], std::max(h.box_L[1], h.box_L[2])) + std::fabs(h.box_t[0]) +
                             std::fabs(h.box_t[1]) + std::fabs(h.box_t[2]);
@@ -1729,6 +1756,7 @@ DirectArgs direct_args(Handle& h, const double* pos, int include_forces) {
 }
 
 void launch_nlist(Handle& h, const double* pos) {
+    if (h.es) { launch_es_list(h); return; }             // cf_kernels_es.hip
     if (h.cluster) { launch_cluster_list(h); return; }   // cf_kernels_cluster.hip
     DirectArgs a = direct_args(h, pos, 0);
     if (a.brute || h.nc[0] < 4 || h.nc[1] < 4 || h.nc[2] < 4)
@@ -1738,6 +1766,7 @@ void launch_nlist(Handle& h, const double* pos) {
 }
 
 void launch_direct(Handle& h, const double* pos, int include_forces) {
+    if (h.es) { launch_pairs_es(h, pos, include_forces); return; }             // cf_kernels_es.hip
     if (h.cluster) { launch_pairs_cluster(h, pos, include_forces); return; }   // cf_kernels_cluster.hip
     DirectArgs a = direct_args(h, pos, include_forces);
     if (a.half) {

@@ -27,6 +27,7 @@ CF_PAIR_LIST_AUTO = 0
 CF_PAIR_LIST_CLUSTER = 1
 CF_PAIR_LIST_ATOM_HALF = 2
 CF_PAIR_LIST_FULL = 3
+CF_PAIR_LIST_OCTANT = 4
 CF_VARIANT_GEMM_DFT = 1
 CF_VARIANT_VECTOR_SPREAD = 2
 CF_VARIANT_MFMA_SPREAD = 4

@@ -76,7 +76,8 @@ class HipCalcCoulForceKernel:
     KSPACE_GRID = 2         # same k-sum via ES-kernel grid (spread, pruned DFT, interpolate)
 
     PAIR_LISTS = {"auto": _cabi.CF_PAIR_LIST_AUTO, "cluster": _cabi.CF_PAIR_LIST_CLUSTER,
-                  "atom_half": _cabi.CF_PAIR_LIST_ATOM_HALF, "full": _cabi.CF_PAIR_LIST_FULL}
+                  "atom_half": _cabi.CF_PAIR_LIST_ATOM_HALF, "full": _cabi.CF_PAIR_LIST_FULL,
+                  "octant": _cabi.CF_PAIR_LIST_OCTANT}
     HANDOVERS = {"event": _cabi.CF_HANDOVER_EVENT, "memory": _cabi.CF_HANDOVER_MEMORY}
 
     def __init__(self, device: int = 0, stream=None, rank: int = 0, world_size: int = 1, kspace_algo: int = 0,
@@ -86,7 +87,7 @@ class HipCalcCoulForceKernel:
         takes it from openmm/reference/SimTKOpenMMRealType.h, ReferenceCoulKernels.cpp:7);
         0 = 138.935456 (OpenMM 7.x), _cabi.ONE_4PI_EPS0_CODATA2018 for OpenMM 8.x.
         pair_list, handover, variants, list_capacity: cf_options fields (include/chargeflux.h):
-        the neighbour-list kind ("auto", "cluster", "atom_half", "full"), the second stream's
+        the neighbour-list kind ("auto", "octant", "cluster", "atom_half", "full"), the second stream's
         fork / join ("event" or the opt-in "memory"), CF_VARIANT_* bits (alternative kernels of the
         same sums) and the cluster-pair list capacity (0 = automatic)."""
         if pair_list not in self.PAIR_LISTS:
@@ -193,7 +194,7 @@ class HipCalcCoulForceKernel:
         return c.value, r.value
 
     def pair_list(self):
-        """The direct-space list in use: "cluster", "atom_half" or "full" ("auto" before the first
+        """The direct-space list in use: "octant", "cluster", "atom_half" or "full" ("auto" before the first
         periodic evaluation and without PBC) -- cf_get_pair_list."""
         k = C.c_int32()
         _cabi.check(self._lib.cf_get_pair_list(self._h, C.byref(k)), self._lib)
