@@ -208,6 +208,8 @@ def main():
                     help="direct-space list (cf_options.pair_list; auto: the 18-cell cluster-pair list on one fp64 rank)")
     ap.add_argument("--handover", default="event", choices=["event", "memory"],
                     help="fork / join of the library's second stream (cf_options.handover; memory: opt-in)")
+    ap.add_argument("--direct-cus", type=int, default=0,
+                    help="CUs the library's second stream (direct chain) may use (cf_options.direct_cus; 0 = all)")
     ap.add_argument("--dt", type=float, default=0.001, help="ps")
     ap.add_argument("--neighbor-skin", type=float, default=None,
                     help="nm; persistent list rebuilt when an atom moved > skin/2 (0 = every step); default "
@@ -235,7 +237,7 @@ def main():
     n_waters = force.getNumFluxWaters() + force.getNumFluxAngles()
     kern = ShardedCoulKernel(system, force, local, kspace_algo=args.kspace_algo, neighbor_skin=args.neighbor_skin,
                              grid_width=args.grid_width, precision=args.precision, handover=args.handover,
-                             pair_list=args.pair_list)
+                             pair_list=args.pair_list, direct_cus=args.direct_cus)
     lo, hi = kern.lo, kern.hi
     alpha, kmax = kern.kernel.ewald_params()
     k_half = (kmax[2] - 1) + (kmax[1] - 1) * (2 * kmax[2] - 1) + (kmax[0] - 1) * (2 * kmax[1] - 1) * (2 * kmax[2] - 1)
@@ -297,6 +299,7 @@ def main():
     elif dom is not None and not args.no_kernel_timing:
         kern.kernel.set_timing(True, phases=[dom])
     builds0, evals0 = kern.kernel.neighbor_stats()
+    fb0 = kern.kernel.fallback_stats()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -313,6 +316,7 @@ def main():
         elapsed = t.item()
     timing = kern.kernel.timing()
     builds1, evals1 = kern.kernel.neighbor_stats()
+    fb1 = kern.kernel.fallback_stats()
     kern.kernel.set_timing(False)
     # force-evaluation pass (after the timed region, not part of it): K more MD steps with two
     # torch events around each execute (the library's stream is torch's current stream) and no
@@ -327,6 +331,10 @@ def main():
     # evaluation adds to a step.  (The event-bracketed figure above reads longer than a whole
     # step at C5 -- 2.82 against 2.69 ms in round 4: two extra event records per step on the
     # library's stream delay the launches they sit between -- so it is reported beside it only.)
+    # (the harness alone integrates without fresh forces: positions and velocities are restored
+    # after it, or the passes below would start from K steps of free flight -- overlapping
+    # molecules, the fp64 rescan fallback on every step: 0.5 -> 4000 ms per step at K = 40)
+    saved = (pos.clone(), vel.clone(), frc.clone())
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -336,6 +344,8 @@ def main():
         kern.replicate_positions(pos)
     torch.cuda.synchronize()
     ms_harness = (time.perf_counter() - t_h0) / args.steps * 1e3
+    pos.copy_(saved[0]); vel.copy_(saved[1]); frc.copy_(saved[2])
+    del saved
     # graph pass (after the timed region, not part of it): K steps with the CoulForce launches
     # replayed as a captured hipGraph, wall clock; measures what graph replay would give `value`
     graph_ms = None
@@ -486,10 +496,11 @@ def main():
                                    f"{dt * 1000:g} fs, " + ("fp64" if args.precision == "double" else
                                                             "mixed precision (fp32 pair kernel)"),
                        "atoms": n, "kmax": list(kmax), "k_half": k_half,
-                       "neighbor_skin_nm": args.neighbor_skin, "handover": args.handover,
+                       "neighbor_skin_nm": args.neighbor_skin, "handover": args.handover, "direct_cus": args.direct_cus,
                        "kspace": {0: "exact k-sum, fp64 MFMA", 1: "exact k-sum, VALU",
                                   2: f"grid (ES kernel W={w_grid}, pruned DFT), same k-set"}[args.kspace_algo],
                        "nlist_builds_in_timed_steps": f"{builds1 - builds0}/{evals1 - evals0}",
+                       "fp64_rescan_fallbacks_in_timed_steps": int(fb1[0] - fb0[0]),
                        "parallelism": f"atom-decomposition x{world}" + (" (RCCL all-reduce of S(k))" if world > 1 else "")},
             "ms_per_force_eval": round(ms_eval_clean, 4),
             "ms_per_harness_step": round(ms_harness, 4),
