@@ -118,9 +118,7 @@ typedef struct cf_options {
                             verification (0 = the production kernels) */
     int32_t list_capacity;   /* cluster-pair list entries per i-cluster; 0 = automatic.  A list that
                             overflows it is evaluated by the fp64 rescan (slow, same results). */
-    int32_t direct_cus;  /* CUs the second stream (the direct chain: cell sort, pair list, pair kernel)
-                            may use, 0 = all: the rest stay free for the reciprocal chain's latency-bound
-                            launches on the caller's stream (a CU-masked stream) */
+    int32_t reserved[1];
 } cf_options;
 
 #define CF_PRECISION_DOUBLE 0

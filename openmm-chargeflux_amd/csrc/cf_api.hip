@@ -527,7 +527,6 @@ CF_EXPORT int cf_create(const cf_params* p, const cf_options* opt, cf_handle** o
             fail(CF_ERR_INVALID, "pair_list must be one of CF_PAIR_LIST_AUTO, _CLUSTER, _ATOM_HALF, _FULL, _OCTANT");
         if (o.variants & ~(0x1F | (15 << 8))) fail(CF_ERR_INVALID, "unknown bits in variants");
         if (o.list_capacity < 0) fail(CF_ERR_INVALID, "list_capacity must be >= 0");
-        if (o.direct_cus < 0) fail(CF_ERR_INVALID, "direct_cus must be >= 0");
         // the memory hand-over is opt-in: hipStreamWaitValue64 runs as a polling kernel on this
         // runtime, so a dispatcher that serializes kernels (rocprofv3 counter collection) can run
         // the wait ahead of its producer and hold the device (a C3 --pmc pass hung, round 4); the
@@ -536,7 +535,6 @@ CF_EXPORT int cf_create(const cf_params* p, const cf_options* opt, cf_handle** o
         h.pair_list = o.pair_list;
         h.variants = o.variants;
         h.list_capacity = o.list_capacity;
-        h.direct_cus = o.direct_cus;
         h.kspace_algo = o.kspace_algo;
         h.stream = (hipStream_t)o.stream;  // NULL = the null stream (orders with torch's default stream)
 
@@ -1418,23 +1416,7 @@ static void launch_end_split(cf_handle* H, int flags, double* forces_dev, double
 static void ensure_aux(cf_handle* H) {
     cf::Handle& h = H->h;
     if (h.aux || !h.overlap || !h.pbc || h.kspace_algo != 2) return;
-    int ncu = 0;
-    check_hip(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, h.device), "hipDeviceGetAttribute");
-    if (h.direct_cus > 0 && h.direct_cus < ncu) {
-        // cf_options.direct_cus: the direct chain's stream on that many CUs, the others left to the
-        // reciprocal chain; the free CUs are spread over the mask (every (ncu / free)-th bit), so
-        // each XCD / shader engine keeps a share of both
-        std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
-        const int nfree = ncu - h.direct_cus;
-        for (int c = 0, kept = 0; c < ncu; c++) {
-            const bool free_cu = (int64_t)(c + 1) * nfree / ncu != (int64_t)c * nfree / ncu;
-            if (!free_cu && kept < h.direct_cus) { mask[c / 32] |= 1u << (c % 32); kept++; }
-        }
-        check_hip(hipExtStreamCreateWithCUMask(&h.aux, (uint32_t)mask.size(), mask.data()),
-                  "hipExtStreamCreateWithCUMask (second stream)");
-    } else {
-        check_hip(hipStreamCreateWithFlags(&h.aux, hipStreamNonBlocking), "hipStreamCreate (second stream)");
-    }
+    check_hip(hipStreamCreateWithFlags(&h.aux, hipStreamNonBlocking), "hipStreamCreate (second stream)");
     // fork / join order two streams of this device only: an agent-scope release is enough (kernel
     // ends already release to the device; the default system-scope fence of an event record
     // writes the L2s back for host visibility, ~15-20 us per fork and per join on the timeline,

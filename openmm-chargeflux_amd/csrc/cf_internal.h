@@ -189,7 +189,6 @@ struct Handle {
     bool cluster = false;
     int pair_list = CF_PAIR_LIST_AUTO;   // cf_options.pair_list
     int list_capacity = 0;      // cf_options.list_capacity (0: automatic)
-    int direct_cus = 0;         // cf_options.direct_cus (0: the second stream on every CU)
     int variants = 0;           // cf_options.variants (CF_VARIANT_*)
     int block_rounds() const { return (variants >> 8) & 15; }   // k_g_bin / k_assemble_energy rounds (0: by N)
     int zcol = 0;               // columns per cell axis of the within-cell sort (k_cell_order; 0 = atom order)

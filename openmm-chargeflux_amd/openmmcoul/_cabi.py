@@ -83,7 +83,7 @@ class cf_options(C.Structure):
         ("pair_list", C.c_int32),
         ("variants", C.c_int32),
         ("list_capacity", C.c_int32),
-        ("direct_cus", C.c_int32),
+        ("reserved", C.c_int32 * 1),
     ]
 
 

@@ -82,12 +82,11 @@ class HipCalcCoulForceKernel:
 
     def __init__(self, device: int = 0, stream=None, rank: int = 0, world_size: int = 1, kspace_algo: int = 0,
                  grid_width: int = 0, precision: str = "double", one_4pi_eps0: float = 0.0,
-                 pair_list: str = "auto", handover: str = "event", variants: int = 0, list_capacity: int = 0,
-                 direct_cus: int = 0):
+                 pair_list: str = "auto", handover: str = "event", variants: int = 0, list_capacity: int = 0):
         """one_4pi_eps0: ONE_4PI_EPS0 of the OpenMM the force is evaluated for (the reference
         takes it from openmm/reference/SimTKOpenMMRealType.h, ReferenceCoulKernels.cpp:7);
         0 = 138.935456 (OpenMM 7.x), _cabi.ONE_4PI_EPS0_CODATA2018 for OpenMM 8.x.
-        pair_list, handover, variants, list_capacity, direct_cus: cf_options fields (include/chargeflux.h):
+        pair_list, handover, variants, list_capacity: cf_options fields (include/chargeflux.h):
         the neighbour-list kind ("auto", "octant", "cluster", "atom_half", "full"), the second stream's
         fork / join ("event" or the opt-in "memory"), CF_VARIANT_* bits (alternative kernels of the
         same sums) and the cluster-pair list capacity (0 = automatic)."""
@@ -99,7 +98,6 @@ class HipCalcCoulForceKernel:
         self._handover = self.HANDOVERS[handover]
         self._variants = int(variants)
         self._list_capacity = int(list_capacity)
-        self._direct_cus = int(direct_cus)
         self._lib = _cabi.load_library()
         self._ke = float(one_4pi_eps0)
         self._grid_width = grid_width
@@ -130,7 +128,6 @@ class HipCalcCoulForceKernel:
         opt.precision = self._precision
         opt.handover, opt.pair_list = self._handover, self._pair_list
         opt.variants, opt.list_capacity = self._variants, self._list_capacity
-        opt.direct_cus = self._direct_cus
         self.destroy()
         _cabi.check(self._lib.cf_create(C.byref(params), C.byref(opt), C.byref(self._h)), self._lib)
         del keep
