@@ -208,6 +208,8 @@ def main():
                     help="direct-space list (cf_options.pair_list; auto: the 18-cell cluster-pair list on one fp64 rank)")
     ap.add_argument("--handover", default="event", choices=["event", "memory"],
                     help="fork / join of the library's second stream (cf_options.handover; memory: opt-in)")
+    ap.add_argument("--variants", type=lambda v: int(v, 0), default=0,
+                    help="cf_options.variants bits (A/B kernels of the same sums; include/chargeflux.h)")
     ap.add_argument("--dt", type=float, default=0.001, help="ps")
     ap.add_argument("--neighbor-skin", type=float, default=None,
                     help="nm; persistent list rebuilt when an atom moved > skin/2 (0 = every step); default "
@@ -235,7 +237,7 @@ def main():
     n_waters = force.getNumFluxWaters() + force.getNumFluxAngles()
     kern = ShardedCoulKernel(system, force, local, kspace_algo=args.kspace_algo, neighbor_skin=args.neighbor_skin,
                              grid_width=args.grid_width, precision=args.precision, handover=args.handover,
-                             pair_list=args.pair_list)
+                             pair_list=args.pair_list, variants=args.variants)
     lo, hi = kern.lo, kern.hi
     alpha, kmax = kern.kernel.ewald_params()
     k_half = (kmax[2] - 1) + (kmax[1] - 1) * (2 * kmax[2] - 1) + (kmax[0] - 1) * (2 * kmax[1] - 1) * (2 * kmax[2] - 1)
@@ -494,7 +496,7 @@ def main():
                                    f"{dt * 1000:g} fs, " + ("fp64" if args.precision == "double" else
                                                             "mixed precision (fp32 pair kernel)"),
                        "atoms": n, "kmax": list(kmax), "k_half": k_half,
-                       "neighbor_skin_nm": args.neighbor_skin, "handover": args.handover,
+                       "neighbor_skin_nm": args.neighbor_skin, "handover": args.handover, "variants": args.variants,
                        "kspace": {0: "exact k-sum, fp64 MFMA", 1: "exact k-sum, VALU",
                                   2: f"grid (ES kernel W={w_grid}, pruned DFT), same k-set"}[args.kspace_algo],
                        "nlist_builds_in_timed_steps": f"{builds1 - builds0}/{evals1 - evals0}",
