@@ -104,8 +104,8 @@ typedef struct cf_options {
                             polling kernel, so a tool that serializes dispatches (rocprofv3 counter
                             collection) can deadlock it.  Same results either way. */
     int32_t pair_list;   /* direct-space neighbour list (periodic):
-                            CF_PAIR_LIST_AUTO (0): cluster-pair half list on one rank in fp64, per-atom
-                              half list on one rank in mixed precision, per-atom full list on several ranks;
+                            CF_PAIR_LIST_AUTO (0): cluster-pair half list on one rank (fp64 and mixed),
+                              per-atom full list on several ranks;
                             CF_PAIR_LIST_CLUSTER (1): the cluster-pair half list wherever its cell window
                               fits (also mixed precision, and several ranks with an ownership filter);
                             CF_PAIR_LIST_ATOM_HALF (2): the per-atom half list on one rank (full on several);
@@ -142,6 +142,8 @@ typedef struct cf_options {
 #define CF_VARIANT_INTERP2 16        /* W <= 8: two atoms per wave (k_g_interp2), not four */
 #define CF_VARIANT_BLOCK_ROUNDS(r) (((r) & 15) << 8)   /* grid bin sort and energy kernels: r rounds of
                                         256 atoms per block (1..8; 0 = by N) */
+#define CF_VARIANT_PAIR_PARTS(p) (((p) & 7) << 12)   /* the cluster-pair loop issued as p launches over
+                                        consecutive cell ranges (1..7; 0 = one) */
 
 /* compute flags */
 #define CF_INCLUDE_FORCES 1

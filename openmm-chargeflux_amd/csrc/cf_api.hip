@@ -214,7 +214,7 @@ void set_cells(cf_handle* H, const double L[3]) {
     const int es_wcap = ((2 * 40960 - cf::es_static_lds_bytes(h.mixed, true) - 256) / 32) & ~15;
     const bool want_es = h.world == 1 && h.pair_list == CF_PAIR_LIST_OCTANT &&
                          per_cell * 8.0 * 1.15 <= es_wcap;
-    const bool want_cluster = want_es || h.pair_list == CF_PAIR_LIST_CLUSTER || (h.pair_list == CF_PAIR_LIST_AUTO && !h.mixed);
+    const bool want_cluster = want_es || h.pair_list == CF_PAIR_LIST_CLUSTER || h.pair_list == CF_PAIR_LIST_AUTO;
     h.half = h.pair_list != CF_PAIR_LIST_FULL && h.pbc &&
              (h.world == 1 || (want_cluster && h.pair_list == CF_PAIR_LIST_CLUSTER)) && nc[0] >= 4 &&
              nc[1] >= 4 && nc[2] >= 4 && per_cell * 18.0 * 1.15 <= 4096.0 && h.n < (1 << 21);
@@ -225,11 +225,12 @@ void set_cells(cf_handle* H, const double L[3]) {
         h.win_cells = (int)ncell;
         h.alloc_epoch++;
     }
-    // cluster-pair half list (cf_kernels_cluster.hip): one rank, fp64, wherever
-    // the per-atom half list applies.  Mixed precision keeps the per-atom list by default: its
-    // fp32 term is cheap, so the cluster kernel's phase A (the fp32 atom tests and the queueing)
-    // costs more than it saves (C5: 1.425 vs 1.235 ms, profiles/r04e_*); CF_PAIR_LIST_CLUSTER forces
-    // it, CF_PAIR_LIST_ATOM_HALF keeps the per-atom list in fp64
+    // cluster-pair half list (cf_kernels_cluster.hip): one rank, fp64 and mixed,
+    // wherever the per-atom half list applies.  In mixed precision its pair kernel is slower than
+    // the per-atom list's (C5: 1.34 vs 1.23 ms) but its list build is 2.5x cheaper (0.07 vs 0.18 ms
+    // per step): C5 2.729 against 2.815 ms/step (profiles/r05l_c5_pair_lists.txt; round 4, before the
+    // skin-gated builder and the k_pairs_cq rework, the other way round: 2.878 vs 2.775).
+    // CF_PAIR_LIST_ATOM_HALF keeps the per-atom list
     h.cluster = h.half && want_cluster;
     h.es = h.cluster && want_es;
     h.zcol = 0;
@@ -525,7 +526,7 @@ CF_EXPORT int cf_create(const cf_params* p, const cf_options* opt, cf_handle** o
             fail(CF_ERR_INVALID, "handover must be CF_HANDOVER_EVENT or CF_HANDOVER_MEMORY");
         if (o.pair_list < CF_PAIR_LIST_AUTO || o.pair_list > CF_PAIR_LIST_OCTANT)
             fail(CF_ERR_INVALID, "pair_list must be one of CF_PAIR_LIST_AUTO, _CLUSTER, _ATOM_HALF, _FULL, _OCTANT");
-        if (o.variants & ~(0x1F | (15 << 8))) fail(CF_ERR_INVALID, "unknown bits in variants");
+        if (o.variants & ~(0x1F | (15 << 8) | (7 << 12))) fail(CF_ERR_INVALID, "unknown bits in variants");
         if (o.list_capacity < 0) fail(CF_ERR_INVALID, "list_capacity must be >= 0");
         // the memory hand-over is opt-in: hipStreamWaitValue64 runs as a polling kernel on this
         // runtime, so a dispatcher that serializes kernels (rocprofv3 counter collection) can run

@@ -164,8 +164,8 @@ def test_half_list_sparse_gas_matches_oracle_with_skin():
 
 @pytest.mark.parametrize("cluster", [False, True], ids=["atom_list", "cluster_list"])
 def test_half_list_mixed_precision(cluster):
-    # the fp32 half-list kernel (the per-atom list, the mixed default, and the cluster-pair list,
-    # pair_list "cluster") against the fp32 full list and the fp64 half list (same k-space)
+    # the fp32 half-list kernel (the per-atom list, and the cluster-pair list -- the mixed default since
+    # round 5) against the fp32 full list and the fp64 half list (same k-space)
     system, force, pos, box = ts.water_box(4000, cutoff=1.0, ewald_tol=1e-4, every_bond_angle=5)
     em, fm, dm, tm = _eval(_kernel(system, force, True, 0, precision="mixed", cluster=cluster), pos, box)
     ef, ff, df, tf = _eval(_kernel(system, force, False, 0, precision="mixed"), pos, box)
