@@ -142,8 +142,6 @@ typedef struct cf_options {
 #define CF_VARIANT_INTERP2 16        /* W <= 8: two atoms per wave (k_g_interp2), not four */
 #define CF_VARIANT_BLOCK_ROUNDS(r) (((r) & 15) << 8)   /* grid bin sort and energy kernels: r rounds of
                                         256 atoms per block (1..8; 0 = by N) */
-#define CF_VARIANT_PAIR_PARTS(p) (((p) & 7) << 12)   /* the cluster-pair loop issued as p launches over
-                                        consecutive cell ranges (1..7; 0 = one) */
 
 /* compute flags */
 #define CF_INCLUDE_FORCES 1

@@ -526,7 +526,7 @@ CF_EXPORT int cf_create(const cf_params* p, const cf_options* opt, cf_handle** o
             fail(CF_ERR_INVALID, "handover must be CF_HANDOVER_EVENT or CF_HANDOVER_MEMORY");
         if (o.pair_list < CF_PAIR_LIST_AUTO || o.pair_list > CF_PAIR_LIST_OCTANT)
             fail(CF_ERR_INVALID, "pair_list must be one of CF_PAIR_LIST_AUTO, _CLUSTER, _ATOM_HALF, _FULL, _OCTANT");
-        if (o.variants & ~(0x1F | (15 << 8) | (7 << 12))) fail(CF_ERR_INVALID, "unknown bits in variants");
+        if (o.variants & ~(0x1F | (15 << 8))) fail(CF_ERR_INVALID, "unknown bits in variants");
         if (o.list_capacity < 0) fail(CF_ERR_INVALID, "list_capacity must be >= 0");
         // the memory hand-over is opt-in: hipStreamWaitValue64 runs as a polling kernel on this
         // runtime, so a dispatcher that serializes kernels (rocprofv3 counter collection) can run

@@ -191,7 +191,6 @@ struct Handle {
     int list_capacity = 0;      // cf_options.list_capacity (0: automatic)
     int variants = 0;           // cf_options.variants (CF_VARIANT_*)
     int block_rounds() const { return (variants >> 8) & 15; }   // k_g_bin / k_assemble_energy rounds (0: by N)
-    int pair_parts() const { const int v = (variants >> 12) & 7; return v ? v : 1; }   // launches of the cluster-pair loop
     int zcol = 0;               // columns per cell axis of the within-cell sort (k_cell_order; 0 = atom order)
     int ncl_cap = 0;            // cluster capacity: N/4 + ncell
     int cl_cells = 0;           // cells cl_start is sized for (+1)

@@ -266,8 +266,9 @@ __global__ void __launch_bounds__(kClBuildThreads) k_cl_build(DirectArgs a, cons
 // coordinates small, so fp32 carries ~1e-7 nm whatever the box size), erfc from the degree-6 fp32
 // table, fp32 i-side sums, fp64 energy, the j side in the same fixed point (an fp32 value times
 // 2^34 is exact in fp64)
-// cell0: the launch covers cells cell0 .. cell0 + gridDim.x - 1 (the pair loop may be issued in
-// parts, CF_VARIANT_PAIR_PARTS)
+// cell0: the launch covers cells cell0 .. cell0 + gridDim.x - 1 (one launch covers every cell: issued
+// in 2-4 parts so that the other stream's DFT stages could take CUs between them, the step got no
+// faster -- the freed CUs went to the next part first, profiles/r05m_pair_parts.txt)
 template <bool TYPES, bool MIXED>
 __global__ void __launch_bounds__(kCqThreads) CF_LDS_UNPAIRED k_pairs_cq(DirectArgs a, int cell0) {
     __shared__ double tab[MIXED ? 1 : kErfcMaxM * (kErfcDeg + 1)];
@@ -605,19 +606,13 @@ void launch_pairs_cluster(Handle& h, const double* pos, int include_forces) {
 // (any reduced box: the pair vector comes from the window cell's lattice translation, which for a
 // pair within rc is the image of the reference's c, b, a minimum image when rc is at most half of
 // each perpendicular width -- set_box checks rc <= L/2, and the cells are at least rc + skin wide)
-// (several parts: each launch's blocks end within ~half a pair launch, so launches of the other
-// stream waiting for CUs -- the DFT stages behind the spread -- get them sooner)
-    const int parts = std::max(1, std::min(h.pair_parts(), ncell));
-    for (int p = 0; p < parts; p++) {
-        const int c0 = (int)((int64_t)p * ncell / parts), c1 = (int)((int64_t)(p + 1) * ncell / parts);
-#define CF_PAIRS_CQ(TY_, MX_) hipLaunchKernelGGL((k_pairs_cq<TY_, MX_>), dim3(c1 - c0), dim3(kCqThreads), 0, h.stream, a, c0)
-        if (h.mixed) {
-            if (a.typ_s) CF_PAIRS_CQ(true, true);
-            else CF_PAIRS_CQ(false, true);
-        } else {
-            if (a.typ_s) CF_PAIRS_CQ(true, false);
-            else CF_PAIRS_CQ(false, false);
-        }
+#define CF_PAIRS_CQ(TY_, MX_) hipLaunchKernelGGL((k_pairs_cq<TY_, MX_>), dim3(ncell), dim3(kCqThreads), 0, h.stream, a, 0)
+    if (h.mixed) {
+        if (a.typ_s) CF_PAIRS_CQ(true, true);
+        else CF_PAIRS_CQ(false, true);
+    } else {
+        if (a.typ_s) CF_PAIRS_CQ(true, false);
+        else CF_PAIRS_CQ(false, false);
     }
 #undef CF_PAIRS_CQ
 }
