@@ -338,9 +338,11 @@ __device__ __forceinline__ double rsqrt_fp64(double r2) {
 
 // d = a*b + c as one VOP3 v_fma_f64.  For a Horner step with a constant addend the compiler
 // otherwise emits v_mov_b64 (constant -> accumulator) + v_fmac_f64: one extra VALU op per step.
+// c is a wave-uniform constant: an SGPR pair operand (round 5; held in VGPRs, the twelve exp
+// coefficients took 24 VGPRs of the 128 the pair kernels may use: 32-40 B/lane of spills, none now)
 __device__ __forceinline__ double fma3(double a, double b, double c) {
     double d;
-    asm("v_fma_f64 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+    asm("v_fma_f64 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "s"(c));
     return d;
 }
 

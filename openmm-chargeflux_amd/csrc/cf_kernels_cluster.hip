@@ -266,11 +266,13 @@ __global__ void __launch_bounds__(kClBuildThreads) k_cl_build(DirectArgs a, cons
 // coordinates small, so fp32 carries ~1e-7 nm whatever the box size), erfc from the degree-6 fp32
 // table, fp32 i-side sums, fp64 energy, the j side in the same fixed point (an fp32 value times
 // 2^34 is exact in fp64)
-// cell0: the launch covers cells cell0 .. cell0 + gridDim.x - 1 (one launch covers every cell: issued
-// in 2-4 parts so that the other stream's DFT stages could take CUs between them, the step got no
-// faster -- the freed CUs went to the next part first, profiles/r05m_pair_parts.txt)
+// One block per cell (xcd_block: XCD blockIdx % 8 takes a contiguous eighth of the cells).  Round 5
+// measured the alternative of persistent blocks taking cells from per-XCD counters and leaving CUs
+// to the other stream's DFT stages: with ~2.3 cells per block the last round of cells leaves most
+// CUs idle, the kernel ran 250 against 171 us and the step gained nothing
+// (profiles/r05o_persistent_pair_kernel.txt).
 template <bool TYPES, bool MIXED>
-__global__ void __launch_bounds__(kCqThreads) CF_LDS_UNPAIRED k_pairs_cq(DirectArgs a, int cell0) {
+__global__ void __launch_bounds__(kCqThreads) CF_LDS_UNPAIRED k_pairs_cq(DirectArgs a) {
     __shared__ double tab[MIXED ? 1 : kErfcMaxM * (kErfcDeg + 1)];
     __shared__ float tabf[MIXED ? kErfcMaxMF * (kErfcDegF + 1) : 1];
     __shared__ double2 ljt[TYPES ? kMaxLjTypes : 1];
@@ -281,8 +283,17 @@ __global__ void __launch_bounds__(kCqThreads) CF_LDS_UNPAIRED k_pairs_cq(DirectA
     __shared__ unsigned long long accw[4][kHalfMaxWin];   // j-side fx, fy, fz, dE/dq (fixed point)
     __shared__ int qbuf[kCqWaves][4][kCqQ];  // per wave, per i atom: ring of hit entries
     __shared__ int wtot, next_ci, nown;
-    const int cell = cell0 + xcd_block();
     const int3 nc = a.nc;
+    if constexpr (TYPES)
+        for (int e = threadIdx.x; e < a.lj_ntypes; e += kCqThreads) ljt[e] = a.lj_tab[e];
+    if constexpr (MIXED) {
+        for (int e = threadIdx.x; e < a.erfc_m_f * (kErfcDegF + 1); e += kCqThreads) tabf[e] = a.erfc_tab_f[e];
+    } else {
+        for (int e = threadIdx.x; e < kErfcMaxM * (kErfcDeg + 1); e += kCqThreads) tab[e] = a.erfc_tab[e];
+    }
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    bool bad = false, bad_list = false;
+    auto process = [&](const int cell) {
     const int cz = cell % nc.z, cy = (cell / nc.z) % nc.y, cx = cell / (nc.y * nc.z);
     if (threadIdx.x == 0) nown = 0;
     __syncthreads();
@@ -296,13 +307,6 @@ __global__ void __launch_bounds__(kCqThreads) CF_LDS_UNPAIRED k_pairs_cq(DirectA
         shd[threadIdx.x] = wr;
         // several ranks: owned atoms in the window (its own cell is window cell 0)
         if (a.own_start && a.own_start[w + 1] > a.own_start[w]) atomicAdd(&nown, 1);
-    }
-    if constexpr (TYPES)
-        for (int e = threadIdx.x; e < a.lj_ntypes; e += kCqThreads) ljt[e] = a.lj_tab[e];
-    if constexpr (MIXED) {
-        for (int e = threadIdx.x; e < a.erfc_m_f * (kErfcDegF + 1); e += kCqThreads) tabf[e] = a.erfc_tab_f[e];
-    } else {
-        for (int e = threadIdx.x; e < kErfcMaxM * (kErfcDeg + 1); e += kCqThreads) tab[e] = a.erfc_tab[e];
     }
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -329,12 +333,10 @@ __global__ void __launch_bounds__(kCqThreads) CF_LDS_UNPAIRED k_pairs_cq(DirectA
     }
     __syncthreads();
 
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int il = lane >> 4, kk = lane & 15;          // phase B: i atom il, lane kk of its 16
     const int jl = lane & 3, el = lane >> 2;           // phase A: entry el of the batch, j atom jl
     int* const qw = qbuf[wv][il];
     const int c0 = a.cl_start[cell], ncl = a.cl_start[cell + 1] - c0;
-    bool bad = false, bad_list = false;
     auto ring = [](int x) { return x >= kCqQ ? x - kCqQ : x; };   // x < 2 kCqQ
     for (;;) {
         int ci = 0;
@@ -566,15 +568,17 @@ __global__ void __launch_bounds__(kCqThreads) CF_LDS_UNPAIRED k_pairs_cq(DirectA
             }
         }
     }
-    {
-        const int why = (__ballot(bad_list) ? kHalfListOverflow : 0) | (__ballot(bad) ? kHalfFixedRange : 0);
-        if (why && lane == 0) atomicOr(a.half_flag, why);
-    }
     if (!a.include_forces) return;
     __syncthreads();
     unsigned long long* out = a.win_out + (size_t)cell * kHalfMaxWin * 4;
     for (int e = threadIdx.x; e < nw; e += kCqThreads)
         reinterpret_cast<ulonglong4*>(out)[e] = make_ulonglong4(accw[0][e], accw[1][e], accw[2][e], accw[3][e]);
+    };   // process
+    process(xcd_block());
+    {
+        const int why = (__ballot(bad_list) ? kHalfListOverflow : 0) | (__ballot(bad) ? kHalfFixedRange : 0);
+        if (why && lane == 0) atomicOr(a.half_flag, why);
+    }
 }
 
 // ---------------------------------------------------------------------------------
@@ -606,7 +610,7 @@ void launch_pairs_cluster(Handle& h, const double* pos, int include_forces) {
 // (any reduced box: the pair vector comes from the window cell's lattice translation, which for a
 // pair within rc is the image of the reference's c, b, a minimum image when rc is at most half of
 // each perpendicular width -- set_box checks rc <= L/2, and the cells are at least rc + skin wide)
-#define CF_PAIRS_CQ(TY_, MX_) hipLaunchKernelGGL((k_pairs_cq<TY_, MX_>), dim3(ncell), dim3(kCqThreads), 0, h.stream, a, 0)
+#define CF_PAIRS_CQ(TY_, MX_) hipLaunchKernelGGL((k_pairs_cq<TY_, MX_>), dim3(ncell), dim3(kCqThreads), 0, h.stream, a)
     if (h.mixed) {
         if (a.typ_s) CF_PAIRS_CQ(true, true);
         else CF_PAIRS_CQ(false, true);

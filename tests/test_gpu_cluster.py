@@ -105,3 +105,4 @@ def test_cluster_list_on_several_ranks_opt_in(world):
     assert abs(ew - e1) <= 1e-11 * np.abs(t1).sum()
     assert np.abs(fw - f1).max() <= 2e-12 * np.abs(f1).max() + 1e-9
     assert np.abs(dw - d1).max() <= 2e-12 * np.abs(d1).max() + 1e-9
+
