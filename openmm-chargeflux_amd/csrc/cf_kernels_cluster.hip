@@ -272,7 +272,7 @@ __global__ void __launch_bounds__(kClBuildThreads) k_cl_build(DirectArgs a, cons
 // CUs idle, the kernel ran 250 against 171 us and the step gained nothing
 // (profiles/r05o_persistent_pair_kernel.txt).
 template <bool TYPES, bool MIXED>
-__global__ void __launch_bounds__(kCqThreads) CF_LDS_UNPAIRED k_pairs_cq(DirectArgs a) {
+__global__ void __launch_bounds__(kCqThreads) CF_LDS_UNPAIRED k_pairs_cq(DirectArgs a, int cell0) {
     __shared__ double tab[MIXED ? 1 : kErfcMaxM * (kErfcDeg + 1)];
     __shared__ float tabf[MIXED ? kErfcMaxMF * (kErfcDegF + 1) : 1];
     __shared__ double2 ljt[TYPES ? kMaxLjTypes : 1];
@@ -574,7 +574,7 @@ __global__ void __launch_bounds__(kCqThreads) CF_LDS_UNPAIRED k_pairs_cq(DirectA
     for (int e = threadIdx.x; e < nw; e += kCqThreads)
         reinterpret_cast<ulonglong4*>(out)[e] = make_ulonglong4(accw[0][e], accw[1][e], accw[2][e], accw[3][e]);
     };   // process
-    process(xcd_block());
+    process(cell0 + xcd_block());
     {
         const int why = (__ballot(bad_list) ? kHalfListOverflow : 0) | (__ballot(bad) ? kHalfFixedRange : 0);
         if (why && lane == 0) atomicOr(a.half_flag, why);
@@ -610,7 +610,7 @@ void launch_pairs_cluster(Handle& h, const double* pos, int include_forces) {
 // (any reduced box: the pair vector comes from the window cell's lattice translation, which for a
 // pair within rc is the image of the reference's c, b, a minimum image when rc is at most half of
 // each perpendicular width -- set_box checks rc <= L/2, and the cells are at least rc + skin wide)
-#define CF_PAIRS_CQ(TY_, MX_) hipLaunchKernelGGL((k_pairs_cq<TY_, MX_>), dim3(ncell), dim3(kCqThreads), 0, h.stream, a)
+#define CF_PAIRS_CQ(TY_, MX_) hipLaunchKernelGGL((k_pairs_cq<TY_, MX_>), dim3(ncell), dim3(kCqThreads), 0, h.stream, a, 0)
     if (h.mixed) {
         if (a.typ_s) CF_PAIRS_CQ(true, true);
         else CF_PAIRS_CQ(false, true);

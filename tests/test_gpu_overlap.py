@@ -21,9 +21,10 @@ def _need_gpu():
         pytest.skip("no HIP device")
 
 
-def _run(overlap, system, force, pos, box, skin, graph=False, steps=4, handover="event"):
+def _run(overlap, system, force, pos, box, skin, graph=False, steps=4, handover="event", variants=0):
     stream = torch.cuda.current_stream().cuda_stream
-    k = HipCalcCoulForceKernel(stream=stream, kspace_algo=2, handover=handover).initialize(system, force)
+    k = HipCalcCoulForceKernel(stream=stream, kspace_algo=2, handover=handover,
+                               variants=variants).initialize(system, force)
     k.set_overlap(overlap)
     if skin:
         k.set_neighbor_skin(skin)
