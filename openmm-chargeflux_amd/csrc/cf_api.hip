@@ -85,12 +85,33 @@ int guarded(F&& f) {
     }
 }
 
+// Device buffers start zeroed: a list, count or index array that some evaluation reads before
+// its first build holds zeros (empty rows, atom 0), never the previous owner's bytes
+void zalloc(void** p, size_t bytes, const char* what) {
+    hipError_t e = hipMalloc(p, bytes);
+    if (e != hipSuccess) fail(CF_ERR_NOMEM, std::string(what) + ": hipMalloc failed: " + hipGetErrorString(e));
+    e = hipMemset(*p, 0, bytes);
+    if (e != hipSuccess) fail(CF_ERR_HIP, std::string(what) + ": hipMemset failed: " + hipGetErrorString(e));
+}
+template <class T>
+void zalloc(T** p, size_t count, const char* what) {
+    zalloc(reinterpret_cast<void**>(p), std::max<size_t>(count, 1) * sizeof(T), what);
+}
+
+// Buffers are freed only once the device is idle: evaluations are asynchronous (the caller
+// need not synchronize between steps) and the second stream's launches of the previous
+// evaluation may still read a list that a box change reallocates
+void free_idle(void* p) {
+    if (!p) return;
+    (void)hipDeviceSynchronize();
+    (void)hipFree(p);
+}
+
 template <class T>
 T* dalloc(cf_handle* H, size_t count) {
     if (count == 0) count = 1;
     void* p = nullptr;
-    hipError_t e = hipMalloc(&p, count * sizeof(T));
-    if (e != hipSuccess) fail(CF_ERR_NOMEM, std::string("hipMalloc failed: ") + hipGetErrorString(e));
+    zalloc(&p, count * sizeof(T), "device buffer");
     H->allocs.push_back(p);
     return static_cast<T*>(p);
 }
@@ -106,7 +127,7 @@ void dfree(cf_handle* H, void* p) {
     if (!p) return;
     auto it = std::find(H->allocs.begin(), H->allocs.end(), p);
     if (it != H->allocs.end()) H->allocs.erase(it);
-    (void)hipFree(p);
+    free_idle(p);
 }
 
 // neighbour-list capacity: the mean count within rc + skin at the default-box density,
@@ -184,16 +205,14 @@ void set_cells(cf_handle* H, const double L[3]) {
     if (ncell > h.ncell_alloc) {
         // grow (not graph-capture safe; only happens when the box grows past the initial grid)
         h.alloc_epoch++;
-        if (h.cell_start) { (void)hipFree(h.cell_start); (void)hipFree(h.cell_end); (void)hipFree(h.cell_cnt); }
-        if (h.own_cnt) { (void)hipFree(h.own_cnt); (void)hipFree(h.own_start); h.own_cnt = h.own_start = nullptr; }
-        cf::check_hip(hipMalloc(&h.cell_start, sizeof(int) * ncell), "cells");
-        cf::check_hip(hipMalloc(&h.cell_end, sizeof(int) * ncell), "cells");
-        cf::check_hip(hipMalloc(&h.cell_cnt, sizeof(int) * ncell), "cells");
-        cf::check_hip(hipMemset(h.cell_cnt, 0, sizeof(int) * ncell), "cells");   // re-zeroed by each build
+        if (h.cell_start) { free_idle(h.cell_start); free_idle(h.cell_end); free_idle(h.cell_cnt); }
+        if (h.own_cnt) { free_idle(h.own_cnt); free_idle(h.own_start); h.own_cnt = h.own_start = nullptr; }
+        zalloc((void**)&h.cell_start, sizeof(int) * ncell, "cells");
+        zalloc((void**)&h.cell_end, sizeof(int) * ncell, "cells");
+        zalloc((void**)&h.cell_cnt, sizeof(int) * ncell, "cells");   // zero; re-zeroed by each build
         if (h.world > 1) {   // owned atoms per cell and their scan (list rows of a multi-rank run)
-            cf::check_hip(hipMalloc(&h.own_cnt, sizeof(int) * ncell), "cells");
-            cf::check_hip(hipMalloc(&h.own_start, sizeof(int) * (ncell + 1)), "cells");
-            cf::check_hip(hipMemset(h.own_cnt, 0, sizeof(int) * ncell), "cells");
+            zalloc((void**)&h.own_cnt, sizeof(int) * ncell, "cells");
+            zalloc((void**)&h.own_start, sizeof(int) * (ncell + 1), "cells");
         }
         h.ncell_alloc = (int)ncell;
     }
@@ -219,9 +238,9 @@ void set_cells(cf_handle* H, const double L[3]) {
              (h.world == 1 || (want_cluster && h.pair_list == CF_PAIR_LIST_CLUSTER)) && nc[0] >= 4 &&
              nc[1] >= 4 && nc[2] >= 4 && per_cell * 18.0 * 1.15 <= 4096.0 && h.n < (1 << 21);
     if (h.half && ncell > h.win_cells) {
-        if (h.win_out) { (void)hipFree(h.win_out); (void)hipFree(h.win_woff); }
-        cf::check_hip(hipMalloc(&h.win_out, sizeof(unsigned long long) * 4 * 4096 * (size_t)ncell), "half-list windows");
-        cf::check_hip(hipMalloc(&h.win_woff, sizeof(int) * 18 * (size_t)ncell), "half-list windows");
+        if (h.win_out) { free_idle(h.win_out); free_idle(h.win_woff); }
+        zalloc((void**)&h.win_out, sizeof(unsigned long long) * 4 * 4096 * (size_t)ncell, "half-list windows");
+        zalloc((void**)&h.win_woff, sizeof(int) * 18 * (size_t)ncell, "half-list windows");
         h.win_cells = (int)ncell;
         h.alloc_epoch++;
     }
@@ -250,16 +269,16 @@ void set_cells(cf_handle* H, const double L[3]) {
         if (h.es) cap = 384;   // the octant builder's row stage (k_es_build); the pool is per block
         if (h.list_capacity > 0) cap = std::max(4, std::min(cap, h.list_capacity));   // cf_options.list_capacity
         if (need > h.ncl_cap || cap != h.cpl_cap || ncell + 1 > h.cl_cells) {
-            if (h.cl_start) { (void)hipFree(h.cl_start); (void)hipFree(h.cl_info); (void)hipFree(h.cl_bb);
-                              (void)hipFree(h.cpl); (void)hipFree(h.cpl_cnt); }
+            if (h.cl_start) { free_idle(h.cl_start); free_idle(h.cl_info); free_idle(h.cl_bb);
+                              free_idle(h.cpl); free_idle(h.cpl_cnt); }
             h.ncl_cap = std::max(need, h.ncl_cap);
             h.cpl_cap = cap;
             h.cl_cells = std::max((int)ncell + 1, h.cl_cells);
-            cf::check_hip(hipMalloc(&h.cl_start, sizeof(int) * h.cl_cells), "cluster table");
-            cf::check_hip(hipMalloc(&h.cl_info, sizeof(int2) * h.ncl_cap), "cluster table");
-            cf::check_hip(hipMalloc(&h.cl_bb, sizeof(float4) * 2 * h.ncl_cap), "cluster table");
-            cf::check_hip(hipMalloc(&h.cpl, sizeof(uint2) * (size_t)h.ncl_cap * (h.es ? 1 : h.cpl_cap)), "cluster-pair list");
-            cf::check_hip(hipMalloc(&h.cpl_cnt, sizeof(int) * h.ncl_cap), "cluster-pair list");
+            zalloc((void**)&h.cl_start, sizeof(int) * h.cl_cells, "cluster table");
+            zalloc((void**)&h.cl_info, sizeof(int2) * h.ncl_cap, "cluster table");
+            zalloc((void**)&h.cl_bb, sizeof(float4) * 2 * h.ncl_cap, "cluster table");
+            zalloc((void**)&h.cpl, sizeof(uint2) * (size_t)h.ncl_cap * (h.es ? 1 : h.cpl_cap), "cluster-pair list");
+            zalloc((void**)&h.cpl_cnt, sizeof(int) * h.ncl_cap, "cluster-pair list");
             h.alloc_epoch++;
         }
         if (h.es) {
@@ -268,17 +287,17 @@ void set_cells(cf_handle* H, const double L[3]) {
             const int rows_max = std::min(1024, (int)(4.0 * std::ceil(per_cell / 4.0) * 1.6) + 64);
             const int pool_cap = (int)(1.6 * 1.15 * (per_cell / 4.0) * est) + 256;
             if (ncell > h.es_cells || rows_max > h.es_rows_max || pool_cap > h.es_pool_cap) {
-                if (h.es_row) { (void)hipFree(h.es_row); (void)hipFree(h.es_pool); (void)hipFree(h.e_blk); }
+                if (h.es_row) { free_idle(h.es_row); free_idle(h.es_pool); free_idle(h.e_blk); }
                 h.es_cells = std::max((int)ncell, h.es_cells);
                 h.es_rows_max = std::max(rows_max, h.es_rows_max);
                 h.es_pool_cap = std::max(pool_cap, h.es_pool_cap);
-                cf::check_hip(hipMalloc(&h.es_row, sizeof(int2) * (size_t)h.es_cells * h.es_rows_max), "octant list");
-                cf::check_hip(hipMalloc(&h.es_pool, sizeof(uint2) * (size_t)h.es_cells * h.es_pool_cap), "octant list");
-                cf::check_hip(hipMalloc(&h.e_blk, sizeof(double) * (size_t)h.es_cells), "octant list");
+                zalloc((void**)&h.es_row, sizeof(int2) * (size_t)h.es_cells * h.es_rows_max, "octant list");
+                zalloc((void**)&h.es_pool, sizeof(uint2) * (size_t)h.es_cells * h.es_pool_cap, "octant list");
+                zalloc((void**)&h.e_blk, sizeof(double) * (size_t)h.es_cells, "octant list");
                 h.alloc_epoch++;
             }
             if (!h.es_part) {
-                cf::check_hip(hipMalloc(&h.es_part, sizeof(ulonglong4) * 8 * (size_t)h.n), "octant window sums");
+                zalloc((void**)&h.es_part, sizeof(ulonglong4) * 8 * (size_t)h.n, "octant window sums");
                 h.alloc_epoch++;
             }
             if (h.es_wcap != es_wcap) {
@@ -287,8 +306,8 @@ void set_cells(cf_handle* H, const double L[3]) {
             }
         }
         if (!h.pos4f) {
-            cf::check_hip(hipMalloc(&h.pos4f, sizeof(float4) * h.n), "fp32 positions");
-            cf::check_hip(hipMalloc(&h.slot_of, sizeof(int) * h.n), "slot map");
+            zalloc((void**)&h.pos4f, sizeof(float4) * h.n, "fp32 positions");
+            zalloc((void**)&h.slot_of, sizeof(int) * h.n, "slot map");
             h.alloc_epoch++;
         }
     }
@@ -768,7 +787,7 @@ CF_EXPORT int cf_destroy(cf_handle* H) {
     if (!H) return CF_OK;
     return guarded([&] {
         (void)hipSetDevice(H->h.device);
-        (void)hipStreamSynchronize(H->h.stream);
+        (void)hipDeviceSynchronize();   // both streams' launches, and any graph still running
         graph_forget(H);
         for (void* p : H->allocs) (void)hipFree(p);
         for (auto& v : H->ev)
@@ -1085,8 +1104,11 @@ struct GraphCache {
     GraphKey key[SEG_COUNT];
     bool rec_split[SEG_COUNT] = {};   // Handle::rec_split as the captured launches leave it (restored on replay)
     int64_t captures = 0, replays = 0;
-    void drop(int s) {
-        if (exec[s]) (void)hipGraphExecDestroy(exec[s]);
+    void drop(int s) {   // (a replaced graph may still run: its launch arguments die with it)
+        if (exec[s]) {
+            (void)hipDeviceSynchronize();
+            (void)hipGraphExecDestroy(exec[s]);
+        }
         exec[s] = nullptr;
     }
 };

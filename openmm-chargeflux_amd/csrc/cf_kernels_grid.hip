@@ -1456,6 +1456,48 @@ __device__ __forceinline__ void interp_stage16(int3 ng, const double* __restrict
     }
 }
 
+// interp_stage16 with the work per thread fixed across x planes: thread t takes the z pair c and
+// the y row b of item t mod (R RC) and every second x plane from t / (R RC) (2 R RC <= threads);
+// its y / z wrap, grid row offset and LDS offset are computed once, each plane costs a row add, an
+// x wrap and the load (round 4's row-by-row form recomputed both wraps and both offsets per row:
+// 194 VALU per thread, a fifth of k_g_interp2's VALU instructions at C3)
+template <int W, int SX>
+__device__ __forceinline__ void interp_stage16p(int3 ng, const double* __restrict__ G, int tx, int ty, int tz,
+                                                double* __restrict__ sg) {
+    constexpr int R = 7 + W;
+    constexpr int RC = (R + 1) / 2;   // z pairs per row
+    constexpr int NIT = R * RC;       // (row, pair) items per plane
+    constexpr int NP = (R + 1) / 2;   // planes of parity 0 (parity 1: R / 2)
+    const int t = threadIdx.x;
+    if (t >= 2 * NIT) return;
+    const int par = t >= NIT ? 1 : 0, it = t - par * NIT;
+    const int b = it / RC, c = it - b * RC;
+    int y = 8 * ty + b, z = 8 * tz + 2 * c;
+    y -= y >= ng.y ? ng.y : 0;
+    z -= z >= ng.z ? ng.z : 0;
+    const int yz = y * ng.z + z, zy = ng.y * ng.z;
+    const int x0 = 8 * tx + par;
+    v2d gv[NP];
+#pragma unroll
+    for (int k = 0; k < NP; k++) {
+        if (k < NP - 1 || par + 2 * k < R) {
+            int x = x0 + 2 * k;
+            x -= x >= ng.x ? ng.x : 0;
+            const unsigned off = (unsigned)(x * zy + yz) * 8u;
+            gv[k] = *reinterpret_cast<const v2d*>(reinterpret_cast<const char*>(G) + off);
+        }
+    }
+    double* d = sg + par * SX + b * R + 2 * c;
+    const bool two = 2 * c + 1 < R;   // the odd R's last pair: one point past the row
+#pragma unroll
+    for (int k = 0; k < NP; k++) {
+        if (k < NP - 1 || par + 2 * k < R) {
+            d[2 * k * SX] = gv[k].x;
+            if (two) d[2 * k * SX + 1] = gv[k].y;
+        }
+    }
+}
+
 template <int W>
 __device__ __forceinline__ void interp_stage(int3 ng, const double* __restrict__ G, int tx, int ty, int tz,
                                              double* __restrict__ sg) {
@@ -1692,7 +1734,8 @@ __global__ void __launch_bounds__(kInterpThreads) CF_LDS_UNPAIRED k_g_interp2(in
     const int s0 = start[tile], s1 = start[tile + 1];
     if (s0 == s1) return;
     const int tz = tile % nb.z, ty = (tile / nb.z) % nb.y, tx = tile / (nb.z * nb.y);
-    interp_stage16<W, SX>(ng, G, tx, ty, tz, sg);
+    if constexpr (2 * R * ((R + 1) / 2) <= kInterpThreads) interp_stage16p<W, SX>(ng, G, tx, ty, tz, sg);
+    else interp_stage16<W, SX>(ng, G, tx, ty, tz, sg);
     __syncthreads();
     const int lane = threadIdx.x & 63, w = wave_id();
     const int h = lane >> 5, jg = (lane >> 4) & 1, k = lane & 15;

@@ -201,3 +201,42 @@ def test_graph_replay_restores_reciprocal_dedq_split():
     torch.cuda.synchronize()
     assert k.graph_stats()[1] >= 1
     assert np.array_equal(k.dedq(), dq_ref)
+
+
+@pytest.mark.parametrize("case", ["C2", "w4k"])
+def test_graph_two_stream_order_under_changing_flags(case):
+    """Fork / join order of the two-stream evaluation (event hand-overs) when graph segments are
+    replayed and re-captured in turn: positions move every call (a segment running on stale
+    charges, cells or lists would show in the bits), the flags alternate (forces + energy, energy
+    only, forces only: each a capture of its own) and some calls get fresh output buffers.  The
+    graph handle must give the eager handle's bits at every call, and with no skin the list must
+    be rebuilt at every evaluation (a direct chain that read the rebuild flag after the join
+    cleared it would skip its build)."""
+    if case == "C2":
+        system, force, pos, box = ts.make("C2")
+    else:
+        system, force, pos, box = ts.water_box(4000, cutoff=1.0, ewald_tol=1e-4, every_bond_angle=5)
+    stream = torch.cuda.current_stream().cuda_stream
+    mk = lambda: HipCalcCoulForceKernel(stream=stream, kspace_algo=2).initialize(system, force)
+    eager, graph = mk(), mk()
+    graph.set_graph(True)
+    pt = torch.tensor(pos, dtype=torch.float64, device="cuda")
+    rng = np.random.default_rng(12)
+    flag_cycle = [(True, True), (False, True), (True, True), (True, False), (True, True)]
+    f_keep = torch.zeros_like(pt)
+    n = 30
+    for s in range(n):
+        fl, en = flag_cycle[s % len(flag_cycle)]
+        out = []
+        for k in (eager, graph):
+            f = torch.zeros_like(pt) if s % 3 == 0 else f_keep.zero_().clone()
+            e = torch.zeros(1, dtype=torch.float64, device="cuda")
+            k.execute_device(pt, box, fl, en, f if fl else None, e if en else None)
+            torch.cuda.synchronize()
+            out.append((e.item(), f.cpu().numpy().copy()))
+        (ea, fa), (eb, fb) = out
+        assert ea == eb and np.array_equal(fa, fb), (s, fl, en)
+        pt += torch.tensor(rng.normal(scale=0.004, size=pos.shape), device="cuda")
+    assert eager.neighbor_stats() == graph.neighbor_stats() == (n, n), (eager.neighbor_stats(), graph.neighbor_stats())
+    caps, reps = graph.graph_stats()
+    assert reps > 0 and caps > 0, (caps, reps)
