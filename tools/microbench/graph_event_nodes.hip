@@ -120,5 +120,73 @@ int main() {
         }
         (void)hipEventDestroy(ev);
     }
+    // (d) as (c) with the graphs launched on the legacy null stream (a torch current stream of 0)
+    // after eager work on it, and the waits on a second non-blocking stream
+    {
+        hipEvent_t ev;
+        (void)hipEventCreateWithFlags(&ev, hipEventDisableTiming | hipEventDisableSystemFence);
+        hipLaunchKernelGGL(k_read, dim3(1), dim3(64), 0, 0, flag, seen);   // eager work on the null stream
+        for (int round = 0; round < 2; round++) {
+            hipGraph_t g = nullptr;
+            hipError_t eb = hipStreamBeginCapture(cap, hipStreamCaptureModeThreadLocal);
+            hipLaunchKernelGGL(k_spin, dim3(1), dim3(64), 0, cap, flag, 2000000L);
+            hipError_t er = hipEventRecordWithFlags(ev, cap, hipEventRecordExternal);
+            hipLaunchKernelGGL(k_read, dim3(1), dim3(64), 0, cap, flag, seen);
+            hipError_t ee = hipStreamEndCapture(cap, &g);
+            hipGraphExec_t x = nullptr;
+            hipError_t ei = (ee == hipSuccess && g) ? hipGraphInstantiate(&x, g, nullptr, nullptr, 0) : ee;
+            int ok = 0;
+            for (int rep = 0; rep < 4 && x; rep++) {
+                (void)hipGraphLaunch(x, 0);
+                (void)hipStreamWaitEvent(aux, ev, 0);
+                hipLaunchKernelGGL(k_read, dim3(1), dim3(64), 0, aux, flag, seen);
+                ok += hipStreamSynchronize(aux) == hipSuccess;
+            }
+            hipError_t es = hipDeviceSynchronize();
+            printf("[null-stream round %d] begin %s, record(External) %s, end %s, instantiate %s, replays ok %d/4, sync %s\n",
+                   round, name(eb), name(er), name(ee), name(ei), ok, name(es));
+            if (x) (void)hipGraphExecDestroy(x);
+            if (g) (void)hipGraphDestroy(g);
+        }
+        (void)hipEventDestroy(ev);
+    }
+    // (e) a captured graph as a child node, an event-record node after it, a second captured graph
+    // as a child node after the record (the explicit form of (c))
+    {
+        hipEvent_t ev;
+        (void)hipEventCreateWithFlags(&ev, hipEventDisableTiming | hipEventDisableSystemFence);
+        hipGraph_t ga = nullptr, gb = nullptr, g = nullptr;
+        (void)hipStreamBeginCapture(cap, hipStreamCaptureModeThreadLocal);
+        hipLaunchKernelGGL(k_spin, dim3(1), dim3(64), 0, cap, flag, 2000000L);
+        (void)hipStreamEndCapture(cap, &ga);
+        (void)hipStreamBeginCapture(cap, hipStreamCaptureModeThreadLocal);
+        hipLaunchKernelGGL(k_read, dim3(1), dim3(64), 0, cap, flag, seen);
+        (void)hipStreamEndCapture(cap, &gb);
+        hipError_t ec = hipGraphCreate(&g, 0);
+        hipGraphNode_t na = nullptr, nr = nullptr, nb = nullptr;
+        hipError_t e1 = hipGraphAddChildGraphNode(&na, g, nullptr, 0, ga);
+        hipError_t e2 = hipGraphAddEventRecordNode(&nr, g, &na, 1, ev);
+        hipError_t e3 = hipGraphAddChildGraphNode(&nb, g, &nr, 1, gb);
+        hipGraphExec_t x = nullptr;
+        hipError_t ei = hipGraphInstantiate(&x, g, nullptr, nullptr, 0);
+        int ok = 0;
+        for (int rep = 0; rep < 4 && x; rep++) {
+            (void)hipMemset(seen, -1, sizeof(int));
+            (void)hipMemset(flag, 0, sizeof(int));
+            (void)hipDeviceSynchronize();
+            (void)hipGraphLaunch(x, 0);
+            (void)hipStreamWaitEvent(aux, ev, 0);
+            hipLaunchKernelGGL(k_read, dim3(1), dim3(64), 0, aux, flag, seen);
+            (void)hipDeviceSynchronize();
+            int h = -1;
+            (void)hipMemcpy(&h, seen, sizeof(int), hipMemcpyDeviceToHost);
+            ok += h == 1;
+        }
+        printf("[child graphs + record node] create %s, child %s, record %s, child %s, instantiate %s, ordered %d/4\n",
+               name(ec), name(e1), name(e2), name(e3), name(ei), ok);
+        if (x) (void)hipGraphExecDestroy(x);
+        (void)hipGraphDestroy(g); (void)hipGraphDestroy(ga); (void)hipGraphDestroy(gb);
+        (void)hipEventDestroy(ev);
+    }
     return 0;
 }
