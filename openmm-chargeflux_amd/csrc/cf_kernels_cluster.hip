@@ -189,6 +189,10 @@ __global__ void __launch_bounds__(kClBuildThreads) k_cl_build(DirectArgs a, cons
         // exclusion e of atom il; an atom with more than 16 exclusions takes the slow loop below)
         int nex = 0;
         bool many = false;
+        // the sorted-slot range of the i atoms' excluded partners: a j cluster whose 4 slots lie
+        // outside it needs no exclusion pass (for molecules, every cluster but the few holding
+        // the i atoms' own molecule partners)
+        int exlo = INT_MAX, exhi = INT_MIN;
         {
             const int il = lane >> 4, e = lane & 15;
             int v = -1;
@@ -203,6 +207,14 @@ __global__ void __launch_bounds__(kClBuildThreads) k_cl_build(DirectArgs a, cons
             const int r = __popcll(has & ((1ull << lane) - 1ull));
             if (v >= 0) exs[wv][r] = v;
             nex = __popcll(has);
+            int mn = v >= 0 ? (v & 0xFFFFFF) : INT_MAX, mx = v >= 0 ? (v & 0xFFFFFF) : INT_MIN;
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) {
+                mn = min(mn, __shfl_xor(mn, o));
+                mx = max(mx, __shfl_xor(mx, o));
+            }
+            exlo = __builtin_amdgcn_readfirstlane(mn);
+            exhi = __builtin_amdgcn_readfirstlane(mx);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -231,8 +243,10 @@ __global__ void __launch_bounds__(kClBuildThreads) k_cl_build(DirectArgs a, cons
                 }
             }
             if (!__ballot(hit)) continue;
-            // exclusions of the i atoms (wave-uniform loop over their partners' sorted slots)
+            // exclusions of the i atoms (wave-uniform loop over their partners' sorted slots), for
+            // the batches with a hit whose slots can hold one of them
             const int jfirst = ent & kHalfSlotMask;
+            if (many || __ballot(hit && jfirst + kClSize > exlo && jfirst <= exhi)) {
             if (!many) {
                 for (int x = 0; x < nex; x++) {
                     const int v = exs[wv][x];
@@ -247,6 +261,7 @@ __global__ void __launch_bounds__(kClBuildThreads) k_cl_build(DirectArgs a, cons
                         if (hit && d >= 0 && d < kClSize) mask &= ~(1u << (4 * il + d));
                     }
                 }
+            }
             }
             hit = hit && mask != 0;
             const unsigned long long bal = __ballot(hit);

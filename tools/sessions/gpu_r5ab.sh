@@ -1,0 +1,26 @@
+#!/bin/bash
+# round 5, session ab: k_cl_build skips the exclusion pass for candidate batches whose slots cannot
+# hold an excluded partner of the i cluster (same list).  Expected: k_cl_build 52-55 -> ~30-35 us
+# per rebuild (alone, breakdown pass), rebuild steps -20 us, C3 step -3..-5 us.
+out=gpurun_out/r5ab
+mkdir -p $out
+R=$GRAFT_REPO_ROOT
+step() { local rc=$1 name=$2; echo "$name rc=$rc"; [ $rc -eq 0 ] || exit $rc; }
+timeout -k 10 400 python -u -m pytest tests/test_gpu_cluster.py tests/test_gpu_half.py tests/test_gpu_octant.py tests/test_gpu_configs.py -x -v --timeout 300 --timeout-method thread > $out/tests.log 2>&1; step $? tests
+grep -E "passed|failed" $out/tests.log | tail -1
+ARGS="--steps 40 --no-cpu-baseline --no-exact-compare"
+for i in 1 2 3; do
+  timeout -k 10 100 python -u bench.py $ARGS > $out/bench$i.json 2> $out/bench$i.err; step $? bench$i
+  python3 -c "
+import json; d = json.loads(open('$out/bench$i.json').read().strip().splitlines()[-1])
+print('c3', d['ms_per_step'], d.get('graph_replay_ms_per_step'), round(d['roofline']['avg_launch_ms'], 4), d['config'].get('nlist_builds_in_timed_steps'))"
+done
+(cd /tmp && export TMPDIR=/tmp && timeout -k 10 200 rocprofv3 --kernel-trace -d $R/$out/trace -o run --output-format csv -- python3 $R/bench.py --steps 40 --warmup 5 --no-cpu-baseline --no-exact-compare > $R/$out/trace.log 2>&1); step $? trace
+python3 - <<'PY'
+import csv, glob
+f = glob.glob("gpurun_out/r5ab/trace/**/*kernel_trace.csv", recursive=True)[0]
+ev = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]) for r in csv.DictReader(open(f)))
+d = [(e[1] - e[0]) / 1e3 for e in ev if "k_cl_build" in e[2]]
+print("k_cl_build, breakdown pass (alone):", [round(x, 1) for x in d[5:45] if x > 5])
+PY
+python3 tools/step_stats.py $out/trace 46 85 | tail -2
