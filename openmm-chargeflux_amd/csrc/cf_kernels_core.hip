@@ -206,9 +206,11 @@ __global__ void __launch_bounds__(256) k_cell_scatter(int n, const int* __restri
     tmp[cstart[key[i]] + rank[i]] = i;
 }
 
-// one wave per cell: final position of each member = cell start + number of members before it in
-// the cell order (members staged in LDS and read by broadcast); multi-rank: an owned member's list
-// row = the cell's first row + number of owned members before it.
+// one 256-thread block per cell: final position of each member = cell start + number of members
+// before it in the cell order (members staged in LDS and read by broadcast, each member's count on
+// one thread: ~0.7 members per thread at C3 instead of ~3 per lane with one wave per cell --
+// round 4's form took 25 us per rebuild at C3, a quarter of the waves on the chip); multi-rank: an
+// owned member's list row = the cell's first row + number of owned members before it.
 // Cell order (zcol = S > 0): the cell is cut into S x S columns along its a and b lattice
 // directions, members sorted by (column, fractional c coordinate, atom index), columns and the
 // direction along c in serpentine order -- so that runs of
@@ -225,14 +227,14 @@ __global__ void __launch_bounds__(256) k_cell_order(int ncell, const int* __rest
                                                     int zcol) {
     // one 64-bit key per member: (column << 58 | quantized c coordinate << 26 | atom index), or the
     // atom index alone -- the rank is then one unsigned compare per member pair
-    __shared__ unsigned long long memk[4][kOrderLds];
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int c = blockIdx.x * 4 + w;
-    if (c >= ncell || !*flag) return;
+    __shared__ unsigned long long memk[kOrderLds];
+    const int tid = threadIdx.x;
+    const int c = blockIdx.x;
+    if (c >= ncell || !*flag) return;   // block-uniform
     const int b = cstart[c], m = cend[c] - b;
     const int* src = tmp + b;
     if (m > kOrderLds) {   // rare (an over-full cell): atom order, read from global memory
-        for (int e = lane; e < m; e += 64) {
+        for (int e = tid; e < m; e += 256) {
             const int v = src[e];
             int r = 0, ro = 0;
             for (int j = 0; j < m; j++) {
@@ -246,7 +248,7 @@ __global__ void __launch_bounds__(256) k_cell_order(int ncell, const int* __rest
         return;
     }
     const int cc[3] = {c / (nc.y * nc.z), (c / nc.z) % nc.y, c % nc.z};
-    for (int e = lane; e < m; e += 64) {
+    for (int e = tid; e < m; e += 256) {
         const int v = src[e];
         unsigned long long key = (unsigned long long)v;
         if (zcol > 0) {
@@ -264,19 +266,17 @@ __global__ void __launch_bounds__(256) k_cell_order(int ncell, const int* __rest
             const unsigned zq = (unsigned)(((col & 1) ? 0.999999 - lc : lc) * 4294967296.0);
             key |= ((unsigned long long)col << 58) | ((unsigned long long)zq << 26);
         }
-        memk[w][e] = key;
+        memk[e] = key;
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    __syncthreads();
     const unsigned long long kIdx = zcol > 0 ? (1ull << 26) - 1 : ~0ull;   // (zcol > 0: n < 2^21, half lists)
-    for (int e = lane; e < m; e += 64) {
-        const unsigned long long kv = memk[w][e];
+    for (int e = tid; e < m; e += 256) {
+        const unsigned long long kv = memk[e];
         const int v = (int)(kv & kIdx);
         int r = 0, ro = 0;
         int j = 0;
         for (; j + 2 <= m; j += 2) {   // two keys per 16-B LDS read (broadcast: every lane reads the same j)
-            const ulonglong2 u2 = *reinterpret_cast<const ulonglong2*>(&memk[w][j]);
+            const ulonglong2 u2 = *reinterpret_cast<const ulonglong2*>(&memk[j]);
             r += (u2.x < kv) + (u2.y < kv);
             if (own_s) {
                 const int ux = (int)(u2.x & kIdx), uy = (int)(u2.y & kIdx);
@@ -284,7 +284,7 @@ __global__ void __launch_bounds__(256) k_cell_order(int ncell, const int* __rest
             }
         }
         if (j < m) {
-            const unsigned long long u = memk[w][j];
+            const unsigned long long u = memk[j];
             r += u < kv;
             if (own_s) ro += u < kv && (int)(u & kIdx) >= lo && (int)(u & kIdx) < hi;
         }
@@ -1695,7 +1695,7 @@ void launch_cell_sort(Handle& h, const double* pos) {
                        h.own_start);
     hipLaunchKernelGGL(k_cell_scatter, dim3(nblk(h.n, 256)), dim3(256), 0, h.stream, h.n, f, h.cell_key, h.atom_val,
                        h.cell_start, h.atom_tmp, ncell, h.cell_cnt, oc);
-    hipLaunchKernelGGL(k_cell_order, dim3(nblk(ncell, 4)), dim3(256), 0, h.stream, ncell, f, h.cell_start,
+    hipLaunchKernelGGL(k_cell_order, dim3(ncell), dim3(256), 0, h.stream, ncell, f, h.cell_start,
                        h.cell_end, h.atom_tmp, h.key_tmp, h.lo, h.hi, h.own_start, oc ? h.own_s : nullptr, pos, L, T,
                        nc, h.zcol);
     hipLaunchKernelGGL(k_cell_commit, dim3(nblk(h.n, 256)), dim3(256), 0, h.stream, h.n, f, h.cell_key, h.key_tmp,
