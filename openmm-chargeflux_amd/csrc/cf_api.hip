@@ -277,7 +277,9 @@ void set_cells(cf_handle* H, const double L[3]) {
             zalloc((void**)&h.cl_start, sizeof(int) * h.cl_cells, "cluster table");
             zalloc((void**)&h.cl_info, sizeof(int2) * h.ncl_cap, "cluster table");
             zalloc((void**)&h.cl_bb, sizeof(float4) * 2 * h.ncl_cap, "cluster table");
-            zalloc((void**)&h.cpl, sizeof(uint2) * (size_t)h.ncl_cap * (h.es ? 1 : h.cpl_cap), "cluster-pair list");
+            // (+ 64 entries: k_pairs_cq reads up to three batches of 16 past an i-cluster's count and
+            // clears the ones beyond it)
+            zalloc((void**)&h.cpl, sizeof(uint2) * ((size_t)h.ncl_cap * (h.es ? 1 : h.cpl_cap) + 64), "cluster-pair list");
             zalloc((void**)&h.cpl_cnt, sizeof(int) * h.ncl_cap, "cluster-pair list");
             h.alloc_epoch++;
         }
@@ -306,7 +308,9 @@ void set_cells(cf_handle* H, const double L[3]) {
             }
         }
         if (!h.pos4f) {
-            zalloc((void**)&h.pos4f, sizeof(float4) * h.n, "fp32 positions");
+            // (+ a cluster's width, zeroed: k_pairs_cq loads all 4 slots of a listed j-cluster, a partial
+            // last cluster included)
+            zalloc((void**)&h.pos4f, sizeof(float4) * (h.n + 4), "fp32 positions");
             zalloc((void**)&h.slot_of, sizeof(int) * h.n, "slot map");
             h.alloc_epoch++;
         }

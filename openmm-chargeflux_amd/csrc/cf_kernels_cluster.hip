@@ -352,7 +352,8 @@ __global__ void __launch_bounds__(kCqThreads) CF_LDS_UNPAIRED k_pairs_cq(DirectA
     const int jl = lane & 3, el = lane >> 2;           // phase A: entry el of the batch, j atom jl
     int* const qw = qbuf[wv][il];
     const int c0 = a.cl_start[cell], ncl = a.cl_start[cell + 1] - c0;
-    auto ring = [](int x) { return x >= kCqQ ? x - kCqQ : x; };   // x < 2 kCqQ
+    // x < 2 kCqQ -> x mod kCqQ (x - kCqQ underflows to a larger unsigned when x < kCqQ)
+    auto ring = [](int x) { return (int)min((unsigned)x, (unsigned)x - (unsigned)kCqQ); };
     for (;;) {
         int ci = 0;
         if (lane == 0) ci = atomicAdd(&next_ci, 1);
@@ -512,11 +513,15 @@ __global__ void __launch_bounds__(kCqThreads) CF_LDS_UNPAIRED k_pairs_cq(DirectA
         // phase A: a batch of 16 entries = 64 j atoms, one per lane (entry el, atom jl), each tested
         // against the 4 i atoms; the next batch's entries and positions are loaded while this
         // one is tested and its hits queued
-        auto entry = [&](int s) { return s + el < ne ? lst[s + el] : make_uint2(0u, 0u); };
-        auto jpos = [&](uint2 en) {
-            const bool on = (en.y >> jl) & 0x1111u;   // any i atom pairs with this j atom
-            return a.pos4f[on ? (int)(en.x & kHalfSlotMask) + jl : inf.x];
+        // (an entry past the count -- the next i-cluster's, or the allocation's padding -- is read
+        // and its pair mask cleared; every slot of a j-cluster is loaded, the mask decides: pos4f is
+        // padded by a cluster's width)
+        auto entry = [&](int s) {
+            uint2 en = lst[s + el];
+            en.y = s + el < ne ? en.y : 0u;
+            return en;
         };
+        auto jpos = [&](uint2 en) { return a.pos4f[(en.x & kHalfSlotMask) + jl]; };
         uint2 en_c = entry(0);
         float4 pj_c = jpos(en_c);
         uint2 en_n = entry(kCqBatch);
@@ -538,21 +543,34 @@ __global__ void __launch_bounds__(kCqThreads) CF_LDS_UNPAIRED k_pairs_cq(DirectA
                 const v2f r2 = dx * dx + dy * dy + dz * dz;
                 // two ballots ANDed on the scalar unit (a ballot of `listed && in range` was
                 // compiled as compare, s_and, select, compare: two VALU instructions more per atom)
-                m[k] = __ballot(r2.x <= a.rcm2f) & __ballot((bits >> (4 * k)) & 1u);
-                m[k + 1] = __ballot(r2.y <= a.rcm2f) & __ballot((bits >> (4 * k + 4)) & 1u);
+                const bool in0 = r2.x <= a.rcm2f, in1 = r2.y <= a.rcm2f;
+                const bool ls0 = (bits >> (4 * k)) & 1u, ls1 = (bits >> (4 * k + 4)) & 1u;
+                m[k] = __builtin_amdgcn_ballot_w64(in0) & __builtin_amdgcn_ballot_w64(ls0);
+                m[k + 1] = __builtin_amdgcn_ballot_w64(in1) & __builtin_amdgcn_ballot_w64(ls1);
                 cnt[k] = __popcll(m[k]);
                 cnt[k + 1] = __popcll(m[k + 1]);
             }
             // room for this batch's hits, then queue them
-            while (q0 + cnt[0] > kCqQ || q1 + cnt[1] > kCqQ || q2 + cnt[2] > kCqQ || q3 + cnt[3] > kCqQ) phase_b();
+            // any q_k + cnt_k > kCqQ, the four as bytes of one word (sums <= kCqQ + 64 + 127 - kCqQ < 256:
+            // no carry between bytes; a byte reaches 128 exactly when its sum exceeds kCqQ) -- scalar ops
+            const unsigned cpack = (unsigned)cnt[0] | ((unsigned)cnt[1] << 8) | ((unsigned)cnt[2] << 16) | ((unsigned)cnt[3] << 24);
+            auto no_room = [&]() {
+                const unsigned qp = (unsigned)q0 | ((unsigned)q1 << 8) | ((unsigned)q2 << 16) | ((unsigned)q3 << 24);
+                return ((qp + cpack + (127u - kCqQ) * 0x01010101u) & 0x80808080u) != 0u;
+            };
+            if (__builtin_expect(no_room(), 0)) {
+                do phase_b(); while (no_room());
+            }
             const int word = (int)((en_c.x & kHalfSlotMask) + jl) | (wc << kHalfSlotBits) |
                              (__float_as_int(pj_c.w) << kShiftBits);
             const int qs[4] = {q0, q1, q2, q3};
 #pragma unroll
             for (int k = 0; k < 4; k++) {
-                if ((m[k] >> lane) & 1ull) {
-                    const int r = __builtin_amdgcn_mbcnt_hi((unsigned)(m[k] >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m[k], 0u));
-                    qbuf[wv][k][ring(qh + qs[k] + r)] = word;
+                if (__builtin_amdgcn_inverse_ballot_w64(m[k])) {   // this lane's bit of m[k]: the mask as exec
+                    // ring position qh + q_k + (hits below this lane): mbcnt adds the base
+                    const unsigned x = __builtin_amdgcn_mbcnt_hi((unsigned)(m[k] >> 32),
+                                                                 __builtin_amdgcn_mbcnt_lo((unsigned)m[k], (unsigned)(qh + qs[k])));
+                    qbuf[wv][k][ring((int)x)] = word;
                 }
             }
             q0 += cnt[0]; q1 += cnt[1]; q2 += cnt[2]; q3 += cnt[3];
