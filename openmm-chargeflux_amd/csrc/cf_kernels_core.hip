@@ -1499,16 +1499,23 @@ __global__ void __launch_bounds__(kNopbcTile) k_nopbc(int n, int lo, int hi, int
 // ---------------------------------------------------------------------------------
 constexpr int kEChunk = 256;
 
-__device__ __forceinline__ void block_sum3(double& a0, double& a1, double& a2, double (*red)[256]) {
-    red[0][threadIdx.x] = a0; red[1][threadIdx.x] = a1; red[2][threadIdx.x] = a2;
-    __syncthreads();
-    for (int w = 128; w > 0; w >>= 1) {
-        if (threadIdx.x < w)
+// block sums of four values, the same fixed order in every block (deterministic): a butterfly
+// within each wave (shfl_xor), then the four waves' sums added in wave order by every thread --
+// one barrier instead of the eight of an LDS tree (round 5: the last block's final sums sit on
+// the step's exposed tail)
+__device__ __forceinline__ void block_sum4(double& a0, double& a1, double& a2, double& a3, double (*red)[4]) {
+    static_assert(kEChunk == 256, "four waves");
 #pragma unroll
-            for (int c = 0; c < 3; c++) red[c][threadIdx.x] += red[c][threadIdx.x + w];
-        __syncthreads();
+    for (int m = 32; m >= 1; m >>= 1) {
+        a0 += __shfl_xor(a0, m); a1 += __shfl_xor(a1, m); a2 += __shfl_xor(a2, m); a3 += __shfl_xor(a3, m);
     }
-    a0 = red[0][0]; a1 = red[1][0]; a2 = red[2][0];
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) { red[w][0] = a0; red[w][1] = a1; red[w][2] = a2; red[w][3] = a3; }
+    __syncthreads();
+    a0 = (red[0][0] + red[1][0]) + (red[2][0] + red[3][0]);
+    a1 = (red[0][1] + red[1][1]) + (red[2][1] + red[3][1]);
+    a2 = (red[0][2] + red[1][2]) + (red[2][2] + red[3][2]);
+    a3 = (red[0][3] + red[1][3]) + (red[2][3] + red[3][3]);
 }
 
 __global__ void __launch_bounds__(kEChunk) k_assemble_energy(int lo, int hi, const int* __restrict__ cs,
@@ -1524,7 +1531,7 @@ __global__ void __launch_bounds__(kEChunk) k_assemble_energy(int lo, int hi, con
                                                              int* __restrict__ flag, int* __restrict__ xrange,
                                                              int* __restrict__ half_flag,
                                                              long long* __restrict__ fallback, int per) {
-    __shared__ double red[3][256];
+    __shared__ double red[4][4];
     double a0 = 0, a1 = 0, a2 = 0;
     // `per` chunks of kEChunk atoms per block at large N: fewer partials and fewer increments
     // of the one ticket address (as k_g_bin); each thread's energies are summed in chunk order
@@ -1573,7 +1580,8 @@ __global__ void __launch_bounds__(kEChunk) k_assemble_energy(int lo, int hi, con
         a0 += e_atom[3 * b]; a1 += e_atom[3 * b + 1]; a2 += e_atom[3 * b + 2];
     }
     }
-    block_sum3(a0, a1, a2, red);
+    double unused = 0;
+    block_sum4(a0, a1, a2, unused, red);
     if (threadIdx.x == 0) {   // agent-scope stores, read back by the last block (last_block_done)
         st_agent(part + 3 * blockIdx.x, a0); st_agent(part + 3 * blockIdx.x + 1, a1); st_agent(part + 3 * blockIdx.x + 2, a2);
     }
@@ -1585,13 +1593,10 @@ __global__ void __launch_bounds__(kEChunk) k_assemble_energy(int lo, int hi, con
     }
     double r = 0;
     for (int k = threadIdx.x; k < nrec; k += 256) r += e_rec_part[k];
-    __syncthreads();
-    block_sum3(a0, a1, a2, red);
-    __syncthreads();
-    double z0 = r, z1 = 0, z2 = 0;
-    block_sum3(z0, z1, z2, red);
+    __syncthreads();   // (red is reused)
+    block_sum4(a0, a1, a2, r, red);
     if (threadIdx.x == 0) {
-        const double t0 = a0, t1 = z0, t2 = a1, t3 = a2;
+        const double t0 = a0, t1 = r, t2 = a1, t3 = a2;
         terms[0] = t0; terms[1] = t1; terms[2] = t2; terms[3] = t3;
         const double e = pbc ? (t0 + t1 + t2 + t3) : t2;
         *energy_int = e;
