@@ -213,10 +213,11 @@ def main():
     ap.add_argument("--dt", type=float, default=0.001, help="ps")
     ap.add_argument("--neighbor-skin", type=float, default=None,
                     help="nm; persistent list rebuilt when an atom moved > skin/2 (0 = every step); default "
-                         "0.15 (C2, C3) or 0.2 (C5), the optima of profiles/r02_skin_sweep_m.txt")
+                         "0.125 (C3), 0.15 (C2) or 0.2 (C5): the optima of the cluster-pair list's re-sweep, "
+                         "profiles/r05an_skin_resweep.txt (round 2's per-atom lists: r02_skin_sweep_m.txt)")
     args = ap.parse_args()
     if args.neighbor_skin is None:
-        args.neighbor_skin = 0.2 if args.config == "C5" else 0.15
+        args.neighbor_skin = {"C5": 0.2, "C3": 0.125}.get(args.config, 0.15)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
