@@ -128,7 +128,7 @@ def cpu_baseline(force, pos, box, k_sample):
 # launches: their bytes are summed).  The pair kernel follows the list kind (cf_get_pair_list).
 PMC_KERNEL = {"kspace_force": ["cf::k_force<"], "kspace_sfac": ["cf::k_sfac<"],
               "grid_spread": ["cf::k_g_spread_mfma<"], "grid_interp": ["cf::k_g_interp2<"]}
-PAIR_KERNEL = {"octant": "cf::k_pairs_es<", "cluster": "cf::k_pairs_cq<", "atom_half": "cf::k_pairs_half<", "full": "cf::k_pairs<"}
+PAIR_KERNEL = {"cluster": "cf::k_pairs_cq<", "atom_half": "cf::k_pairs_half<", "full": "cf::k_pairs<"}
 
 
 def pair_count(force, pos, box):
@@ -204,7 +204,7 @@ def main():
     ap.add_argument("--graph", type=int, default=0,
                     help="1: replay each step's CoulForce launches as a captured hipGraph (cf_set_graph) in the "
                          "timed region")
-    ap.add_argument("--pair-list", default="auto", choices=["auto", "octant", "cluster", "atom_half", "full"],
+    ap.add_argument("--pair-list", default="auto", choices=["auto", "cluster", "atom_half", "full"],
                     help="direct-space list (cf_options.pair_list; auto: the 18-cell cluster-pair list on one fp64 rank)")
     ap.add_argument("--handover", default="event", choices=["event", "memory"],
                     help="fork / join of the library's second stream (cf_options.handover; memory: opt-in)")

@@ -27,7 +27,8 @@ extern "C" {
 #define CF_EXPORT __attribute__((visibility("default")))
 #endif
 
-#define CF_API_VERSION 3   /* 2: cf_params.one_4pi_eps0; 3: cf_options.handover, pair_list, variants, list_capacity */
+#define CF_API_VERSION 4   /* 2: cf_params.one_4pi_eps0; 3: cf_options.handover, pair_list, variants, list_capacity;
+                              4: device index guards (cf_get_device_errors), cf_compute_openmm, octant list removed */
 
 /* Error codes (negative).  cf_last_error() returns the message of the last failure
  * on the calling thread.  Mirrors the reference's OpenMMException paths. */
@@ -109,10 +110,8 @@ typedef struct cf_options {
                             CF_PAIR_LIST_CLUSTER (1): the cluster-pair half list wherever its cell window
                               fits (also mixed precision, and several ranks with an ownership filter);
                             CF_PAIR_LIST_ATOM_HALF (2): the per-atom half list on one rank (full on several);
-                            CF_PAIR_LIST_FULL (3): the per-atom full (two-sided) list;
-                            CF_PAIR_LIST_OCTANT (4): the octant (eighth-shell) cluster-pair list on one
-                              rank (fp64 or mixed): an 8-cell window per block, both sides of every pair
-                              in fixed point.
+                            CF_PAIR_LIST_FULL (3): the per-atom full (two-sided) list.
+                            (API 3's CF_PAIR_LIST_OCTANT (4) was removed in API 4: CF_ERR_INVALID.)
                             Same pair set and the same results up to the fp64 summation order. */
     int32_t variants;    /* CF_VARIANT_* bits: alternative kernels of the same sums, kept for A/B
                             verification (0 = the production kernels) */
@@ -131,7 +130,6 @@ typedef struct cf_options {
 #define CF_PAIR_LIST_CLUSTER 1
 #define CF_PAIR_LIST_ATOM_HALF 2
 #define CF_PAIR_LIST_FULL 3
-#define CF_PAIR_LIST_OCTANT 4
 
 /* cf_options.variants (grid k-space; each equal to the production kernel to <= 1e-12 relative) */
 #define CF_VARIANT_GEMM_DFT 1        /* the DFT stages as fp64-MFMA complex GEMMs (k_g_cgemm), not the
@@ -186,7 +184,9 @@ CF_EXPORT int cf_set_neighbor_skin(cf_handle* h, double skin);
 CF_EXPORT int cf_update_parameters(cf_handle* h, const cf_params* params);
 /* The direct-space list the handle evaluates with (cf_options.pair_list resolved for this system and
  * box: CF_PAIR_LIST_CLUSTER, CF_PAIR_LIST_ATOM_HALF or CF_PAIR_LIST_FULL; CF_PAIR_LIST_AUTO before the
- * first periodic evaluation and without periodic boundaries). */
+ * first periodic evaluation and without periodic boundaries).  A cluster or per-atom half list that
+ * does not fit the box (fewer than 4 cells per axis, an 18-cell window over 4096 atoms at the
+ * density of the box, several ranks without CF_PAIR_LIST_CLUSTER) resolves to CF_PAIR_LIST_FULL. */
 CF_EXPORT int cf_get_pair_list(const cf_handle* h, int32_t* kind);
 /* Number of neighbour-list builds and evaluations since cf_create. */
 CF_EXPORT int cf_get_neighbor_stats(const cf_handle* h, int64_t* builds, int64_t* evaluations);
@@ -201,6 +201,23 @@ CF_EXPORT int cf_get_neighbor_stats(const cf_handle* h, int64_t* builds, int64_t
 #define CF_FALLBACK_FIXED_POINT 4   /* a partner-side term beyond the fixed-point range (|F| >= 2^16) */
 CF_EXPORT int cf_get_fallback_stats(const cf_handle* h, int64_t* half_list_fallbacks, int64_t* rows_rescanned,
                                     int32_t* reasons);
+
+/* Device index guards.  The kernels check the data-dependent indices they are about to address
+ * (cell and grid-bin bounds, the cluster table, list entries) against the buffers they index;
+ * an index outside its buffer -- impossible by construction, so a bug or corrupted device
+ * memory -- skips the access and sets a CF_GUARD_* bit instead of faulting the GPU.  The bit is
+ * copied to host-mapped memory at the end of the evaluation, and every later entry point of the
+ * handle (cf_compute*, cf_synchronize, cf_get_charges / _dedq / _energy_terms; cf_compute_host in
+ * the same call) then returns CF_ERR_STATE naming the guard.  Sticky: re-create the handle.
+ * cf_get_device_errors synchronises the handle's streams and returns the bits (0 = none). */
+#define CF_GUARD_CELL_BOUNDS 1
+#define CF_GUARD_CLUSTER_TABLE 2
+#define CF_GUARD_LIST_ENTRY 4
+#define CF_GUARD_GRID_BINS 8
+#define CF_GUARD_NEIGHBOR 16
+#define CF_GUARD_ATOM_INDEX 32   /* cf_compute_openmm: an atom_index entry outside [0, N) */
+#define CF_GUARD_REBUILD_FLAG 64 /* the neighbour-list rebuild flag found clear on a handle without a skin */
+CF_EXPORT int cf_get_device_errors(cf_handle* h, int32_t* bits);
 
 /*
  * Replaces ReferenceCalcCoulForceKernel::execute (ReferenceCoulKernels.cpp:424-636).
@@ -218,6 +235,36 @@ CF_EXPORT int cf_get_fallback_stats(const cf_handle* h, int64_t* half_list_fallb
  */
 CF_EXPORT int cf_compute(cf_handle* h, const double* pos_dev, const double* box9, int flags,
                          double* forces_dev, double* energy_dev);
+
+/*
+ * The same evaluation on an OpenMM GPU platform's own device buffers, without copies -- the
+ * conventions the reference's CUDA platform binds its kernels to (CudaCalcCoulForceKernel::execute,
+ * platforms/cuda/src/CudaCoulKernels.cpp:523-600: cu.getPosq(), cu.getAtomIndexArray(),
+ * cu.getForce(), cu.getEnergyBuffer(), cu.getPaddedNumAtoms()).  Single rank only.
+ *   posq        [N] real4 in the platform's sorted order: posq[s] = (x, y, z, w) of atom
+ *               atom_index[s] (nm; w -- the platform's charge slot -- is never read or written).
+ *               posq_kind: CF_POSQ_DOUBLE4 (double precision: double4) or CF_POSQ_FLOAT4
+ *               (single / mixed precision: float4; posq_correction, if not NULL, is the mixed
+ *               platform's float4 posqCorrection, added in fp64)
+ *   atom_index  [N] int32 DEVICE array: sorted slot -> atom index (cu.getAtomIndexArray())
+ *   padded_n    paddedNumAtoms: the stride of the force planes (>= N)
+ *   force_buf   [3 * padded_n] long long DEVICE array, fixed point in units of 2^-32 kJ/mol/nm, the
+ *               x, y, z planes one after the other, indexed by sorted slot: forces are ADDED
+ *               (OpenMM's conversion (long long)(f * 2^32), 64-bit atomic adds).  NULL: no forces.
+ *   energy_buf  DEVICE address of one energy-buffer element (cu.getEnergyBuffer()): the energy
+ *               is ADDED to it; energy_kind CF_ENERGY_DOUBLE (mixed / double: `mixed` = double)
+ *               or CF_ENERGY_FLOAT (single).  NULL: not written.
+ * Energy semantics and flags as cf_compute.  The positions are gathered into the handle's atom
+ * order and the forces scattered back by two small kernels on the handle's stream (~2 x 3 us at
+ * C3); everything between is cf_compute's device-resident path (graph replay included).
+ */
+#define CF_POSQ_DOUBLE4 0
+#define CF_POSQ_FLOAT4 1
+#define CF_ENERGY_DOUBLE 0
+#define CF_ENERGY_FLOAT 1
+CF_EXPORT int cf_compute_openmm(cf_handle* h, const void* posq, const void* posq_correction, int32_t posq_kind,
+                                const int32_t* atom_index, int32_t padded_n, const double* box9, int flags,
+                                long long* force_buf, void* energy_buf, int32_t energy_kind);
 
 /* Split-phase form for multi-GPU: begin computes charges and this rank's partial
  * structure factors; the caller all-reduces (sum) the buffer returned by

@@ -32,6 +32,7 @@ static const char* kPhaseNames[PH_COUNT] = {"flux_terms", "atoms_prep", "cell_so
 constexpr int kMaxTimed = 8192;
 
 static void graph_forget(cf_handle* H);   // hipGraph replay cache (cf_set_graph), below
+static void graph_invalidate(cf_handle* H);
 struct GraphCache;
 static GraphCache* graph_active(cf_handle* H);
 
@@ -45,6 +46,9 @@ struct cf_handle {
     double* pos_host_dev = nullptr;   // cf_compute_host staging
     double* frc_host_dev = nullptr;
     double* ene_host_dev = nullptr;
+    double* om_pos = nullptr;         // cf_compute_openmm: atom-order fp64 positions, forces, energy
+    double* om_frc = nullptr;
+    double* om_ene = nullptr;
     double default_box[9] = {};
     const double* pos_pending = nullptr;
     double box9_last[9] = {};   // box of the begun evaluation (graph key of its end segment)
@@ -52,6 +56,7 @@ struct cf_handle {
     // parameters, not which atoms the flux terms and exclusions connect)
     std::vector<int4> topo_terms;
     std::vector<int> topo_ex_start, topo_ex_list;
+    GraphCache* graph = nullptr;   // cf_set_graph (owned; freed by graph_forget)
 };
 
 namespace {
@@ -98,12 +103,19 @@ void zalloc(T** p, size_t count, const char* what) {
     zalloc(reinterpret_cast<void**>(p), std::max<size_t>(count, 1) * sizeof(T), what);
 }
 
-// Buffers are freed only once the device is idle: evaluations are asynchronous (the caller
-// need not synchronize between steps) and the second stream's launches of the previous
-// evaluation may still read a list that a box change reallocates
-void free_idle(void* p) {
+// The handle's launches have drained: both of its streams (a replayed graph runs on one of them).
+// Not hipDeviceSynchronize: that would also wait for the caller's other streams (torch, RCCL).
+void drain_handle(const cf::Handle& h) {
+    (void)hipStreamSynchronize(h.stream);
+    if (h.aux) (void)hipStreamSynchronize(h.aux);
+}
+
+// Buffers are freed only once the handle's launches have drained: evaluations are asynchronous
+// (the caller need not synchronize between steps) and the second stream's launches of the
+// previous evaluation may still read a list that a box change reallocates
+void free_idle(const cf::Handle& h, void* p) {
     if (!p) return;
-    (void)hipDeviceSynchronize();
+    drain_handle(h);
     (void)hipFree(p);
 }
 
@@ -127,7 +139,15 @@ void dfree(cf_handle* H, void* p) {
     if (!p) return;
     auto it = std::find(H->allocs.begin(), H->allocs.end(), p);
     if (it != H->allocs.end()) H->allocs.erase(it);
-    free_idle(p);
+    free_idle(H->h, p);
+}
+
+// a buffer that captured launches point to was reallocated: the graphs are dropped now (the key's
+// alloc_epoch would re-capture them anyway; dropping them here means no exec holding a freed
+// address survives the reallocation)
+void bump_epoch(cf_handle* H) {
+    H->h.alloc_epoch++;
+    graph_invalidate(H);
 }
 
 // neighbour-list capacity: the mean count within rc + skin at the default-box density,
@@ -150,7 +170,7 @@ void alloc_nlist(cf_handle* H, double skin) {
     h.nl = nullptr;
     h.nb_cap = cap;
     h.nl = dalloc<int>(H, (size_t)4 * h.nb_cap * rows);
-    h.alloc_epoch++;
+    bump_epoch(H);
     if (!h.nl_cnt) h.nl_cnt = dalloc<int>(H, (size_t)4 * rows);
 }
 
@@ -203,10 +223,12 @@ void set_cells(cf_handle* H, const double L[3]) {
     }
     int64_t ncell = (int64_t)nc[0] * nc[1] * nc[2];
     if (ncell > h.ncell_alloc) {
-        // grow (not graph-capture safe; only happens when the box grows past the initial grid)
-        h.alloc_epoch++;
-        if (h.cell_start) { free_idle(h.cell_start); free_idle(h.cell_end); free_idle(h.cell_cnt); }
-        if (h.own_cnt) { free_idle(h.own_cnt); free_idle(h.own_start); h.own_cnt = h.own_start = nullptr; }
+        // grow (when the box grows past the initial grid).  Host side of an evaluation only, never
+        // inside a capture (host_prologue runs before run_segment); graphs that point to the old
+        // arrays are dropped (bump_epoch)
+        bump_epoch(H);
+        if (h.cell_start) { free_idle(h, h.cell_start); free_idle(h, h.cell_end); free_idle(h, h.cell_cnt); }
+        if (h.own_cnt) { free_idle(h, h.own_cnt); free_idle(h, h.own_start); h.own_cnt = h.own_start = nullptr; }
         zalloc((void**)&h.cell_start, sizeof(int) * ncell, "cells");
         zalloc((void**)&h.cell_end, sizeof(int) * ncell, "cells");
         zalloc((void**)&h.cell_cnt, sizeof(int) * ncell, "cells");   // zero; re-zeroed by each build
@@ -228,21 +250,16 @@ void set_cells(cf_handle* H, const double L[3]) {
     // 0.336 / 0.304 against 0.255 / 0.197 ms rank-0 (profiles/r04ag_*): a thin slab's cells and
     // their window neighbours run whole 1024-thread blocks with the 128-KB window for few owned atoms
     const double per_cell = (double)h.n / (double)ncell;
-    // octant list (cf_kernels_es.hip): one rank, an 8-cell window that two 512-thread
-    // blocks per CU hold in LDS (water density: 1 500 atoms, cap ~1 900)
-    const int es_wcap = ((2 * 40960 - cf::es_static_lds_bytes(h.mixed, true) - 256) / 32) & ~15;
-    const bool want_es = h.world == 1 && h.pair_list == CF_PAIR_LIST_OCTANT &&
-                         per_cell * 8.0 * 1.15 <= es_wcap;
-    const bool want_cluster = want_es || h.pair_list == CF_PAIR_LIST_CLUSTER || h.pair_list == CF_PAIR_LIST_AUTO;
+    const bool want_cluster = h.pair_list == CF_PAIR_LIST_CLUSTER || h.pair_list == CF_PAIR_LIST_AUTO;
     h.half = h.pair_list != CF_PAIR_LIST_FULL && h.pbc &&
              (h.world == 1 || (want_cluster && h.pair_list == CF_PAIR_LIST_CLUSTER)) && nc[0] >= 4 &&
              nc[1] >= 4 && nc[2] >= 4 && per_cell * 18.0 * 1.15 <= 4096.0 && h.n < (1 << 21);
     if (h.half && ncell > h.win_cells) {
-        if (h.win_out) { free_idle(h.win_out); free_idle(h.win_woff); }
+        if (h.win_out) { free_idle(h, h.win_out); free_idle(h, h.win_woff); }
         zalloc((void**)&h.win_out, sizeof(unsigned long long) * 4 * 4096 * (size_t)ncell, "half-list windows");
         zalloc((void**)&h.win_woff, sizeof(int) * 18 * (size_t)ncell, "half-list windows");
         h.win_cells = (int)ncell;
-        h.alloc_epoch++;
+        bump_epoch(H);
     }
     // cluster-pair half list (cf_kernels_cluster.hip): one rank, fp64 and mixed,
     // wherever the per-atom half list applies.  In mixed precision its pair kernel is slower than
@@ -251,7 +268,6 @@ void set_cells(cf_handle* H, const double L[3]) {
     // skin-gated builder and the k_pairs_cq rework, the other way round: 2.878 vs 2.775).
     // CF_PAIR_LIST_ATOM_HALF keeps the per-atom list
     h.cluster = h.half && want_cluster;
-    h.es = h.cluster && want_es;
     h.zcol = 0;
     if (h.cluster) {
         // within-cell z-columns of ~12 atoms (k_cell_order): clusters of 4 consecutive slots stay compact
@@ -266,11 +282,10 @@ void set_cells(cf_handle* H, const double L[3]) {
         const double rl = h.cutoff + h.list_skin + ext;
         const double est = 0.5 * 4.0 / 3.0 * M_PI * rl * rl * rl * rho / 4.0 + 8.0;
         int cap = std::min(1536, ((int)(2.2 * est) + 64 + 15) / 16 * 16);
-        if (h.es) cap = 384;   // the octant builder's row stage (k_es_build); the pool is per block
         if (h.list_capacity > 0) cap = std::max(4, std::min(cap, h.list_capacity));   // cf_options.list_capacity
         if (need > h.ncl_cap || cap != h.cpl_cap || ncell + 1 > h.cl_cells) {
-            if (h.cl_start) { free_idle(h.cl_start); free_idle(h.cl_info); free_idle(h.cl_bb);
-                              free_idle(h.cpl); free_idle(h.cpl_cnt); }
+            if (h.cl_start) { free_idle(h, h.cl_start); free_idle(h, h.cl_info); free_idle(h, h.cl_bb);
+                              free_idle(h, h.cpl); free_idle(h, h.cpl_cnt); }
             h.ncl_cap = std::max(need, h.ncl_cap);
             h.cpl_cap = cap;
             h.cl_cells = std::max((int)ncell + 1, h.cl_cells);
@@ -279,40 +294,16 @@ void set_cells(cf_handle* H, const double L[3]) {
             zalloc((void**)&h.cl_bb, sizeof(float4) * 2 * h.ncl_cap, "cluster table");
             // (+ 64 entries: k_pairs_cq reads up to three batches of 16 past an i-cluster's count and
             // clears the ones beyond it)
-            zalloc((void**)&h.cpl, sizeof(uint2) * ((size_t)h.ncl_cap * (h.es ? 1 : h.cpl_cap) + 64), "cluster-pair list");
+            zalloc((void**)&h.cpl, sizeof(uint2) * ((size_t)h.ncl_cap * h.cpl_cap + 64), "cluster-pair list");
             zalloc((void**)&h.cpl_cnt, sizeof(int) * h.ncl_cap, "cluster-pair list");
-            h.alloc_epoch++;
-        }
-        if (h.es) {
-            // rows: the clusters of 4 octant cells; pool: the block's entries, ~89 % of its cell's
-            // clusters' half-space partners plus the short cross-pair rows, x1.6 + 256
-            const int rows_max = std::min(1024, (int)(4.0 * std::ceil(per_cell / 4.0) * 1.6) + 64);
-            const int pool_cap = (int)(1.6 * 1.15 * (per_cell / 4.0) * est) + 256;
-            if (ncell > h.es_cells || rows_max > h.es_rows_max || pool_cap > h.es_pool_cap) {
-                if (h.es_row) { free_idle(h.es_row); free_idle(h.es_pool); free_idle(h.e_blk); }
-                h.es_cells = std::max((int)ncell, h.es_cells);
-                h.es_rows_max = std::max(rows_max, h.es_rows_max);
-                h.es_pool_cap = std::max(pool_cap, h.es_pool_cap);
-                zalloc((void**)&h.es_row, sizeof(int2) * (size_t)h.es_cells * h.es_rows_max, "octant list");
-                zalloc((void**)&h.es_pool, sizeof(uint2) * (size_t)h.es_cells * h.es_pool_cap, "octant list");
-                zalloc((void**)&h.e_blk, sizeof(double) * (size_t)h.es_cells, "octant list");
-                h.alloc_epoch++;
-            }
-            if (!h.es_part) {
-                zalloc((void**)&h.es_part, sizeof(ulonglong4) * 8 * (size_t)h.n, "octant window sums");
-                h.alloc_epoch++;
-            }
-            if (h.es_wcap != es_wcap) {
-                h.es_wcap = es_wcap;
-                cf::es_set_lds_limit(32 * es_wcap);
-            }
+            bump_epoch(H);
         }
         if (!h.pos4f) {
             // (+ a cluster's width, zeroed: k_pairs_cq loads all 4 slots of a listed j-cluster, a partial
             // last cluster included)
             zalloc((void**)&h.pos4f, sizeof(float4) * (h.n + 4), "fp32 positions");
             zalloc((void**)&h.slot_of, sizeof(int) * h.n, "slot map");
-            h.alloc_epoch++;
+            bump_epoch(H);
         }
     }
 }
@@ -547,8 +538,9 @@ CF_EXPORT int cf_create(const cf_params* p, const cf_options* opt, cf_handle** o
         h.mixed = o.precision == CF_PRECISION_MIXED;
         if (o.handover != CF_HANDOVER_EVENT && o.handover != CF_HANDOVER_MEMORY)
             fail(CF_ERR_INVALID, "handover must be CF_HANDOVER_EVENT or CF_HANDOVER_MEMORY");
-        if (o.pair_list < CF_PAIR_LIST_AUTO || o.pair_list > CF_PAIR_LIST_OCTANT)
-            fail(CF_ERR_INVALID, "pair_list must be one of CF_PAIR_LIST_AUTO, _CLUSTER, _ATOM_HALF, _FULL, _OCTANT");
+        if (o.pair_list < CF_PAIR_LIST_AUTO || o.pair_list > CF_PAIR_LIST_FULL)
+            fail(CF_ERR_INVALID, "pair_list must be one of CF_PAIR_LIST_AUTO, _CLUSTER, _ATOM_HALF, _FULL "
+                                 "(the octant list of API 3 was removed in API 4)");
         if (o.variants & ~(0x1F | (15 << 8))) fail(CF_ERR_INVALID, "unknown bits in variants");
         if (o.list_capacity < 0) fail(CF_ERR_INVALID, "list_capacity must be >= 0");
         // the memory hand-over is opt-in: hipStreamWaitValue64 runs as a polling kernel on this
@@ -670,6 +662,11 @@ CF_EXPORT int cf_create(const cf_params* p, const cf_options* opt, cf_handle** o
         h.e_part = dalloc<double>(H, 3 * ((size_t)n / 256 + 2));
         h.energy_dev = dalloc<double>(H, 1);
         h.e_ticket = dalloc<int>(H, cf::kNumTickets);
+        h.err_dev = dalloc<int>(H, 1);
+        check_hip(hipHostMalloc((void**)&h.err_host, sizeof(int), hipHostMallocMapped | hipHostMallocCoherent),
+                  "hipHostMalloc (guard word)");
+        *h.err_host = 0;
+        check_hip(hipHostGetDevicePointer((void**)&h.err_host_dev, h.err_host, 0), "hipHostGetDevicePointer");
         check_hip(hipMemset(h.e_ticket, 0, sizeof(int) * cf::kNumTickets), "memset");
         check_hip(hipMemset(h.dedq, 0, sizeof(double) * n), "memset");
         check_hip(hipMemset(h.f_part, 0, sizeof(double) * 3 * n), "memset");
@@ -782,6 +779,7 @@ CF_EXPORT int cf_create(const cf_params* p, const cf_options* opt, cf_handle** o
     });
     if (rc != CF_OK && H) {
         for (void* p2 : H->allocs) (void)hipFree(p2);
+        if (H->h.err_host) (void)hipHostFree(H->h.err_host);
         delete H;
     }
     return rc;
@@ -791,7 +789,7 @@ CF_EXPORT int cf_destroy(cf_handle* H) {
     if (!H) return CF_OK;
     return guarded([&] {
         (void)hipSetDevice(H->h.device);
-        (void)hipDeviceSynchronize();   // both streams' launches, and any graph still running
+        drain_handle(H->h);   // both streams' launches, and any graph still running
         graph_forget(H);
         for (void* p : H->allocs) (void)hipFree(p);
         for (auto& v : H->ev)
@@ -800,8 +798,6 @@ CF_EXPORT int cf_destroy(cf_handle* H) {
         if (H->h.cl_start) { (void)hipFree(H->h.cl_start); (void)hipFree(H->h.cl_info); (void)hipFree(H->h.cl_bb);
                              (void)hipFree(H->h.cpl); (void)hipFree(H->h.cpl_cnt); }
         if (H->h.pos4f) { (void)hipFree(H->h.pos4f); (void)hipFree(H->h.slot_of); }
-        if (H->h.es_row) { (void)hipFree(H->h.es_row); (void)hipFree(H->h.es_pool); (void)hipFree(H->h.e_blk); }
-        if (H->h.es_part) (void)hipFree(H->h.es_part);
         if (H->h.cell_start) (void)hipFree(H->h.cell_start);
         if (H->h.cell_end) (void)hipFree(H->h.cell_end);
         if (H->h.cell_cnt) (void)hipFree(H->h.cell_cnt);
@@ -810,6 +806,7 @@ CF_EXPORT int cf_destroy(cf_handle* H) {
         if (H->h.aux) (void)hipStreamDestroy(H->h.aux);
         if (H->h.ev_fork) (void)hipEventDestroy(H->h.ev_fork);
         if (H->h.ev_join) (void)hipEventDestroy(H->h.ev_join);
+        if (H->h.err_host) (void)hipHostFree(H->h.err_host);
         delete H;
     });
 }
@@ -836,7 +833,7 @@ CF_EXPORT int cf_set_neighbor_skin(cf_handle* H, double skin) {
         check_hip(hipStreamSynchronize(h.stream), "stream sync");
         h.skin = skin;
         h.list_valid = false;
-        h.alloc_epoch++;   // captured graphs baked in the old list state (pos_ref, capacity): re-capture
+        bump_epoch(H);   // captured graphs baked in the old list state (pos_ref, capacity): re-capture
         if (!h.pbc) return;
         alloc_nlist(H, skin);
         if (skin > 0 && !h.pos_ref) h.pos_ref = dalloc<double>(H, (size_t)3 * h.n);
@@ -893,7 +890,7 @@ CF_EXPORT int cf_update_parameters(cf_handle* H, const cf_params* p) {
             }
         }
         h.list_valid = false;   // sorted LJ / types are refreshed by the next list build
-        h.alloc_epoch++;        // lj_ntypes / typ_s are kernel arguments of captured graphs: re-capture
+        bump_epoch(H);          // lj_ntypes / typ_s are kernel arguments of captured graphs: re-capture
     });
 }
 
@@ -918,8 +915,7 @@ CF_EXPORT int cf_get_pair_list(const cf_handle* H, int32_t* kind) {
     if (!H || !kind) { g_err = "null argument"; return CF_ERR_INVALID; }
     const cf::Handle& h = H->h;
     *kind = !h.pbc || h.nc[0] == 0 ? CF_PAIR_LIST_AUTO
-                                   : (h.es ? CF_PAIR_LIST_OCTANT
-                                      : (h.cluster ? CF_PAIR_LIST_CLUSTER : (h.half ? CF_PAIR_LIST_ATOM_HALF : CF_PAIR_LIST_FULL)));
+                                   : (h.cluster ? CF_PAIR_LIST_CLUSTER : (h.half ? CF_PAIR_LIST_ATOM_HALF : CF_PAIR_LIST_FULL));
     return CF_OK;
 }
 
@@ -1108,35 +1104,39 @@ struct GraphCache {
     GraphKey key[SEG_COUNT];
     bool rec_split[SEG_COUNT] = {};   // Handle::rec_split as the captured launches leave it (restored on replay)
     int64_t captures = 0, replays = 0;
-    void drop(int s) {   // (a replaced graph may still run: its launch arguments die with it)
+    // a replaced graph may still run on one of the handle's streams (its launch arguments die with
+    // it): drain them first -- the handle's streams only, not the device (the caller's torch or RCCL
+    // streams are not ours to wait for)
+    void drop(int s, const cf::Handle& h) {
         if (exec[s]) {
-            (void)hipDeviceSynchronize();
+            drain_handle(h);
             (void)hipGraphExecDestroy(exec[s]);
         }
         exec[s] = nullptr;
     }
+    void drop_all(const cf::Handle& h) {
+        for (int s = 0; s < SEG_COUNT; s++) drop(s, h);
+    }
 };
 
-static std::vector<std::pair<cf_handle*, GraphCache>>& graph_caches() {
-    static std::vector<std::pair<cf_handle*, GraphCache>> v;
-    return v;
-}
+// the handle's cache (one per handle, owned by it: no process-wide table whose entries could
+// outlive or be confused with a destroyed handle)
 static GraphCache* graph_of(cf_handle* H, bool create) {
-    for (auto& e : graph_caches())
-        if (e.first == H) return &e.second;
-    if (!create) return nullptr;
-    graph_caches().emplace_back(H, GraphCache());
-    return &graph_caches().back().second;
+    if (!H->graph && create) H->graph = new GraphCache();
+    return H->graph;
 }
 static void graph_forget(cf_handle* H) {
-    auto& v = graph_caches();
-    for (size_t i = 0; i < v.size(); i++)
-        if (v[i].first == H) {
-            for (int s = 0; s < SEG_COUNT; s++) v[i].second.drop(s);
-            if (v[i].second.cap) (void)hipStreamDestroy(v[i].second.cap);
-            v.erase(v.begin() + i);
-            return;
-        }
+    GraphCache* g = H->graph;
+    if (!g) return;
+    g->drop_all(H->h);
+    if (g->cap) (void)hipStreamDestroy(g->cap);
+    delete g;
+    H->graph = nullptr;
+}
+// every captured segment is dropped (a buffer its launches point to was reallocated); the cache
+// stays enabled and re-captures on the next call
+static void graph_invalidate(cf_handle* H) {
+    if (H->graph) H->graph->drop_all(H->h);
 }
 // graph mode for this call (timed evaluations run eagerly: replays could not record the events)
 static GraphCache* graph_active(cf_handle* H) {
@@ -1152,7 +1152,7 @@ static void run_segment(cf_handle* H, GraphCache* g, int seg, const GraphKey& k,
     cf::Handle& h = H->h;
     if (!g) { launches(); return; }
     if (!g->exec[seg] || !(k == g->key[seg])) {
-        g->drop(seg);
+        g->drop(seg, h);
         hipStream_t user = h.stream;
         h.stream = g->cap;
         hipGraph_t graph = nullptr;
@@ -1170,9 +1170,11 @@ static void run_segment(cf_handle* H, GraphCache* g, int seg, const GraphKey& k,
         }
         h.stream = user;
         check_hip(e, "hipStreamBeginCapture / EndCapture");
-        e = hipGraphInstantiate(&g->exec[seg], graph, nullptr, nullptr, 0);
+        hipGraphExec_t ex = nullptr;
+        e = hipGraphInstantiate(&ex, graph, nullptr, nullptr, 0);
         (void)hipGraphDestroy(graph);
-        check_hip(e, "hipGraphInstantiate");
+        check_hip(e, "hipGraphInstantiate");   // (a failed instantiation leaves exec[seg] null)
+        g->exec[seg] = ex;
         g->key[seg] = k;
         g->rec_split[seg] = h.rec_split;
         g->captures++;
@@ -1495,7 +1497,7 @@ CF_EXPORT int cf_set_overlap(cf_handle* H, int enable) {
         check_hip(hipSetDevice(H->h.device), "hipSetDevice");
         H->h.overlap = enable != 0;
         if (GraphCache* g = graph_of(H, false))   // captured launches follow the old stream layout
-            for (int seg = 0; seg < SEG_COUNT; seg++) g->drop(seg);
+            g->drop_all(H->h);
         if (H->h.overlap) ensure_aux(H);
     });
 }
@@ -1507,12 +1509,45 @@ CF_EXPORT int cf_get_graph_stats(const cf_handle* H, int64_t* captures, int64_t*
     return CF_OK;
 }
 
+// ---- device index guards ------------------------------------------------------------------------
+// A kernel that meets an index outside the buffer it is about to address (cf_internal.h kGuard*)
+// skips the access and sets a bit of Handle::err_dev; k_assemble_energy copies a nonzero value to
+// the pinned, mapped err_host.  Every later entry point of the handle then fails with CF_ERR_STATE
+// (sticky: the evaluation that tripped it is incomplete).  The check is one host read, no sync.
+static std::string guard_names(int v) {
+    static const char* names[] = {"cell bounds", "cluster table", "cluster-pair entry", "grid bins",
+                                  "neighbour entry", "atom_index entry", "rebuild flag"};
+    std::string s;
+    for (int b = 0; b < 7; b++)
+        if (v & (1 << b)) s += std::string(s.empty() ? "" : ", ") + names[b];
+    return s;
+}
+static void guard_check(const cf::Handle& h) {
+    const int v = h.err_host ? __atomic_load_n(h.err_host, __ATOMIC_ACQUIRE) : 0;
+    if (v)
+        fail(CF_ERR_STATE, "a device index guard tripped in an earlier evaluation (" + guard_names(v) +
+                               "); its results are incomplete and the handle must be re-created");
+}
+
+// the guard bits of the handle's evaluations so far (synchronises the handle's streams)
+CF_EXPORT int cf_get_device_errors(cf_handle* H, int32_t* bits) {
+    return guarded([&] {
+        if (!H || !bits) fail(CF_ERR_INVALID, "null argument");
+        check_hip(hipSetDevice(H->h.device), "hipSetDevice");
+        drain_handle(H->h);
+        int v = 0;
+        check_hip(hipMemcpy(&v, H->h.err_dev, sizeof(int), hipMemcpyDeviceToHost), "D2H guard word");
+        *bits = v;
+    });
+}
+
 // ---- the evaluation entry points -----------------------------------------------------------------
 CF_EXPORT int cf_compute_begin(cf_handle* H, const double* pos_dev, const double* box9, int flags) {
     return guarded([&] {
         if (!H || !pos_dev) fail(CF_ERR_INVALID, "null argument");
         cf::Handle& h = H->h;
         if (h.pending_flags >= 0) fail(CF_ERR_STATE, "cf_compute_begin called twice without cf_compute_end");
+        guard_check(h);
         check_hip(hipSetDevice(h.device), "hipSetDevice");
         const bool reusable = host_prologue(H, box9);
         ensure_aux(H);
@@ -1591,6 +1626,7 @@ CF_EXPORT int cf_compute(cf_handle* H, const double* pos_dev, const double* box9
         if (!H || !pos_dev) fail(CF_ERR_INVALID, "null argument");
         cf::Handle& h = H->h;
         if (h.pending_flags >= 0) fail(CF_ERR_STATE, "cf_compute during a begun evaluation");
+        guard_check(h);
         check_hip(hipSetDevice(h.device), "hipSetDevice");
         const bool reusable = host_prologue(H, box9);
         ensure_aux(H);
@@ -1598,6 +1634,43 @@ CF_EXPORT int cf_compute(cf_handle* H, const double* pos_dev, const double* box9
         launch_full(H, pos_dev, flags, reusable, forces_dev, energy_dev, graph_active(H), box9);
         h.pending_flags = -1;
         launch_check(h, "compute");
+    });
+}
+
+// OpenMM GPU-platform buffers (include/chargeflux.h; the reference's CUDA platform,
+// CudaCoulKernels.cpp:523-600): gather posq by atomIndex into atom-order fp64 positions, the
+// device-resident evaluation, scatter the forces into the fixed-point planes and add the energy
+CF_EXPORT int cf_compute_openmm(cf_handle* H, const void* posq, const void* posq_correction, int32_t posq_kind,
+                                const int32_t* atom_index, int32_t padded_n, const double* box9, int flags,
+                                long long* force_buf, void* energy_buf, int32_t energy_kind) {
+    return guarded([&] {
+        if (!H || !posq || !atom_index) fail(CF_ERR_INVALID, "null argument");
+        cf::Handle& h = H->h;
+        if (h.world > 1) fail(CF_ERR_STATE, "cf_compute_openmm is single-rank only");
+        if (posq_kind != CF_POSQ_DOUBLE4 && posq_kind != CF_POSQ_FLOAT4)
+            fail(CF_ERR_INVALID, "posq_kind must be CF_POSQ_DOUBLE4 or CF_POSQ_FLOAT4");
+        if (posq_correction && posq_kind != CF_POSQ_FLOAT4)
+            fail(CF_ERR_INVALID, "posq_correction goes with CF_POSQ_FLOAT4 (the mixed-precision platform)");
+        if (energy_kind != CF_ENERGY_DOUBLE && energy_kind != CF_ENERGY_FLOAT)
+            fail(CF_ERR_INVALID, "energy_kind must be CF_ENERGY_DOUBLE or CF_ENERGY_FLOAT");
+        if (padded_n < h.n) fail(CF_ERR_INVALID, "padded_n must be >= the number of particles");
+        if (h.pending_flags >= 0) fail(CF_ERR_STATE, "cf_compute_openmm during a begun evaluation");
+        guard_check(h);
+        check_hip(hipSetDevice(h.device), "hipSetDevice");
+        if (!H->om_pos) {
+            H->om_pos = dalloc<double>(H, (size_t)3 * h.n);
+            H->om_frc = dalloc<double>(H, (size_t)3 * h.n);
+            H->om_ene = dalloc<double>(H, 1);
+        }
+        const bool fw = force_buf && (flags & CF_INCLUDE_FORCES);
+        cf::launch_om_gather(h, posq, posq_correction, posq_kind, atom_index, H->om_pos);
+        if (fw) check_hip(hipMemsetAsync(H->om_frc, 0, sizeof(double) * 3 * h.n, h.stream), "memset forces");
+        const int rc = cf_compute(H, H->om_pos, box9, flags, fw ? H->om_frc : nullptr, energy_buf ? H->om_ene : nullptr);
+        if (rc != CF_OK) throw CfError(rc, g_err);
+        if (fw || energy_buf)
+            cf::launch_om_scatter(h, atom_index, H->om_frc, padded_n, fw ? force_buf : nullptr, H->om_ene, energy_buf,
+                                  energy_kind);
+        launch_check(h, "compute_openmm");
     });
 }
 
@@ -1626,6 +1699,7 @@ CF_EXPORT int cf_compute_host(cf_handle* H, const double* pos_host, const double
                       "D2H forces");
         check_hip(hipMemcpyAsync(&e, H->ene_host_dev, sizeof(double), hipMemcpyDeviceToHost, h.stream), "D2H energy");
         check_hip(hipStreamSynchronize(h.stream), "sync");
+        guard_check(h);   // (this evaluation's guards: k_assemble_energy has run)
         if (forces_host && (flags & CF_INCLUDE_FORCES))
             for (size_t k = 0; k < 3 * (size_t)n; k++) forces_host[k] += f[k];
         if (energy_host) *energy_host = e;
@@ -1636,6 +1710,7 @@ CF_EXPORT int cf_get_charges(cf_handle* H, double* out) {
     return guarded([&] {
         if (!H || !out) fail(CF_ERR_INVALID, "null argument");
         check_hip(hipStreamSynchronize(H->h.stream), "sync");
+        guard_check(H->h);
         check_hip(hipMemcpy(out, H->h.q, sizeof(double) * H->h.n, hipMemcpyDeviceToHost), "D2H charges");
     });
 }
@@ -1644,6 +1719,7 @@ CF_EXPORT int cf_get_dedq(cf_handle* H, double* out) {
     return guarded([&] {
         if (!H || !out) fail(CF_ERR_INVALID, "null argument");
         check_hip(hipStreamSynchronize(H->h.stream), "sync");
+        guard_check(H->h);
         check_hip(hipMemcpy(out, H->h.dedq, sizeof(double) * H->h.n, hipMemcpyDeviceToHost), "D2H dedq");
         if (H->h.rec_split) {   // (direct + excl) + rec, as k_assemble_energy adds them
             std::vector<double> r(H->h.n);
@@ -1657,6 +1733,7 @@ CF_EXPORT int cf_get_energy_terms(cf_handle* H, double terms[4]) {
     return guarded([&] {
         if (!H || !terms) fail(CF_ERR_INVALID, "null argument");
         check_hip(hipStreamSynchronize(H->h.stream), "sync");
+        guard_check(H->h);
         check_hip(hipMemcpy(terms, H->h.terms_dev, sizeof(double) * 4, hipMemcpyDeviceToHost), "D2H terms");
     });
 }
@@ -1705,6 +1782,7 @@ CF_EXPORT int cf_synchronize(cf_handle* H) {
     return guarded([&] {
         if (!H) fail(CF_ERR_INVALID, "null handle");
         check_hip(hipStreamSynchronize(H->h.stream), "sync");
+        guard_check(H->h);
     });
 }
 

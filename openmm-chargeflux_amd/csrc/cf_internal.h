@@ -167,6 +167,12 @@ struct Handle {
                                           // rescan of every atom); list rows rescanned after an
                                           // overflow; union of the half-list reasons (CF_FALLBACK_*)
     int64_t n_evals = 0;
+    // device index guards (kGuard* bits): a kernel that meets an index outside the buffer it is
+    // about to address sets a bit here and skips the access; k_assemble_energy copies a nonzero
+    // value into err_host (pinned, mapped), which every entry point checks (cf_api.hip guard_check)
+    int* err_dev = nullptr;     // [1] device
+    int* err_host = nullptr;    // [1] host-mapped pinned copy (read by the host)
+    int* err_host_dev = nullptr;// its device address (written by k_assemble_energy)
     // cell-sort scratch (the sort kernels run only when the device flag asks for a rebuild;
     // k_cell_commit then copies the new order to the live arrays)
     int* key_tmp = nullptr; int* atom_tmp = nullptr;
@@ -201,17 +207,6 @@ struct Handle {
     uint2* cpl = nullptr;       // [ncl_cap][cpl_cap] (first slot of j | window cell << 21, pair mask)
     int* cpl_cnt = nullptr;     // [ncl_cap]
     float4* pos4f = nullptr;    // [N] sorted wrapped fp32 (x, y, z, LJ type bits)
-    // octant (eighth-shell) cluster-pair list (cf_kernels_es.hip): one rank, the
-    // cluster table above, an 8-cell window per block, both sides summed in the window
-    bool es = false;
-    int es_wcap = 0;            // window atoms per k_pairs_es block (dynamic LDS: 32 B each)
-    int es_rows_max = 0;        // rows (clusters of octant positions 0..3) per block
-    int es_pool_cap = 0;        // list entries per block
-    int es_cells = 0;           // cells es_row / es_pool / e_blk are sized for
-    int2* es_row = nullptr;     // [ncell][es_rows_max] (offset in the block's pool, count; -1 = overflowed)
-    uint2* es_pool = nullptr;   // [ncell][es_pool_cap] (first slot of j | octant position << 21, pair mask)
-    ulonglong4* es_part = nullptr;   // [8][N] each atom's window sums from the 8 octants holding it
-    double* e_blk = nullptr;    // [ncell] pair energy per octant block
     int* slot_of = nullptr;     // [N] atom -> sorted slot (exclusion masks of the list build)
     // k-space (MFMA path)
     int npad = 0;               // owned rows of the phase tables, padded to the S-pass tile
@@ -278,10 +273,6 @@ void launch_nlist(Handle& h, const double* pos);
 void launch_cluster_list(Handle& h);                   // cluster table, bounding boxes, cluster-pair list (rebuild only)
 void launch_pairs_cluster(Handle& h, const double* pos, int include_forces);   // k_pairs_cq
 void launch_cluster_table(Handle& h);                  // k_cl_scan + k_cl_bbox (rebuild only)
-void launch_es_list(Handle& h);                        // cluster table + k_es_build (rebuild only)
-void launch_pairs_es(Handle& h, const double* pos, int include_forces);        // k_pairs_es
-int es_static_lds_bytes(bool mixed, bool types);
-void es_set_lds_limit(int bytes);
 void launch_direct(Handle& h, const double* pos, int include_forces);          // the pair kernel
 void launch_direct_finish(Handle& h, const double* pos, int include_forces);   // overflow rescan + exclusions
 void launch_recip_add(Handle& h);   // dedq, f_part += reciprocal partials
@@ -313,6 +304,12 @@ double* grid_reduce_buffer(Handle& h, int64_t* count);
 void launch_grid_coeffs(Handle& h, int include_energy);
 void launch_grid_dft_inv(Handle& h);
 void launch_grid_interp(Handle& h, bool split = false);   // split: store into dedq_rec / f_rec
+
+// OpenMM GPU-platform buffers (cf_kernels_openmm.hip, cf_compute_openmm)
+void launch_om_gather(Handle& h, const void* posq, const void* corr, int posq_kind, const int* atom_index,
+                      double* pos);
+void launch_om_scatter(Handle& h, const int* atom_index, const double* frc, int padded, long long* fbuf,
+                       const double* ene, void* ebuf, int energy_kind);
 
 void check_hip(hipError_t e, const char* what);
 
@@ -385,6 +382,17 @@ __device__ __forceinline__ int xcd_block() {
 // last-block tickets (Handle::e_ticket[]): the energy reduction, the cell-count bounds, the
 // grid-bin bounds
 constexpr int kTicketEnergy = 0, kTicketCells = 1, kTicketGrid = 2, kNumTickets = 4;
+
+// device index guards (Handle::err_dev): each bit names the invariant that failed; the kernel
+// skips the access it guards.  All of these hold by construction -- a set bit is a bug (or
+// corrupted device memory), reported as CF_ERR_STATE by the next entry point (cf_api.hip)
+constexpr int kGuardCellBounds = 1;    // k_cell_order: a cell's member range past the atom count
+constexpr int kGuardClusterTable = 2;  // k_cl_scan: more clusters than the cluster table holds
+constexpr int kGuardListEntry = 4;     // k_cl_build / k_pairs_cq: a list entry's slot or window cell out of range
+constexpr int kGuardGridBins = 8;      // k_g_bin / k_g_order_taps: bin bounds past the owned atom count
+constexpr int kGuardNeighbor = 16;     // k_nlist / k_nlist_wave: a partner slot past the atom count
+constexpr int kGuardAtomIndex = 32;    // k_om_gather: an OpenMM atomIndex entry outside [0, N) (caller data)
+constexpr int kGuardRebuildFlag = 64;  // k_cell_commit: the rebuild flag clear on a handle without a skin
 
 // ---- counting-sort helpers shared by the cell and grid-bin sorts ----------------------
 // atomicAdd(&cnt[key], 1) aggregated over runs of equal keys in consecutive lanes (spatially

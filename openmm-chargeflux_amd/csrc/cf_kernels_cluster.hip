@@ -66,7 +66,8 @@ __device__ __forceinline__ int window_cell(int k, int cx, int cy, int cz, int3 n
 // block), then per cell its clusters' (first slot, count) and fp32 bounding boxes
 // ---------------------------------------------------------------------------------
 __global__ void __launch_bounds__(1024) k_cl_scan(int ncell, const int* __restrict__ flag, const int* __restrict__ cstart,
-                                                  const int* __restrict__ cend, int* __restrict__ cl_start) {
+                                                  const int* __restrict__ cend, int* __restrict__ cl_start, int ncl_cap,
+                                                  int* __restrict__ err) {
     __shared__ int sh[1024];
     if (!*flag) return;
     int carry = 0;
@@ -78,7 +79,12 @@ __global__ void __launch_bounds__(1024) k_cl_scan(int ncell, const int* __restri
         carry += sh[1023];
         __syncthreads();
     }
-    if (threadIdx.x == 0) cl_start[ncell] = carry;
+    if (threadIdx.x == 0) {
+        cl_start[ncell] = carry;
+        // guard: sum ceil(n_c / 4) <= n / 4 + ncell = the table's size (cf_api.hip set_cells); the
+        // kernels after it skip every cell whose clusters would pass the end
+        if (carry > ncl_cap) atomicOr(err, kGuardClusterTable);
+    }
 }
 
 // boxes in the cell's corner frame (pos4f); lo.w = the cluster's x key for the half rule: the
@@ -87,11 +93,13 @@ __global__ void __launch_bounds__(256) k_cl_bbox(int ncell, const int* __restric
                                                  const int* __restrict__ cend, const int* __restrict__ cl_start,
                                                  const float4* __restrict__ pos4f, int2* __restrict__ cl_info,
                                                  float4* __restrict__ cl_bb, int3 nc, double3 L, double3 T,
-                                                 const int* __restrict__ atom_sorted, int lo, int hi, int n) {
+                                                 const int* __restrict__ atom_sorted, int lo, int hi, int n,
+                                                 int ncl_cap) {
     const int lane = threadIdx.x & 63;
     const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (c >= ncell || !*flag) return;
     const int b = cstart[c], e = cend[c], k0 = cl_start[c];
+    if (cl_start[c + 1] > ncl_cap) return;   // guard (k_cl_scan flagged it)
     const double ox = lattice(L, T, (double)(c / (nc.y * nc.z)) / nc.x, (double)((c / nc.z) % nc.y) / nc.y,
                               (double)(c % nc.z) / nc.z).x;
     for (int k = lane; k * kClSize < e - b; k += 64) {
@@ -177,6 +185,7 @@ __global__ void __launch_bounds__(kClBuildThreads) k_cl_build(DirectArgs a, cons
     __syncthreads();
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int c0 = a.cl_start[cell], c1 = a.cl_start[cell + 1];
+    if (c1 > a.ncl_cap) return;   // guard (k_cl_scan flagged it; block-uniform)
     for (int ci = c0 + wv; ci < c1; ci += kClBuildThreads / 64) {
         const float4 ilo = cl_bb[2 * ci], ihi = cl_bb[2 * ci + 1];
         const float xki = ilo.w;
@@ -307,7 +316,7 @@ __global__ void __launch_bounds__(kCqThreads) CF_LDS_UNPAIRED k_pairs_cq(DirectA
         for (int e = threadIdx.x; e < kErfcMaxM * (kErfcDeg + 1); e += kCqThreads) tab[e] = a.erfc_tab[e];
     }
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    bool bad = false, bad_list = false;
+    bool bad = false, bad_list = false, bad_idx = false;
     auto process = [&](const int cell) {
     const int cz = cell % nc.z, cy = (cell / nc.z) % nc.y, cx = cell / (nc.y * nc.z);
     if (threadIdx.x == 0) nown = 0;
@@ -352,6 +361,7 @@ __global__ void __launch_bounds__(kCqThreads) CF_LDS_UNPAIRED k_pairs_cq(DirectA
     const int jl = lane & 3, el = lane >> 2;           // phase A: entry el of the batch, j atom jl
     int* const qw = qbuf[wv][il];
     const int c0 = a.cl_start[cell], ncl = a.cl_start[cell + 1] - c0;
+    if (c0 + ncl > a.ncl_cap) return;   // guard (k_cl_scan flagged it; block-uniform)
     // x < 2 kCqQ -> x mod kCqQ (x - kCqQ underflows to a larger unsigned when x < kCqQ)
     auto ring = [](int x) { return (int)min((unsigned)x, (unsigned)x - (unsigned)kCqQ); };
     for (;;) {
@@ -518,7 +528,13 @@ __global__ void __launch_bounds__(kCqThreads) CF_LDS_UNPAIRED k_pairs_cq(DirectA
         // padded by a cluster's width)
         auto entry = [&](int s) {
             uint2 en = lst[s + el];
-            en.y = s + el < ne ? en.y : 0u;
+            const bool listed = s + el < ne && en.y != 0u;
+            // guard: a listed entry's j cluster lies inside the sorted slots and its window cell is
+            // one of the 18 (k_cl_build writes no other); an entry past the count reads slot 0
+            const bool bad_en = listed && ((en.x & kHalfSlotMask) >= (unsigned)a.n || (en.x >> kHalfSlotBits) >= kHalfWin);
+            bad_idx |= bad_en;
+            en.x = listed && !bad_en ? en.x : 0u;
+            en.y = listed && !bad_en ? en.y : 0u;
             return en;
         };
         auto jpos = [&](uint2 en) { return a.pos4f[(en.x & kHalfSlotMask) + jl]; };
@@ -611,6 +627,10 @@ __global__ void __launch_bounds__(kCqThreads) CF_LDS_UNPAIRED k_pairs_cq(DirectA
     {
         const int why = (__ballot(bad_list) ? kHalfListOverflow : 0) | (__ballot(bad) ? kHalfFixedRange : 0);
         if (why && lane == 0) atomicOr(a.half_flag, why);
+        if (__ballot(bad_idx) && lane == 0) {
+            atomicOr(a.half_flag, kHalfListOverflow);   // the pair sums are incomplete: k_excl rescans
+            atomicOr(a.err, kGuardListEntry);
+        }
     }
 }
 
@@ -621,11 +641,11 @@ void launch_cluster_table(Handle& h) {
     DirectArgs a = direct_args(h, nullptr, 0);
     const int ncell = h.nc[0] * h.nc[1] * h.nc[2];
     hipLaunchKernelGGL(k_cl_scan, dim3(1), dim3(1024), 0, h.stream, ncell, h.skin_flag, h.cell_start, h.cell_end,
-                       h.cl_start);
+                       h.cl_start, h.ncl_cap, h.err_dev);
     hipLaunchKernelGGL(k_cl_bbox, dim3((ncell + 3) / 4), dim3(256), 0, h.stream, ncell, h.skin_flag, h.cell_start,
                        h.cell_end, h.cl_start, h.pos4f, h.cl_info, h.cl_bb, make_int3(h.nc[0], h.nc[1], h.nc[2]),
                        make_double3(h.box_L[0], h.box_L[1], h.box_L[2]), make_double3(h.box_t[0], h.box_t[1], h.box_t[2]),
-                       a.atom_sorted, a.lo, a.hi, a.n);
+                       a.atom_sorted, a.lo, a.hi, a.n, h.ncl_cap);
 }
 
 void launch_cluster_list(Handle& h) {

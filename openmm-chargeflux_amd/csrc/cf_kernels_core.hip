@@ -156,7 +156,8 @@ __global__ void __launch_bounds__(256) k_cell_hist(int n, const int* __restrict_
                                                    double3 L, double3 T, int3 nc, int* __restrict__ key, int* __restrict__ rank,
                                                    int* __restrict__ cnt, int* __restrict__ ticket,
                                                    int* __restrict__ cstart, int* __restrict__ cend, int lo, int hi,
-                                                   int* __restrict__ own_cnt, int* __restrict__ own_start) {
+                                                   int* __restrict__ own_cnt, int* __restrict__ own_start,
+                                                   int* __restrict__ err) {
     __shared__ int sh[256];
     if (!*flag) return;   // uniform over the grid
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -183,7 +184,15 @@ __global__ void __launch_bounds__(256) k_cell_hist(int n, const int* __restrict_
     if (valid) rank[i] = r;
     if (own_cnt) (void)wave_agg_inc(own_cnt, k, valid && i >= lo && i < hi);
     if (!last_block_done(ticket)) return;
-    block_counts_to_bounds<256>(nc.x * nc.y * nc.z, cnt, cstart, cend, false, sh);
+    const int ncell = nc.x * nc.y * nc.z;
+    block_counts_to_bounds<256>(ncell, cnt, cstart, cend, false, sh);
+    // guard: the counts add up to the atoms (k_cell_scatter re-zeroes them after each build); bounds
+    // that do not are replaced by empty cells, so no kernel after this one indexes past N
+    __syncthreads();
+    if (ld_agent(cend + ncell - 1) != n) {
+        for (int c = threadIdx.x; c < ncell; c += blockDim.x) { cstart[c] = 0; cend[c] = 0; }
+        if (threadIdx.x == 0) atomicOr(err, kGuardCellBounds);
+    }
     if (own_cnt) {
         __syncthreads();
         block_counts_to_bounds<256>(nc.x * nc.y * nc.z, own_cnt, own_start, nullptr, true, sh);
@@ -195,7 +204,7 @@ __global__ void __launch_bounds__(256) k_cell_hist(int n, const int* __restrict_
 __global__ void __launch_bounds__(256) k_cell_scatter(int n, const int* __restrict__ flag, const int* __restrict__ key,
                                                       const int* __restrict__ rank, const int* __restrict__ cstart,
                                                       int* __restrict__ tmp, int ncell, int* __restrict__ cnt,
-                                                      int* __restrict__ own_cnt) {
+                                                      int* __restrict__ own_cnt, int* __restrict__ err) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (!*flag) return;
     for (int c = i; c < ncell; c += gridDim.x * blockDim.x) {
@@ -203,7 +212,9 @@ __global__ void __launch_bounds__(256) k_cell_scatter(int n, const int* __restri
         if (own_cnt) own_cnt[c] = 0;
     }
     if (i >= n) return;
-    tmp[cstart[key[i]] + rank[i]] = i;
+    const int k = key[i], s = (unsigned)k < (unsigned)ncell ? cstart[k] + rank[i] : -1;
+    if ((unsigned)s >= (unsigned)n) { atomicOr(err, kGuardCellBounds); return; }   // guard
+    tmp[s] = i;
 }
 
 // one 256-thread block per cell: final position of each member = cell start + number of members
@@ -224,7 +235,7 @@ __global__ void __launch_bounds__(256) k_cell_order(int ncell, const int* __rest
                                                     const int* __restrict__ tmp, int* __restrict__ out, int lo, int hi,
                                                     const int* __restrict__ own_start, int* __restrict__ own_s,
                                                     const double* __restrict__ pos, double3 L, double3 T, int3 nc,
-                                                    int zcol) {
+                                                    int zcol, int n, int* __restrict__ err) {
     // one 64-bit key per member: (column << 58 | quantized c coordinate << 26 | atom index), or the
     // atom index alone -- the rank is then one unsigned compare per member pair
     __shared__ unsigned long long memk[kOrderLds];
@@ -232,6 +243,10 @@ __global__ void __launch_bounds__(256) k_cell_order(int ncell, const int* __rest
     const int c = blockIdx.x;
     if (c >= ncell || !*flag) return;   // block-uniform
     const int b = cstart[c], m = cend[c] - b;
+    if (b < 0 || m < 0 || b + m > n) {   // guard (k_cell_hist's bounds hold by construction)
+        if (tid == 0) atomicOr(err, kGuardCellBounds);
+        return;
+    }
     const int* src = tmp + b;
     if (m > kOrderLds) {   // rare (an over-full cell): atom order, read from global memory
         for (int e = tid; e < m; e += 256) {
@@ -307,13 +322,19 @@ __global__ void __launch_bounds__(256) k_cell_commit(int n, const int* __restric
                                                      double4* __restrict__ pos4s, double2* __restrict__ ljs,
                                                      const int* __restrict__ atype, int* __restrict__ typ_s,
                                                      double* __restrict__ pos_ref, long long* __restrict__ n_builds,
-                                                     float4* __restrict__ pos4f, int* __restrict__ slot_of, int3 nc) {
+                                                     float4* __restrict__ pos4f, int* __restrict__ slot_of, int3 nc,
+                                                     int* __restrict__ err) {
     int s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= n) return;
     double4 p4;
     int i, c;
-    if (*flag) {
+    const bool rebuild = *flag != 0;
+    // guard: a kept list needs the build positions; without a skin (pos_ref null) every evaluation
+    // sets the rebuild flag first (launch_force_rebuild), so a clear flag here is a broken ordering
+    if (!rebuild && !pos_ref) { if (s == 0) atomicOr(err, kGuardRebuildFlag); return; }
+    if (rebuild) {
         i = idx_new[s];
+        if ((unsigned)i >= (unsigned)n) { atomicOr(err, kGuardCellBounds); return; }   // guard
         c = key[i];
         key_s[s] = key[i];
         idx_s[s] = i;
@@ -327,6 +348,7 @@ __global__ void __launch_bounds__(256) k_cell_commit(int n, const int* __restric
         if (s == 0) *n_builds += 1;
     } else {
         i = idx_s[s];
+        if ((unsigned)i >= (unsigned)n) { atomicOr(err, kGuardCellBounds); return; }   // guard
         c = pos4f ? key_s[s] : 0;
         double3 x = ld3(pos, i), r = ld3(pos_ref, i);
         const double3 w = wrap_by(x, floor3(fractional(r, L, T)), L, T);
@@ -412,8 +434,8 @@ __device__ __forceinline__ void scan_cells(const DirectArgs& a, int s, double4 p
                     if (ord++ % nparts != part) continue;
                     // the image of the wrapped neighbour cell adjacent to this one (a lattice translate)
                     const double3 sh = lattice(a.L, a.T, kx - 1, ky - 1, kz - 1);
-                    int t1 = a.cend[c];
-                    for (int t = a.cstart[c]; t < t1; t++) {
+                    const int t1 = min(a.cend[c], a.n);   // (bounds past N are a guard case: k_cell_hist)
+                    for (int t = max(a.cstart[c], 0); t < t1; t++) {
                         double4 pj = a.pos4s[t];
                         double dx = pi.x - (pj.x + sh.x), dy = pi.y - (pj.y + sh.y), dz = pi.z - (pj.z + sh.z);
                         double r2 = dx * dx + dy * dy + dz * dz;
@@ -786,22 +808,16 @@ __device__ __forceinline__ void store_pairs(const PairAcc& acc, const DirectArgs
 // (VGPRs -> occupancy).  The
 // operation order per atom is that of one fused loop: pair sums, then exclusions in list
 // order, then dE/dq_self + sum.
-// (add_f, add_dq: the half list's partner-side sums of the atom, added to the stored pair sums;
-// base_part false: they are the whole pair sums -- the octant list sums both sides in its windows)
+// (add_f, add_dq: the half list's partner-side sums of the atom, added to the stored pair sums)
 __device__ __forceinline__ void excl_atom(const DirectArgs& a, int i, double3 add_f = make_double3(0.0, 0.0, 0.0),
-                                          double add_dq = 0.0, bool base_part = true) {
+                                          double add_dq = 0.0) {
     const double ke = a.ke;
     const double two_over_sqrtpi = 1.1283791670955126;
     const int ex0 = a.ex_start[i], exc = a.ex_start[i + 1] - ex0;
     double fx = 0, fy = 0, fz = 0, dq = 0, ex_e = 0;
     if (a.include_forces) {
-        if (base_part) {
-            fx = a.f_part[3 * i] + add_f.x; fy = a.f_part[3 * i + 1] + add_f.y; fz = a.f_part[3 * i + 2] + add_f.z;
-            dq = a.dedq[i] + add_dq;
-        } else {
-            fx = add_f.x; fy = add_f.y; fz = add_f.z;
-            dq = add_dq;
-        }
+        fx = a.f_part[3 * i] + add_f.x; fy = a.f_part[3 * i + 1] + add_f.y; fz = a.f_part[3 * i + 2] + add_f.z;
+        dq = a.dedq[i] + add_dq;
     }
     if (exc) {
         double3 xi = ld3(a.pos, i);
@@ -914,6 +930,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))
     for (int m = 1; m < LPA; m <<= 1) over = __shfl_xor(over, m) || over;
     if (over) active = false;
     PairAcc acc;
+    bool bad_entry = false;
     if (active) {
         const double4 pi = a.pos4s[ss];
         const double2 li = a.ljs[ss];
@@ -921,7 +938,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))
         constexpr int kMask = (1 << kShiftBits) - 1;
         struct Cand { double4 p; double2 lj; };
         auto gather = [&](int e, bool ok) {
-            const int t = ok ? (e & kMask) : 0;
+            int t = ok ? (e & kMask) : 0;
+            if ((unsigned)t >= (unsigned)a.n) { bad_entry = true; t = 0; }   // guard (k_nlist writes t < n)
             Cand cd;
             cd.p = a.pos4s[t];
             cd.lj = TYPES ? ljt[(unsigned)e >> kShiftBits] : a.ljs[t];
@@ -943,6 +961,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))
         acc.fx += __shfl_xor(acc.fx, m); acc.fy += __shfl_xor(acc.fy, m); acc.fz += __shfl_xor(acc.fz, m);
         acc.dq += __shfl_xor(acc.dq, m); acc.e += __shfl_xor(acc.e, m);
     }
+    if (__ballot(bad_entry) && (threadIdx.x & 63) == 0) atomicOr(a.err, kGuardNeighbor);
     if (!active || g != 0) return;
     store_pairs(acc, a, i);
 }
@@ -1391,25 +1410,7 @@ __global__ void __launch_bounds__(256) k_excl(DirectArgs a) {
         pair_rescan(a, a.erfc_tab, s, i);
         if (!a.half && a.fallback) atomicAdd((unsigned long long*)&a.fallback[1], 1ull);
     }
-    if (a.es && !over) {   // octant list: both sides from the 8 octant windows holding s; the pair
-                           // energy per block, carried by atoms 0..ncell-1 into the fixed-order sum
-        const int ncell = a.nc.x * a.nc.y * a.nc.z;
-        a.e_atom[3 * i + 1] = i < ncell ? a.e_blk[i] : 0.0;
-        if (a.include_forces) {
-            ulonglong4 v[8];
-#pragma unroll
-            for (int p = 0; p < 8; p++) v[p] = a.es_part[(size_t)p * a.n + s];
-            long long sx = 0, sy = 0, sz = 0, sq = 0;
-#pragma unroll
-            for (int p = 0; p < 8; p++) {
-                sx += (long long)v[p].x; sy += (long long)v[p].y; sz += (long long)v[p].z; sq += (long long)v[p].w;
-            }
-            excl_atom(a, i, make_double3((double)sx * kFixInv, (double)sy * kFixInv, (double)sz * kFixInv),
-                      (double)sq * kFixInv, false);
-        } else {
-            excl_atom(a, i);
-        }
-    } else if (a.half && !over && a.include_forces) {    // the partner-side sums of the half list
+    if (a.half && !over && a.include_forces) {    // the partner-side sums of the half list
         double3 f;
         double dq;
         half_window_sums(a, s, f, dq);
@@ -1530,7 +1531,8 @@ __global__ void __launch_bounds__(kEChunk) k_assemble_energy(int lo, int hi, con
                                                              double* __restrict__ energy_int, int* __restrict__ ticket,
                                                              int* __restrict__ flag, int* __restrict__ xrange,
                                                              int* __restrict__ half_flag,
-                                                             long long* __restrict__ fallback, int per) {
+                                                             long long* __restrict__ fallback, int per,
+                                                             const int* __restrict__ err, int* __restrict__ err_host) {
     __shared__ double red[4][4];
     double a0 = 0, a1 = 0, a2 = 0;
     // `per` chunks of kEChunk atoms per block at large N: fewer partials and fewer increments
@@ -1607,6 +1609,12 @@ __global__ void __launch_bounds__(kEChunk) k_assemble_energy(int lo, int hi, con
             *half_flag = 0;
         }
         if (xrange) { xrange[0] = INT_MAX; xrange[1] = INT_MIN; }   // re-arm the grid x-slab
+        // a tripped index guard (sticky: the handle stays failed) becomes visible to the host
+        // (pinned, mapped) without any synchronisation; the normal path reads one word
+        if (err && err_host) {
+            const int v = ld_agent(err);
+            if (v) __hip_atomic_store(err_host, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
     }
 }
 
@@ -1697,16 +1705,17 @@ void launch_cell_sort(Handle& h, const double* pos) {
     const double3 T = make_double3(h.box_t[0], h.box_t[1], h.box_t[2]);
     hipLaunchKernelGGL(k_cell_hist, dim3(nblk(h.n, 256)), dim3(256), 0, h.stream, h.n, f, pos, L, T, nc, h.cell_key,
                        h.atom_val, h.cell_cnt, h.e_ticket + kTicketCells, h.cell_start, h.cell_end, h.lo, h.hi, oc,
-                       h.own_start);
+                       h.own_start, h.err_dev);
     hipLaunchKernelGGL(k_cell_scatter, dim3(nblk(h.n, 256)), dim3(256), 0, h.stream, h.n, f, h.cell_key, h.atom_val,
-                       h.cell_start, h.atom_tmp, ncell, h.cell_cnt, oc);
+                       h.cell_start, h.atom_tmp, ncell, h.cell_cnt, oc, h.err_dev);
     hipLaunchKernelGGL(k_cell_order, dim3(ncell), dim3(256), 0, h.stream, ncell, f, h.cell_start,
                        h.cell_end, h.atom_tmp, h.key_tmp, h.lo, h.hi, h.own_start, oc ? h.own_s : nullptr, pos, L, T,
-                       nc, h.zcol);
+                       nc, h.zcol, h.n, h.err_dev);
     hipLaunchKernelGGL(k_cell_commit, dim3(nblk(h.n, 256)), dim3(256), 0, h.stream, h.n, f, h.cell_key, h.key_tmp,
                        pos, h.q, h.lj, L, T, h.cell_key_sorted, h.atom_sorted, h.pos4s, h.ljs,
                        h.atom_type, h.typ_s,
-                       h.pos_ref, h.n_builds_dev, h.cluster ? h.pos4f : nullptr, h.cluster ? h.slot_of : nullptr, nc);
+                       h.pos_ref, h.n_builds_dev, h.cluster ? h.pos4f : nullptr, h.cluster ? h.slot_of : nullptr, nc,
+                       h.err_dev);
 }
 
 void launch_force_rebuild(Handle& h) {
@@ -1748,9 +1757,8 @@ DirectArgs direct_args(Handle& h, const double* pos, int include_forces) {
     a.fallback = h.n_fallback_dev;
     a.cl_start = h.cl_start; a.cl_info = h.cl_info; a.cpl = h.cpl; a.cpl_cnt = h.cpl_cnt; a.cpl_cap = h.cpl_cap;
     a.pos4f = h.pos4f; a.slot_of = h.slot_of;
-    a.es = h.es ? 1 : 0;
-    a.es_row = h.es_row; a.es_pool = h.es_pool; a.es_rows_max = h.es_rows_max; a.es_pool_cap = h.es_pool_cap;
-    a.es_part = h.es_part; a.e_blk = h.e_blk;
+    a.ncl_cap = h.ncl_cap;
+    a.err = h.err_dev;
     {   // fp32 prefilter: |d| from fp32 coordinates of magnitude <= ~2 L carries an error below 8 ulp(L)
         const double Lmax = std::max(h.box_L[0], std::max(h.box_L[1], h.box_L[2])) + std::fabs(h.box_t[0]) +
                             std::fabs(h.box_t[1]) + std::fabs(h.box_t[2]);
@@ -1761,7 +1769,6 @@ DirectArgs direct_args(Handle& h, const double* pos, int include_forces) {
 }
 
 void launch_nlist(Handle& h, const double* pos) {
-    if (h.es) { launch_es_list(h); return; }             // cf_kernels_es.hip
     if (h.cluster) { launch_cluster_list(h); return; }   // cf_kernels_cluster.hip
     DirectArgs a = direct_args(h, pos, 0);
     if (a.brute || h.nc[0] < 4 || h.nc[1] < 4 || h.nc[2] < 4)
@@ -1771,7 +1778,6 @@ void launch_nlist(Handle& h, const double* pos) {
 }
 
 void launch_direct(Handle& h, const double* pos, int include_forces) {
-    if (h.es) { launch_pairs_es(h, pos, include_forces); return; }             // cf_kernels_es.hip
     if (h.cluster) { launch_pairs_cluster(h, pos, include_forces); return; }   // cf_kernels_cluster.hip
     DirectArgs a = direct_args(h, pos, include_forces);
     if (a.half) {
@@ -1859,7 +1865,7 @@ void launch_assemble_energy(Handle& h, double* forces_out, int include_energy, d
                        h.rec_split ? reinterpret_cast<const double4*>(h.f_rec) : nullptr,
                        make_double3(h.gp.ng[0] / h.box_L[0], h.gp.ng[1] / h.box_L[1], h.gp.ng[2] / h.box_L[2]), h.e_atom, h.e_part, h.e_rec_part, nrec, h.pbc,
                        h.terms_dev, energy_out, h.energy_dev, h.e_ticket + kTicketEnergy, h.skin_flag, h.g_xrange,
-                       h.half ? h.half_flag : nullptr, h.n_fallback_dev, per);
+                       h.half ? h.half_flag : nullptr, h.n_fallback_dev, per, h.err_dev, h.err_host_dev);
 }
 
 }  // namespace cf

@@ -101,7 +101,8 @@ __global__ void __launch_bounds__(256) k_g_bin(int lo, int nown, const double* _
                                                const double* __restrict__ q, double3 L, int3 ng, int W, int3 nb,
                                                double4* __restrict__ srec, int4* __restrict__ g0u,
                                                int* __restrict__ rank, int* __restrict__ cnt, int* __restrict__ xr,
-                                               int* __restrict__ ticket, int* __restrict__ start, int per) {
+                                               int* __restrict__ ticket, int* __restrict__ start, int per,
+                                               int* __restrict__ err) {
     __shared__ int sh[256];
     // `per` rounds of 256 atoms per block: the ticket of last_block_done is one address that
     // every block increments, so fewer, longer blocks at large N (launch_grid_sort)
@@ -161,17 +162,28 @@ __global__ void __launch_bounds__(256) k_g_bin(int lo, int nown, const double* _
     if (valid) rank[io] = r;
     }
     if (!last_block_done(ticket)) return;
-    block_counts_to_bounds<256>(nb.x * nb.y * nb.z, cnt, start, nullptr, true, sh);
+    const int nbins = nb.x * nb.y * nb.z;
+    block_counts_to_bounds<256>(nbins, cnt, start, nullptr, true, sh);
+    // guard: the counts add up to the owned atoms (k_g_scatter re-zeroes them each evaluation);
+    // bounds that do not are replaced by empty bins, so no spread, tap or interpolation kernel
+    // indexes past the owned atoms
+    __syncthreads();
+    if (ld_agent(start + nbins) != nown) {
+        for (int b = threadIdx.x; b <= nbins; b += blockDim.x) start[b] = 0;
+        if (threadIdx.x == 0) atomicOr(err, kGuardGridBins);
+    }
 }
 
 // also re-zeroes the bin counts (consumed by k_g_bin's bounds) for the next evaluation
 __global__ void __launch_bounds__(256) k_g_scatter(int nown, const int4* __restrict__ g0u, const int* __restrict__ rank,
                                                    const int* __restrict__ start, int* __restrict__ tmp, int nbins,
-                                                   int* __restrict__ cnt) {
+                                                   int* __restrict__ cnt, int* __restrict__ err) {
     const int io = blockIdx.x * blockDim.x + threadIdx.x;
     for (int b = io; b < nbins; b += gridDim.x * blockDim.x) cnt[b] = 0;
     if (io >= nown) return;
-    tmp[start[g0u[io].w] + rank[io]] = io;
+    const int bin = g0u[io].w, s = (unsigned)bin < (unsigned)nbins ? start[bin] + rank[io] : -1;
+    if ((unsigned)s >= (unsigned)nown) { atomicOr(err, kGuardGridBins); return; }   // guard
+    tmp[s] = io;
 }
 
 // taps of every sorted atom in bin-aligned rows: taps[slot][d][p], p in [0, 24), is the
@@ -205,7 +217,7 @@ __global__ void __launch_bounds__(256) k_g_order_taps(int nbins, const int* __re
                                                       const int* __restrict__ tmp, int* __restrict__ order, int Wr,
                                                       double beta, int3 ng, const double4* __restrict__ srec,
                                                       const int4* __restrict__ g0u, double* __restrict__ taps,
-                                                      int4* __restrict__ g0s) {
+                                                      int4* __restrict__ g0s, int nown, int* __restrict__ err) {
     __shared__ int mem[kOtWaves][kOtLds];
     __shared__ int srt[kOtWaves][kOtLds];
     __shared__ double4 srl[kOtWaves][64];   // sorted members' srec / g0u (bins of <= 64 members)
@@ -218,6 +230,10 @@ __global__ void __launch_bounds__(256) k_g_order_taps(int nbins, const int* __re
     if (b >= nbins) return;   // wave-uniform
     const int b0 = start[b], m = start[b + 1] - b0;
     if (m == 0) return;
+    if (b0 < 0 || m < 0 || b0 + m > nown) {   // guard (k_g_bin's bounds hold by construction)
+        if (lane == 0) atomicOr(err, kGuardGridBins);
+        return;
+    }
     const int* src = tmp + b0;
     const bool fast = m <= 64, in_lds = m <= kOtLds;
     if (fast) {   // members in registers: rank by wave-uniform lane reads, their srec / g0u
@@ -2120,17 +2136,18 @@ void launch_grid_sort(Handle& h, const double* pos) {
     // at least ~512 blocks of 256 atoms each round; up to 8 rounds per block (C5: 5, C3: 1)
     const int per = h.block_rounds() > 0 ? std::min(8, h.block_rounds()) : std::max(1, std::min(8, nown / (256 * 512)));
     hipLaunchKernelGGL(k_g_bin, dim3(nblk(nown, 256 * per)), dim3(256), 0, h.stream, h.lo, nown, pos, h.q, L, ng, p.W,
-                       nb, h.g_srec, h.g_g0u, h.g_rank, h.g_cnt, h.g_xrange, h.e_ticket + kTicketGrid, h.g_start, per);
+                       nb, h.g_srec, h.g_g0u, h.g_rank, h.g_cnt, h.g_xrange, h.e_ticket + kTicketGrid, h.g_start, per,
+                       h.err_dev);
     hipLaunchKernelGGL(k_g_scatter, dim3(nblk(nown, 256)), dim3(256), 0, h.stream, nown, h.g_g0u, h.g_rank, h.g_start,
-                       h.g_tmp, p.nbins, h.g_cnt);
+                       h.g_tmp, p.nbins, h.g_cnt, h.err_dev);
     if (p.W == 14) hipLaunchKernelGGL(k_g_order_taps<14>, dim3(nblk(p.nbins, kOtWaves)), dim3(256), 0, h.stream, p.nbins, h.g_start, h.g_tmp,
-                       h.g_order, p.W, p.beta, ng, h.g_srec, h.g_g0u, h.g_taps, h.g_g0s);
+                       h.g_order, p.W, p.beta, ng, h.g_srec, h.g_g0u, h.g_taps, h.g_g0s, nown, h.err_dev);
     else if (p.W == 13) hipLaunchKernelGGL(k_g_order_taps<13>, dim3(nblk(p.nbins, kOtWaves)), dim3(256), 0, h.stream, p.nbins, h.g_start, h.g_tmp,
-                       h.g_order, p.W, p.beta, ng, h.g_srec, h.g_g0u, h.g_taps, h.g_g0s);
+                       h.g_order, p.W, p.beta, ng, h.g_srec, h.g_g0u, h.g_taps, h.g_g0s, nown, h.err_dev);
     else if (p.W == 8) hipLaunchKernelGGL(k_g_order_taps<8>, dim3(nblk(p.nbins, kOtWaves)), dim3(256), 0, h.stream, p.nbins, h.g_start, h.g_tmp,
-                       h.g_order, p.W, p.beta, ng, h.g_srec, h.g_g0u, h.g_taps, h.g_g0s);
+                       h.g_order, p.W, p.beta, ng, h.g_srec, h.g_g0u, h.g_taps, h.g_g0s, nown, h.err_dev);
     else hipLaunchKernelGGL(k_g_order_taps<0>, dim3(nblk(p.nbins, kOtWaves)), dim3(256), 0, h.stream, p.nbins, h.g_start, h.g_tmp,
-                       h.g_order, p.W, p.beta, ng, h.g_srec, h.g_g0u, h.g_taps, h.g_g0s);
+                       h.g_order, p.W, p.beta, ng, h.g_srec, h.g_g0u, h.g_taps, h.g_g0s, nown, h.err_dev);
 }
 
 #define CF_GRID_W_DISPATCH(W_, CALL) \

@@ -139,12 +139,8 @@ struct DirectArgs {
     const float4* pos4f;        // [N] fp32 (x, y, z, LJ type bits)
     const int* slot_of;         // [N] atom -> sorted slot
     float rcm2f;                // prefilter radius^2: rc with a margin above the fp32 rounding of |d|
-    // octant list (cf_kernels_es.hip)
-    int es;                     // k_pairs_es ran: k_excl takes both sides from es_part
-    const int2* es_row; const uint2* es_pool;
-    int es_rows_max, es_pool_cap;
-    ulonglong4* es_part;        // [8][N]
-    double* e_blk;              // [ncell]
+    int ncl_cap;                // clusters cl_info / cpl_cnt / cpl hold
+    int* err;                   // [1] device index guards (kGuard* bits, cf_internal.h)
 };
 
 __device__ __forceinline__ int own_slot(const DirectArgs& a, int c) { return a.own_s ? a.own_s[c] : c; }

@@ -27,7 +27,6 @@ CF_PAIR_LIST_AUTO = 0
 CF_PAIR_LIST_CLUSTER = 1
 CF_PAIR_LIST_ATOM_HALF = 2
 CF_PAIR_LIST_FULL = 3
-CF_PAIR_LIST_OCTANT = 4
 CF_VARIANT_GEMM_DFT = 1
 CF_VARIANT_VECTOR_SPREAD = 2
 CF_VARIANT_MFMA_SPREAD = 4
@@ -39,6 +38,17 @@ def CF_VARIANT_BLOCK_ROUNDS(r: int) -> int:
     return (int(r) & 15) << 8
 
 
+CF_GUARD_CELL_BOUNDS = 1
+CF_GUARD_CLUSTER_TABLE = 2
+CF_GUARD_LIST_ENTRY = 4
+CF_GUARD_GRID_BINS = 8
+CF_GUARD_NEIGHBOR = 16
+CF_GUARD_ATOM_INDEX = 32
+CF_GUARD_REBUILD_FLAG = 64
+CF_POSQ_DOUBLE4 = 0
+CF_POSQ_FLOAT4 = 1
+CF_ENERGY_DOUBLE = 0
+CF_ENERGY_FLOAT = 1
 CF_INCLUDE_FORCES = 1
 CF_INCLUDE_ENERGY = 2
 ONE_4PI_EPS0 = 138.935456                    # OpenMM 7.x headers: cf_params.one_4pi_eps0 = 0
@@ -123,6 +133,9 @@ SIGNATURES = [
                                         C.POINTER(C.c_int32)]),
     ("cf_get_graph_stats", C.c_int, [C.c_void_p, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
     ("cf_get_pair_list", C.c_int, [C.c_void_p, C.POINTER(C.c_int32)]),
+    ("cf_get_device_errors", C.c_int, [C.c_void_p, C.POINTER(C.c_int32)]),
+    ("cf_compute_openmm", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_int32, DP,
+                                    C.c_int, C.c_void_p, C.c_void_p, C.c_int32]),
 ]
 
 _lib = None

@@ -76,8 +76,7 @@ class HipCalcCoulForceKernel:
     KSPACE_GRID = 2         # same k-sum via ES-kernel grid (spread, pruned DFT, interpolate)
 
     PAIR_LISTS = {"auto": _cabi.CF_PAIR_LIST_AUTO, "cluster": _cabi.CF_PAIR_LIST_CLUSTER,
-                  "atom_half": _cabi.CF_PAIR_LIST_ATOM_HALF, "full": _cabi.CF_PAIR_LIST_FULL,
-                  "octant": _cabi.CF_PAIR_LIST_OCTANT}
+                  "atom_half": _cabi.CF_PAIR_LIST_ATOM_HALF, "full": _cabi.CF_PAIR_LIST_FULL}
     HANDOVERS = {"event": _cabi.CF_HANDOVER_EVENT, "memory": _cabi.CF_HANDOVER_MEMORY}
 
     def __init__(self, device: int = 0, stream=None, rank: int = 0, world_size: int = 1, kspace_algo: int = 0,
@@ -87,7 +86,7 @@ class HipCalcCoulForceKernel:
         takes it from openmm/reference/SimTKOpenMMRealType.h, ReferenceCoulKernels.cpp:7);
         0 = 138.935456 (OpenMM 7.x), _cabi.ONE_4PI_EPS0_CODATA2018 for OpenMM 8.x.
         pair_list, handover, variants, list_capacity: cf_options fields (include/chargeflux.h):
-        the neighbour-list kind ("auto", "octant", "cluster", "atom_half", "full"), the second stream's
+        the neighbour-list kind ("auto", "cluster", "atom_half", "full"), the second stream's
         fork / join ("event" or the opt-in "memory"), CF_VARIANT_* bits (alternative kernels of the
         same sums) and the cluster-pair list capacity (0 = automatic)."""
         if pair_list not in self.PAIR_LISTS:
@@ -194,7 +193,7 @@ class HipCalcCoulForceKernel:
         return c.value, r.value
 
     def pair_list(self):
-        """The direct-space list in use: "octant", "cluster", "atom_half" or "full" ("auto" before the first
+        """The direct-space list in use: "cluster", "atom_half" or "full" ("auto" before the first
         periodic evaluation and without PBC) -- cf_get_pair_list."""
         k = C.c_int32()
         _cabi.check(self._lib.cf_get_pair_list(self._h, C.byref(k)), self._lib)
@@ -246,6 +245,30 @@ class HipCalcCoulForceKernel:
         _cabi.check(self._lib.cf_compute(self._h, C.c_void_p(positions.data_ptr()), _dp(b9),
                                          self._flags(includeForces, includeEnergy), C.c_void_p(fptr),
                                          C.c_void_p(eptr)), self._lib)
+
+    def execute_openmm(self, posq, atom_index, padded_n, box=None, includeForces=True, includeEnergy=True,
+                       force_buffer=None, energy_buffer=None, posq_correction=None):
+        """Execute on an OpenMM GPU platform's own buffers (cf_compute_openmm; the reference's CUDA
+        platform binds them at CudaCoulKernels.cpp:523-600): posq (N, 4) float64 or float32 torch
+        tensor in the platform's sorted order, atom_index (N,) int32 (sorted slot -> atom),
+        force_buffer (3 * padded_n,) int64 fixed point (2^-32 kJ/mol/nm, x | y | z planes by sorted
+        slot) ADDED to, energy_buffer a one-element float64 / float32 tensor ADDED to; posq_correction
+        (N, 4) float32 for the mixed-precision platform.  posq is never written."""
+        import torch
+        kind = _cabi.CF_POSQ_FLOAT4 if posq.dtype == torch.float32 else _cabi.CF_POSQ_DOUBLE4
+        ekind = _cabi.CF_ENERGY_FLOAT if (energy_buffer is not None and energy_buffer.dtype == torch.float32) \
+            else _cabi.CF_ENERGY_DOUBLE
+        b9 = _box9(box)
+        ptr = lambda t: C.c_void_p(t.data_ptr()) if t is not None else None
+        _cabi.check(self._lib.cf_compute_openmm(self._h, ptr(posq), ptr(posq_correction), kind, ptr(atom_index),
+                                                int(padded_n), _dp(b9), self._flags(includeForces, includeEnergy),
+                                                ptr(force_buffer), ptr(energy_buffer), ekind), self._lib)
+
+    def device_errors(self):
+        """CF_GUARD_* bits of the device index guards tripped so far (0 = none; synchronises)."""
+        v = C.c_int32()
+        _cabi.check(self._lib.cf_get_device_errors(self._h, C.byref(v)), self._lib)
+        return v.value
 
     # split-phase (multi-GPU): begin -> all-reduce kspace_buffer -> end
     def begin(self, positions, box=None, includeForces=True, includeEnergy=True):

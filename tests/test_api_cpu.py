@@ -31,7 +31,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_api_version_and_error_without_device():
     lib = _cabi.load_library()
-    assert lib.cf_api_version() == 3   # 2: cf_params.one_4pi_eps0; 3: cf_options.handover, pair_list, variants, list_capacity
+    assert lib.cf_api_version() == 4   # 3: cf_options.handover, pair_list, variants, list_capacity; 4: guards, cf_compute_openmm
     if torch.cuda.is_available():
         pytest.skip("a HIP device is present")
     system, force, pos, box = ts.water_box(20, cutoff=0.4)

@@ -87,6 +87,47 @@ def test_graph_recaptures_for_new_buffers_and_flags():
     assert k.graph_stats()[0] == caps
 
 
+@pytest.mark.parametrize("case", ["C2", "w4k"])
+def test_graph_recapture_sequence_keeps_guards_clear(case):
+    """Regression for the round-5 illegal memory access (r5z, first attempt, inside
+    test_graph_recaptures_for_new_buffers_and_flags): the same call sequence -- graph mode, fresh
+    output buffers every call, an energy-only evaluation between force evaluations (each flag set
+    its own capture, so every segment re-captures in turn), then timing on (eager) -- repeated on
+    fresh handles, on C2 (per-atom full list) and on a 12k-atom box (cluster-pair list), with the
+    device index guards on.  Every call must give the eager handle's bits and no guard may trip
+    (cf_get_device_errors == 0): an index outside its buffer would be skipped and reported here
+    instead of faulting."""
+    if case == "C2":
+        system, force, pos, box = ts.make("C2")
+    else:
+        system, force, pos, box = ts.water_box(4000, cutoff=1.0, ewald_tol=1e-4, every_bond_angle=5)
+    stream = torch.cuda.current_stream().cuda_stream
+    pt = torch.tensor(pos, dtype=torch.float64, device="cuda")
+    ref = HipCalcCoulForceKernel(stream=stream, kspace_algo=2).initialize(system, force)
+    e0, f0 = ref.execute_host(pos, box)
+    for rep in range(3):
+        k = HipCalcCoulForceKernel(stream=stream, kspace_algo=2).initialize(system, force).set_graph(True)
+        for _ in range(3):
+            for buf in range(2):
+                f = torch.zeros_like(pt)
+                e = torch.zeros(1, dtype=torch.float64, device="cuda")
+                k.execute_device(pt, box, True, True, f, e)
+                torch.cuda.synchronize()
+                assert e.item() == e0 and np.array_equal(f.cpu().numpy(), f0), (rep, buf)
+            e = torch.zeros(1, dtype=torch.float64, device="cuda")
+            k.execute_device(pt, box, False, True, None, e)
+            torch.cuda.synchronize()
+            assert e.item() == pytest.approx(e0, rel=1e-12, abs=1e-9)
+        k.set_timing(True)
+        f = torch.zeros_like(pt)
+        k.execute_device(pt, box, True, True, f, None)
+        torch.cuda.synchronize()
+        assert np.array_equal(f.cpu().numpy(), f0)
+        assert k.device_errors() == 0
+        k.destroy()
+    assert ref.device_errors() == 0
+
+
 @pytest.mark.parametrize("world", [2, 4])
 def test_graph_segments_of_a_decomposed_step_are_bitwise_eager(world):
     """Multi-rank split calls (begin / direct / end) replayed as three graphs per rank, with the
@@ -201,6 +242,39 @@ def test_graph_replay_restores_reciprocal_dedq_split():
     torch.cuda.synchronize()
     assert k.graph_stats()[1] >= 1
     assert np.array_equal(k.dedq(), dq_ref)
+
+
+def test_graph_flag_alternation_without_host_syncs():
+    """The shape of test_graph_replay_restores_reciprocal_dedq_split, where the round-6 session r6c
+    saw an illegal memory access: graph mode on C2 (no skin), forces / energy-only / forces captures
+    and a replay queued back to back with no host synchronisation between the calls, repeated on
+    fresh handles.  Since round 6 every data-dependent index of the C2 kernels is guarded (cell and
+    grid-bin bounds that do not add up to the atoms become empty cells / bins, list entries past N,
+    a clear rebuild flag without a skin): a broken invariant shows as CF_GUARD_* bits here, and the
+    results must be the eager handle's bits."""
+    from openmmcoul import _cabi
+    system, force, pos, box = ts.make("C2")
+    stream = torch.cuda.current_stream().cuda_stream
+    pt = torch.tensor(pos, dtype=torch.float64, device="cuda")
+    ref = HipCalcCoulForceKernel(stream=stream, kspace_algo=2).initialize(system, force)
+    e0, f0 = ref.execute_host(pos, box)
+    for rep in range(8):
+        k = HipCalcCoulForceKernel(stream=stream, kspace_algo=2).initialize(system, force).set_graph(True)
+        fs = [torch.zeros_like(pt) for _ in range(3)]
+        es = [torch.zeros(1, dtype=torch.float64, device="cuda") for _ in range(4)]
+        k.execute_device(pt, box, True, True, fs[0], es[0])
+        k.execute_device(pt, box, False, True, None, es[1])
+        k.execute_device(pt, box, True, True, fs[1], es[2])
+        k.execute_device(pt, box, True, True, fs[2], es[3])
+        torch.cuda.synchronize()
+        bits = k.device_errors()
+        assert bits == 0, (rep, bits)
+        for f in fs:
+            assert np.array_equal(f.cpu().numpy(), f0), rep
+        assert [e.item() for e in es[:1] + es[2:]] == [e0, e0, e0], rep
+        assert es[1].item() == pytest.approx(e0, rel=1e-12, abs=1e-9)
+        k.destroy()
+    assert ref.device_errors() == 0
 
 
 @pytest.mark.parametrize("case", ["C2", "w4k"])
