@@ -1014,7 +1014,7 @@ static void launch_begin(cf_handle* H, const double* pos_dev, int flags, bool re
         } else if (forces || energy) {   // no owned atoms: a zero partial S(k) (all-reduced by the caller)
             int64_t cnt = 0;
             double* buf = cf::kspace_reduce_buffer(h, &cnt);
-            check_hip(hipMemsetAsync(buf, 0, sizeof(double) * cnt, h.stream), "memset S");
+            cf::launch_zero(h, buf, cnt);   // (a kernel, not a memset node, when captured: cf_kernels_core.hip)
             if (h.kspace_algo == 1) cf::launch_kspace_kvec(h);   // read by the coefficient pass
         }
     }

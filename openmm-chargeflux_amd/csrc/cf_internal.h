@@ -268,7 +268,8 @@ std::vector<double> erfc_table_deg(double xmax, int deg, double width, int max_m
 void launch_flux_terms(Handle& h, const double* pos);
 void launch_atoms_prep(Handle& h, const double* pos, bool skin_check);   // q, self term [, skin_flag |= moved > list_skin/2]
 void launch_cell_sort(Handle& h, const double* pos);
-void launch_force_rebuild(Handle& h);                   // skin_flag = 1
+void launch_force_rebuild(Handle& h);                   // skin_flag = 1 (a kernel: graph-capture safe)
+void launch_zero(Handle& h, double* p, int64_t n);      // p[0, n) = 0 (a kernel: graph-capture safe)
 void launch_nlist(Handle& h, const double* pos);
 void launch_cluster_list(Handle& h);                   // cluster table, bounding boxes, cluster-pair list (rebuild only)
 void launch_pairs_cluster(Handle& h, const double* pos, int include_forces);   // k_pairs_cq

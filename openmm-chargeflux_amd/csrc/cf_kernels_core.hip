@@ -1718,8 +1718,28 @@ void launch_cell_sort(Handle& h, const double* pos) {
                        h.err_dev);
 }
 
+// the rebuild flag set by a one-thread kernel, not hipMemsetD32Async: in graph mode a captured memset
+// node was seen to leave the flag clear when the direct chain's graph was replayed (C2, no skin:
+// the forces / energy-only / forces captures and a replay queued without host syncs,
+// CF_GUARD_REBUILD_FLAG, profiles/r06h_graph_flag_probe.txt); a kernel node is ordered like the
+// chain's other kernels
+__global__ void k_set_flag(int* __restrict__ flag) {
+    if (threadIdx.x == 0) *flag = 1;
+}
+
 void launch_force_rebuild(Handle& h) {
-    check_hip(hipMemsetD32Async(h.skin_flag, 1, 1, h.stream), "set rebuild flag");
+    hipLaunchKernelGGL(k_set_flag, dim3(1), dim3(64), 0, h.stream, h.skin_flag);
+}
+
+// zero-fill by a kernel, for the same reason (launch sequences that may be captured into graphs
+// use no memset nodes)
+__global__ void __launch_bounds__(256) k_zero(double* __restrict__ p, int64_t n) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) p[i] = 0.0;
+}
+
+void launch_zero(Handle& h, double* p, int64_t n) {
+    if (n <= 0) return;
+    hipLaunchKernelGGL(k_zero, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 2048)), dim3(256), 0, h.stream, p, n);
 }
 
 DirectArgs direct_args(Handle& h, const double* pos, int include_forces) {
