@@ -150,13 +150,15 @@ void bump_epoch(cf_handle* H) {
     graph_invalidate(H);
 }
 
-// neighbour-list capacity: the mean count within rc + skin at the default-box density,
-// split over kSeg = 4 sub-lists, x2 + margin (k_excl rescans the cells for any
-// atom that overflows, so this is a speed knob, not a correctness limit)
-void alloc_nlist(cf_handle* H, double skin) {
+// neighbour-list capacity: the mean count within rc + skin at the density of the denser of the
+// default box and the current one (v_current, 0 = not known yet), split over kSeg = 4 sub-lists,
+// x2 + margin (k_excl rescans the cells for any atom that overflows, so this is a speed knob, not
+// a correctness limit: a compressed box no longer sends rows to the slow rescan on every call)
+void alloc_nlist(cf_handle* H, double skin, double v_current = 0.0) {
     cf::Handle& h = H->h;
     const double* b = H->default_box;
     double V = b[0] * b[4] * b[8];
+    if (v_current > 0) V = std::min(V, v_current);
     double r = h.cutoff + skin;
     double mean = 4.0 / 3.0 * M_PI * r * r * r * h.n / V;
     int cap = (int)std::min<double>(h.n, 0.5 * mean + 64);
@@ -239,6 +241,8 @@ void set_cells(cf_handle* H, const double L[3]) {
         h.ncell_alloc = (int)ncell;
     }
     h.nc[0] = nc[0]; h.nc[1] = nc[1]; h.nc[2] = nc[2];
+    // the per-atom lists' capacity follows the current box's density too (grows only)
+    if (h.nl) alloc_nlist(H, h.list_skin, L[0] * L[1] * L[2]);
     // half neighbour list: one rank (fp64 or mixed), the wave-cooperative builder (>= 4
     // cells per axis), cells small enough for the kernel's LDS window (18 cells <= 4096 atoms,
     // with a margin for density variation: k_pairs_half flags the rare evaluation that does not

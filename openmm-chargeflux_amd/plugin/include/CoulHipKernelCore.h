@@ -11,6 +11,9 @@
 #ifndef COUL_HIP_KERNEL_CORE_H_
 #define COUL_HIP_KERNEL_CORE_H_
 
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
 #include <stdexcept>
 #include <string>
 
@@ -93,7 +96,21 @@ public:
         double e = 0.0;
         check(cf_compute_host(h_, pos, pbc_ ? box9 : nullptr, flags(include_forces, include_energy), forces_accum, &e),
               "cf_compute_host");
+        watch_fallbacks();   // (the host path has synchronised: one small read)
         return e;
+    }
+
+    // an OpenMM GPU platform's own buffers (cf_compute_openmm: posq + atomIndex in, 2^32 fixed-point
+    // force planes and an energy-buffer element out -- the conventions the reference's CUDA
+    // platform binds, CudaCoulKernels.cpp:523-600); asynchronous on the handle's stream
+    void execute_openmm(const void* posq, const void* posq_correction, int posq_kind, const int* atom_index,
+                        int padded_n, const double* box9, bool include_forces, bool include_energy,
+                        long long* force_buf, void* energy_buf, int energy_kind) {
+        require();
+        check(cf_compute_openmm(h_, posq, posq_correction, posq_kind, atom_index, padded_n, pbc_ ? box9 : nullptr,
+                                flags(include_forces, include_energy), force_buf, energy_buf, energy_kind),
+              "cf_compute_openmm");
+        if (++device_calls_ % kFallbackPoll == 0) watch_fallbacks();   // (synchronises: amortised)
     }
 
     // the same on device buffers (a HIP platform's positions / forces): asynchronous on the stream
@@ -103,10 +120,20 @@ public:
         check(cf_compute(h_, pos_dev, pbc_ ? box9 : nullptr, flags(include_forces, include_energy), forces_dev,
                          energy_dev),
               "cf_compute");
+        if (++device_calls_ % kFallbackPoll == 0) watch_fallbacks();
     }
 
     cf_handle* handle() const { return h_; }
     int num_particles() const { return n_; }
+
+    // Evaluations that fell back to the fp64 cell rescan (cf_get_fallback_stats: a neighbour list
+    // or window that overflowed, a term beyond the fixed-point range) -- correct, several times
+    // slower.  The first one seen is reported once on stderr (COUL_HIP_QUIET=1 silences it); this
+    // counter stays readable.
+    long long fallback_evaluations() {
+        watch_fallbacks();
+        return fallbacks_;
+    }
 
 private:
     static int flags(bool f, bool e) { return (f ? CF_INCLUDE_FORCES : 0) | (e ? CF_INCLUDE_ENERGY : 0); }
@@ -117,10 +144,32 @@ private:
         if (h_) cf_destroy(h_);
         h_ = nullptr;
     }
+    static constexpr long long kFallbackPoll = 1000;   // device-path calls between checks
+    void watch_fallbacks() {
+        if (!h_) return;
+        int64_t evals = 0, rows = 0;
+        int32_t reasons = 0;
+        if (cf_get_fallback_stats(h_, &evals, &rows, &reasons) != CF_OK) return;
+        const long long total = (long long)evals + (long long)rows;
+        if (total > fallbacks_ && !warned_) {
+            warned_ = true;
+            const char* quiet = std::getenv("COUL_HIP_QUIET");
+            if (!quiet || quiet[0] != '1')
+                std::fprintf(stderr,
+                             "CoulForce (HIP): %lld evaluation(s) took the fp64 rescan fallback and %lld list row(s) "
+                             "were rescanned (reasons 0x%x: 1 = cell window full, 2 = list overflow, 4 = fixed-point "
+                             "range) -- correct but slow; check the neighbour-list capacity and cell geometry "
+                             "(DESIGN.md 4.4). Reported once.\n",
+                             (long long)evals, (long long)rows, (unsigned)reasons);
+        }
+        fallbacks_ = total;
+    }
     cf_handle* h_ = nullptr;
     int n_ = 0;
     bool pbc_ = false;
     double ke_ = 0.0;
+    long long device_calls_ = 0, fallbacks_ = 0;
+    bool warned_ = false;
 };
 
 }  // namespace coulhip

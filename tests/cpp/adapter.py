@@ -25,6 +25,7 @@ def load():
     L = C.CDLL(LIB)
     L.cfa_last_error.restype = C.c_char_p
     L.cfa_marshal.argtypes = [C.POINTER(Flat), C.c_int, DP, DP, DP, DP, IP, IP, DP, IP, DP, IP, DP, DP, DP]
+    L.cfa_execute_count.argtypes = [C.POINTER(Flat), DP, C.c_int, DP, DP, C.c_int, DP, DP, C.POINTER(C.c_longlong)]
     L.cfa_execute.argtypes = [C.POINTER(Flat), C.POINTER(Flat), DP, C.c_int, C.c_int, DP, DP, C.c_int, C.c_int,
                               DP, DP]
     return L
@@ -89,3 +90,22 @@ def execute(force, default_box, pos, box, kspace_algo=2, precision=0, include_fo
         raise RuntimeError(f"cfa_execute failed ({rc}): {L.cfa_last_error().decode()}")
     del keep, keep2
     return e.value, forces
+
+
+def execute_count(force, default_box, pos, box, calls, kspace_algo=2):
+    """KernelCore::initialize + `calls` x execute_host -> (energy, forces summed over the calls,
+    KernelCore::fallback_evaluations())."""
+    L = load()
+    f, keep = flat(force)
+    db = np.ascontiguousarray(np.asarray(default_box, np.float64).reshape(9))
+    b9 = np.ascontiguousarray(np.asarray(box, np.float64).reshape(9))
+    p = np.ascontiguousarray(np.asarray(pos, np.float64).reshape(-1, 3))
+    forces = np.zeros_like(p)
+    e = C.c_double()
+    n = C.c_longlong()
+    rc = L.cfa_execute_count(C.byref(f), db.ctypes.data_as(DP), kspace_algo, p.ctypes.data_as(DP),
+                             b9.ctypes.data_as(DP), int(calls), forces.ctypes.data_as(DP), C.byref(e), C.byref(n))
+    if rc:
+        raise RuntimeError(f"cfa_execute_count failed ({rc}): {L.cfa_last_error().decode()}")
+    del keep
+    return e.value, forces, n.value

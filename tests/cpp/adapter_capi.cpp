@@ -117,4 +117,20 @@ __attribute__((visibility("default"))) int cfa_execute(const Flat* f, const Flat
     });
 }
 
+// Initialize on f and execute `calls` times on host arrays; *fallbacks = KernelCore::fallback_evaluations()
+// (the plugin's slow-path counter; its first increase is reported once on stderr)
+__attribute__((visibility("default"))) int cfa_execute_count(const Flat* f, const double* default_box, int kspace_algo,
+                                                             const double* pos, const double* box9, int calls,
+                                                             double* forces, double* energy, long long* fallbacks) {
+    return guarded([&] {
+        CoulPlugin::CoulForce force = build(*f);
+        coulhip::Options o;
+        o.kspace_algo = kspace_algo;
+        coulhip::KernelCore core;
+        core.initialize(force, f->n, default_box, o);
+        for (int c = 0; c < calls; c++) *energy = core.execute_host(pos, box9, true, true, forces);
+        *fallbacks = core.fallback_evaluations();
+    });
+}
+
 }  // extern "C"

@@ -76,3 +76,21 @@ def test_plugin_parameter_update_matches_oracle(_gpu):
     ref = Oracle(f2, box).execute(pos, box)
     assert abs(e - ref["energy"]) <= 1e-9 * abs(ref["energy"]) + 1e-8
     assert np.abs(f - ref["forces"]).max() <= 1e-8
+
+
+@pytest.mark.gpu
+def test_plugin_reports_the_rescan_fallback_once(_gpu, capfd):
+    """Two waters 0.02 nm apart: a partner-side term beyond the half list's fixed-point range sends
+    every evaluation to the fp64 rescan (correct, slow).  The plugin counts them
+    (KernelCore::fallback_evaluations) and says so once on stderr, not once per step."""
+    system, force, pos, box = ts.water_box(4000, cutoff=1.0, ewald_tol=1e-4)
+    p = pos.copy()
+    p[3:6] = p[0:3] + np.array([0.02, 0.0, 0.0])
+    e, f, n = adapter.execute_count(force, box, p, box, 3)
+    assert n >= 3, n
+    err = capfd.readouterr().err
+    assert err.count("fp64 rescan fallback") == 1, err
+    # a normal box: no fallback, no message
+    e, f, n = adapter.execute_count(force, box, pos, box, 2)
+    assert n == 0
+    assert "fallback" not in capfd.readouterr().err
