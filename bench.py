@@ -480,6 +480,31 @@ def main():
         host = {"ms_per_force_eval": round(ms_h, 4), "bytes_h2d": int(pos_h.nbytes), "bytes_d2h": int(f_h.nbytes),
                 "note": "cf_compute_host with host positions/forces, wall clock over 20 calls (each syncs); "
                         "compare ms_per_force_eval (device-resident)"}
+    openmm_buf = None
+    if world == 1 and not args.no_exact_compare:
+        # an OpenMM GPU platform's own buffers (cf_compute_openmm: sorted posq + atomIndex in,
+        # 2^32 fixed-point force planes and an energy element out; no copies): the device-resident
+        # rate through that boundary, events around each call as ms_per_force_eval's pass
+        perm = torch.randperm(n, generator=torch.Generator().manual_seed(3)).to(dev)
+        posq = torch.cat([pos[perm], torch.zeros(n, 1, dtype=torch.float64, device=dev)], 1).contiguous()
+        aidx = perm.to(torch.int32).contiguous()
+        padded = (n + 31) // 32 * 32
+        fbuf = torch.zeros(3 * padded, dtype=torch.int64, device=dev)
+        ebuf = torch.zeros(1, dtype=torch.float64, device=dev)
+        for _ in range(3):
+            kern.kernel.execute_openmm(posq, aidx, padded, box, True, True, fbuf, ebuf)
+        evs = []
+        for _ in range(args.steps):
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            kern.kernel.execute_openmm(posq, aidx, padded, box, True, True, fbuf, ebuf)
+            b.record()
+            evs.append((a, b))
+        torch.cuda.synchronize()
+        openmm_buf = {"ms_per_force_eval": round(float(np.mean([a.elapsed_time(b) for a, b in evs])), 4),
+                      "note": "cf_compute_openmm on OpenMM GPU-platform buffers (double4 posq in a shuffled "
+                              "atomIndex order, long long force planes of paddedNumAtoms); compare "
+                              "ms_per_force_eval"}
 
     if rank == 0:
         cpu = None
@@ -521,6 +546,7 @@ def main():
             "kernels_roofline": others,
             "exact_kspace": exact,
             "host_boundary": host,
+            "openmm_gpu_buffers": openmm_buf,
             "cpu_baseline": cpu,
         }
         if cpu:
