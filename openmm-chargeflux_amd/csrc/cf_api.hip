@@ -767,7 +767,10 @@ CF_EXPORT int cf_create(const cf_params* p, const cf_options* opt, cf_handle** o
                     check_hip(hipMemcpy(h.g_xrange, init, sizeof(init), hipMemcpyHostToDevice), "x-slab init");
                 }
                 h.t_part = dalloc<double>(H, no * 4);
-                h.e_rec_part = dalloc<double>(H, (size_t)(gp.NX * gp.NY * gp.KZ + 255) / 256 + 1);
+                // energy partials: k_g_coeffs' blocks of 256 modes, or the fused forward x stage's blocks
+                // of >= 16 sequences (one rank, launch_grid_dft_fwd)
+                h.e_rec_part = dalloc<double>(H, std::max<size_t>((size_t)(gp.NX * gp.NY * gp.KZ + 255) / 256,
+                                                                  (size_t)gp.NY * gp.KZ / 16 + 2) + 1);
             } else {
                 int blocks_k = (int)((h.khalf + 255) / 256);
                 h.sk_nchunk = std::max(1, std::min((2048 + blocks_k - 1) / blocks_k, std::max(1, nown / 256)));

@@ -954,6 +954,17 @@ struct Dft8 {
     int W, ngx;
 };
 
+// the coefficient pass (k_g_coeffs) fused into the forward x stage on one rank (COEF): the stage
+// writes f = w_z c a conj(S) / phih instead of B, and its blocks' energy partials (round 6: one
+// launch and one pass over B fewer on the reciprocal chain's exposed tail)
+struct Coef {
+    int KX, KY, KZ;
+    double3 rec;
+    double cst, one_4a2;
+    const double *dx, *dy, *dz;
+    double* e_part;
+};
+
 constexpr int kD8Seq = 64, kD8BC = 8;
 constexpr int kDft8Mt[] = {4, 8, 9, 16, 17};   // class-size paddings instantiated (CF_D8_MT)
 
@@ -988,9 +999,9 @@ __device__ __forceinline__ void cmac(v2d& acc, v2d y, double2 t) {
 // thread does one (sequence, b) 8-point DFT per chunk; the next chunk's 8 inputs are loaded
 // into registers before the current chunk's class sums, so the global latency overlaps the
 // FMAs.  The twist table (class-dependent) is read from LDS, the [Q][mt] rows as scalar loads.
-template <int MT, bool CIN, int SEQ>
+template <int MT, bool CIN, int SEQ, bool COEF = false>
 __global__ void __launch_bounds__(8 * SEQ) k_g_dft8_fwd(Dft8 d, const double2* __restrict__ twist,
-                                                        const double2* __restrict__ tq) {
+                                                        const double2* __restrict__ tq, Coef cf = Coef{}) {
     constexpr int NR = CIN ? 8 : 5, SP = SEQ + 1, NT = 8 * SEQ;
     extern __shared__ v2d sm8[];
     v2d* sY = sm8;                       // [kD8BC][NR][SP]
@@ -1055,12 +1066,52 @@ __global__ void __launch_bounds__(8 * SEQ) k_g_dft8_fwd(Dft8 d, const double2* _
         __syncthreads();
     }
     const int s = s0 + sq;
-    if (s >= d.nseq) return;
-    const long base = (long)(s / d.sdiv) * d.c1 + (long)(s % d.sdiv) * d.c0;
-    const int cnt = d.rc[r], j0 = d.rj[r];
+    if constexpr (!COEF) {
+        if (s >= d.nseq) return;
+        const long base = (long)(s / d.sdiv) * d.c1 + (long)(s % d.sdiv) * d.c0;
+        const int cnt = d.rc[r], j0 = d.rj[r];
 #pragma unroll
-    for (int t = 0; t < MT; t++)
-        if (t < cnt) reinterpret_cast<v2d*>(d.out)[base + (long)(j0 + 8 * t) * d.cj] = acc[t];
+        for (int t = 0; t < MT; t++)
+            if (t < cnt) reinterpret_cast<v2d*>(d.out)[base + (long)(j0 + 8 * t) * d.cj] = acc[t];
+    } else {
+        // x stage: sequence s = (ny index, nz), mode j = nx + KX - 1 -- the element k_g_coeffs
+        // calls t = (j NY + ny index) KZ + nz; the same coefficient and energy per element
+        // (RCK:528, 549-551), the energy summed per block in a fixed order
+        __shared__ double red[8 * SEQ / 64];
+        double e = 0;
+        if (s < d.nseq) {
+            const long base = (long)(s / d.sdiv) * d.c1 + (long)(s % d.sdiv) * d.c0;
+            const int cnt = d.rc[r], j0 = d.rj[r];
+            const int nz = s % cf.KZ, ny = s / cf.KZ - (cf.KY - 1);
+            const double ky = ny * cf.rec.y, kz = nz * cf.rec.z;
+            const double wz = nz > 0 ? 2.0 : 1.0;
+            const double Dyz = cf.dy[abs(ny)] * cf.dz[nz];
+#pragma unroll
+            for (int t = 0; t < MT; t++) {
+                if (t < cnt) {
+                    const int j = j0 + 8 * t, nx = j - (cf.KX - 1);
+                    const double kx = nx * cf.rec.x;
+                    const double k2 = kx * kx + ky * ky + kz * kz;
+                    const double a = k2 > 0 ? exp(-k2 * 0.25 * cf.one_4a2) / k2 : 0.0;
+                    const double D = cf.dx[abs(nx)] * Dyz;
+                    const double sr = acc[t].x * D, si = acc[t].y * D;
+                    e += 0.5 * wz * cf.cst * a * (sr * sr + si * si);
+                    const double c = wz * cf.cst * a * D;
+                    reinterpret_cast<v2d*>(d.out)[base + (long)j * d.cj] = v2d{c * sr, -c * si};
+                }
+            }
+        }
+#pragma unroll
+        for (int m = 32; m >= 1; m >>= 1) e += __shfl_xor(e, m);
+        if (lane == 0) red[wave_id()] = e;
+        __syncthreads();
+        if (tid == 0) {
+            double tot = 0;
+#pragma unroll
+            for (int w = 0; w < 8 * SEQ / 64; w++) tot += red[w];
+            cf.e_part[blockIdx.x] = tot;
+        }
+    }
 }
 
 // analysis along z of the real grid rows (contiguous along n): 8 rows per block, NB waves;
@@ -2267,7 +2318,7 @@ static Dft8 d8_stage(const Handle& h, int axis) {
         default: CALL(17); break; \
     }
 
-static void d8_fwd(Handle& h, int axis, const void* in, void* out) {
+static void d8_fwd(Handle& h, int axis, const void* in, void* out, const Coef* cf = nullptr) {
     Dft8 d = d8_stage(h, axis);
     d.in = in; d.out = out;
     const int nb = nblk(d.nseq, kD8Seq);
@@ -2289,6 +2340,16 @@ static void d8_fwd(Handle& h, int axis, const void* in, void* out) {
     const int seq = small ? 16 : 64;
     const dim3 grid((unsigned)nblk(d.nseq, seq));
     const size_t lds2 = (size_t)(kD8BC * (axis == 2 ? 5 : 8) * (seq + 1) + 8 * d.Q) * sizeof(double2);
+    if (cf) {   // the x stage with the coefficient pass fused (one rank): its blocks' energy partials
+        h.e_rec_nblk = (int)grid.x;
+#define CF_D8FC_(MT_, SEQ_) \
+    hipLaunchKernelGGL((k_g_dft8_fwd<MT_, true, SEQ_, true>), grid, dim3(8 * SEQ_), lds2, h.stream, d, twist, tq, *cf)
+#define CF_D8FC(MT_) if (small) CF_D8FC_(MT_, 16); else CF_D8FC_(MT_, 64);
+        CF_D8_MT(h.gp.mt[axis], CF_D8FC)
+#undef CF_D8FC
+#undef CF_D8FC_
+        return;
+    }
 #define CF_D8F_(MT_, CIN_, SEQ_) \
     hipLaunchKernelGGL((k_g_dft8_fwd<MT_, CIN_, SEQ_>), grid, dim3(8 * SEQ_), lds2, h.stream, d, twist, tq)
 #define CF_D8F(MT_)                                         \
@@ -2327,12 +2388,28 @@ static void d8_inv(Handle& h, int axis, const void* in, void* out) {
 #undef CF_D8I
 }
 
+// one rank with the factorized stages: the coefficient pass rides on the forward x stage (there
+// is no all-reduce of B(n) between them); several ranks reduce B(n) first (launch_grid_coeffs)
+static bool coef_fused(const Handle& h) { return h.gp.dft8 && h.world == 1; }
+
+static Coef coef_args(const Handle& h) {
+    const GridPlan& p = h.gp;
+    const double V = h.box_L[0] * h.box_L[1] * h.box_L[2];
+    return Coef{p.KX, p.KY, p.KZ, recip_vec(h), 4.0 / V * kPi * h.ke, 1.0 / (h.alpha * h.alpha), h.g_deconv[0],
+                h.g_deconv[1], h.g_deconv[2], h.e_rec_part};
+}
+
 void launch_grid_dft_fwd(Handle& h) {
     const GridPlan& p = h.gp;
     if (p.dft8) {
         d8_fwd(h, 2, h.g_grid, h.g_t1);
         d8_fwd(h, 1, h.g_t1, h.g_t2);
-        d8_fwd(h, 0, h.g_t2, h.g_b);
+        if (coef_fused(h)) {
+            const Coef cf = coef_args(h);
+            d8_fwd(h, 0, h.g_t2, h.g_b, &cf);
+        } else {
+            d8_fwd(h, 0, h.g_t2, h.g_b);
+        }
         return;
     }
     const int ngx = p.ng[0], ngy = p.ng[1], ngz = p.ng[2], KZ = p.KZ, NY = p.NY, NX = p.NX;
@@ -2354,6 +2431,7 @@ double* grid_reduce_buffer(Handle& h, int64_t* count) {
 }
 
 void launch_grid_coeffs(Handle& h, int include_energy) {
+    if (coef_fused(h)) return;   // done by the forward x stage (launch_grid_dft_fwd)
     const GridPlan& p = h.gp;
     const double V = h.box_L[0] * h.box_L[1] * h.box_L[2];
     const double cst = 4.0 / V * kPi * h.ke;   // RCK:517
