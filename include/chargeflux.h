@@ -115,8 +115,10 @@ typedef struct cf_options {
                             Same pair set and the same results up to the fp64 summation order. */
     int32_t variants;    /* CF_VARIANT_* bits: alternative kernels of the same sums, kept for A/B
                             verification (0 = the production kernels) */
-    int32_t list_capacity;   /* cluster-pair list entries per i-cluster; 0 = automatic.  A list that
-                            overflows it is evaluated by the fp64 rescan (slow, same results). */
+    int32_t list_capacity;   /* neighbour-list capacity cap: cluster-pair entries per i-cluster, and
+                            entries per sub-list of the per-atom lists; 0 = automatic (the density of
+                            the denser of the default and the current box).  A list that overflows it
+                            is evaluated by the fp64 rescan (slow, same results; tests force it). */
     int32_t reserved[1];
 } cf_options;
 

@@ -162,6 +162,7 @@ void alloc_nlist(cf_handle* H, double skin, double v_current = 0.0) {
     double r = h.cutoff + skin;
     double mean = 4.0 / 3.0 * M_PI * r * r * r * h.n / V;
     int cap = (int)std::min<double>(h.n, 0.5 * mean + 64);
+    if (h.list_capacity > 0) cap = std::max(4, std::min(cap, h.list_capacity));   // cf_options.list_capacity
     const size_t rows = std::max(h.hi - h.lo, 1);  // one row per owned atom
     // a sub-list's entries are addressed by 32-bit offsets from its row (k_nlist_wave): cap * rows
     // < 2^31 (a clamped capacity only sends more rows to the overflow rescan)

@@ -304,7 +304,8 @@ __global__ void __launch_bounds__(kCqThreads) CF_LDS_UNPAIRED k_pairs_cq(DirectA
     __shared__ int wdel[kHalfWin];          // window offset - first sorted slot
     __shared__ float4 shf[kHalfWin];        // corner offset of each window cell (phase A, window_cell)
     __shared__ double3 shd[kHalfWin];       // wrap translation of each window cell (phase B, window_cell)
-    __shared__ unsigned long long accw[4][kHalfMaxWin];   // j-side fx, fy, fz, dE/dq (fixed point)
+    // j-side fx, fy, fz, dE/dq in fixed point: 64-bit (2^-34) in fp64, 32-bit (2^-13) in mixed precision
+    __shared__ std::conditional_t<MIXED, unsigned, unsigned long long> accw[4][kHalfMaxWin];
     __shared__ int qbuf[kCqWaves][4][kCqQ];  // per wave, per i atom: ring of hit entries
     __shared__ int wtot, next_ci, nown;
     const int3 nc = a.nc;
@@ -469,10 +470,10 @@ __global__ void __launch_bounds__(kCqThreads) CF_LDS_UNPAIRED k_pairs_cq(DirectA
                         acc.fx += fx; acc.fy += fy; acc.fz += fz;
                         acc.dq = fmaf(qj, ec, acc.dq);
                         bad |= !(fmaxf(fmaxf(fabsf(fx), fabsf(fy)), fmaxf(fabsf(fz), fabsf(dqj))) < (float)kFixMax);
-                        atomicAdd(&accw[0][slot], to_fix(-(double)fx));
-                        atomicAdd(&accw[1][slot], to_fix(-(double)fy));
-                        atomicAdd(&accw[2][slot], to_fix(-(double)fz));
-                        atomicAdd(&accw[3][slot], to_fix((double)dqj));
+                        atomicAdd(&accw[0][slot], to_fix32(-fx));
+                        atomicAdd(&accw[1][slot], to_fix32(-fy));
+                        atomicAdd(&accw[2][slot], to_fix32(-fz));
+                        atomicAdd(&accw[3][slot], to_fix32(dqj));
                     }
                     acc.e += (double)fmaf(qq, ec, es6 * (sig6 - 1.0f));   // the whole pair energy
                 }
@@ -619,9 +620,14 @@ __global__ void __launch_bounds__(kCqThreads) CF_LDS_UNPAIRED k_pairs_cq(DirectA
     }
     if (!a.include_forces) return;
     __syncthreads();
-    unsigned long long* out = a.win_out + (size_t)cell * kHalfMaxWin * 4;
-    for (int e = threadIdx.x; e < nw; e += kCqThreads)
-        reinterpret_cast<ulonglong4*>(out)[e] = make_ulonglong4(accw[0][e], accw[1][e], accw[2][e], accw[3][e]);
+    if constexpr (MIXED) {   // 16 B per slot (k_excl reads win_out as uint4 when DirectArgs::win32)
+        uint4* out = reinterpret_cast<uint4*>(a.win_out) + (size_t)cell * kHalfMaxWin;
+        for (int e = threadIdx.x; e < nw; e += kCqThreads) out[e] = make_uint4(accw[0][e], accw[1][e], accw[2][e], accw[3][e]);
+    } else {
+        unsigned long long* out = a.win_out + (size_t)cell * kHalfMaxWin * 4;
+        for (int e = threadIdx.x; e < nw; e += kCqThreads)
+            reinterpret_cast<ulonglong4*>(out)[e] = make_ulonglong4(accw[0][e], accw[1][e], accw[2][e], accw[3][e]);
+    }
     };   // process
     process(cell0 + xcd_block());
     {

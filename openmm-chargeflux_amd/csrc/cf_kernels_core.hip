@@ -1254,16 +1254,27 @@ __device__ __forceinline__ void half_window_sums(const DirectArgs& a, int s, dou
             b[u] = (wrap_cell(cx - o.x, nc.x) * nc.y + wrap_cell(cy - o.y, nc.y)) * nc.z + wrap_cell(cz - o.z, nc.z);
             slot[u] = a.win_woff[b[u] * kHalfWin + k0 + u] + jj;
         }
-        ulonglong4 v[kBatch];
+        if (a.win32) {   // (kernel-uniform) 32-bit sums, 16 B per slot
+            uint4 v[kBatch];
 #pragma unroll
-        for (int u = 0; u < kBatch; u++) v[u] = reinterpret_cast<const ulonglong4*>(a.win_out)[(size_t)b[u] * kHalfMaxWin + slot[u]];
+            for (int u = 0; u < kBatch; u++) v[u] = reinterpret_cast<const uint4*>(a.win_out)[(size_t)b[u] * kHalfMaxWin + slot[u]];
 #pragma unroll
-        for (int u = 0; u < kBatch; u++) {
-            sx += (long long)v[u].x; sy += (long long)v[u].y; sz += (long long)v[u].z; sq += (long long)v[u].w;
+            for (int u = 0; u < kBatch; u++) {
+                sx += (int)v[u].x; sy += (int)v[u].y; sz += (int)v[u].z; sq += (int)v[u].w;
+            }
+        } else {
+            ulonglong4 v[kBatch];
+#pragma unroll
+            for (int u = 0; u < kBatch; u++) v[u] = reinterpret_cast<const ulonglong4*>(a.win_out)[(size_t)b[u] * kHalfMaxWin + slot[u]];
+#pragma unroll
+            for (int u = 0; u < kBatch; u++) {
+                sx += (long long)v[u].x; sy += (long long)v[u].y; sz += (long long)v[u].z; sq += (long long)v[u].w;
+            }
         }
     }
-    f = make_double3((double)sx * kFixInv, (double)sy * kFixInv, (double)sz * kFixInv);
-    dq = (double)sq * kFixInv;
+    const double inv = a.win32 ? kFix32Inv : kFixInv;
+    f = make_double3((double)sx * inv, (double)sy * inv, (double)sz * inv);
+    dq = (double)sq * inv;
 }
 
 // ---------------------------------------------------------------------------------
@@ -1778,6 +1789,7 @@ DirectArgs direct_args(Handle& h, const double* pos, int include_forces) {
     a.cl_start = h.cl_start; a.cl_info = h.cl_info; a.cpl = h.cpl; a.cpl_cnt = h.cpl_cnt; a.cpl_cap = h.cpl_cap;
     a.pos4f = h.pos4f; a.slot_of = h.slot_of;
     a.ncl_cap = h.ncl_cap;
+    a.win32 = h.mixed && h.cluster ? 1 : 0;
     a.err = h.err_dev;
     {   // fp32 prefilter: |d| from fp32 coordinates of magnitude <= ~2 L carries an error below 8 ulp(L)
         const double Lmax = std::max(h.box_L[0], std::max(h.box_L[1], h.box_L[2])) + std::fabs(h.box_t[0]) +

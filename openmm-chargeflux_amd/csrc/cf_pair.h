@@ -91,6 +91,13 @@ constexpr double kFixInv = 1.0 / 17179869184.0;
 constexpr double kFixMagic = 6755399441055744.0;       // 1.5 * 2^52
 constexpr long long kFixMagicBits = 0x4338000000000000LL;
 constexpr double kFixMax = 65536.0;
+// mixed precision on the cluster-pair list (DirectArgs::win32): the partner-side sums in 32-bit fixed
+// point, 2^-13 kJ/mol/nm (1.2e-4: below the fp32 pair terms' own rounding at |F| ~ 1e3, against the
+// C5 bar of 1e-4 RMS relative), range +-2^18 per window slot; half the LDS window (64 KB) and half
+// of win_out's bytes written by the pair kernel and read back by k_excl
+constexpr float kFix32Scale = 8192.0f;   // 2^13
+constexpr double kFix32Inv = 1.0 / 8192.0;
+__device__ __forceinline__ unsigned to_fix32(float v) { return (unsigned)__float2int_rn(v * kFix32Scale); }
 // why half_flag was raised (bits; cf_get_fallback_stats reports their union)
 constexpr int kHalfWindowFull = 1;     // a cell's 18-cell window holds more than kHalfMaxWin atoms
 constexpr int kHalfListOverflow = 2;   // a row's sub-list overflowed, or the builder could not place it
@@ -140,6 +147,7 @@ struct DirectArgs {
     const int* slot_of;         // [N] atom -> sorted slot
     float rcm2f;                // prefilter radius^2: rc with a margin above the fp32 rounding of |d|
     int ncl_cap;                // clusters cl_info / cpl_cnt / cpl hold
+    int win32;                  // win_out holds 32-bit fixed-point sums (uint4 per slot): mixed precision, cluster list
     int* err;                   // [1] device index guards (kGuard* bits, cf_internal.h)
 };
 

@@ -220,8 +220,11 @@ def test_c5_mixed_rank_split(c5, world):
     # one rank walks the half list (each pair once), four ranks the full list: the fp32 pair
     # terms round differently (observed |dE| 2.6e-3 kJ/mol = 2e-11 of sum|terms|)
     assert abs(e4 - e1) <= 1e-10 * np.abs(t1).sum()
-    # fp32 per-lane force sums: the list kind and a rank's lanes-per-atom choice change their rounding
-    assert np.abs(f4 - f1).max() <= 1e-6 * np.abs(f1).max()
+    # fp32 per-lane force sums: the list kind and a rank's lanes-per-atom choice change their rounding;
+    # since round 6 the one-rank cluster list also rounds each partner-side term to the 32-bit fixed
+    # point's 2^-13 kJ/mol/nm (cf_pair.h kFix32Scale; observed 6.1e-3 = 2.4e-6 max|F| at 4 ranks),
+    # far inside the C5 accuracy bar against fp64 (RMS relative 1e-4, test_c5_mixed_precision_vs_fp64)
+    assert np.abs(f4 - f1).max() <= 5e-6 * np.abs(f1).max()
 
 
 def test_c5_dft8_matches_gemm_stages(c5):

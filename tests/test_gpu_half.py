@@ -30,8 +30,8 @@ def _need_gpu():
 
 def _kernel(system, force, half, algo=0, skin=0.0, precision="double", cluster=True, cap=0):
     """half: the half list (the cluster-pair form unless cluster=False: the per-atom half list);
-    else the full two-sided list (cf_options.pair_list); cap: a cluster-pair list capacity that
-    overflows (cf_options.list_capacity)."""
+    else the full two-sided list (cf_options.pair_list); cap: a list capacity that overflows
+    (cf_options.list_capacity: cluster-pair entries per i-cluster, per-atom entries per sub-list)."""
     pl = ("cluster" if cluster else "atom_half") if half else "full"
     k = HipCalcCoulForceKernel(kspace_algo=algo, precision=precision, pair_list=pl,
                                list_capacity=cap).initialize(system, force)
@@ -80,14 +80,15 @@ def test_half_list_bitwise_reproducible_with_skin():
 
 
 def test_half_list_fallback_on_list_overflow():
-    # a default box 2.5x wider sizes the list capacity for a 16x lower density: every list
-    # overflows, the half-list evaluation is flagged and k_excl rescans every atom in fp64
+    # a list capacity (cf_options.list_capacity) far below the density: every list overflows, the
+    # half-list evaluation is flagged and k_excl rescans every atom in fp64.  (Before round 6 a
+    # default box 2.5x wider did this; the capacity now also follows the current box's density.)
     system, force, pos, box = ts.water_box(4000, cutoff=1.0, ewald_tol=1e-4)
     big = [[2.5 * box[i][j] for j in range(3)] for i in range(3)]
     system.setDefaultPeriodicBoxVectors(*big)
     # (the checker is the full-list kernel on the same default box: the oracle's k-sum over the
     # 16x larger k-vector set of the wide default box takes minutes on one host core)
-    k = _kernel(system, force, True, cluster=False)   # (the cluster list sizes itself from the current box)
+    k = _kernel(system, force, True, cluster=False, cap=24)
     ef, ff = _kernel(system, force, False).execute_host(pos, box)
     for _ in range(2):
         e, f = k.execute_host(pos, box)
@@ -115,13 +116,14 @@ def _sparse_gas():
 
 
 def _dense_overflow():
-    # list capacity sized for a 16x lower density (as test_half_list_fallback_on_list_overflow)
+    # a default box 2.5x larger (16x lower density); since round 6 the automatic capacity follows the
+    # current box too, so the overflow is forced with cf_options.list_capacity
     system, force, pos, box = ts.water_box(4000, cutoff=1.0, ewald_tol=1e-4)
     system.setDefaultPeriodicBoxVectors(*[[2.5 * box[i][j] for j in range(3)] for i in range(3)])
     return system, force, pos, box
 
 
-@pytest.mark.parametrize("make,cluster,cap", [(_sparse_gas, False, 0), (_dense_overflow, False, 0), (_dense_overflow, True, 24)],
+@pytest.mark.parametrize("make,cluster,cap", [(_sparse_gas, False, 0), (_dense_overflow, False, 24), (_dense_overflow, True, 24)],
                          ids=["block_frame_misfit", "list_overflow", "cluster_list_overflow"])
 def test_half_list_fallbacks_persist_over_kept_lists(make, cluster, cap):
     """A fallback raised when the list is BUILT (rows the builder could not encode, overflowed

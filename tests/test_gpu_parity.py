@@ -224,17 +224,19 @@ def test_error_behaviour():
 
 @pytest.mark.parametrize("skin", [0.0, 0.1])
 def test_neighbor_list_overflow_rescan(skin):
-    # The list capacity is sized from the DEFAULT box density (alloc_nlist).  A default box
-    # 2.5x wider per axis than the box the positions live in makes every atom ~16x denser than
-    # planned, so every sub-list overflows and k_excl rescans each atom's cells: the result
-    # must still equal the oracle's (the reference has no capacity at all).
+    # A list capacity far below the density (cf_options.list_capacity: 8 entries per sub-list) makes
+    # every sub-list overflow, so k_excl rescans each atom's cells: the result must still equal the
+    # oracle's (the reference has no capacity at all).  The default box is 2.5x wider per axis than
+    # the box the positions live in (kmax comes from the default box; before round 6 that alone
+    # overflowed the lists, whose capacity now also follows the current box).
     system, force, pos, box = ts.make("C2")
     big = [[2.5 * box[i][j] for j in range(3)] for i in range(3)]
     system.setDefaultPeriodicBoxVectors(*big)
-    k = HipCalcCoulForceKernel().initialize(system, force)
+    k = HipCalcCoulForceKernel(list_capacity=8).initialize(system, force)
     if skin:
         k.set_neighbor_skin(skin)
     o = Oracle(force, big)
     assert k.ewald_params()[1] == o.ewald()[1]
     for _ in range(2):   # build, then (skin) a kept list
         _compare(_run(k, pos, box), o.execute(pos, box))
+    assert k.fallback_stats()[1] > 0   # rows rescanned

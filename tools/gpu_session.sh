@@ -35,6 +35,8 @@ run() {   # name, log, seconds, command...
     [ $rc -eq 0 ] || fail $name $log $rc
 }
 cfgargs() { case $1 in c5) echo "--config C5 --precision mixed";; c3_mixed) echo "--precision mixed";; *) echo "";; esac; }
+# (the C5 CPU-baseline sample runs minutes without output: the box's silence guard would kill it)
+benchargs() { case $1 in c5) echo "--no-cpu-baseline";; *) echo "";; esac; }
 PROF_ARGS="--steps 5 --warmup 2 --no-cpu-baseline --no-exact-compare"
 for st in "$@"; do
     case $st in
@@ -47,7 +49,7 @@ for st in "$@"; do
         tail -3 $out/smoke.log;;
     bench_*)
         cfg=${st#bench_}
-        timeout -k 10 400 python -u bench.py $(cfgargs $cfg) > $out/$st.json 2> $out/$st.err
+        timeout -k 10 400 python -u bench.py $(cfgargs $cfg) $(benchargs $cfg) > $out/$st.json 2> $out/$st.err
         rc=$?; echo "STEP $st rc=$rc"; [ $rc -eq 0 ] || fail $st $out/$st.err $rc
         tail -c 2500 $out/$st.json; echo;;
     trace_*)
