@@ -1373,7 +1373,10 @@ static void launch_full(cf_handle* H, const double* pos_dev, int flags, bool reu
         });
         join_wait(h);
     } else {
-        run_segment(H, g, SEG_PRO, key, [&] { launch_prologue(H, pos_dev, reusable); });
+        // the prologue's two kernels run eagerly even in graph mode: an event recorded right after
+        // a graph launch reached the waiting queue ~8 us later than one after a kernel (C3 traces,
+        // profiles/r06l_c3_timeline_graph_step.txt: fork gap 13.2 us against 5.0 eager)
+        launch_prologue(H, pos_dev, reusable);
         fork_aux(h);
         on_aux(H, g, SEG_DCH, key, dch);
         join_post(h);
