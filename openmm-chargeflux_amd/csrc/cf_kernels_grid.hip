@@ -60,6 +60,38 @@ __device__ __forceinline__ double es_val(double t, double hw_inv, double beta) {
     return u > 0.0 ? exp_nonpos(beta * (u * rsqrt_fp64(u) - 1.0)) : 0.0;
 }
 
+// Mixed precision (CF_PRECISION_MIXED): the same taps in fp32 -- v_rsq_f32 and v_exp_f32 instead of
+// the fp64 Newton step and exp polynomial (~45 fp64 VALU slots per tap against ~10).  t = g - s
+// is formed in fp64 (s is a grid coordinate up to ng) and only then rounded, and the exponent
+// beta (sqrt(u) - 1) is taken as -beta z^2 / (1 + sqrt(u)): the difference form cancels near the
+// centre (u -> 1), where its absolute error beta * 6e-8 ~ 1e-6 biased every tap the same way
+// (C5: the reciprocal energy moved by -0.97 kJ/mol, r6v); this form's error is ~1e-7 relative
+// to the exponent.  Below the W <= 8 grid's own ~1e-6 (the mixed bars: tests/test_gpu_configs.py).
+__device__ __forceinline__ float es_arg_f(float z, float u, float rs, float b) {
+    return -b * (z * z) * __frcp_rn(1.0f + u * rs);
+}
+
+__device__ __forceinline__ void es_tap_f(double t, double hw_inv, double beta, double& v, double& dv) {
+    const float z = (float)(t * hw_inv);
+    const float u = 1.0f - z * z;
+    if (u > 0.0f) {
+        const float rs = __frsqrt_rn(u);
+        const float b = (float)beta;
+        const float vf = __expf(es_arg_f(z, u, rs, b));
+        v = vf;
+        dv = vf * b * z * rs * (float)hw_inv;
+    } else {
+        v = 0.0;
+        dv = 0.0;
+    }
+}
+
+__device__ __forceinline__ double es_val_f(double t, double hw_inv, double beta) {
+    const float z = (float)(t * hw_inv);
+    const float u = 1.0f - z * z;
+    return u > 0.0f ? (double)__expf(es_arg_f(z, u, __frsqrt_rn(u), (float)beta)) : 0.0;
+}
+
 // ---------------------------------------------------------------------------------
 // Multi-rank x-slab: on a rank that owns a spatially compact set of atoms, only the grid
 // x-planes its atoms' taps reach carry data.  xr[0..1] = min / max over owned atoms of the
@@ -211,8 +243,9 @@ __device__ __forceinline__ void wave_sync() {
 // whenever either was nonzero -- written into a zeroed LDS copy of the rows, which the wave
 // then stores to the bin's contiguous slot range in consecutive 16 B per lane.
 // WT > 0: the kernel width as a compile-time constant (the tap index divisions become
-// multiplies; 14 = the fp64 default, 8 = mixed precision); WT = 0: W at run time
-template <int WT>
+// multiplies; 14 = the fp64 default, 8 = mixed precision); WT = 0: W at run time.  F32: the taps
+// evaluated in fp32 (mixed precision, es_val_f), stored as fp64 like the others
+template <int WT, bool F32 = false>
 __global__ void __launch_bounds__(256) k_g_order_taps(int nbins, const int* __restrict__ start,
                                                       const int* __restrict__ tmp, int* __restrict__ order, int Wr,
                                                       double beta, int3 ng, const double4* __restrict__ srec,
@@ -298,7 +331,8 @@ __global__ void __launch_bounds__(256) k_g_order_taps(int nbins, const int* __re
             }
             // q folded into the x row; bin-aligned point (g0 mod 8) + m, g0 mod 8 == wrapped
             // g0 mod 8 (ng is a multiple of 8)
-            rw[u * kTapStride + d * kRow + (g0 & 7) + mm] = scale * es_val((double)(g0 + mm) - sd, hw_inv, beta);
+            const double t = (double)(g0 + mm) - sd;
+            rw[u * kTapStride + d * kRow + (g0 & 7) + mm] = scale * (F32 ? es_val_f(t, hw_inv, beta) : es_val(t, hw_inv, beta));
         }
         wave_sync();
         const size_t s0 = (size_t)b0 + c0;
@@ -1939,7 +1973,7 @@ __device__ __forceinline__ double row_sum4(double pv, double px, double py, doub
 // at W <= 8).  Taps: lanes jg = 0 evaluate x tap k, lanes jg = 1 z tap k (one pass; a row rotation
 // by 8 gives the jg = 0 lanes their z tap); y taps 2n + jg in lane (jg, n < NJ), broadcast to the
 // lanes of each half-row by row_newbcast with a bank mask.  Otherwise as k_g_interp2.
-template <int W>
+template <int W, bool F32 = false>
 __global__ void __launch_bounds__(kInterpThreads) CF_LDS_UNPAIRED k_g_interp4(int3 ng, int3 nb, const int* __restrict__ start,
                                                               const int4* __restrict__ g0s,
                                                               const double4* __restrict__ srec, double beta,
@@ -1980,12 +2014,18 @@ __global__ void __launch_bounds__(kInterpThreads) CF_LDS_UNPAIRED k_g_interp4(in
         {
             const double sd = jg ? sr.z : sr.x;
             double v = 0, dv = 0;
-            if (k < W) es_tap(ceil(sd - 0.5 * W) + k - sd, hw_inv, beta, v, dv);
+            if (k < W) {
+                if constexpr (F32) es_tap_f(ceil(sd - 0.5 * W) + k - sd, hw_inv, beta, v, dv);
+                else es_tap(ceil(sd - 0.5 * W) + k - sd, hw_inv, beta, v, dv);
+            }
             xv = v; xd = dv;                              // lanes jg = 0: x tap k (the DPP sources)
             const double rv = row_ror8(v), rdv = row_ror8(dv);   // lane (0, k) <- lane (1, k)
             zv = jg ? v : rv; zd = jg ? dv : rdv;
         }
-        if (k < NJ && 2 * k + jg < W) es_tap(ceil(sr.y - 0.5 * W) + (2 * k + jg) - sr.y, hw_inv, beta, yv, yd);
+        if (k < NJ && 2 * k + jg < W) {
+            if constexpr (F32) es_tap_f(ceil(sr.y - 0.5 * W) + (2 * k + jg) - sr.y, hw_inv, beta, yv, yd);
+            else es_tap(ceil(sr.y - 0.5 * W) + (2 * k + jg) - sr.y, hw_inv, beta, yv, yd);
+        }
         xv = dpp_ready(xv); xd = dpp_ready(xd); yv = dpp_ready(yv); yd = dpp_ready(yd);
         const int rx = g.x & 7, ry = g.y & 7, rz = g.z & 7;
         const double* base = sg + (rx * R + ry) * R + rz + (k < W ? k : 0);
@@ -2191,14 +2231,17 @@ void launch_grid_sort(Handle& h, const double* pos) {
                        h.err_dev);
     hipLaunchKernelGGL(k_g_scatter, dim3(nblk(nown, 256)), dim3(256), 0, h.stream, nown, h.g_g0u, h.g_rank, h.g_start,
                        h.g_tmp, p.nbins, h.g_cnt, h.err_dev);
-    if (p.W == 14) hipLaunchKernelGGL(k_g_order_taps<14>, dim3(nblk(p.nbins, kOtWaves)), dim3(256), 0, h.stream, p.nbins, h.g_start, h.g_tmp,
-                       h.g_order, p.W, p.beta, ng, h.g_srec, h.g_g0u, h.g_taps, h.g_g0s, nown, h.err_dev);
-    else if (p.W == 13) hipLaunchKernelGGL(k_g_order_taps<13>, dim3(nblk(p.nbins, kOtWaves)), dim3(256), 0, h.stream, p.nbins, h.g_start, h.g_tmp,
-                       h.g_order, p.W, p.beta, ng, h.g_srec, h.g_g0u, h.g_taps, h.g_g0s, nown, h.err_dev);
-    else if (p.W == 8) hipLaunchKernelGGL(k_g_order_taps<8>, dim3(nblk(p.nbins, kOtWaves)), dim3(256), 0, h.stream, p.nbins, h.g_start, h.g_tmp,
-                       h.g_order, p.W, p.beta, ng, h.g_srec, h.g_g0u, h.g_taps, h.g_g0s, nown, h.err_dev);
-    else hipLaunchKernelGGL(k_g_order_taps<0>, dim3(nblk(p.nbins, kOtWaves)), dim3(256), 0, h.stream, p.nbins, h.g_start, h.g_tmp,
-                       h.g_order, p.W, p.beta, ng, h.g_srec, h.g_g0u, h.g_taps, h.g_g0s, nown, h.err_dev);
+#define CF_OT(WT_, F_) hipLaunchKernelGGL((k_g_order_taps<WT_, F_>), dim3(nblk(p.nbins, kOtWaves)), dim3(256), 0, h.stream, \
+                                          p.nbins, h.g_start, h.g_tmp, h.g_order, p.W, p.beta, ng, h.g_srec, h.g_g0u,  \
+                                          h.g_taps, h.g_g0s, nown, h.err_dev)
+    if (h.mixed && p.W <= 9) {   // fp32 taps (es_val_f): the mixed grid (W = 14 keeps the fp64 grid's taps)
+        if (p.W == 8) CF_OT(8, true);
+        else CF_OT(0, true);
+    } else if (p.W == 14) CF_OT(14, false);
+    else if (p.W == 13) CF_OT(13, false);
+    else if (p.W == 8) CF_OT(8, false);
+    else CF_OT(0, false);
+#undef CF_OT
 }
 
 #define CF_GRID_W_DISPATCH(W_, CALL) \
@@ -2468,10 +2511,13 @@ void launch_grid_interp(Handle& h, bool split) {
     const int3 ng = make_int3(p.ng[0], p.ng[1], p.ng[2]), nb = make_int3(p.nb[0], p.nb[1], p.nb[2]);
     const double3 gs = make_double3(p.ng[0] / h.box_L[0], p.ng[1] / h.box_L[1], p.ng[2] / h.box_L[2]);
     const size_t R = 7 + p.W;
-    // W <= 8: four atoms per wave (k_g_interp4); else two (k_g_interp2); CF_VARIANT_INTERP1: one (k_g_interp)
+    // W <= 8: four atoms per wave (k_g_interp4; fp32 taps in mixed precision); else two (k_g_interp2);
+    // CF_VARIANT_INTERP1: one (k_g_interp)
 #define CF_INTERP(W_)                                                                                               \
-    hipLaunchKernelGGL(!p.interp2 ? k_g_interp<W_> : (W_ <= 8 && p.interp4) ? k_g_interp4<(W_ <= 8 ? W_ : 8)>      \
-                                                                           : k_g_interp2<W_>,                          \
+    hipLaunchKernelGGL(!p.interp2 ? k_g_interp<W_>                                                                 \
+                       : (W_ <= 8 && p.interp4) ? (h.mixed ? k_g_interp4<(W_ <= 8 ? W_ : 8), true>                     \
+                                                           : k_g_interp4<(W_ <= 8 ? W_ : 8), false>)                   \
+                                                : k_g_interp2<W_>,                                                     \
                        dim3(p.nbins), dim3(kInterpThreads),                                                         \
                        (!p.interp2 || (W_ <= 8 && p.interp4) ? R * R : (size_t)interp_plane_stride<W_>()) * R *     \
                            sizeof(double),                                                                          \
