@@ -22,8 +22,10 @@ out=gpurun_out/$TAG
 mkdir -p $out profiles
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 fail() {   # step name, log file, rc
-    echo "STEP $1 FAILED rc=$3 (log kept as profiles/${TAG}_FAILED_$1.log)"
+    echo "STEP $1 FAILED rc=$3 (log kept as profiles/${TAG}_FAILED_$1.log and $out/FAILED_$1.log)"
     [ -f "$2" ] && cp "$2" "profiles/${TAG}_FAILED_$1.log"
+    # (gpurun merges only gpurun_out/ back from the box: this copy is the one that returns)
+    [ -f "$2" ] && cp "$2" "$out/FAILED_$1.log"
     exit $3
 }
 run() {   # name, log, seconds, command...
