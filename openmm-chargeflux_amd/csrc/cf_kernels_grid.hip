@@ -224,6 +224,8 @@ __global__ void __launch_bounds__(256) k_g_scatter(int nown, const int4* __restr
 // window p = 8*db + i, so no per-atom offset is needed to address the taps.
 constexpr int kRow = 24;
 constexpr int kTapStride = 3 * kRow;
+constexpr int kRowF32 = 16;                 // fp32 rows (GridPlan::taps_f32, W <= 9): points 0..15
+constexpr int kTapStrideF32 = 3 * kRowF32;  // floats per atom
 constexpr int kOtWaves = 4;     // bins per 256-thread block: one wave per bin, no block barriers
 constexpr int kOtLds = 128;     // members per bin staged in LDS (denser bins read global memory)
 constexpr int kOtChunk = 8;     // atoms whose tap rows are assembled in LDS at a time (16, 24 slower)
@@ -244,7 +246,8 @@ __device__ __forceinline__ void wave_sync() {
 // then stores to the bin's contiguous slot range in consecutive 16 B per lane.
 // WT > 0: the kernel width as a compile-time constant (the tap index divisions become
 // multiplies; 14 = the fp64 default, 8 = mixed precision); WT = 0: W at run time.  F32: the taps
-// evaluated in fp32 (mixed precision, es_val_f), stored as fp64 like the others
+// evaluated in fp32 (mixed precision, es_val_f) and, when W <= 9 (GridPlan::taps_f32), stored as
+// fp32 rows of 16 points (taps then holds floats: [slot][3][16])
 template <int WT, bool F32 = false>
 __global__ void __launch_bounds__(256) k_g_order_taps(int nbins, const int* __restrict__ start,
                                                       const int* __restrict__ tmp, int* __restrict__ order, int Wr,
@@ -336,7 +339,13 @@ __global__ void __launch_bounds__(256) k_g_order_taps(int nbins, const int* __re
         }
         wave_sync();
         const size_t s0 = (size_t)b0 + c0;
-        if (W <= 9) {   // taps end at point (g0 mod 8) + W - 1 <= 15: points 16..23 stay the zeros
+        if (F32 && W <= 9) {   // fp32 rows of 16 points (kRowF32), 48 floats per atom: 4 floats per lane
+            for (int e = lane; e < mc * 12; e += 64) {
+                const int ad = e >> 2, qd = e & 3;   // (atom, axis), quarter of the 16 points
+                const double* r = rw + (ad / 3) * kTapStride + (ad % 3) * kRow + 4 * qd;
+                reinterpret_cast<float4*>(taps)[s0 * 12 + e] = make_float4((float)r[0], (float)r[1], (float)r[2], (float)r[3]);
+            }
+        } else if (W <= 9) {   // taps end at point (g0 mod 8) + W - 1 <= 15: points 16..23 stay the zeros
                         // written at allocation (cf_create), so a row is 8 pairs of its 12
             for (int e = lane; e < mc * 24; e += 64) {
                 const int pr = (e / 8) * 12 + (e & 7);   // (atom, axis) = e / 8
@@ -392,10 +401,13 @@ __device__ __forceinline__ void fma8_row_bcast(double (&acc)[8], double xv, doub
         : "v"(xv), "v"(yz));
 }
 
-template <int NS, int kSpPass>
+// TF: fp32 tap rows (GridPlan::taps_f32, NS = 2): a 16-B piece is half a window (4 floats), widened
+// to fp64 as it is staged; the sums stay fp64
+template <int NS, int kSpPass, bool TF = false>
 __global__ void __launch_bounds__(256) CF_LDS_UNPAIRED k_g_spread_tile(int3 ng, int3 nb, const int* __restrict__ start,
                                                        const double* __restrict__ taps, const int4* __restrict__ g0s,
                                                        double* __restrict__ grid, const int* __restrict__ xr, int W) {
+    static_assert(!TF || NS == 2, "fp32 rows hold points 0..15: windows db = 0, 1");
     constexpr int NB3 = NS * NS * NS;
     static_assert(NS <= 3, "tile offsets are packed in 2 bits per axis");
     constexpr int kStD = 2 * kSpPass * kSpWin > 4 * 8 * 64 ? 2 * kSpPass * kSpWin : 4 * 8 * 64;
@@ -483,29 +495,49 @@ __global__ void __launch_bounds__(256) CF_LDS_UNPAIRED k_g_spread_tile(int3 ng, 
         __syncthreads();
         if (nseg == 0) continue;
         // staging: 16-B piece e of the pass = atom e / 12, axis (e % 12) / 4, quarter e % 4 of the window
-        constexpr int kPieces = kSpPass * kSpWin / 2;          // 768 at 64 atoms per pass
-        constexpr int kPer = (kPieces + 255) / 256;             // 3 per thread at 64
-        v2d r[kPer];
+        // (TF: atom e / 6, axis (e % 6) / 2, half e % 2 of the window: 4 floats, staged as 4 doubles)
+        constexpr int kPP = TF ? kSpWin / 4 : kSpWin / 2;      // pieces per atom
+        constexpr int kPieces = kSpPass * kPP;                  // 768 at 64 atoms per pass (TF: 384)
+        constexpr int kPer = (kPieces + 255) / 256;             // 3 per thread at 64 (TF: 2)
+        using Piece = std::conditional_t<TF, float4, v2d>;
+        Piece r[kPer];
         auto fetch = [&](int base, int n) {
 #pragma unroll
             for (int q = 0; q < kPer; q++) {
                 const int e = min(t + 256 * q, kPieces - 1);
-                const int a = e / 12, c = e - 12 * a, d = c >> 2, h = c & 3;
+                const int a = e / kPP, c = e - kPP * a;
                 const int u = base + min(a, n - 1);
                 const int sb = src[u];
-                const int db = (sb >> (4 - 2 * d)) & 3;
-                const int off = (sb >> 6) * kTapStride + d * kRow + 8 * db;
-                r[q] = *reinterpret_cast<const v2d*>(taps + off + 2 * h);
-                // atoms past the pass end are staged as zero windows, so that the compute loop
-                // reads whole groups of four without bounds checks (adds exact zeros)
-                if (a >= n) r[q] = v2d{0.0, 0.0};
+                if constexpr (TF) {
+                    const int d = c >> 1, h = c & 1;
+                    const int db = (sb >> (4 - 2 * d)) & 3;
+                    const float* tf = reinterpret_cast<const float*>(taps);
+                    r[q] = *reinterpret_cast<const float4*>(tf + (sb >> 6) * kTapStrideF32 + d * kRowF32 + 8 * db + 4 * h);
+                    if (a >= n) r[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+                } else {
+                    const int d = c >> 2, h = c & 3;
+                    const int db = (sb >> (4 - 2 * d)) & 3;
+                    const int off = (sb >> 6) * kTapStride + d * kRow + 8 * db;
+                    r[q] = *reinterpret_cast<const v2d*>(taps + off + 2 * h);
+                    // atoms past the pass end are staged as zero windows, so that the compute loop
+                    // reads whole groups of four without bounds checks (adds exact zeros)
+                    if (a >= n) r[q] = v2d{0.0, 0.0};
+                }
             }
         };
         auto stage = [&](double* buf) {
 #pragma unroll
             for (int q = 0; q < kPer; q++) {
                 const int e = t + 256 * q;
-                if (kPieces % 256 == 0 || e < kPieces) reinterpret_cast<v2d*>(buf)[e] = r[q];
+                if (kPieces % 256 == 0 || e < kPieces) {
+                    if constexpr (TF) {
+                        v2d* o = reinterpret_cast<v2d*>(buf) + 2 * e;
+                        o[0] = v2d{(double)r[q].x, (double)r[q].y};
+                        o[1] = v2d{(double)r[q].z, (double)r[q].w};
+                    } else {
+                        reinterpret_cast<v2d*>(buf)[e] = r[q];
+                    }
+                }
             }
         };
         const int npass = (nseg + kSpPass - 1) / kSpPass;
@@ -2151,6 +2183,9 @@ void grid_plan(Handle& h, int width, double sigma) {
     p.spread_mfma_all = (h.variants & CF_VARIANT_MFMA_SPREAD) != 0;
     p.interp2 = !(h.variants & CF_VARIANT_INTERP1);
     p.interp4 = !(h.variants & CF_VARIANT_INTERP2);
+    // mixed precision on the vector spread (W <= 9): fp32 tap rows of 16 points (k_g_order_taps F32,
+    // k_g_spread_tile TF): half the row bytes written and a third of the window bytes read
+    p.taps_f32 = h.mixed && p.W <= 9 && !p.spread_mfma_all;
     for (int d = 0; d < 3; d++) {
         const int K = h.kmax[d], J = d == 2 ? K : 2 * K - 1, k0 = d == 2 ? 0 : -(K - 1);
         int mx = 0;
@@ -2234,7 +2269,7 @@ void launch_grid_sort(Handle& h, const double* pos) {
 #define CF_OT(WT_, F_) hipLaunchKernelGGL((k_g_order_taps<WT_, F_>), dim3(nblk(p.nbins, kOtWaves)), dim3(256), 0, h.stream, \
                                           p.nbins, h.g_start, h.g_tmp, h.g_order, p.W, p.beta, ng, h.g_srec, h.g_g0u,  \
                                           h.g_taps, h.g_g0s, nown, h.err_dev)
-    if (h.mixed && p.W <= 9) {   // fp32 taps (es_val_f): the mixed grid (W = 14 keeps the fp64 grid's taps)
+    if (p.taps_f32) {   // fp32 taps (es_val_f), stored as fp32 rows: the mixed grid's vector spread
         if (p.W == 8) CF_OT(8, true);
         else CF_OT(0, true);
     } else if (p.W == 14) CF_OT(14, false);
@@ -2264,8 +2299,8 @@ void launch_grid_sort(Handle& h, const double* pos) {
 void launch_grid_spread(Handle& h) {
     const GridPlan& p = h.gp;
     const int3 ng = make_int3(p.ng[0], p.ng[1], p.ng[2]), nb = make_int3(p.nb[0], p.nb[1], p.nb[2]);
-#define CF_SPT(NS_, P_) hipLaunchKernelGGL((k_g_spread_tile<NS_, P_>), dim3(p.nbins), dim3(256), 0, h.stream, \
-                                               ng, nb, h.g_start, h.g_taps, h.g_g0s, h.g_grid, h.g_xrange, p.W)
+#define CF_SPT(NS_, P_, TF_) hipLaunchKernelGGL((k_g_spread_tile<NS_, P_, TF_>), dim3(p.nbins), dim3(256), 0, h.stream, \
+                                                    ng, nb, h.g_start, h.g_taps, h.g_g0s, h.g_grid, h.g_xrange, p.W)
     // the matrix-core form (16 x 8 x 8 tiles, 4 distinct x bins) for W > 9; at W <= 9 (the mixed
     // C5 grid) the vector form with its 8^3 tiles and 8 source bins measured faster (322 against
     // 330 us at C5: the 16-wide x tile doubles the zero-tap share of a narrow kernel)
@@ -2282,8 +2317,9 @@ void launch_grid_spread(Handle& h) {
     }
     // a first tap in bin B reaches tiles B .. B + NS - 1: NS = 2 when W <= 9 (8 source bins per
     // tile instead of 27).  Passes of 32 atoms at W = 14 (64 / 128 measured slower at C3)
-    if (p.W <= 9) CF_SPT(2, 64);
-    else CF_SPT(3, 32);
+    if (p.taps_f32) CF_SPT(2, 64, true);
+    else if (p.W <= 9) CF_SPT(2, 64, false);
+    else CF_SPT(3, 32, false);
 #undef CF_SPT
 }
 
