@@ -83,6 +83,7 @@ struct GridPlan {
     bool interp2 = true;     // two atoms per wave, taps by DPP row broadcast (CF_VARIANT_INTERP1: k_g_interp)
     bool interp4 = true;     // W <= 8: four atoms per wave (CF_VARIANT_INTERP2: k_g_interp2)
     bool taps_f32 = false;   // mixed precision, W <= 9, vector spread: tap rows stored as fp32 (16 points)
+    bool grid_f32 = false;   // mixed precision, W <= 8: the real grid stored as fp32 (spread -> z stages -> interp4)
 };
 
 struct Handle {

@@ -403,10 +403,11 @@ __device__ __forceinline__ void fma8_row_bcast(double (&acc)[8], double xv, doub
 
 // TF: fp32 tap rows (GridPlan::taps_f32, NS = 2): a 16-B piece is half a window (4 floats), widened
 // to fp64 as it is staged; the sums stay fp64
-template <int NS, int kSpPass, bool TF = false>
+template <int NS, int kSpPass, bool TF = false, bool GF = false>
 __global__ void __launch_bounds__(256) CF_LDS_UNPAIRED k_g_spread_tile(int3 ng, int3 nb, const int* __restrict__ start,
                                                        const double* __restrict__ taps, const int4* __restrict__ g0s,
                                                        double* __restrict__ grid, const int* __restrict__ xr, int W) {
+    // GF: the grid is fp32 (GridPlan::grid_f32): each point's fp64 sum rounded once as it is stored
     static_assert(!TF || NS == 2, "fp32 rows hold points 0..15: windows db = 0, 1");
     constexpr int NB3 = NS * NS * NS;
     static_assert(NS <= 3, "tile offsets are packed in 2 bits per axis");
@@ -585,7 +586,9 @@ __global__ void __launch_bounds__(256) CF_LDS_UNPAIRED k_g_spread_tile(int3 ng, 
     for (int h = 0; h < 2; h++) {
         const int pt = t + 256 * h, i = pt >> 6, l = pt & 63;
         const double v = ((red[i * 64 + l] + red[(8 + i) * 64 + l]) + red[(16 + i) * 64 + l]) + red[(24 + i) * 64 + l];
-        grid[((size_t)(8 * tx + i) * ng.y + 8 * ty + (l >> 3)) * ng.z + 8 * tz + (l & 7)] = v;
+        const size_t o = ((size_t)(8 * tx + i) * ng.y + 8 * ty + (l >> 3)) * ng.z + 8 * tz + (l & 7);
+        if constexpr (GF) reinterpret_cast<float*>(grid)[o] = (float)v;
+        else grid[o] = v;
     }
 }
 
@@ -1193,7 +1196,7 @@ __global__ void __launch_bounds__(8 * SEQ) k_g_dft8_fwd(Dft8 d, const double2* _
 constexpr int kZR = 8;    // rows per block of the z analysis
 constexpr int kZIR = 16;  // rows per block of the z synthesis
 
-template <int MT, int NB>
+template <int MT, int NB, bool GF = false>   // GF: fp32 grid rows (GridPlan::grid_f32)
 __global__ void __launch_bounds__(64 * NB) k_g_dft8_zfwd(Dft8 d, const double2* __restrict__ twist,
                                                          const double2* __restrict__ tq) {
     extern __shared__ v2d sm8[];
@@ -1208,7 +1211,8 @@ __global__ void __launch_bounds__(64 * NB) k_g_dft8_zfwd(Dft8 d, const double2* 
         return;
     const int tid = threadIdx.x;
     for (int e = tid; e < 8 * Q; e += 64 * NB) stw[e] = reinterpret_cast<const v2d*>(twist)[e];
-    const double* in = reinterpret_cast<const double*>(d.in);
+    using GT = std::conditional_t<GF, float, double>;
+    const GT* in = reinterpret_cast<const GT*>(d.in);
     for (int it = tid; it < R * Q; it += 64 * NB) {
         const int row = it / Q, b = it - row * Q;
         const int s = s0 + row;
@@ -1217,7 +1221,7 @@ __global__ void __launch_bounds__(64 * NB) k_g_dft8_zfwd(Dft8 d, const double2* 
         v2d x[8], y[8];
 #pragma unroll
         for (int a = 0; a < 8; a++) {
-            const double v = in[base + (long)Q * a];
+            const double v = (double)in[base + (long)Q * a];
             x[a] = v2d{ok ? v : 0.0, 0.0};
         }
         dft8(x, y);
@@ -1282,7 +1286,7 @@ __global__ void __launch_bounds__(64 * NB) k_g_dft8_zfwd(Dft8 d, const double2* 
 // once; then the outputs x[Qa + b] are formed per (row, b) item with lane-consecutive b, so each
 // a-slice of a row is written as one contiguous run (the sequence-lane kernel wrote 64-byte
 // pieces per b chunk: 1.55x the grid's bytes written at C5).
-template <int MT, int NB>
+template <int MT, int NB, bool GF = false>   // GF: fp32 grid rows (GridPlan::grid_f32)
 __global__ void __launch_bounds__(64 * NB) k_g_dft8_zinv(Dft8 d, const double2* __restrict__ twist,
                                                          const double2* __restrict__ tq) {
     extern __shared__ v2d sm8[];
@@ -1342,7 +1346,8 @@ __global__ void __launch_bounds__(64 * NB) k_g_dft8_zinv(Dft8 d, const double2* 
     }
     __syncthreads();
     const double c = 0.70710678118654752440;
-    double* out = reinterpret_cast<double*>(d.out);
+    using GT = std::conditional_t<GF, float, double>;
+    GT* out = reinterpret_cast<GT*>(d.out);
     for (int it = tid; it < R * Q; it += 64 * NB) {
         const int rw = it / Q, b = it - rw * Q;
         const int s = s0 + rw;
@@ -1364,7 +1369,7 @@ __global__ void __launch_bounds__(64 * NB) k_g_dft8_zinv(Dft8 d, const double2* 
         x[7] = o + v1 + P2.y + v3;
         const long base = (long)s * d.s1 + b;
 #pragma unroll
-        for (int a = 0; a < 8; a++) out[base + (long)Q * a] = x[a];
+        for (int a = 0; a < 8; a++) out[base + (long)Q * a] = (GT)x[a];
     }
 }
 
@@ -1550,7 +1555,7 @@ constexpr int interp_plane_stride() {
     return s;
 }
 
-template <int W, int SX = (7 + W) * (7 + W)>
+template <int W, int SX = (7 + W) * (7 + W), bool GF = false>   // GF: an fp32 grid, widened as staged
 __device__ __forceinline__ void interp_stage16(int3 ng, const double* __restrict__ G, int tx, int ty, int tz,
                                                double* __restrict__ sg) {
     constexpr int R = 7 + W;
@@ -1573,8 +1578,13 @@ __device__ __forceinline__ void interp_stage16(int3 ng, const double* __restrict
             int x = 8 * tx + (in ? a : 0), y = 8 * ty + (in ? b : 0);
             x -= x >= ng.x ? ng.x : 0;
             y -= y >= ng.y ? ng.y : 0;
-            const unsigned off = (unsigned)(x * zy + y * ng.z + z) * 8u;
-            gv[q] = *reinterpret_cast<const v2d*>(reinterpret_cast<const char*>(G) + off);
+            const unsigned idx = (unsigned)(x * zy + y * ng.z + z);
+            if constexpr (GF) {
+                const float2 f = reinterpret_cast<const float2*>(G)[idx >> 1];   // (z even: 8-B aligned)
+                gv[q] = v2d{(double)f.x, (double)f.y};
+            } else {
+                gv[q] = *reinterpret_cast<const v2d*>(reinterpret_cast<const char*>(G) + idx * 8u);
+            }
             a += kDA; b += kDB;
             if (b >= R) { b -= R; a += 1; }
         }
@@ -2005,7 +2015,7 @@ __device__ __forceinline__ double row_sum4(double pv, double px, double py, doub
 // at W <= 8).  Taps: lanes jg = 0 evaluate x tap k, lanes jg = 1 z tap k (one pass; a row rotation
 // by 8 gives the jg = 0 lanes their z tap); y taps 2n + jg in lane (jg, n < NJ), broadcast to the
 // lanes of each half-row by row_newbcast with a bank mask.  Otherwise as k_g_interp2.
-template <int W, bool F32 = false>
+template <int W, bool F32 = false, bool GF = false>   // F32: fp32 taps; GF: fp32 grid (GridPlan::grid_f32)
 __global__ void __launch_bounds__(kInterpThreads) CF_LDS_UNPAIRED k_g_interp4(int3 ng, int3 nb, const int* __restrict__ start,
                                                               const int4* __restrict__ g0s,
                                                               const double4* __restrict__ srec, double beta,
@@ -2026,7 +2036,7 @@ __global__ void __launch_bounds__(kInterpThreads) CF_LDS_UNPAIRED k_g_interp4(in
     const int s0 = start[tile], s1 = start[tile + 1];
     if (s0 == s1) return;
     const int tz = tile % nb.z, ty = (tile / nb.z) % nb.y, tx = tile / (nb.z * nb.y);
-    interp_stage16<W>(ng, G, tx, ty, tz, sg);
+    interp_stage16<W, (7 + W) * (7 + W), GF>(ng, G, tx, ty, tz, sg);
     __syncthreads();
     const int lane = threadIdx.x & 63, w = wave_id();
     const int q = lane >> 4, jg = (lane >> 3) & 1, k = lane & 7;
@@ -2200,6 +2210,18 @@ void grid_plan(Handle& h, int width, double sigma) {
             if (mx <= m) { p.mt[d] = m; break; }
         if (p.mt[d] == 0) p.dft8 = false;
     }
+    // the fp32 real grid (mixed precision): every kernel that touches it has an fp32 form -- the
+    // vector spread's store, the z row stages (k_g_dft8_zfwd / zinv, when their LDS fits: d8_fwd /
+    // d8_inv) and k_g_interp4's halo staging; the sums stay fp64.  Half the grid's bytes written
+    // by the spread and the synthesis and read by the analysis and the interpolation's halos.
+    {
+        const int Q = p.ng[2] / 8;
+        int J = 0;
+        for (int r = 0; r < 8; r++) J += p.rc[2][r];
+        const bool zrow = (size_t)(kZR * Q * 5 + 8 * Q + kZR * J) * 16 <= 64 * 1024 &&
+                          (size_t)(kZIR * Q * 4 + 8 * Q) * 16 <= 64 * 1024;
+        p.grid_f32 = p.taps_f32 && p.W <= 8 && p.dft8 && zrow && p.interp2 && p.interp4;
+    }
 }
 
 void grid_tables(const Handle& h, std::vector<double2> tw[3], std::vector<double2> tw8[3], std::vector<double> deconv[3]) {
@@ -2299,8 +2321,8 @@ void launch_grid_sort(Handle& h, const double* pos) {
 void launch_grid_spread(Handle& h) {
     const GridPlan& p = h.gp;
     const int3 ng = make_int3(p.ng[0], p.ng[1], p.ng[2]), nb = make_int3(p.nb[0], p.nb[1], p.nb[2]);
-#define CF_SPT(NS_, P_, TF_) hipLaunchKernelGGL((k_g_spread_tile<NS_, P_, TF_>), dim3(p.nbins), dim3(256), 0, h.stream, \
-                                                    ng, nb, h.g_start, h.g_taps, h.g_g0s, h.g_grid, h.g_xrange, p.W)
+#define CF_SPT(NS_, P_, TF_, GF_) hipLaunchKernelGGL((k_g_spread_tile<NS_, P_, TF_, GF_>), dim3(p.nbins), dim3(256), 0, \
+                                                    h.stream, ng, nb, h.g_start, h.g_taps, h.g_g0s, h.g_grid, h.g_xrange, p.W)
     // the matrix-core form (16 x 8 x 8 tiles, 4 distinct x bins) for W > 9; at W <= 9 (the mixed
     // C5 grid) the vector form with its 8^3 tiles and 8 source bins measured faster (322 against
     // 330 us at C5: the 16-wide x tile doubles the zero-tap share of a narrow kernel)
@@ -2317,9 +2339,10 @@ void launch_grid_spread(Handle& h) {
     }
     // a first tap in bin B reaches tiles B .. B + NS - 1: NS = 2 when W <= 9 (8 source bins per
     // tile instead of 27).  Passes of 32 atoms at W = 14 (64 / 128 measured slower at C3)
-    if (p.taps_f32) CF_SPT(2, 64, true);
-    else if (p.W <= 9) CF_SPT(2, 64, false);
-    else CF_SPT(3, 32, false);
+    if (p.grid_f32) CF_SPT(2, 64, true, true);
+    else if (p.taps_f32) CF_SPT(2, 64, true, false);
+    else if (p.W <= 9) CF_SPT(2, 64, false, false);
+    else CF_SPT(3, 32, false, false);
 #undef CF_SPT
 }
 
@@ -2407,7 +2430,9 @@ static void d8_fwd(Handle& h, int axis, const void* in, void* out, const Coef* c
     const size_t lds = (size_t)(kZR * d.Q * 5 + 8 * d.Q + kZR * J) * sizeof(double2);
     if (axis == 2 && lds <= 64 * 1024) {   // grid rows: the row kernel (4 waves, each a quarter of b)
         const dim3 g((unsigned)nblk(d.nseq, kZR));
-#define CF_D8Z(MT_) hipLaunchKernelGGL((k_g_dft8_zfwd<MT_, 4>), g, dim3(256), lds, h.stream, d, twist, tq)
+#define CF_D8Z(MT_)                                                                                     \
+    if (h.gp.grid_f32) hipLaunchKernelGGL((k_g_dft8_zfwd<MT_, 4, true>), g, dim3(256), lds, h.stream, d, twist, tq); \
+    else hipLaunchKernelGGL((k_g_dft8_zfwd<MT_, 4, false>), g, dim3(256), lds, h.stream, d, twist, tq)
         CF_D8_MT(h.gp.mt[axis], CF_D8Z)
 #undef CF_D8Z
         return;
@@ -2448,7 +2473,9 @@ static void d8_inv(Handle& h, int axis, const void* in, void* out) {
         const double2* tw0 = h.g_tw8[axis];
         const double2* tq0 = tw0 + 8 * d.Q;
         const dim3 g((unsigned)nblk(d.nseq, kZIR));
-#define CF_D8ZI(MT_) hipLaunchKernelGGL((k_g_dft8_zinv<MT_, 2>), g, dim3(128), lds, h.stream, d, tw0, tq0)
+#define CF_D8ZI(MT_)                                                                                    \
+    if (h.gp.grid_f32) hipLaunchKernelGGL((k_g_dft8_zinv<MT_, 2, true>), g, dim3(128), lds, h.stream, d, tw0, tq0); \
+    else hipLaunchKernelGGL((k_g_dft8_zinv<MT_, 2, false>), g, dim3(128), lds, h.stream, d, tw0, tq0)
         CF_D8_MT(h.gp.mt[axis], CF_D8ZI)
 #undef CF_D8ZI
         return;
@@ -2551,8 +2578,9 @@ void launch_grid_interp(Handle& h, bool split) {
     // CF_VARIANT_INTERP1: one (k_g_interp)
 #define CF_INTERP(W_)                                                                                               \
     hipLaunchKernelGGL(!p.interp2 ? k_g_interp<W_>                                                                 \
-                       : (W_ <= 8 && p.interp4) ? (h.mixed ? k_g_interp4<(W_ <= 8 ? W_ : 8), true>                     \
-                                                           : k_g_interp4<(W_ <= 8 ? W_ : 8), false>)                   \
+                       : (W_ <= 8 && p.interp4) ? (p.grid_f32 ? k_g_interp4<(W_ <= 8 ? W_ : 8), true, true>            \
+                                                   : h.mixed ? k_g_interp4<(W_ <= 8 ? W_ : 8), true, false>            \
+                                                             : k_g_interp4<(W_ <= 8 ? W_ : 8), false, false>)          \
                                                 : k_g_interp2<W_>,                                                     \
                        dim3(p.nbins), dim3(kInterpThreads),                                                         \
                        (!p.interp2 || (W_ <= 8 && p.interp4) ? R * R : (size_t)interp_plane_stride<W_>()) * R *     \
