@@ -376,6 +376,7 @@ __global__ void __launch_bounds__(kCqThreads) CF_LDS_UNPAIRED k_pairs_cq(DirectA
         const double4 pi = a.pos4s[islot];
         const double2 li = TYPES ? ljt[__float_as_int(a.pos4f[islot].w)] : a.ljs[islot];
         const double kqis = a.ke * pi.w * kFixScale;   // k_e q_i in fixed-point units
+        const float kef = (float)a.ke, kqisf = kef * (float)pi.w * kFix32Scale;   // (mixed: 2^13 units)
         // the 4 i atoms' fp32 positions, wave-uniform (phase A tests every lane's j against all 4)
         float4 pif[4];   // (readfirstlane: kept in SGPRs, VOP2 operands of the tests)
         auto sgpr = [](float v) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v))); };
@@ -442,7 +443,7 @@ __global__ void __launch_bounds__(kCqThreads) CF_LDS_UNPAIRED k_pairs_cq(DirectA
                 if (act && r2 <= (float)a.rc2) {
                     const int slot = wdel[(wq >> kHalfSlotBits) & 31] + j;
                     const double2 ljd = TYPES ? ljt[(unsigned)wq >> kShiftBits] : a.ljs[j];
-                    const float ke = (float)a.ke, qi = (float)pi.w;
+                    const float qi = (float)pi.w;
                     const float inv_r = rsqrtf(r2);
                     const float ar = (float)a.alpha * (r2 * inv_r);
                     const float y = ar * (float)a.erfc_scale_f;
@@ -459,21 +460,24 @@ __global__ void __launch_bounds__(kCqThreads) CF_LDS_UNPAIRED k_pairs_cq(DirectA
                     s2 *= s2;
                     const float sig6 = s2 * s2 * s2;
                     const float es6 = sig6 * (float)li.y * (float)ljd.y;
-                    const float qj = ke * qjv * inv_r;
+                    const float qj = kef * qjv * inv_r;
                     const float qq = qi * qj;
                     if (a.include_forces) {
+                        // -F_ij and dE/dq_j in fixed-point units (x -2^13 / x 2^13: exact), the
+                        // i side accumulated in the same units (unscaled at the end, exactly)
                         const float inv_r2 = inv_r * inv_r;
-                        const float dEdR = qq * inv_r2 * fmaf(ar * e2, 1.1283791670955126f, ec) +
-                                           es6 * (12.0f * sig6 - 6.0f) * inv_r2;
-                        const float fx = dEdR * dx, fy = dEdR * dy, fz = dEdR * dz;
-                        const float dqj = ke * qi * inv_r * ec;
-                        acc.fx += fx; acc.fy += fy; acc.fz += fz;
+                        const float ndEdRs = (qq * inv_r2 * fmaf(ar * e2, 1.1283791670955126f, ec) +
+                                              es6 * (12.0f * sig6 - 6.0f) * inv_r2) * -kFix32Scale;
+                        const float nfx = ndEdRs * dx, nfy = ndEdRs * dy, nfz = ndEdRs * dz;
+                        const float dqjs = kqisf * inv_r * ec;
+                        acc.fx += nfx; acc.fy += nfy; acc.fz += nfz;
                         acc.dq = fmaf(qj, ec, acc.dq);
-                        bad |= !(fmaxf(fmaxf(fabsf(fx), fabsf(fy)), fmaxf(fabsf(fz), fabsf(dqj))) < (float)kFixMax);
-                        atomicAdd(&accw[0][slot], to_fix32(-fx));
-                        atomicAdd(&accw[1][slot], to_fix32(-fy));
-                        atomicAdd(&accw[2][slot], to_fix32(-fz));
-                        atomicAdd(&accw[3][slot], to_fix32(dqj));
+                        bad |= !(fmaxf(fmaxf(fabsf(nfx), fabsf(nfy)), fmaxf(fabsf(nfz), fabsf(dqjs))) <
+                                 (float)kFixMax * kFix32Scale);
+                        atomicAdd(&accw[0][slot], scaled_to_fix32(nfx));
+                        atomicAdd(&accw[1][slot], scaled_to_fix32(nfy));
+                        atomicAdd(&accw[2][slot], scaled_to_fix32(nfz));
+                        atomicAdd(&accw[3][slot], scaled_to_fix32(dqjs));
                     }
                     acc.e += (double)fmaf(qq, ec, es6 * (sig6 - 1.0f));   // the whole pair energy
                 }
@@ -606,10 +610,10 @@ __global__ void __launch_bounds__(kCqThreads) CF_LDS_UNPAIRED k_pairs_cq(DirectA
             a.e_atom[3 * i + 1] = acc.e;
             if (a.include_forces) {
                 a.dedq[i] = acc.dq;
-                if constexpr (MIXED) {
-                    a.f_part[3 * i] = acc.fx;
-                    a.f_part[3 * i + 1] = acc.fy;
-                    a.f_part[3 * i + 2] = acc.fz;
+                if constexpr (MIXED) {   // accumulated as -F in 2^13 units
+                    a.f_part[3 * i] = acc.fx * -(double)kFix32Inv;
+                    a.f_part[3 * i + 1] = acc.fy * -(double)kFix32Inv;
+                    a.f_part[3 * i + 2] = acc.fz * -(double)kFix32Inv;
                 } else {   // accumulated as -F in fixed-point units
                     a.f_part[3 * i] = acc.fx * -kFixInv;
                     a.f_part[3 * i + 1] = acc.fy * -kFixInv;

@@ -98,6 +98,13 @@ constexpr double kFixMax = 65536.0;
 constexpr float kFix32Scale = 8192.0f;   // 2^13
 constexpr double kFix32Inv = 1.0 / 8192.0;
 __device__ __forceinline__ unsigned to_fix32(float v) { return (unsigned)__float2int_rn(v * kFix32Scale); }
+// an already scaled value (v * 2^13) to the 32-bit fixed point: floor(vs + 0.5) in one instruction
+// (v_cvt_rpi_i32_f32; round-to-nearest but for exact ties, which round up instead of to even)
+__device__ __forceinline__ unsigned scaled_to_fix32(float vs) {
+    int r;
+    asm("v_cvt_rpi_i32_f32 %0, %1" : "=v"(r) : "v"(vs));
+    return (unsigned)r;
+}
 // why half_flag was raised (bits; cf_get_fallback_stats reports their union)
 constexpr int kHalfWindowFull = 1;     // a cell's 18-cell window holds more than kHalfMaxWin atoms
 constexpr int kHalfListOverflow = 2;   // a row's sub-list overflowed, or the builder could not place it
