@@ -16,6 +16,8 @@
 #   pmc_c3 / pmc_c5                        three separate --pmc passes of the bench command +
 #                                          tools/pmc_summary.py (needs trace_<cfg> first)
 #   py=SCRIPT[:ARGS]  python -u SCRIPT ARGS (a probe under tools/), output in TAG/SCRIPT.log
+#   trace_py=SCRIPT[:ARGS]                 rocprofv3 --kernel-trace --stats of such a probe
+#   (ARGS: comma-separated, e.g. py=tools/scaling_probe.py:--worlds,1,8,--no-timing)
 set -o pipefail
 TAG=$1; shift
 out=gpurun_out/$TAG
@@ -54,6 +56,13 @@ for st in "$@"; do
         timeout -k 10 400 python -u bench.py $(cfgargs $cfg) $(benchargs $cfg) > $out/$st.json 2> $out/$st.err
         rc=$?; echo "STEP $st rc=$rc"; [ $rc -eq 0 ] || fail $st $out/$st.err $rc
         tail -c 2500 $out/$st.json; echo;;
+    trace_py=*)   # rocprofv3 --kernel-trace --stats of a probe: trace_py=SCRIPT[:ARGS]
+        spec=${st#trace_py=}; script=${spec%%:*}; args=""; [ "$spec" != "$script" ] && args=${spec#*:}
+        name=trace_$(basename $script .py)
+        (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/$out/$name -o run \
+            --output-format csv -- python3 $R/$script ${args//,/ } > $R/$out/$name.log 2>&1)
+        rc=$?; echo "STEP $st rc=$rc"; [ $rc -eq 0 ] || fail $name $out/$name.log $rc
+        python3 tools/prof_stats.py $out/$name/run_kernel_stats.csv 2>/dev/null | head -30;;
     trace_*)
         cfg=${st#trace_}
         (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/$out/trace_$cfg -o run \

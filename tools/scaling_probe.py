@@ -24,11 +24,12 @@ from openmmcoul import testsystems as ts  # noqa: E402
 from openmmcoul.distributed import ShardedCoulKernel  # noqa: E402
 
 
-def probe(system, force, pos_np, box, world, steps, skin, algo=2, timing=True, graph=False, precision="double"):
+def probe(system, force, pos_np, box, world, steps, skin, algo=2, timing=True, graph=False, precision="double",
+          pair_list="auto"):
     dev = torch.device("cuda", 0)
     stream = torch.cuda.current_stream(dev).cuda_stream
     k = HipCalcCoulForceKernel(device=0, stream=stream, rank=0, world_size=world, kspace_algo=algo,
-                               precision=precision).initialize(system, force)
+                               precision=precision, pair_list=pair_list).initialize(system, force)
     if skin > 0:
         k.set_neighbor_skin(skin)
     if graph:
@@ -69,7 +70,7 @@ def probe(system, force, pos_np, box, world, steps, skin, algo=2, timing=True, g
     tm = k.timing()
     k.set_timing(False)
     gpu = {p: v[0] / steps for p, v in tm.items()}
-    return {"world": world, "owned": hi - lo, "graph": graph, "ms_per_step": round(wall, 4),
+    return {"world": world, "owned": hi - lo, "graph": graph, "pair_list": k.pair_list(), "ms_per_step": round(wall, 4),
             "host_enqueue_ms_per_step": round(host / steps * 1e3, 4),
             "lib_gpu_ms_per_step": round(sum(gpu.values()), 4),
             "phases": {p: round(v, 4) for p, v in gpu.items()}}
@@ -85,11 +86,13 @@ def main():
     ap.add_argument("--precision", default="double", help="double | mixed (C5)")
     ap.add_argument("--no-timing", action="store_true", help="no per-phase events (clean wall time)")
     ap.add_argument("--graph", action="store_true", help="replay the launches as hipGraphs (implies --no-timing)")
+    ap.add_argument("--pair-list", default="auto", help="auto | cluster | atom_half | full (cf_options.pair_list)")
     args = ap.parse_args()
     system, force, pos_np, box = ts.make(args.config)
     for w in args.worlds:
         print(json.dumps(probe(system, force, pos_np, box, w, args.steps, args.neighbor_skin, args.kspace_algo,
-                               not (args.no_timing or args.graph), args.graph, args.precision)), flush=True)
+                               not (args.no_timing or args.graph), args.graph, args.precision,
+                               args.pair_list)), flush=True)
 
 
 if __name__ == "__main__":
