@@ -1326,6 +1326,26 @@ static void join_wait(cf::Handle& h) {
               "hipStreamWaitValue64 (join)");
 }
 
+// Inside a capture on `cap`: an event-wait node on `ev` after everything captured so far, and
+// every later captured launch after it.  (hipStreamWaitEvent on an event recorded outside the
+// capture, even with hipEventWaitExternal, was refused at the end of the capture as unjoined
+// work.)  The node waits, when the graph is launched, for the event's record enqueued last.
+static void capture_event_wait(hipStream_t cap, hipEvent_t ev) {
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    unsigned long long id = 0;
+    hipGraph_t graph = nullptr;
+    const hipGraphNode_t* deps = nullptr;
+    size_t nd = 0;
+    check_hip(hipStreamGetCaptureInfo_v2(cap, &st, &id, &graph, &deps, &nd), "hipStreamGetCaptureInfo_v2");
+    if (st != hipStreamCaptureStatusActive || !graph) fail(CF_ERR_STATE, "capture_event_wait: stream is not capturing");
+    std::vector<hipGraphNode_t> dep(deps, deps + nd);
+    hipGraphNode_t w = nullptr;
+    check_hip(hipGraphAddEventWaitNode(&w, graph, dep.empty() ? nullptr : dep.data(), dep.size(), ev),
+              "hipGraphAddEventWaitNode");
+    check_hip(hipStreamUpdateCaptureDependencies(cap, &w, 1, hipStreamSetCaptureDependencies),
+              "hipStreamUpdateCaptureDependencies");
+}
+
 static void launch_full(cf_handle* H, const double* pos_dev, int flags, bool reusable, double* forces_dev,
                         double* energy_dev, GraphCache* g, const double* box9) {
     cf::Handle& h = H->h;
@@ -1380,6 +1400,22 @@ static void launch_full(cf_handle* H, const double* pos_dev, int flags, bool reu
         fork_aux(h);
         on_aux(H, g, SEG_DCH, key, dch);
         join_post(h);
+        if (g) {
+            // graph mode: the join's wait (an external event-wait node: it waits for the record
+            // enqueued just above, after the direct chain's graph) and the energy / chain-rule
+            // kernel end the reciprocal chain's graph, so the caller's queue crosses no graph
+            // boundary between the interpolation and k_assemble_energy (an eager wait and launch
+            // after the graph left a ~15 us gap there, against ~6 us eager)
+            const GraphKey key_rec = make_key(h, pos_dev, forces_dev, energy_dev, flags, reusable, box9);
+            run_segment(H, g, SEG_REC, key_rec, [&] {
+                rec();
+                capture_event_wait(h.stream, h.ev_join);
+                h.rec_split = forces != 0;
+                cf::launch_assemble_energy(h, (forces && forces_dev) ? forces_dev : nullptr, energy, energy_dev);
+            });
+            h.rec_split = forces != 0;
+            return;
+        }
         run_segment(H, g, SEG_REC, key, rec);
         join_wait(h);
     }
