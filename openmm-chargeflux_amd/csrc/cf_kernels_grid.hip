@@ -1385,6 +1385,11 @@ __global__ void __launch_bounds__(8 * SEQ) k_g_dft8_inv(Dft8 d, const double2* _
     extern __shared__ v2d sm8[];
     v2d* sZ = sm8;                      // [kD8BC][8][SP]
     v2d* stw = sm8 + kD8BC * 8 * SP;    // [8][Q]
+    // the [Q][mt] rows in LDS (broadcast reads): as wave-uniform scalar loads every b step waited
+    // on them, and a scalar load's wait covers the LDS reads too (one counter): C3 inverse stages
+    // 28.5 -> 27.0 us, C5 153 -> 146 (r6ai; the same staging in the analysis made it slower,
+    // 36.5 -> 40.1 and 151 -> 161: its larger LDS footprint costs blocks per CU)
+    v2d* stq = stw + 8 * d.Q;           // [Q][MT]
     const int s0 = blockIdx.x * SEQ;
     if (d.xmode == 1 && d.xr &&
         !x_range_in_slab(s0 / d.xdiv, min(s0 + SEQ - 1, d.nseq - 1) / d.xdiv, d.xr, d.W, d.ngx))
@@ -1392,6 +1397,7 @@ __global__ void __launch_bounds__(8 * SEQ) k_g_dft8_inv(Dft8 d, const double2* _
     const int tid = threadIdx.x, lane = tid & 63;
     const int sq = lane % SEQ, r = wave_id() * (64 / SEQ) + lane / SEQ;
     for (int e = tid; e < 8 * d.Q; e += NT) stw[e] = reinterpret_cast<const v2d*>(twist)[e];
+    for (int e = tid; e < d.Q * MT; e += NT) stq[e] = reinterpret_cast<const v2d*>(tq)[e];
     const int s = s0 + sq;
     v2d cv[MT];
     {
@@ -1412,12 +1418,15 @@ __global__ void __launch_bounds__(8 * SEQ) k_g_dft8_inv(Dft8 d, const double2* _
     for (int bc = kD8BC * blockIdx.y; bc < d.Q; bc += kD8BC * gridDim.y) {
         const int nb = min(kD8BC, d.Q - bc);
         const v2d* twr = stw + r * d.Q + bc;
-        const double2* tqb = tq + (long)bc * MT;
+        const v2d* tqb = stq + bc * MT;
 #pragma unroll 2
         for (int b = 0; b < nb; b++) {
             v2d z = v2d{0.0, 0.0}, zt = v2d{0.0, 0.0};
 #pragma unroll
-            for (int t = 0; t < MT; t++) cmac(z, cv[t], tqb[b * MT + t]);
+            for (int t = 0; t < MT; t++) {
+                const v2d q = tqb[b * MT + t];
+                cmac(z, cv[t], make_double2(q.x, q.y));
+            }
             const v2d tw = twr[b];
             cmac(zt, z, make_double2(tw.x, tw.y));   // w^{b k_r} sum_t c_t w_Q^{b t}
             sZ[(b * 8 + r) * SP + sq] = zt;
@@ -2486,7 +2495,7 @@ static void d8_inv(Handle& h, int axis, const void* in, void* out) {
     const dim3 grid((unsigned)nb, (unsigned)std::max(1, std::min(nchunks, 2048 / nb)));
     const double2* twist = h.g_tw8[axis];
     const double2* tq = twist + 8 * d.Q;
-    const size_t lds2 = (size_t)(kD8BC * 8 * (kD8Seq + 1) + 8 * d.Q) * sizeof(double2);
+    const size_t lds2 = (size_t)(kD8BC * 8 * (kD8Seq + 1) + 8 * d.Q + d.Q * h.gp.mt[axis]) * sizeof(double2);
 #define CF_D8I(MT_)                                                                                            \
     if (axis == 2) hipLaunchKernelGGL((k_g_dft8_inv<MT_, true, kD8Seq>), grid, dim3(8 * kD8Seq), lds2, h.stream, d, twist, tq); \
     else hipLaunchKernelGGL((k_g_dft8_inv<MT_, false, kD8Seq>), grid, dim3(8 * kD8Seq), lds2, h.stream, d, twist, tq)
