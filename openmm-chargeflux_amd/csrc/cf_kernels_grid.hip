@@ -32,6 +32,7 @@ static inline int nblk(int64_t n, int b) { return (int)((n + b - 1) / b); }
 
 // native 2-vector for register staging (HIP's double2 struct arrays stay in scratch memory)
 typedef double v2d __attribute__((ext_vector_type(2)));
+typedef float v2f __attribute__((ext_vector_type(2)));   // packed fp32 (v_pk_fma_f32)
 
 // wave index within the workgroup as a wave-uniform (SGPR) value, so that everything
 // derived from it is scalar (the compiler treats threadIdx.x >> 6 as divergent)
@@ -403,12 +404,18 @@ __device__ __forceinline__ void fma8_row_bcast(double (&acc)[8], double xv, doub
 
 // TF: fp32 tap rows (GridPlan::taps_f32, NS = 2): a 16-B piece is half a window (4 floats), widened
 // to fp64 as it is staged; the sums stay fp64
-template <int NS, int kSpPass, bool TF = false, bool GF = false>
+template <int NS, int kSpPass, bool TF = false, bool GF = false, bool FA = false>
 __global__ void __launch_bounds__(256) CF_LDS_UNPAIRED k_g_spread_tile(int3 ng, int3 nb, const int* __restrict__ start,
                                                        const double* __restrict__ taps, const int4* __restrict__ g0s,
                                                        double* __restrict__ grid, const int* __restrict__ xr, int W) {
-    // GF: the grid is fp32 (GridPlan::grid_f32): each point's fp64 sum rounded once as it is stored
+    // GF: the grid is fp32 (GridPlan::grid_f32): each point's fp64 sum rounded once as it is stored.
+    // FA (mixed precision, with TF and GF): the windows staged as fp32 and the per-wave sums in fp32,
+    // eight packed FMAs' worth in four v_pk_fma_f32 per (atom, lane) with the x window read as two
+    // broadcast 16-B LDS loads (the fp64 form: eight DPP row-broadcast FMAs); the 4 waves' partial
+    // tiles are added in fp64 in a fixed order.  Each grid point sums ~20 contributions at C5:
+    // fp32 rounding ~1e-7 relative, under the mixed grid's own error.
     static_assert(!TF || NS == 2, "fp32 rows hold points 0..15: windows db = 0, 1");
+    static_assert(!FA || (TF && GF), "fp32 arithmetic on the fp32 rows and grid only");
     constexpr int NB3 = NS * NS * NS;
     static_assert(NS <= 3, "tile offsets are packed in 2 bits per axis");
     constexpr int kStD = 2 * kSpPass * kSpWin > 4 * 8 * 64 ? 2 * kSpPass * kSpWin : 4 * 8 * 64;
@@ -446,6 +453,7 @@ __global__ void __launch_bounds__(256) CF_LDS_UNPAIRED k_g_spread_tile(int3 ng, 
     double acc[8];
 #pragma unroll
     for (int i = 0; i < 8; i++) acc[i] = 0.0;
+    v2f accf[4] = {v2f{0.f, 0.f}, v2f{0.f, 0.f}, v2f{0.f, 0.f}, v2f{0.f, 0.f}};   // (FA: x = 2k, 2k + 1)
     for (int seg0 = 0; seg0 < total; seg0 += kSpMaxSrc) {
         const int nall = min(kSpMaxSrc, total - seg0);
         __syncthreads();   // previous segment's passes done with src
@@ -531,7 +539,9 @@ __global__ void __launch_bounds__(256) CF_LDS_UNPAIRED k_g_spread_tile(int3 ng, 
             for (int q = 0; q < kPer; q++) {
                 const int e = t + 256 * q;
                 if (kPieces % 256 == 0 || e < kPieces) {
-                    if constexpr (TF) {
+                    if constexpr (FA) {   // fp32 staging: piece e is floats 4e .. 4e + 3
+                        reinterpret_cast<float4*>(buf)[e] = r[q];
+                    } else if constexpr (TF) {
                         v2d* o = reinterpret_cast<v2d*>(buf) + 2 * e;
                         o[0] = v2d{(double)r[q].x, (double)r[q].y};
                         o[1] = v2d{(double)r[q].z, (double)r[q].w};
@@ -542,14 +552,40 @@ __global__ void __launch_bounds__(256) CF_LDS_UNPAIRED k_g_spread_tile(int3 ng, 
             }
         };
         const int npass = (nseg + kSpPass - 1) / kSpPass;
+        // staging buffer p (FA: fp32 windows, half the bytes)
+        auto sbuf = [&](int p) { return FA ? (double*)(reinterpret_cast<float*>(st) + (p & 1) * kSpPass * kSpWin)
+                                           : st + (p & 1) * kSpPass * kSpWin; };
         fetch(0, min(kSpPass, nseg));
-        stage(st);
+        stage(sbuf(0));
         __syncthreads();
         for (int p = 0; p < npass; p++) {
             const int base = p * kSpPass, n = min(kSpPass, nseg - base);
             if (p + 1 < npass) fetch(base + kSpPass, min(kSpPass, nseg - base - kSpPass));
-            const double* buf = st + (p & 1) * kSpPass * kSpWin;
-            {
+            const double* buf = sbuf(p);
+            if constexpr (FA) {
+                static_assert(kSpPass % 16 == 0, "four-atom groups");
+                const float* fb = reinterpret_cast<const float*>(buf);
+                const int yo = 8 + y, zo = 16 + (lane & 7);
+                for (int a = w; a < n; a += 16) {
+                    float4 xa[4], xb[4];
+                    float yz[4];
+#pragma unroll
+                    for (int u = 0; u < 4; u++) {
+                        const float* r = fb + (a + 4 * u) * kSpWin;
+                        xa[u] = *reinterpret_cast<const float4*>(r);       // x taps 0..3 (a broadcast)
+                        xb[u] = *reinterpret_cast<const float4*>(r + 4);   // x taps 4..7
+                        yz[u] = r[yo] * r[zo];
+                    }
+#pragma unroll
+                    for (int u = 0; u < 4; u++) {
+                        const v2f s2 = v2f{yz[u], yz[u]};
+                        accf[0] = v2f{xa[u].x, xa[u].y} * s2 + accf[0];
+                        accf[1] = v2f{xa[u].z, xa[u].w} * s2 + accf[1];
+                        accf[2] = v2f{xb[u].x, xb[u].y} * s2 + accf[2];
+                        accf[3] = v2f{xb[u].z, xb[u].w} * s2 + accf[3];
+                    }
+                }
+            } else {
                 // lane l reads x tap (l & 7) of the staged window, so lane i of every 16-lane row
                 // holds tap i, and each FMA takes tap i by a row broadcast of its operand
                 // (row_newbcast:i, 64-bit DPP): every operand comes from the LDS with 8-B per-lane
@@ -572,13 +608,17 @@ __global__ void __launch_bounds__(256) CF_LDS_UNPAIRED k_g_spread_tile(int3 ng, 
                     for (int u = 0; u < 4; u++) fma8_row_bcast(acc, xv[u], yv[u] * zv[u]);
                 }
             }
-            if (p + 1 < npass) stage(st + ((p + 1) & 1) * kSpPass * kSpWin);
+            if (p + 1 < npass) stage(sbuf(p + 1));
             __syncthreads();
         }
     }
     // the 4 waves' partial tiles, summed in fixed wave order
     __syncthreads();
     double* red = st;   // [4][8][64]
+    if constexpr (FA) {
+#pragma unroll
+        for (int k = 0; k < 4; k++) { acc[2 * k] = accf[k].x; acc[2 * k + 1] = accf[k].y; }
+    }
 #pragma unroll
     for (int i = 0; i < 8; i++) red[(w * 8 + i) * 64 + lane] = acc[i];
     __syncthreads();
@@ -2079,8 +2119,8 @@ __global__ void __launch_bounds__(kInterpThreads) CF_LDS_UNPAIRED k_g_interp4(in
         }
         xv = dpp_ready(xv); xd = dpp_ready(xd); yv = dpp_ready(yv); yd = dpp_ready(yd);
         const int rx = g.x & 7, ry = g.y & 7, rz = g.z & 7;
-        const double* base = sg + (rx * R + ry) * R + rz + (k < W ? k : 0);
         double t0[NJ], t1[NJ];   // row 0 initialises them (products: no zero fill)
+        const double* base = sg + (rx * R + ry) * R + rz + (k < W ? k : 0);
         double gv[2][NJ];
         auto load_row = [&](int i, double (&gg)[NJ]) {
 #pragma unroll
@@ -2330,7 +2370,7 @@ void launch_grid_sort(Handle& h, const double* pos) {
 void launch_grid_spread(Handle& h) {
     const GridPlan& p = h.gp;
     const int3 ng = make_int3(p.ng[0], p.ng[1], p.ng[2]), nb = make_int3(p.nb[0], p.nb[1], p.nb[2]);
-#define CF_SPT(NS_, P_, TF_, GF_) hipLaunchKernelGGL((k_g_spread_tile<NS_, P_, TF_, GF_>), dim3(p.nbins), dim3(256), 0, \
+#define CF_SPT(NS_, P_, TF_, GF_, FA_) hipLaunchKernelGGL((k_g_spread_tile<NS_, P_, TF_, GF_, FA_>), dim3(p.nbins), dim3(256), 0, \
                                                     h.stream, ng, nb, h.g_start, h.g_taps, h.g_g0s, h.g_grid, h.g_xrange, p.W)
     // the matrix-core form (16 x 8 x 8 tiles, 4 distinct x bins) for W > 9; at W <= 9 (the mixed
     // C5 grid) the vector form with its 8^3 tiles and 8 source bins measured faster (322 against
@@ -2348,10 +2388,10 @@ void launch_grid_spread(Handle& h) {
     }
     // a first tap in bin B reaches tiles B .. B + NS - 1: NS = 2 when W <= 9 (8 source bins per
     // tile instead of 27).  Passes of 32 atoms at W = 14 (64 / 128 measured slower at C3)
-    if (p.grid_f32) CF_SPT(2, 64, true, true);
-    else if (p.taps_f32) CF_SPT(2, 64, true, false);
-    else if (p.W <= 9) CF_SPT(2, 64, false, false);
-    else CF_SPT(3, 32, false, false);
+    if (p.grid_f32) CF_SPT(2, 64, true, true, true);
+    else if (p.taps_f32) CF_SPT(2, 64, true, false, false);
+    else if (p.W <= 9) CF_SPT(2, 64, false, false, false);
+    else CF_SPT(3, 32, false, false, false);
 #undef CF_SPT
 }
 
