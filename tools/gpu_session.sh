@@ -51,6 +51,11 @@ for st in "$@"; do
     smoke)
         run smoke $out/smoke.log 200 python -u -c "import __graft_entry__ as g; g.smoke()"
         tail -3 $out/smoke.log;;
+    bench=*)   # bench=ARGS (comma-separated): one bench line with these arguments
+        a=${st#bench=}; tagf=$(echo "$a" | tr -c 'A-Za-z0-9.' '_')
+        timeout -k 10 400 python -u bench.py ${a//,/ } > $out/bench_$tagf.json 2> $out/bench_$tagf.err
+        rc=$?; echo "STEP bench $a rc=$rc"; [ $rc -eq 0 ] || fail bench_$tagf $out/bench_$tagf.err $rc
+        python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[2], d['ms_per_step'], d.get('graph_replay_ms_per_step'))" $out/bench_$tagf.json "$a";;
     bench_*)
         cfg=${st#bench_}
         timeout -k 10 400 python -u bench.py $(cfgargs $cfg) $(benchargs $cfg) > $out/$st.json 2> $out/$st.err
