@@ -694,18 +694,38 @@ __global__ void __launch_bounds__(kWaveNL * kSeg) k_nlist_wave(DirectArgs a) {
                     const int us = (((ds >> 4) << 2) | (ds & 3)) - (u0 + c0);
                     if (us >= 0 && us < 16) bits &= ~(1u << us);
                 }
-                while (bits) {
+                // the hits of the chunk, one per trip; the next hit's staged index is read before
+                // this one is emitted (a trip's LDS read sat on its dependency chain: with one wave
+                // per SIMD at W = 8 its latency was exposed on every trip, r06ap; rebuilds 155-180 ->
+                // 156-169 us, r06aq)
+                if (bits) {
                     int v = __builtin_ctz(bits);
                     bits &= bits - 1;
-                    const int cj = cand_j[c0 + v];
-                    emit(slot_of(cb, u0 + c0 + v), cj & kJMask, a.typ_s ? (int)((unsigned)cj >> kShiftBits) : code);
+                    int cj = cand_j[c0 + v];
+                    for (;;) {
+                        const int vn = bits ? __builtin_ctz(bits) : v;
+                        const int cjn = cand_j[c0 + vn];
+                        emit(slot_of(cb, u0 + c0 + v), cj & kJMask, a.typ_s ? (int)((unsigned)cj >> kShiftBits) : code);
+                        if (!bits) break;
+                        bits &= bits - 1;
+                        v = vn;
+                        cj = cjn;
+                    }
                 }
             } else {
-                while (bits) {
+                if (bits) {
                     int v = __builtin_ctz(bits);
                     bits &= bits - 1;
-                    const int cj = cand_j[c0 + v];
-                    put_entry(slot_of(cb, u0 + c0 + v) | (hk << kHalfSlotBits) | (cj & ~kJMask), cj & kJMask);
+                    int cj = cand_j[c0 + v];
+                    for (;;) {
+                        const int vn = bits ? __builtin_ctz(bits) : v;
+                        const int cjn = cand_j[c0 + vn];
+                        put_entry(slot_of(cb, u0 + c0 + v) | (hk << kHalfSlotBits) | (cj & ~kJMask), cj & kJMask);
+                        if (!bits) break;
+                        bits &= bits - 1;
+                        v = vn;
+                        cj = cjn;
+                    }
                 }
             }
         }
