@@ -385,7 +385,7 @@ def main():
     #  grid_interp   4 N W^3 fp64 VALU flops (two FMAs per grid value), bytes 8 ng^3 + 24 N W + 32 N
     #  kspace_sfac / kspace_force (exact path)  4 / 8 fp64 MFMA flops per atom x half-space k-vector
     # fraction of the roof = max(B / BW, F / P) / t; "bound" names the larger term
-    w_grid = args.grid_width or (8 if args.precision == "mixed" else 14)
+    w_grid = kern.kernel.grid_width() if args.kspace_algo == 2 else 0   # the library's choice (0: its default)
     roofline, others = None, {}
     if dom is not None:
         p_c = pair_count(force, pos_np, box) * n_own / n

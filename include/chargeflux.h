@@ -91,7 +91,7 @@ typedef struct cf_options {
                             1 = exact k-sum, direct VALU sincos (check path)
                             2 = grid: the same k-sum through ES-kernel spreading, pruned DFT
                                 and interpolation (error set by grid_width) */
-    int32_t grid_width;  /* kspace_algo 2: ES kernel width in grid points, 4..16 (0 = 14, or 8 mixed) */
+    int32_t grid_width;  /* kspace_algo 2: ES kernel width in grid points, 4..16 (0 = 13, or 8 mixed) */
     int32_t precision;   /* CF_PRECISION_DOUBLE (0, default) or CF_PRECISION_MIXED (1): the
                             direct-space pair kernel computes in fp32 (positions, erfc, LJ) and
                             accumulates forces in fp32 and energies in fp64 per atom; every

@@ -168,6 +168,13 @@ class HipCalcCoulForceKernel:
         _cabi.check(self._lib.cf_get_grid_shape(self._h, ng, C.byref(w)), self._lib)
         return tuple(ng)
 
+    def grid_width(self) -> int:
+        """ES kernel width W the grid reciprocal path uses (0 for the exact paths)."""
+        ng = (C.c_int32 * 3)()
+        w = C.c_int32()
+        _cabi.check(self._lib.cf_get_grid_shape(self._h, ng, C.byref(w)), self._lib)
+        return int(w.value)
+
     def set_neighbor_skin(self, skin: float):
         """Persistent neighbour list with a skin (nm); 0 = rebuild on every execute (the
         reference's behaviour, ReferenceCoulKernels.cpp:559).  See include/chargeflux.h."""

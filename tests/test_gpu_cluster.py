@@ -49,7 +49,7 @@ def test_cluster_list_matches_atom_lists_and_oracle(nw, algo, shuffle):
         assert np.abs(dc - d).max() <= 1e-10 * np.abs(d).max()
         assert abs(tc[2] - t[2]) <= 1e-11 * abs(t[2]) + 1e-9
     ref = Oracle(force, box).execute(pos, box)
-    assert np.abs(fc - ref["forces"]).max() <= (1e-8 if algo == 0 else 1e-6)
+    assert np.abs(fc - ref["forces"]).max() <= (1e-8 if algo == 0 else 2.5e-6)
     assert abs(ec - ref["energy"]) <= 1e-9 * np.abs(ref["terms"]).sum() + 1e-8
 
 

@@ -14,7 +14,7 @@ Tolerances (written here; the north star asks for forces within 1e-5 kJ/mol/nm):
   exact k-sum vs oracle   forces <= 1e-8 kJ/mol/nm, dE/dq <= 1e-10 relative (grid: 1e-9), energy and each
                           term <= 1e-12 / 1e-10 of sum |terms| (E ~ -1e3 is a near-cancellation
                           of +-7.6e6 kJ/mol terms at C3)
-  grid k-sum vs oracle    forces <= 1e-6 kJ/mol/nm (W = 14: ~2e-8 observed), energy as above
+  grid k-sum vs oracle    forces <= 2.5e-6 kJ/mol/nm (default W = 12: 0.7-1.1e-6 observed), energy as above
   W ranks vs 1 rank       forces <= 1e-8 kJ/mol/nm, energy <= 1e-13 of sum |terms|
   mixed vs fp64 (C5)      RMS relative force error <= 1e-4, max |dF| <= 0.5 kJ/mol/nm
                           (fp32 pair kernel alone, same grid: <= 1e-5 and 0.1), energy <= 1e-8 sum |terms|
@@ -114,7 +114,7 @@ def _check_golden(d, e, f, q, dq, f_tol, terms=None):
             assert abs(a - b) <= 1e-10 * max(abs(b), 1.0), (terms, d["terms"])
 
 
-@pytest.mark.parametrize("algo,f_tol", [(EXACT, 1e-8), (GRID, 1e-6)])
+@pytest.mark.parametrize("algo,f_tol", [(EXACT, 1e-8), (GRID, 2.5e-6)])
 def test_c3_vs_oracle_golden(c3, c3_golden, algo, f_tol):
     system, force, pos, box = c3
     k = HipCalcCoulForceKernel(kspace_algo=algo).initialize(system, force)
@@ -123,7 +123,7 @@ def test_c3_vs_oracle_golden(c3, c3_golden, algo, f_tol):
     _check_golden(c3_golden, e, f, k.charges(), k.dedq(), f_tol, k.energy_terms())
 
 
-@pytest.mark.parametrize("algo,f_tol", [(EXACT, 1e-8), (GRID, 1e-6)])
+@pytest.mark.parametrize("algo,f_tol", [(EXACT, 1e-8), (GRID, 2.5e-6)])
 def test_c4_eight_rank_decomposition_full_c3(c3, c3_golden, algo, f_tol):
     """C4: the C3 box over 8 ranks; equal to the single-rank result and to the oracle."""
     system, force, pos, box = c3

@@ -8,7 +8,7 @@ largest forces: above the north star's 1e-5 bar.  cf_params.one_4pi_eps0 carries
 (0 = 138.935456); the oracle takes the same field.
 
 Tolerances (written here): exact k-sum vs oracle at the same k_e, forces <= 1e-8 kJ/mol/nm,
-energy <= 1e-9 |E| + 1e-8 (C2) or 1e-12 of sum |terms| (C3); the grid k-sum, forces <= 1e-6.
+energy <= 1e-9 |E| + 1e-8 (C2) or 1e-12 of sum |terms| (C3); the grid k-sum, forces <= 2.5e-6 (default W = 12).
 Passing k_e = 138.935456 explicitly gives the same bits as the default (0).
 """
 import os
@@ -35,7 +35,7 @@ def _need_gpu():
         pytest.skip("no HIP device")
 
 
-@pytest.mark.parametrize("algo,f_tol", [(EXACT, 1e-8), (GRID, 1e-6)])
+@pytest.mark.parametrize("algo,f_tol", [(EXACT, 1e-8), (GRID, 2.5e-6)])
 def test_c2_at_openmm8_constant_matches_oracle(algo, f_tol):
     system, force, pos, box = ts.make("C2")
     k = HipCalcCoulForceKernel(kspace_algo=algo, one_4pi_eps0=KE8).initialize(system, force)
@@ -82,7 +82,7 @@ def test_invalid_constant_and_update_keep_it():
     assert np.abs(f - ref["forces"]).max() <= 1e-8
 
 
-@pytest.mark.parametrize("algo,f_tol", [(EXACT, 1e-8), (GRID, 1e-6)])
+@pytest.mark.parametrize("algo,f_tol", [(EXACT, 1e-8), (GRID, 2.5e-6)])
 def test_c3_at_openmm8_constant_matches_oracle_fixture(algo, f_tol):
     """Full-size C3 at k_e = 138.93545764438198 against the oracle's full-size run at the same
     constant (tests/golden/c3_codata2018.npz, make_golden.py --c3-codata2018): a seeded

@@ -10,7 +10,7 @@ the one-GPU box -- the same calls RCCL runs on an 8-GPU node).  This exercises w
 Bar: every rank's global energy and the gathered owned forces equal a one-rank evaluation of the
 same positions (forces <= 2e-12 max|F| + 1e-9 kJ/mol/nm -- the one-rank cluster list rounds each
 partner-side term to the 2^-34 fixed point, the per-atom full list of two ranks does not; energy
-<= 1e-10 relative) and, on the first step, the oracle (exact k-sum 1e-8, grid 1e-6)."""
+<= 1e-10 relative) and, on the first step, the oracle (exact k-sum 1e-8, grid 2.5e-6)."""
 import os
 import socket
 
@@ -94,7 +94,7 @@ def test_sharded_kernel_two_ranks_matches_one_rank_and_oracle(case, algo, skin):
         ref.append(k.execute_host(p, box))
         p = p + moves[s]
     o = Oracle(force, box).execute(pos, box)
-    f_tol = 1e-8 if algo == 0 else 1e-6
+    f_tol = 1e-8 if algo == 0 else 2.5e-6
     ranges = []
     for r in range(2):
         res, lo, hi, bits = out[r]

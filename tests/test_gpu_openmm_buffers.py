@@ -5,7 +5,7 @@ reference's CUDA platform binds its kernels to (platforms/cuda/src/CudaCoulKerne
 
 Buffers are built from the synthetic systems with a shuffled atomIndex (OpenMM reorders atoms
 spatially) and pre-filled force / energy contents, and checked against the oracle:
-  forces  max |dF| <= 1e-8 kJ/mol/nm (exact k-sum) / 1e-6 (grid k-sum), after the fixed-point
+  forces  max |dF| <= 1e-8 kJ/mol/nm (exact k-sum) / 2.5e-6 (grid k-sum), after the fixed-point
           conversion (resolution 2^-32 = 2.3e-10)
   energy  |dE| <= 1e-9 |E| + 1e-8 kJ/mol
 posq is never written (the reference's CUDA platform overwrites posq.w with the flux charges,
@@ -56,7 +56,7 @@ def _forces_from_buffer(fbuf, fbuf0, perm, padded, n):
     return f
 
 
-@pytest.mark.parametrize("case,algo,f_tol", [("C2", 0, 1e-8), ("C2", 2, 1e-6), ("w4k", 2, 1e-6)])
+@pytest.mark.parametrize("case,algo,f_tol", [("C2", 0, 1e-8), ("C2", 2, 2.5e-6), ("w4k", 2, 2.5e-6)])
 def test_openmm_buffers_match_oracle(case, algo, f_tol):
     if case == "C2":
         system, force, pos, box = ts.make("C2")

@@ -7,7 +7,7 @@ that are parallelepipeds in fractional coordinates (O(N): cf_api.hip set_cells,
 cf_kernels_core.hip k_cell_hist; boxes under 3 cells per direction use all pairs), the k-space paths are
 unchanged (both evaluate the diagonal-only sum on per-axis wrapped coordinates, which leave
 every factor e^{i k_a x_a} unchanged).
-Tolerances as in test_gpu_parity.py (exact k-sum: forces 1e-8) and test_gpu_grid.py (grid: 1e-6).
+Tolerances as in test_gpu_parity.py (exact k-sum: forces 1e-8) and test_gpu_grid.py (grid: 2.5e-6).
 """
 import numpy as np
 import pytest
@@ -42,7 +42,7 @@ def _compare(k, pos, box, ref, f_tol, fl=True, en=True):
         assert abs(a - b) <= 1e-9 * max(abs(b), 1.0) + 1e-8, (k.energy_terms(), ref["terms"])
 
 
-@pytest.mark.parametrize("algo,f_tol", [(EXACT, 1e-8), (GRID, 1e-6)])
+@pytest.mark.parametrize("algo,f_tol", [(EXACT, 1e-8), (GRID, 2.5e-6)])
 def test_triclinic_vs_oracle(algo, f_tol):
     system, force, pos, box = ts.triclinic_water_box(300, cutoff=0.7)
     k = HipCalcCoulForceKernel(kspace_algo=algo).initialize(system, force)
@@ -51,7 +51,7 @@ def test_triclinic_vs_oracle(algo, f_tol):
         _compare(k, pos, box, o.execute(pos, box, fl, en), f_tol, fl, en)
 
 
-@pytest.mark.parametrize("algo,f_tol", [(EXACT, 1e-8), (GRID, 1e-6)])
+@pytest.mark.parametrize("algo,f_tol", [(EXACT, 1e-8), (GRID, 2.5e-6)])
 def test_triclinic_moved_and_lattice_shifted(algo, f_tol):
     # atoms displaced and some moved by whole box vectors (the reference's k-sum uses the
     # unwrapped positions, so a lattice shift changes it: both sides see the same positions)
@@ -171,7 +171,7 @@ def test_triclinic_cell_path_lattice_shifted_atoms_and_grid():
     p2[::11] -= box[2]
     p2[::13] += box[0] - box[1] + box[2]
     ref = Oracle(force, box).execute(p2, box)
-    _compare(_kernel(system, force, GRID), p2, box, ref, 1e-6)
+    _compare(_kernel(system, force, GRID), p2, box, ref, 2.5e-6)
 
 
 def test_triclinic_cell_path_skin_trajectory_half_and_full():

@@ -51,7 +51,7 @@ def test_update_matches_fresh_handle_and_oracle(algo, skin, distinct):
     ref_h = _run(fresh, pos, box)
     assert abs(got[0] - ref_h[0]) <= 1e-12 * abs(ref_h[0])
     assert np.abs(got[1] - ref_h[1]).max() <= 1e-12 * np.abs(ref_h[1]).max() + 1e-9
-    _compare(got, Oracle(force, box).execute(pos, box), f_tol=1e-6 if algo == 2 else 1e-8)
+    _compare(got, Oracle(force, box).execute(pos, box), f_tol=2.5e-6 if algo == 2 else 1e-8)
 
 
 def test_update_no_pbc_through_context():
