@@ -2345,7 +2345,7 @@ void launch_grid_sort(Handle& h, const double* pos) {
         else CF_OT(0, true);
     } else if (p.W == 14) CF_OT(14, false);
     else if (p.W == 13) CF_OT(13, false);
-    else if (p.W == 12) CF_OT(12, false);   // the fp64 default
+    else if (p.W == 12) CF_OT(12, false);
     else if (p.W == 8) CF_OT(8, false);
     else CF_OT(0, false);
 #undef CF_OT

@@ -14,7 +14,7 @@ Tolerances (written here; the north star asks for forces within 1e-5 kJ/mol/nm):
   exact k-sum vs oracle   forces <= 1e-8 kJ/mol/nm, dE/dq <= 1e-10 relative (grid: 1e-9), energy and each
                           term <= 1e-12 / 1e-10 of sum |terms| (E ~ -1e3 is a near-cancellation
                           of +-7.6e6 kJ/mol terms at C3)
-  grid k-sum vs oracle    forces <= 2.5e-6 kJ/mol/nm (default W = 12: 0.7-1.1e-6 observed), energy as above
+  grid k-sum vs oracle    forces <= 2.5e-6 kJ/mol/nm (default W = 13: 5e-8 observed on the bench's positions), energy as above
   W ranks vs 1 rank       forces <= 1e-8 kJ/mol/nm, energy <= 1e-13 of sum |terms|
   mixed vs fp64 (C5)      RMS relative force error <= 1e-4, max |dF| <= 0.5 kJ/mol/nm
                           (fp32 pair kernel alone, same grid: <= 1e-5 and 0.1), energy <= 1e-8 sum |terms|

@@ -8,7 +8,7 @@ largest forces: above the north star's 1e-5 bar.  cf_params.one_4pi_eps0 carries
 (0 = 138.935456); the oracle takes the same field.
 
 Tolerances (written here): exact k-sum vs oracle at the same k_e, forces <= 1e-8 kJ/mol/nm,
-energy <= 1e-9 |E| + 1e-8 (C2) or 1e-12 of sum |terms| (C3); the grid k-sum, forces <= 2.5e-6 (default W = 12).
+energy <= 1e-9 |E| + 1e-8 (C2) or 1e-12 of sum |terms| (C3); the grid k-sum, forces <= 2.5e-6 (default W = 13).
 Passing k_e = 138.935456 explicitly gives the same bits as the default (0).
 """
 import os

@@ -5,7 +5,7 @@ ReferenceCoulKernels.cpp:513-556 and against the exact fp64-MFMA k-sum.
 The grid evaluates the reference's own truncated k-sum (same k-set, weights and current
 box); its only error is the ES-kernel quadrature error, set by the kernel width W.
 Tolerances (written here; north star: forces within 1e-5 kJ/mol/nm):
-  forces   max |dF|         <= 2.5e-6 kJ/mol/nm (default W = 12: 0.7-1.1e-6 at C3, ~5e-7 small; W = 14 ~1e-8)
+  forces   max |dF|         <= 2.5e-6 kJ/mol/nm (default W = 13: 5e-8 on the bench's C3 positions; W = 14 ~1e-8)
   energy   |dE|             <= 1e-9 |E| + 1e-8 kJ/mol
   dE/dq    max |d(dE/dq)|   <= 1e-9 max|dE/dq| + 1e-9
   charges  max |dq|         <= 1e-12 e (untouched by the k-space method)
