@@ -644,9 +644,9 @@ CF_EXPORT int cf_create(const cf_params* p, const cf_options* opt, cf_handle** o
             // with W adjusted for equal accuracy.  Default width: the smallest W
             // whose quadrature error (max |dF| against the exact k-sum) stays within the k-space
             // budget of a quarter of the north star's 1e-5 kJ/mol/nm, i.e. 2.5e-6, at every C3
-            // configuration measured: W = 13 in fp64 (W = 12 reached 6.6e-6 at C3's initial
-            // positions; W = 14 gives ~1e-8 at +3 % step time), W = 8 in mixed precision (bar:
-            // 1e-4 RMS relative)
+            // configuration measured: W = 13 in fp64 (5.9e-8 at C3's initial positions; W = 12
+            // reached 6.6e-6 there; W = 14: 6.9e-8 at +3-4 % step time), W = 8 in mixed precision
+            // (bar: 1e-4 RMS relative)
             if (h.kspace_algo == 2) cf::grid_plan(h, o.grid_width ? o.grid_width : (h.mixed ? 8 : 13), 2.0);
         }
 
