@@ -480,10 +480,10 @@ __device__ __forceinline__ int block_exclusive_scan_t(int v, int* sh) {
 // (and end[c] = start[c + 1] when end != null; start[m] = total when total_at_end), by the NT
 // threads of one block, in tiles of 8 NT counts: each thread issues the loads of kBoundsU
 // tiles at once (one memory latency per kBoundsU tiles, not one per count or per tile: the
-// C5 grid's 32k bins are 16 tiles at NT = 256)
+// C5 grid's 32k bins are 16 tiles at NT = 256).  Returns the total (in every thread).
 constexpr int kBoundsU = 4;
 template <int NT>
-__device__ __forceinline__ void block_counts_to_bounds(int m, int* cnt, int* start, int* end, bool total_at_end,
+__device__ __forceinline__ int block_counts_to_bounds(int m, int* cnt, int* start, int* end, bool total_at_end,
                                                        int* sh) {
     __shared__ int tile[8 * NT];
     const int t = threadIdx.x;
@@ -523,6 +523,7 @@ __device__ __forceinline__ void block_counts_to_bounds(int m, int* cnt, int* sta
         }
     }
     if (total_at_end && t == 0) start[m] = carry;
+    return carry;
 }
 
 }  // namespace cf

@@ -185,11 +185,12 @@ __global__ void __launch_bounds__(256) k_cell_hist(int n, const int* __restrict_
     if (own_cnt) (void)wave_agg_inc(own_cnt, k, valid && i >= lo && i < hi);
     if (!last_block_done(ticket)) return;
     const int ncell = nc.x * nc.y * nc.z;
-    block_counts_to_bounds<256>(ncell, cnt, cstart, cend, false, sh);
+    const int total = block_counts_to_bounds<256>(ncell, cnt, cstart, cend, false, sh);
     // guard: the counts add up to the atoms (k_cell_scatter re-zeroes them after each build); bounds
-    // that do not are replaced by empty cells, so no kernel after this one indexes past N
-    __syncthreads();
-    if (ld_agent(cend + ncell - 1) != n) {
+    // that do not are replaced by empty cells, so no kernel after this one indexes past N (the
+    // scan's total, block-uniform: no read-back of cend[ncell - 1])
+    if (total != n) {
+        __syncthreads();   // every thread's bounds stores before they are overwritten
         for (int c = threadIdx.x; c < ncell; c += blockDim.x) { cstart[c] = 0; cend[c] = 0; }
         if (threadIdx.x == 0) atomicOr(err, kGuardCellBounds);
     }

@@ -196,12 +196,13 @@ __global__ void __launch_bounds__(256) k_g_bin(int lo, int nown, const double* _
     }
     if (!last_block_done(ticket)) return;
     const int nbins = nb.x * nb.y * nb.z;
-    block_counts_to_bounds<256>(nbins, cnt, start, nullptr, true, sh);
+    const int total = block_counts_to_bounds<256>(nbins, cnt, start, nullptr, true, sh);
     // guard: the counts add up to the owned atoms (k_g_scatter re-zeroes them each evaluation);
     // bounds that do not are replaced by empty bins, so no spread, tap or interpolation kernel
-    // indexes past the owned atoms
-    __syncthreads();
-    if (ld_agent(start + nbins) != nown) {
+    // indexes past the owned atoms (the scan's total, block-uniform: no read-back of start[nbins]
+    // on the critical path)
+    if (total != nown) {
+        __syncthreads();   // every thread's bounds stores before they are overwritten
         for (int b = threadIdx.x; b <= nbins; b += blockDim.x) start[b] = 0;
         if (threadIdx.x == 0) atomicOr(err, kGuardGridBins);
     }
