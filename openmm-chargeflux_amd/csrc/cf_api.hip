@@ -768,7 +768,9 @@ CF_EXPORT int cf_create(const cf_params* p, const cf_options* opt, cf_handle** o
                 // W <= 9: k_g_order_taps stores points 0..15 of each row only; 16..23 stay zero
                 check_hip(hipMemset(h.g_taps, 0, sizeof(double) * no * 72), "memset taps");
                 if (h.world > 1) {
-                    h.g_xrange = dalloc<int>(H, 3);
+                    // [0..2] the slab (min, max first tap, reference tap); then k_g_bin's per-block
+                    // (min, max), one pair per block of its launch (<= one block per 256 owned atoms)
+                    h.g_xrange = dalloc<int>(H, 3 + 2 * ((size_t)no / 256 + 1));
                     const int init[3] = {INT_MAX, INT_MIN, 0};
                     check_hip(hipMemcpy(h.g_xrange, init, sizeof(init), hipMemcpyHostToDevice), "x-slab init");
                 }

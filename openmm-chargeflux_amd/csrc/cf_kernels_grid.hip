@@ -137,6 +137,11 @@ __global__ void __launch_bounds__(256) k_g_bin(int lo, int nown, const double* _
                                                int* __restrict__ ticket, int* __restrict__ start, int per,
                                                int* __restrict__ err) {
     __shared__ int sh[256];
+    __shared__ int xs[2][4];
+    // several ranks: this thread's x-slab extremes over its rounds, reduced per block and written
+    // to the block's own slot of xr; the last block reduces the slots (two same-address atomics
+    // from every wave serialized at one L2 channel; k_g_bin took 17 us at W = 8 for 12k atoms, r06ax)
+    int bmin = INT_MAX, bmax = INT_MIN;
     // `per` rounds of 256 atoms per block: the ticket of last_block_done is one address that
     // every block increments, so fewer, longer blocks at large N (launch_grid_sort)
     for (int it = 0; it < per; it++) {
@@ -148,7 +153,6 @@ __global__ void __launch_bounds__(256) k_g_bin(int lo, int nown, const double* _
         double s0 = u0 * ng.x;
         if (s0 >= ng.x) s0 -= ng.x;
         const int gref = (int)ceil(s0 - 0.5 * W);
-        int rmin = INT_MAX, rmax = INT_MIN;
         if (valid) {
             double u = pos[3 * (lo + io)] / L.x;
             u -= floor(u);
@@ -157,15 +161,8 @@ __global__ void __launch_bounds__(256) k_g_bin(int lo, int nown, const double* _
             int rel = ((int)ceil(sd - 0.5 * W) - gref) % ng.x;
             rel += rel < 0 ? ng.x : 0;
             rel -= rel >= ng.x / 2 ? ng.x : 0;
-            rmin = rmax = rel;
-        }
-        for (int off = 32; off > 0; off >>= 1) {
-            rmin = min(rmin, __shfl_xor(rmin, off));
-            rmax = max(rmax, __shfl_xor(rmax, off));
-        }
-        if ((threadIdx.x & 63) == 0 && rmin <= rmax) {
-            atomicMin(&xr[0], rmin);
-            atomicMax(&xr[1], rmax);
+            bmin = min(bmin, rel);
+            bmax = max(bmax, rel);
         }
         if (io == 0) xr[2] = gref;
     }
@@ -194,7 +191,32 @@ __global__ void __launch_bounds__(256) k_g_bin(int lo, int nown, const double* _
     const int r = wave_agg_inc(cnt, bin, valid);
     if (valid) rank[io] = r;
     }
+    const int wv = threadIdx.x >> 6;
+    auto block_minmax = [&](int& mn, int& mx) {   // over the block's 4 waves, into every thread
+        for (int off = 32; off > 0; off >>= 1) {
+            mn = min(mn, __shfl_xor(mn, off));
+            mx = max(mx, __shfl_xor(mx, off));
+        }
+        if ((threadIdx.x & 63) == 0) { xs[0][wv] = mn; xs[1][wv] = mx; }
+        __syncthreads();
+        mn = min(min(xs[0][0], xs[0][1]), min(xs[0][2], xs[0][3]));
+        mx = max(max(xs[1][0], xs[1][1]), max(xs[1][2], xs[1][3]));
+    };
+    if (xr) {   // (block-uniform)
+        block_minmax(bmin, bmax);
+        if (threadIdx.x == 0) { st_agent(xr + 3 + 2 * blockIdx.x, bmin); st_agent(xr + 4 + 2 * blockIdx.x, bmax); }
+    }
     if (!last_block_done(ticket)) return;
+    if (xr) {
+        int mn = INT_MAX, mx = INT_MIN;
+        for (int b = threadIdx.x; b < (int)gridDim.x; b += blockDim.x) {
+            mn = min(mn, ld_agent(xr + 3 + 2 * b));
+            mx = max(mx, ld_agent(xr + 4 + 2 * b));
+        }
+        __syncthreads();   // (xs is reused)
+        block_minmax(mn, mx);
+        if (threadIdx.x == 0) { xr[0] = mn; xr[1] = mx; }   // read by the later kernels of the chain
+    }
     const int nbins = nb.x * nb.y * nb.z;
     const int total = block_counts_to_bounds<256>(nbins, cnt, start, nullptr, true, sh);
     // guard: the counts add up to the owned atoms (k_g_scatter re-zeroes them each evaluation);
