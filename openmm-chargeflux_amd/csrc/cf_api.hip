@@ -1063,7 +1063,7 @@ static void launch_end(cf_handle* H, int flags, double* forces_dev, double* ener
     if (h.pbc && (forces || energy) && (h.hi > h.lo || h.rank == 0)) {
         Timed t(H, PH_COEFFS);
         if (h.kspace_algo == 0) cf::launch_kspace_coeffs(h, energy);
-        else if (h.kspace_algo == 2) cf::launch_grid_coeffs(h, energy);
+        else if (h.kspace_algo == 2) cf::launch_grid_coeffs(h, energy, forces && h.hi > h.lo);   // (the inverse below)
         else cf::launch_kspace_direct_coeffs(h, energy);
     }
     if (h.hi > h.lo) {
@@ -1251,7 +1251,7 @@ static void launch_rec_fwd(cf_handle* H, const double* pos_dev) {
 }
 static void launch_rec_end(cf_handle* H, int flags) {
     cf::Handle& h = H->h;
-    { Timed t(H, PH_COEFFS); cf::launch_grid_coeffs(h, flags & CF_INCLUDE_ENERGY); }
+    { Timed t(H, PH_COEFFS); cf::launch_grid_coeffs(h, flags & CF_INCLUDE_ENERGY, (flags & CF_INCLUDE_FORCES) != 0); }
     if (flags & CF_INCLUDE_FORCES) {
         { Timed t(H, PH_GDFTI); cf::launch_grid_dft_inv(h); }
         { Timed t(H, PH_GINTERP); cf::launch_grid_interp(h, true); }

@@ -221,6 +221,8 @@ struct Handle {
     double* t_part = nullptr;   // [nparts][Nown][4]
     double* e_rec_part = nullptr; // [nblk]
     int e_rec_nblk = 0;
+    int coef_inv = 0;           // several ranks: the next inverse x stage applies the coefficients (1; 2: and
+                                // writes the energy partials) -- set by launch_grid_coeffs
     // k-space (grid path)
     GridPlan gp;
     double* g_grid = nullptr;   // [ngx][ngy][ngz] spread charges, later the potential grid
@@ -304,7 +306,7 @@ void launch_grid_sort(Handle& h, const double* pos);
 void launch_grid_spread(Handle& h);
 void launch_grid_dft_fwd(Handle& h);
 double* grid_reduce_buffer(Handle& h, int64_t* count);
-void launch_grid_coeffs(Handle& h, int include_energy);
+void launch_grid_coeffs(Handle& h, int include_energy, bool inverse_follows);
 void launch_grid_dft_inv(Handle& h);
 void launch_grid_interp(Handle& h, bool split = false);   // split: store into dedq_rec / f_rec
 

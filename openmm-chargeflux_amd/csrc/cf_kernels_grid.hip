@@ -1441,9 +1441,13 @@ __global__ void __launch_bounds__(64 * NB) k_g_dft8_zinv(Dft8 d, const double2* 
 // class and forms Z[b][r] for the chunk; then each thread turns one (sequence, b) into the
 // outputs n = Qa + b.  b chunks are independent, so they are also dealt over gridDim.y blocks
 // of the same sequences.
-template <int MT, bool ROUT, int SEQ>
+// COEF (several ranks, the x stage): the coefficient pass of k_g_coeffs applied as the all-reduced
+// B(n) is loaded (f = w_z c a conj(S) / phih, S = B D), with the energy of each element summed by
+// the blockIdx.y = 0 blocks (each loads every element of its sequences once) into e_part[blockIdx.x]
+// -- the same per-element arithmetic as the forward x stage's COEF form on one rank
+template <int MT, bool ROUT, int SEQ, bool COEF = false>
 __global__ void __launch_bounds__(8 * SEQ) k_g_dft8_inv(Dft8 d, const double2* __restrict__ twist,
-                                                        const double2* __restrict__ tq) {
+                                                        const double2* __restrict__ tq, Coef cf = Coef{}) {
     constexpr int SP = SEQ + 1, NT = 8 * SEQ;
     extern __shared__ v2d sm8[];
     v2d* sZ = sm8;                      // [kD8BC][8][SP]
@@ -1472,6 +1476,44 @@ __global__ void __launch_bounds__(8 * SEQ) k_g_dft8_inv(Dft8 d, const double2* _
             const bool okt = ok && t < cnt;
             const v2d v = reinterpret_cast<const v2d*>(d.in)[okt ? base + (long)(j0 + 8 * t) * d.cj : 0];
             cv[t] = okt ? v : v2d{0.0, 0.0};
+        }
+        if constexpr (COEF) {
+            // sequence s = (ny index, nz), mode j = nx + KX - 1, as in k_g_dft8_fwd's COEF form
+            // (RCK:528, 549-551)
+            __shared__ double red[8 * SEQ / 64];
+            double e = 0;
+            if (ok) {
+                const int nz = s % cf.KZ, ny = s / cf.KZ - (cf.KY - 1);
+                const double ky = ny * cf.rec.y, kz = nz * cf.rec.z;
+                const double wz = nz > 0 ? 2.0 : 1.0;
+                const double Dyz = cf.dy[abs(ny)] * cf.dz[nz];
+#pragma unroll
+                for (int t = 0; t < MT; t++) {
+                    if (t < cnt) {
+                        const int j = j0 + 8 * t, nx = j - (cf.KX - 1);
+                        const double kx = nx * cf.rec.x;
+                        const double k2 = kx * kx + ky * ky + kz * kz;
+                        const double a = k2 > 0 ? exp(-k2 * 0.25 * cf.one_4a2) / k2 : 0.0;
+                        const double D = cf.dx[abs(nx)] * Dyz;
+                        const double sr = cv[t].x * D, si = cv[t].y * D;
+                        e += 0.5 * wz * cf.cst * a * (sr * sr + si * si);
+                        const double c = wz * cf.cst * a * D;
+                        cv[t] = v2d{c * sr, -c * si};
+                    }
+                }
+            }
+            if (cf.e_part && blockIdx.y == 0) {   // (block-uniform)
+#pragma unroll
+                for (int m = 32; m >= 1; m >>= 1) e += __shfl_xor(e, m);
+                if (lane == 0) red[wave_id()] = e;
+                __syncthreads();
+                if (tid == 0) {
+                    double tot = 0;
+#pragma unroll
+                    for (int w = 0; w < 8 * SEQ / 64; w++) tot += red[w];
+                    cf.e_part[blockIdx.x] = tot;
+                }
+            }
         }
     }
     const int sl = ROUT ? (tid >> 3) : (tid % SEQ), bl = ROUT ? (tid & 7) : (tid / SEQ);
@@ -2537,7 +2579,7 @@ static void d8_fwd(Handle& h, int axis, const void* in, void* out, const Coef* c
 #undef CF_D8F_
 }
 
-static void d8_inv(Handle& h, int axis, const void* in, void* out) {
+static void d8_inv(Handle& h, int axis, const void* in, void* out, const Coef* cf = nullptr) {
     Dft8 d = d8_stage(h, axis);
     d.in = in; d.out = out;
     if (axis == 0) d.xmode = 0;   // synthesis along x: every plane is written (inputs are complete)
@@ -2560,6 +2602,14 @@ static void d8_inv(Handle& h, int axis, const void* in, void* out) {
     const double2* twist = h.g_tw8[axis];
     const double2* tq = twist + 8 * d.Q;
     const size_t lds2 = (size_t)(kD8BC * 8 * (kD8Seq + 1) + 8 * d.Q + d.Q * h.gp.mt[axis]) * sizeof(double2);
+    if (cf) {   // the x stage with the coefficient pass (several ranks): its x-blocks' energy partials
+        h.e_rec_nblk = (int)grid.x;
+#define CF_D8IC(MT_) \
+    hipLaunchKernelGGL((k_g_dft8_inv<MT_, false, kD8Seq, true>), grid, dim3(8 * kD8Seq), lds2, h.stream, d, twist, tq, *cf)
+        CF_D8_MT(h.gp.mt[axis], CF_D8IC)
+#undef CF_D8IC
+        return;
+    }
 #define CF_D8I(MT_)                                                                                            \
     if (axis == 2) hipLaunchKernelGGL((k_g_dft8_inv<MT_, true, kD8Seq>), grid, dim3(8 * kD8Seq), lds2, h.stream, d, twist, tq); \
     else hipLaunchKernelGGL((k_g_dft8_inv<MT_, false, kD8Seq>), grid, dim3(8 * kD8Seq), lds2, h.stream, d, twist, tq)
@@ -2609,8 +2659,13 @@ double* grid_reduce_buffer(Handle& h, int64_t* count) {
     return reinterpret_cast<double*>(h.g_b);
 }
 
-void launch_grid_coeffs(Handle& h, int include_energy) {
+void launch_grid_coeffs(Handle& h, int include_energy, bool inverse_follows) {
+    h.coef_inv = 0;
     if (coef_fused(h)) return;   // done by the forward x stage (launch_grid_dft_fwd)
+    if (h.gp.dft8 && inverse_follows) {   // several ranks: done by the inverse x stage (launch_grid_dft_inv)
+        h.coef_inv = include_energy ? 2 : 1;
+        return;
+    }
     const GridPlan& p = h.gp;
     const double V = h.box_L[0] * h.box_L[1] * h.box_L[2];
     const double cst = 4.0 / V * kPi * h.ke;   // RCK:517
@@ -2624,7 +2679,14 @@ void launch_grid_coeffs(Handle& h, int include_energy) {
 void launch_grid_dft_inv(Handle& h) {
     const GridPlan& p = h.gp;
     if (p.dft8) {
-        d8_inv(h, 0, h.g_b, h.g_t2);
+        if (h.coef_inv) {   // the coefficient pass on the all-reduced B(n), as the x stage loads it
+            Coef cf = coef_args(h);
+            if (h.coef_inv == 1) cf.e_part = nullptr;
+            h.coef_inv = 0;
+            d8_inv(h, 0, h.g_b, h.g_t2, &cf);
+        } else {
+            d8_inv(h, 0, h.g_b, h.g_t2);
+        }
         d8_inv(h, 1, h.g_t2, h.g_t1);
         d8_inv(h, 2, h.g_t1, h.g_grid);
         return;
